@@ -1,0 +1,384 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE
+implementation (caterer-z-t/GRiD, read-only at /root/reference).
+
+Run in the build container only (the GPU box has no /root/reference):
+
+    python tests/golden/make_golden.py
+
+What it writes (all small):
+  g1/  file-level cohort, genome-scale mode (no window), chrom filter chr1 with
+       chr10/chr2 decoy lines, a repeat mask, read counts, IBS + IBD neighbour
+       files; expected outputs of reference steps 4,5,6,7 (IBS) and 7 (IBD,
+       weighted) run through the reference's own step functions.
+  g1b/ file-level cohort crossing the 8192-element NumPy reduction block
+       (M > 8192 bins), LPA-style window off.
+  g1c/ LPA-style window (chrom/start_bp/end_bp set), kd-tree k-NN path.
+  g2.npz   normalize_matrix on widths 8191/8192/8193/16385/... with NaN holes,
+           a zero row, an all-NaN column and a zero column.
+  g3.json  find_neighbors_sklearn on tie-free hundredth matrices (brute and
+           kd-tree paths).
+  g4.json  _run_phasing/_compute_imp on IBS-style and IBD-weighted lists.
+  g5.json  %.2f / %.3f formatting edge cases.
+  meta.json  library versions of the oracle run.
+
+pysam is stubbed exactly as the reference's own test/conftest.py:9-11 does.
+"""
+from __future__ import annotations
+
+import gzip
+import json
+import os
+import shutil
+import sys
+import tempfile
+from pathlib import Path
+from unittest.mock import MagicMock
+
+import numpy as np
+import yaml
+
+REF = Path("/root/reference")
+HERE = Path(__file__).resolve().parent
+
+sys.modules.setdefault("pysam", MagicMock())
+sys.path.insert(0, str(REF))
+
+from rich.console import Console  # noqa: E402
+
+import grid.cli  # noqa: E402
+from grid.utils import normalize_mosdepth as ref_norm  # noqa: E402
+from grid.utils import find_neighbors as ref_fn  # noqa: E402
+from grid.utils import compute_dipcn as ref_dip  # noqa: E402
+from grid.utils import hi_inference as ref_hi  # noqa: E402
+
+CONSOLE = Console(theme=grid.cli.grid_theme, quiet=True)
+
+
+# ------------------------------------------------------------ synthesis ----
+def synth_cohort(rng, n, m, n_clusters, bin_size=1000, start0=0):
+    """Depth hundredths (n x m) with per-bin base depth, cluster offsets,
+    per-sample scale, CNVs and gamma noise."""
+    base = rng.gamma(20.0, 1.5, size=m)
+    clus = rng.integers(0, n_clusters, size=n)
+    offs = 1.0 + rng.uniform(-0.08, 0.08, size=(n_clusters, m))
+    scale = rng.uniform(0.6, 1.4, size=n)
+    cnv = np.ones((n, m))
+    hit = rng.random((n, m)) < 0.02
+    cnv[hit] = rng.choice([0.5, 1.5], size=hit.sum())
+    lam = base[None, :] * offs[clus] * scale[:, None] * cnv
+    noise = rng.gamma(40.0, 1.0 / 40.0, size=(n, m))
+    q = np.maximum(0, np.rint(lam * noise * 100)).astype(np.int64)
+    starts = start0 + np.arange(m) * bin_size
+    return q, starts, clus
+
+
+def write_bed(path, chrom_rows):
+    with gzip.open(path, "wt") as f:
+        for chrom, s, e, q in chrom_rows:
+            f.write(f"{chrom}\t{s}\t{e}\t{q // 100}.{q % 100:02d}\n")
+
+
+def make_file_cohort(root: Path, rng, n, m, chrom, window=None, decoys=True,
+                     bin_size=1000, start0=0, n_clusters=4):
+    root.mkdir(parents=True, exist_ok=True)
+    md = root / "mosdepth"
+    md.mkdir(exist_ok=True)
+    q, starts, clus = synth_cohort(rng, n, m, n_clusters, bin_size, start0)
+    ids = [f"S{i:04d}" for i in range(n)]
+    for i, sid in enumerate(ids):
+        rows = []
+        if decoys:
+            # chr10 lines: start with "chr1" -> kept by the startswith filter
+            # (reference quirk Q2); first 30 collide with chr1 coordinates
+            # (last-wins, Q1), the rest are new coordinates.
+            for b in range(30):
+                rows.append(("chr10", int(starts[b]), int(starts[b] + bin_size), int(q[i, b] // 2 + 150)))
+            for b in range(3):
+                s = int(starts[-1] + (b + 5) * bin_size)
+                rows.append(("chr10", s, s + bin_size, int(3000 + 7 * i + b)))
+            rows.append(("chr2", 0, bin_size, 5000))
+        for b in range(m):
+            rows.append((chrom, int(starts[b]), int(starts[b] + bin_size), int(q[i, b])))
+        # a malformed line (skipped by the reference: < 4 fields)
+        rows_txt = rows
+        name = f"{sid}_LPA.regions.bed.gz" if i % 3 else f"{sid}.regions.bed.gz"
+        write_bed(md / name, rows_txt)
+    # a stray file for a sample not in the list
+    write_bed(md / "ZZ9999_LPA.regions.bed.gz", [(chrom, int(starts[0]), int(starts[0] + bin_size), 4000)])
+    # sample list: all + one with no file
+    (root / "samples.txt").write_text("\n".join(ids + ["S9998"]) + "\n")
+    # repeat mask: a handful of intervals, chrom without 'chr' prefix for one
+    lines = ["# repeat mask", ""]
+    for b in rng.choice(m, size=max(1, m // 40), replace=False):
+        s = int(starts[b]) + 200
+        lines.append(f"{chrom}\t{s}\t{s + 300}\tAluY")
+    lines.append(f"{chrom.replace('chr', '')}\t{int(starts[min(7, m-1)])}\t{int(starts[min(7, m-1)]) + 10}")
+    lines.append("chrX\t1")
+    (root / "mask.bed").write_text("\n".join(lines) + "\n")
+    # read counts (count_reads format, header replaced by pandas names=)
+    cnt = ["Sample\tchr6:1-2"]
+    for i, sid in enumerate(ids):
+        if i == 3:
+            cnt.append(f"{sid}\tError")
+            continue
+        if i == 5:
+            continue
+        cn = rng.choice([1.0, 1.5, 2.0, 2.5])
+        cnt.append(f"{sid}\t{int(rng.poisson(cn * 400 * (0.6 + (i % 7) * 0.1)))}")
+    (root / "counts.tsv").write_text("\n".join(cnt) + "\n")
+    # IBS (computeIBSpbwt) neighbours: header + ID hap nbrInd cMlen cMedge IDnbr hapNbr
+    ibs = ["ID\thap\tnbrInd\tcMlen\tcMedge\tIDnbr\thapNbr"]
+    for i, sid in enumerate(ids):
+        same = [j for j in range(n) if clus[j] == clus[i]]
+        for hap in (1, 2):
+            k = int(rng.integers(0, 14))
+            for t in range(k):
+                j = int(rng.choice(same))
+                ibs.append(f"{sid}\t{hap}\t{j}\t{rng.uniform(0.5, 9):.3f}\t0.1\t{ids[j]}\t{int(rng.integers(1, 3))}")
+        if i % 9 == 0:
+            ibs.append(f"{sid}\t3\t0\t1.0\t0.1\t{ids[0]}\t1")       # invalid hap
+            ibs.append(f"{sid}\t1\t0\t1.0\t0.1\tNOPE\t1")           # unknown id
+            ibs.append(f"{sid}\t1\t0\t1.0")                          # short line
+    with gzip.open(root / "ibs.tsv.gz", "wt") as f:
+        f.write("\n".join(ibs) + "\n")
+    # IBD (iLASH): FID1 HAP_ID1 FID2 HAP_ID2 CHR BP1 BP2 SNP_BP1 SNP_BP2 LENGTH MATCH
+    ibd = []
+    for t in range(n * 8):
+        i, j = int(rng.integers(0, n)), int(rng.integers(0, n))
+        h1, h2 = int(rng.integers(0, 2)), int(rng.integers(0, 2))
+        bp1 = int(rng.integers(0, 4_000_000))
+        bp2 = bp1 + int(rng.integers(1000, 3_000_000))
+        ibd.append(f"{ids[i]}\t{ids[i]}_{h1}\t{ids[j]}\t{ids[j]}_{h2}\t6\t{bp1}\t{bp2}\t{bp1}\t{bp2}"
+                   f"\t{rng.uniform(0.2, 12):.4f}\t{rng.uniform(0.5, 1.0):.3f}")
+    (root / "ibd.txt").write_text("\n".join(ibd) + "\n")
+    cfg = {
+        "samples_file": str(root / "samples.txt"),
+        "output_dir": str(root / "out"),
+        "threads": 1,
+        "chrom": chrom,
+        "output_file_type": "tsv",
+        "index": {"run": False},
+        "count_reads": {"run": False, "output_file_prefix": "counts"},
+        "mosdepth": {
+            "run": False,
+            "work_dir": str(md),
+            "remove_intermediate": False,
+            "normalize": {"run": True, "min_depth": 20, "max_depth": 100, "top_frac": 0.1,
+                          "output_file_prefix": "normalized", "repeat_mask_file": str(root / "mask.bed")},
+            "neighbors": {"run": True, "output_file_prefix": "neighbors", "num_neighbors": 5,
+                          "zmax": 2.0, "sigma2_max": 1000},
+        },
+        "compute_diploid_genotypes": {"run": True, "output_file_prefix": "dipcn", "n_nbr": 4},
+        "compute_haploid_genotypes": {"run": True, "output_file_prefix": "haploid", "method": "ibs",
+                                      "min_neighbors": 1, "max_neighbors": 10, "n_iters": 100,
+                                      "ibs_output": str(root / "ibs.tsv.gz")},
+    }
+    if window:
+        cfg["start_bp"], cfg["end_bp"] = window
+    return cfg
+
+
+def run_reference(cfg, root: Path):
+    """Run the reference's step functions (not the CLI: it would also try the
+    OOS steps)."""
+    out = Path(cfg["output_dir"])
+    out.mkdir(parents=True, exist_ok=True)
+    (out / "counts.tsv").write_text((root / "counts.tsv").read_text())
+    ref_norm.normalize_mosdepth(cfg, CONSOLE)
+    ref_fn.find_neighbors(cfg, CONSOLE)
+    ref_dip.compute_diploid_genotypes(cfg, CONSOLE)
+    ref_hi.hi_inference(cfg, CONSOLE)
+    # IBD, weighted, as a second step-7 run
+    cfg2 = json.loads(json.dumps(cfg))
+    hc = cfg2["compute_haploid_genotypes"]
+    hc.update({"method": "ibd", "ibd_output": str(root / "ibd.txt"), "weighted": True,
+               "weight_scale": 1_000_000, "min_length": 0.5, "min_match": 0.7,
+               "output_file_prefix": "haploid_ibd", "min_neighbors": 2, "max_neighbors": 6,
+               "n_iters": 37})
+    cfg2.setdefault("start_bp", 1_500_000)
+    cfg2.setdefault("end_bp", 1_600_000)
+    ref_hi.hi_inference(cfg2, CONSOLE)
+    return cfg2
+
+
+def check_tie_free(norm_gz: Path, k: int, zmax: float, sigma2_max: float):
+    """Exact-integer check that no row of the reference's k-NN input has a
+    distance tie inside its first k+2 neighbours (sklearn's tie order is
+    unspecified)."""
+    ids, ratios, z, _ = ref_fn.read_normalized_data(norm_gz)
+    z = np.nan_to_num(np.clip(z, -zmax, zmax), nan=0.0)
+    idx, _ = ref_fn.filter_regions_by_variance(ratios, 1.0, sigma2_max)
+    q = np.rint(z[:, idx] * 100).astype(np.int64)
+    g = q @ q.T
+    n = np.diag(g)
+    d2 = n[:, None] + n[None, :] - 2 * g
+    for i in range(len(ids)):
+        row = np.sort(d2[i])[: k + 3]
+        if len(set(row.tolist())) != len(row):
+            return False
+    return True
+
+
+def finalize_cohort(name, root: Path, cfg, cfg_ibd):
+    dst = HERE / name
+    if dst.exists():
+        shutil.rmtree(dst)
+    (dst / "expected").mkdir(parents=True)
+    (dst / "inputs").mkdir()
+    shutil.copytree(root / "mosdepth", dst / "inputs" / "mosdepth")
+    for f in ("samples.txt", "mask.bed", "counts.tsv", "ibs.tsv.gz", "ibd.txt"):
+        shutil.copy(root / f, dst / "inputs" / f)
+    out = Path(cfg["output_dir"])
+    # store expected outputs decompressed-content-identical (re-gzip small)
+    for f in out.iterdir():
+        shutil.copy(f, dst / "expected" / f.name)
+
+    def rel(c):
+        c = json.loads(json.dumps(c))
+        c["samples_file"] = "inputs/samples.txt"
+        c["output_dir"] = "out"
+        c["mosdepth"]["work_dir"] = "inputs/mosdepth"
+        c["mosdepth"]["normalize"]["repeat_mask_file"] = "inputs/mask.bed"
+        hc = c["compute_haploid_genotypes"]
+        if "ibs_output" in hc:
+            hc["ibs_output"] = "inputs/ibs.tsv.gz"
+        if "ibd_output" in hc:
+            hc["ibd_output"] = "inputs/ibd.txt"
+        return c
+
+    (dst / "config.yaml").write_text(yaml.safe_dump(rel(cfg), sort_keys=False))
+    (dst / "config_ibd.yaml").write_text(yaml.safe_dump(rel(cfg_ibd), sort_keys=False))
+
+
+def file_cohort(name, seed, n, m, chrom, window=None, decoys=True, start0=0, bin_size=1000,
+                k=None, n_clusters=4):
+    for attempt in range(20):
+        rng = np.random.default_rng(seed + 1000 * attempt)
+        tmp = Path(tempfile.mkdtemp(prefix=f"golden_{name}_"))
+        cfg = make_file_cohort(tmp, rng, n, m, chrom, window, decoys, bin_size, start0, n_clusters)
+        if k is not None:
+            cfg["mosdepth"]["neighbors"]["num_neighbors"] = k
+        cfg_ibd = run_reference(cfg, tmp)
+        norm = Path(cfg["output_dir"]) / "normalized.tsv.gz"
+        if check_tie_free(norm, cfg["mosdepth"]["neighbors"]["num_neighbors"], 2.0, 1000):
+            finalize_cohort(name, tmp, cfg, cfg_ibd)
+            shutil.rmtree(tmp)
+            print(f"{name}: ok (seed attempt {attempt})")
+            return
+        shutil.rmtree(tmp)
+    raise RuntimeError(f"{name}: could not make a tie-free cohort")
+
+
+# ---------------------------------------------------------------- vectors --
+def g2():
+    rng = np.random.default_rng(2)
+    out = {}
+    cases = [(4, 5), (3, 130), (2, 8191), (2, 8192), (2, 8193), (2, 16385), (6, 300)]
+    for ci, (n, m) in enumerate(cases):
+        q = rng.integers(1, 9000, size=(n, m)).astype(np.float64)
+        mat = q / 100.0
+        mat[rng.random((n, m)) < 0.05] = np.nan
+        if ci == 6:
+            mat[:, 3] = np.nan          # all-NaN column
+            mat[:, 4] = 0.0             # zero column (mu = 0 -> not transformed)
+            mat[2, :] = 0.0             # zero row (row mean 0 -> NaN row)
+        with np.errstate(all="ignore"):
+            raw = np.nanmean(mat, axis=1)
+            z, ratios, mu, var = ref_norm.normalize_matrix(mat)
+        keys = sorted(ratios)
+        out[f"c{ci}_in"] = mat
+        out[f"c{ci}_raw"] = raw
+        out[f"c{ci}_z"] = z
+        out[f"c{ci}_mu"] = mu
+        out[f"c{ci}_var"] = var
+        out[f"c{ci}_rkeys"] = np.array(keys, dtype=np.int64)
+        out[f"c{ci}_rvals"] = np.array([ratios[k] for k in keys])
+        for tf in (0.0, 0.1, 0.5, 0.9):
+            out[f"c{ci}_sel_{tf}"] = np.array(ref_norm.select_high_variance_regions(ratios, tf), dtype=np.int64)
+    np.savez_compressed(HERE / "g2.npz", **out)
+    print("g2: ok")
+
+
+def g3():
+    rng = np.random.default_rng(3)
+    cases = []
+    for (n, r, k) in [(50, 40, 10), (50, 8, 6), (12, 20, 30), (3, 1, 5), (40, 16, 39)]:
+        for attempt in range(200):
+            q = rng.integers(-200, 201, size=(n, r))
+            g = q @ q.T
+            nn = np.diag(g)
+            d2 = nn[:, None] + nn[None, :] - 2 * g
+            ok = all(len(set(np.sort(d2[i]).tolist())) == n for i in range(n))
+            if ok or n > 40:
+                break
+        data = q / 100.0
+        ids = [f"X{i:03d}" for i in range(n)]
+        res = ref_fn.find_neighbors_sklearn(data, ids, n_neighbors=k)
+        cases.append({"q": q.tolist(), "k": k,
+                      "res": {sid: [[nb, float(d).hex()] for nb, d in lst] for sid, lst in res.items()}})
+    (HERE / "g3.json").write_text(json.dumps(cases))
+    print("g3: ok")
+
+
+def g4():
+    rng = np.random.default_rng(4)
+    cases = []
+    for (n, min_nbr, iters, weighted) in [(30, 1, 100, False), (25, 0, 7, False), (40, 3, 50, False),
+                                          (30, 2, 20, True), (1, 1, 5, False)]:
+        irr = [float(x) for x in rng.uniform(0.2, 4.0, size=n)]
+        if n > 3:
+            irr[2] = 0.0
+        hap_nbrs = []
+        for h in range(2 * n):
+            k = int(rng.integers(0, 8))
+            lst = []
+            for _ in range(k):
+                nb = int(rng.integers(0, 2 * n))
+                w = float(rng.uniform(0.05, 1.0)) if weighted else 1.0
+                lst.append((nb, w))
+            if h % 11 == 0:
+                lst.append((h, 1.0))                    # self neighbour
+            if h % 13 == 0 and lst:
+                lst.append(lst[0])                      # duplicate
+            hap_nbrs.append(lst)
+        hap, mean = ref_hi._run_phasing(irr, hap_nbrs, min_nbr, iters, CONSOLE)
+        imp = [ref_hi._compute_imp(i, hap, hap_nbrs, mean) for i in range(n)]
+        cases.append({"irr": [x.hex() for x in irr], "nbrs": [[[a, b.hex()] for a, b in l] for l in hap_nbrs],
+                      "min_nbr": min_nbr, "iters": iters,
+                      "hap": [x.hex() for x in hap], "mean": mean.hex(),
+                      "imp": [[a.hex(), b.hex()] for a, b in imp]})
+    (HERE / "g4.json").write_text(json.dumps(cases))
+    print("g4: ok")
+
+
+def g5():
+    vals = [0.125, 0.135, 2.675, -0.001, -0.0, 0.0, -0.005, 0.005, 1e-9, -1e-9, 123456.785,
+            0.045, 1.005, 2.5e-3, -2.5e-3, 99.995, -99.995, float("inf")]
+    rng = np.random.default_rng(5)
+    vals += [float(x) for x in rng.uniform(-5, 5, 200)]
+    vals += [float(k) / 200.0 for k in range(-400, 401)]     # exact-ish halves of hundredths
+    vals += [float(k) / 2000.0 for k in range(-60, 61)]      # halves of thousandths
+    (HERE / "g5.json").write_text(json.dumps([[v.hex(), f"{v:.2f}", f"{v:.3f}"] for v in vals]))
+    print("g5: ok")
+
+
+def main():
+    import sklearn
+    import pandas
+    os.environ.setdefault("OMP_NUM_THREADS", "1")
+    file_cohort("g1", 11, 40, 2400, "chr1", decoys=True)
+    file_cohort("g1b", 21, 10, 8600, "chr1", decoys=False)
+    file_cohort("g1c", 31, 30, 60, "chr6", window=(160_605_062, 160_647_661), decoys=False,
+                start0=160_590_000, k=7)
+    g2()
+    g3()
+    g4()
+    g5()
+    meta = {"numpy": np.__version__, "sklearn": sklearn.__version__, "pandas": pandas.__version__,
+            "python": sys.version.split()[0], "reference": str(REF)}
+    (HERE / "meta.json").write_text(json.dumps(meta, indent=1))
+
+
+if __name__ == "__main__":
+    main()
