@@ -1,0 +1,243 @@
+"""ctypes binding of libgridhip.so (include/grid_abi.h).
+
+This is the only module that talks to the native library.  There is no CPU
+fallback: if the library is missing, was not built, or no gfx950 device is
+visible, every compute entry point raises ``GridNativeError``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("GRID_AMD_LIB", _HERE / "_lib" / "libgridhip.so"))
+
+GRID_OK, GRID_EINVAL, GRID_EHIP, GRID_EZERODIV, GRID_EUNSUPPORTED, GRID_ERANGE = range(6)
+MISSING = -(2 ** 31)          # GRID_MISSING / GRID_ZQ_NAN
+ZQ_NAN = -(2 ** 31)
+ZQ_NEG0 = -(2 ** 31) + 1
+BLOCK = 8192
+
+_i64, _i32, _f64, _vp = C.c_int64, C.c_int32, C.c_double, C.c_void_p
+
+# name -> argtypes (all return int)
+_SIGS = {
+    "grid_abi_version": [],
+    "grid_device_count": [C.POINTER(C.c_int)],
+    "grid_ctx_create": [C.c_int, C.POINTER(_vp)],
+    "grid_ctx_destroy": [_vp],
+    "grid_ctx_set_stream": [_vp, _vp],
+    "grid_sync": [_vp],
+    "grid_dev_alloc": [_vp, C.c_size_t, C.POINTER(_vp)],
+    "grid_dev_free": [_vp, _vp],
+    "grid_h2d": [_vp, _vp, _vp, C.c_size_t],
+    "grid_d2h": [_vp, _vp, _vp, C.c_size_t],
+    "grid_d2d": [_vp, _vp, _vp, C.c_size_t],
+    "grid_memset": [_vp, _vp, C.c_int, C.c_size_t],
+    "grid_event_record": [_vp, C.c_int],
+    "grid_event_elapsed": [_vp, C.c_int, C.c_int, C.POINTER(C.c_float)],
+    "grid_norm_row_blocks": [_vp, _vp, _i64, _i64, _i64, _vp, _vp],
+    "grid_norm_row_means": [_vp, _vp, _vp, _i64, _i64, _vp],
+    "grid_norm_col_means": [_vp, _vp, _i64, _i64, _i64, _vp, _vp],
+    "grid_norm_col_vars": [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
+    "grid_sort_valid": [_vp, _vp, _i64, _vp, C.POINTER(_i64)],
+    "grid_select_gt": [_vp, _vp, _i64, _f64, _vp, C.POINTER(_i64)],
+    "grid_round_decimals": [_vp, _vp, _i64, C.c_int, _vp],
+    "grid_gather_f64": [_vp, _vp, _vp, _i64, _vp],
+    "grid_colmap_range": [_vp, _vp, _i64, _f64, _f64, _vp, C.POINTER(_i64)],
+    "grid_norm_zquant": [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _f64, _vp, _i64, _vp, _i32,
+                         _vp, _i64, C.POINTER(_i32)],
+    "grid_knn_gram": [_vp, _vp, _i64, _i64, _i64, _i32, _vp],
+    "grid_knn_topk": [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _vp, _vp, _vp],
+    "grid_dipcn": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, C.POINTER(_i32)],
+    "grid_hi_levels": [_i64, _vp, _vp, _vp, _vp, C.POINTER(_i32)],
+    "grid_hi_phase": [_vp, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _i32, _vp, _vp, _vp],
+    "grid_format_hundredths": [_vp, _i64, _vp, _i64, C.POINTER(_i64)],
+}
+EXPORTS = tuple(_SIGS) + ("grid_last_error",)
+
+
+class GridNativeError(RuntimeError):
+    """The HIP native path failed or is unavailable (no silent fallback)."""
+
+
+_lib = None
+
+
+def load():
+    """Load libgridhip.so once.  If torch is already imported, the library
+    binds to torch's HIP runtime (same soname), so torch device pointers and
+    streams can be passed straight through."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise GridNativeError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                              "or `make -C grid_amd/csrc`")
+    lib = C.CDLL(str(LIB_PATH), mode=C.RTLD_GLOBAL)
+    for name, args in _SIGS.items():
+        f = getattr(lib, name)
+        f.argtypes = args
+        f.restype = C.c_int
+    lib.grid_last_error.argtypes = []
+    lib.grid_last_error.restype = C.c_char_p
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str = ""):
+    if rc == GRID_OK:
+        return
+    msg = load().grid_last_error().decode(errors="replace")
+    if rc == GRID_EZERODIV:
+        raise ZeroDivisionError(msg or "float division by zero")
+    raise GridNativeError(f"{what}: {msg} (code {rc})")
+
+
+def call(name: str, *args):
+    check(getattr(load(), name)(*args), name)
+
+
+def ptr(a) -> int:
+    """Address of a numpy array, DevBuf or torch tensor."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        if not a.flags.c_contiguous:
+            raise ValueError("array must be C-contiguous")
+        return a.ctypes.data
+    if isinstance(a, DevBuf):
+        return a.ptr
+    if hasattr(a, "data_ptr"):
+        return a.data_ptr()
+    return int(a)
+
+
+class Device:
+    """One HIP context (one GPU, one stream).  Not shared across threads."""
+
+    def __init__(self, device: int = 0, stream=None):
+        lib = load()
+        self.index = device
+        h = _vp()
+        check(lib.grid_ctx_create(device, C.byref(h)), "grid_ctx_create")
+        self.ctx = h.value
+        if stream is not None:
+            self.set_stream(stream)
+
+    def set_stream(self, stream):
+        s = stream if isinstance(stream, int) or stream is None else stream.cuda_stream
+        call("grid_ctx_set_stream", self.ctx, s)
+
+    def sync(self):
+        call("grid_sync", self.ctx)
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            load().grid_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- memory -----------------------------------------------------------
+    def alloc(self, shape, dtype) -> "DevBuf":
+        return DevBuf(self, shape, dtype)
+
+    def upload(self, a: np.ndarray) -> "DevBuf":
+        a = np.ascontiguousarray(a)
+        b = DevBuf(self, a.shape, a.dtype)
+        call("grid_h2d", self.ctx, b.ptr, a.ctypes.data, a.nbytes)
+        return b
+
+    def zeros(self, shape, dtype) -> "DevBuf":
+        b = DevBuf(self, shape, dtype)
+        b.zero()
+        return b
+
+    def record(self, slot: int):
+        call("grid_event_record", self.ctx, slot)
+
+    def elapsed_ms(self, a: int, b: int) -> float:
+        f = C.c_float()
+        call("grid_event_elapsed", self.ctx, a, b, C.byref(f))
+        return float(f.value)
+
+
+class DevBuf:
+    """Device allocation with a numpy-style shape/dtype."""
+
+    def __init__(self, dev: Device, shape, dtype):
+        self.dev = dev
+        self.shape = tuple(int(s) for s in (shape if isinstance(shape, (tuple, list)) else (shape,)))
+        self.dtype = np.dtype(dtype)
+        self.nbytes = int(np.prod(self.shape, dtype=np.int64)) * self.dtype.itemsize
+        h = _vp()
+        call("grid_dev_alloc", dev.ctx, self.nbytes, C.byref(h))
+        self.ptr = h.value
+
+    def zero(self):
+        call("grid_memset", self.dev.ctx, self.ptr, 0, self.nbytes)
+        return self
+
+    def fill_bytes(self, v: int):
+        call("grid_memset", self.dev.ctx, self.ptr, v, self.nbytes)
+        return self
+
+    def numpy(self) -> np.ndarray:
+        out = np.empty(self.shape, dtype=self.dtype)
+        call("grid_d2h", self.dev.ctx, out.ctypes.data, self.ptr, self.nbytes)
+        return out
+
+    def copy_from(self, a: np.ndarray):
+        a = np.ascontiguousarray(a, dtype=self.dtype)
+        assert a.nbytes <= self.nbytes
+        call("grid_h2d", self.dev.ctx, self.ptr, a.ctypes.data, a.nbytes)
+
+    def free(self):
+        if self.ptr:
+            load().grid_dev_free(self.dev.ctx, self.ptr)
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            if self.ptr and self.dev.ctx:
+                self.free()
+        except Exception:
+            pass
+
+
+def device_count() -> int:
+    n = C.c_int()
+    call("grid_device_count", C.byref(n))
+    return n.value
+
+
+def format_hundredths(v: np.ndarray) -> str:
+    """Exact "%.2f" text of integer hundredths, tab-joined (host C++)."""
+    v = np.ascontiguousarray(v, dtype=np.int32)
+    cap = 16 * v.size + 16
+    buf = C.create_string_buffer(cap)
+    n = _i64()
+    call("grid_format_hundredths", v.ctypes.data if v.size else None, v.size, buf, cap, C.byref(n))
+    return buf.raw[: n.value].decode("ascii")
+
+
+def hi_levels(off: np.ndarray, nbr: np.ndarray):
+    """Level schedule of the in-place Gauss-Seidel sweep (host C++)."""
+    off = np.ascontiguousarray(off, dtype=np.int64)
+    nbr = np.ascontiguousarray(nbr, dtype=np.int32)
+    n = (len(off) - 1) // 2
+    order = np.empty(max(n, 1), dtype=np.int32)
+    loff = np.empty(n + 2, dtype=np.int32)
+    nl = _i32()
+    call("grid_hi_levels", n, off.ctypes.data, nbr.ctypes.data if nbr.size else None, order.ctypes.data,
+         loff.ctypes.data, C.byref(nl))
+    return order[:n], loff[: nl.value + 1], nl.value

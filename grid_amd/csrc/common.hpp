@@ -1,0 +1,66 @@
+// Shared helpers for libgridhip.so (gfx950).  Not part of the ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+
+#include "grid_abi.h"
+
+struct grid_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipStream_t own = nullptr;
+  void *scratch = nullptr;     // grows on demand (hipcub temp storage etc.)
+  size_t scratch_bytes = 0;
+  void *pinned = nullptr;      // small pinned host buffer for scalars
+  hipEvent_t ev[8] = {};
+};
+
+void grid_set_error(const char *fmt, ...);
+int grid_scratch(grid_ctx *ctx, size_t bytes, void **p);
+
+#define HIPCHK(x)                                                                  \
+  do {                                                                             \
+    hipError_t e_ = (x);                                                           \
+    if (e_ != hipSuccess) {                                                        \
+      grid_set_error("%s:%d %s: %s", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      return GRID_EHIP;                                                            \
+    }                                                                              \
+  } while (0)
+
+#define REQUIRE(cond, ...)          \
+  do {                              \
+    if (!(cond)) {                  \
+      grid_set_error(__VA_ARGS__);  \
+      return GRID_EINVAL;           \
+    }                               \
+  } while (0)
+
+#define LAUNCHCHK()                                                               \
+  do {                                                                            \
+    hipError_t e_ = hipGetLastError();                                            \
+    if (e_ != hipSuccess) {                                                       \
+      grid_set_error("%s:%d launch: %s", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      return GRID_EHIP;                                                           \
+    }                                                                             \
+  } while (0)
+
+// Exact decimal rounding: the integer k such that Python's f"{v:.Nf}" prints
+// k / 10^N (correctly rounded, ties-to-even on the exact binary value of v).
+// p = v*s is rounded; e = fma(v, s, -p) is the exact residual, so when p lies
+// exactly on a half-integer the sign of e says on which side v*s really is.
+__host__ __device__ inline double round_dec_k(double v, double s) {
+  double p = v * s;
+  double e = fma(v, s, -p);
+  double k = rint(p);
+  double diff = p - k;
+  if (diff == 0.5 || diff == -0.5) {
+    if (e > 0.0) k = ceil(p);
+    else if (e < 0.0) k = floor(p);
+  }
+  return k;
+}
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }

@@ -1,0 +1,351 @@
+// Runtime, memory, sort/select utilities and host formatting for libgridhip.so.
+#include <hipcub/hipcub.hpp>
+
+#include <cstdarg>
+#include <cstring>
+#include <vector>
+
+#include "common.hpp"
+
+static thread_local char g_err[1024] = "";
+
+void grid_set_error(const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof g_err, fmt, ap);
+  va_end(ap);
+}
+
+int grid_scratch(grid_ctx *ctx, size_t bytes, void **p) {
+  if (bytes > ctx->scratch_bytes) {
+    if (ctx->scratch) {
+      HIPCHK(hipStreamSynchronize(ctx->stream));
+      HIPCHK(hipFree(ctx->scratch));
+      ctx->scratch = nullptr;
+    }
+    size_t nb = bytes + bytes / 4 + 4096;
+    HIPCHK(hipMalloc(&ctx->scratch, nb));
+    ctx->scratch_bytes = nb;
+  }
+  *p = ctx->scratch;
+  return GRID_OK;
+}
+
+extern "C" {
+
+const char *grid_last_error(void) { return g_err; }
+int grid_abi_version(void) { return 1; }
+
+int grid_device_count(int *n) {
+  HIPCHK(hipGetDeviceCount(n));
+  return GRID_OK;
+}
+
+int grid_ctx_create(int device, grid_ctx **out) {
+  REQUIRE(out, "out is NULL");
+  int nd = 0;
+  HIPCHK(hipGetDeviceCount(&nd));
+  REQUIRE(device >= 0 && device < nd, "device %d out of range (%d visible)", device, nd);
+  HIPCHK(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, device));
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    grid_set_error("device %d is %s; libgridhip is built for gfx950 only", device, prop.gcnArchName);
+    return GRID_EUNSUPPORTED;
+  }
+  grid_ctx *c = new grid_ctx();
+  c->device = device;
+  HIPCHK(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
+  c->stream = c->own;
+  HIPCHK(hipHostMalloc(&c->pinned, 4096, hipHostMallocDefault));
+  for (auto &e : c->ev) HIPCHK(hipEventCreate(&e));
+  *out = c;
+  return GRID_OK;
+}
+
+int grid_ctx_destroy(grid_ctx *ctx) {
+  if (!ctx) return GRID_OK;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->scratch) (void)hipFree(ctx->scratch);
+  if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+  for (auto &e : ctx->ev) (void)hipEventDestroy(e);
+  if (ctx->own) (void)hipStreamDestroy(ctx->own);
+  delete ctx;
+  return GRID_OK;
+}
+
+int grid_ctx_set_stream(grid_ctx *ctx, void *s) {
+  REQUIRE(ctx, "ctx is NULL");
+  ctx->stream = s ? (hipStream_t)s : ctx->own;
+  return GRID_OK;
+}
+
+int grid_sync(grid_ctx *ctx) {
+  REQUIRE(ctx, "ctx is NULL");
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return GRID_OK;
+}
+
+int grid_dev_alloc(grid_ctx *ctx, size_t bytes, void **p) {
+  REQUIRE(ctx && p, "bad args");
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipMalloc(p, bytes ? bytes : 16));
+  return GRID_OK;
+}
+
+int grid_dev_free(grid_ctx *ctx, void *p) {
+  REQUIRE(ctx, "ctx is NULL");
+  if (p) {
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipFree(p));
+  }
+  return GRID_OK;
+}
+
+int grid_h2d(grid_ctx *ctx, void *d, const void *h, size_t bytes) {
+  if (!bytes) return GRID_OK;
+  HIPCHK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return GRID_OK;
+}
+
+int grid_d2h(grid_ctx *ctx, void *h, const void *d, size_t bytes) {
+  if (!bytes) return GRID_OK;
+  HIPCHK(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return GRID_OK;
+}
+
+int grid_d2d(grid_ctx *ctx, void *d, const void *s, size_t bytes) {
+  if (!bytes) return GRID_OK;
+  HIPCHK(hipMemcpyAsync(d, s, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+  return GRID_OK;
+}
+
+int grid_memset(grid_ctx *ctx, void *d, int v, size_t bytes) {
+  if (!bytes) return GRID_OK;
+  HIPCHK(hipMemsetAsync(d, v, bytes, ctx->stream));
+  return GRID_OK;
+}
+
+int grid_event_record(grid_ctx *ctx, int slot) {
+  REQUIRE(ctx && slot >= 0 && slot < 8, "bad event slot");
+  HIPCHK(hipEventRecord(ctx->ev[slot], ctx->stream));
+  return GRID_OK;
+}
+
+int grid_event_elapsed(grid_ctx *ctx, int a, int b, float *ms) {
+  REQUIRE(ctx && a >= 0 && a < 8 && b >= 0 && b < 8 && ms, "bad event slot");
+  HIPCHK(hipEventSynchronize(ctx->ev[b]));
+  HIPCHK(hipEventElapsedTime(ms, ctx->ev[a], ctx->ev[b]));
+  return GRID_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------- kernels ----
+struct NotNaN {
+  __device__ bool operator()(const double &x) const { return x == x; }
+};
+
+__global__ void k_gt_flags(const double *v, int64_t n, double thr, uint8_t *f) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) f[i] = (v[i] > thr) ? 1 : 0;   // NaN > thr is false
+}
+
+__global__ void k_round_dec(const double *v, int64_t n, double s, double *out) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double x = v[i];
+  if (!(x == x) || isinf(x)) { out[i] = x; return; }
+  double k = round_dec_k(x, s);
+  double r = k / s;                     // correctly rounded == strtod(text)
+  if (k == 0.0 && signbit(x)) r = -0.0;
+  out[i] = r;
+}
+
+__global__ void k_gather(const double *v, const int32_t *idx, int64_t n, double *out) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = v[idx[i]];
+}
+
+__global__ void k_keep_flags(const double *r, int64_t n, double smin, double smax, int32_t *f) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double x = r[i];
+  f[i] = (x == x && !isinf(x) && x >= smin && x <= smax) ? 1 : 0;
+}
+
+__global__ void k_colmap_fix(const int32_t *flags, int32_t *map, int64_t n) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && !flags[i]) map[i] = -1;
+}
+
+extern "C" {
+
+int grid_sort_valid(grid_ctx *ctx, const double *d_v, int64_t n, double *d_sorted,
+                    int64_t *h_nvalid) {
+  REQUIRE(ctx && h_nvalid && n >= 0, "bad args");
+  if (n == 0) { *h_nvalid = 0; return GRID_OK; }
+  // compact non-NaN into d_sorted (temporary), then radix sort into scratch, copy back
+  size_t b_sel = 0, b_sort = 0;
+  int64_t *d_num = nullptr;
+  HIPCHK(hipcub::DeviceSelect::If(nullptr, b_sel, d_v, d_sorted, d_num, (int)n, NotNaN(), ctx->stream));
+  HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, b_sort, d_sorted, d_sorted, (int)n, 0, 64, ctx->stream));
+  size_t off_keys = ((b_sel > b_sort ? b_sel : b_sort) + 255) & ~size_t(255);
+  size_t off_num = off_keys + (((size_t)n * 8 + 255) & ~size_t(255));
+  void *s = nullptr;
+  int rc = grid_scratch(ctx, off_num + 256, &s);
+  if (rc) return rc;
+  char *base = (char *)s;
+  double *keys = (double *)(base + off_keys);
+  d_num = (int64_t *)(base + off_num);
+  HIPCHK(hipcub::DeviceSelect::If(base, b_sel, d_v, keys, d_num, (int)n, NotNaN(), ctx->stream));
+  HIPCHK(hipMemcpyAsync(ctx->pinned, d_num, 8, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  int64_t nv = *(int64_t *)ctx->pinned;
+  *h_nvalid = nv;
+  if (nv > 0)
+    HIPCHK(hipcub::DeviceRadixSort::SortKeys(base, b_sort, keys, d_sorted, (int)nv, 0, 64, ctx->stream));
+  LAUNCHCHK();
+  return GRID_OK;
+}
+
+int grid_select_gt(grid_ctx *ctx, const double *d_v, int64_t n, double thr, int32_t *d_idx,
+                   int64_t *h_count) {
+  REQUIRE(ctx && h_count && n >= 0, "bad args");
+  if (n == 0) { *h_count = 0; return GRID_OK; }
+  size_t b = 0;
+  hipcub::CountingInputIterator<int32_t> it(0);
+  int64_t *d_num = nullptr;
+  uint8_t *flags = nullptr;
+  HIPCHK(hipcub::DeviceSelect::Flagged(nullptr, b, it, flags, d_idx, d_num, (int)n, ctx->stream));
+  size_t off_f = (b + 255) & ~size_t(255);
+  size_t off_num = off_f + (((size_t)n + 255) & ~size_t(255));
+  void *s = nullptr;
+  int rc = grid_scratch(ctx, off_num + 256, &s);
+  if (rc) return rc;
+  char *base = (char *)s;
+  flags = (uint8_t *)(base + off_f);
+  d_num = (int64_t *)(base + off_num);
+  hipLaunchKernelGGL(k_gt_flags, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, ctx->stream, d_v, n, thr, flags);
+  LAUNCHCHK();
+  HIPCHK(hipcub::DeviceSelect::Flagged(base, b, it, flags, d_idx, d_num, (int)n, ctx->stream));
+  HIPCHK(hipMemcpyAsync(ctx->pinned, d_num, 8, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  *h_count = *(int64_t *)ctx->pinned;
+  return GRID_OK;
+}
+
+int grid_round_decimals(grid_ctx *ctx, const double *d_v, int64_t n, int decimals, double *d_out) {
+  REQUIRE(ctx && decimals >= 0 && decimals <= 6, "bad args");
+  if (n <= 0) return GRID_OK;
+  double s = 1.0;
+  for (int i = 0; i < decimals; i++) s *= 10.0;
+  hipLaunchKernelGGL(k_round_dec, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, ctx->stream, d_v, n, s, d_out);
+  LAUNCHCHK();
+  return GRID_OK;
+}
+
+int grid_gather_f64(grid_ctx *ctx, const double *d_v, const int32_t *d_idx, int64_t n, double *d_out) {
+  REQUIRE(ctx, "ctx is NULL");
+  if (n <= 0) return GRID_OK;
+  hipLaunchKernelGGL(k_gather, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, ctx->stream, d_v, d_idx, n, d_out);
+  LAUNCHCHK();
+  return GRID_OK;
+}
+
+int grid_colmap_range(grid_ctx *ctx, const double *d_r, int64_t n, double smin, double smax,
+                      int32_t *d_colmap, int64_t *h_ruse) {
+  REQUIRE(ctx && h_ruse, "bad args");
+  if (n <= 0) { *h_ruse = 0; return GRID_OK; }
+  size_t b = 0;
+  int32_t *flags = nullptr;
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, b, flags, d_colmap, (int)n, ctx->stream));
+  size_t off_f = (b + 255) & ~size_t(255);
+  void *s = nullptr;
+  int rc = grid_scratch(ctx, off_f + (size_t)n * 4 + 256, &s);
+  if (rc) return rc;
+  char *base = (char *)s;
+  flags = (int32_t *)(base + off_f);
+  hipLaunchKernelGGL(k_keep_flags, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, ctx->stream, d_r, n, smin, smax, flags);
+  LAUNCHCHK();
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(base, b, flags, d_colmap, (int)n, ctx->stream));
+  int32_t last_map = 0, last_flag = 0;
+  HIPCHK(hipMemcpyAsync(ctx->pinned, d_colmap + n - 1, 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipMemcpyAsync((char *)ctx->pinned + 8, flags + n - 1, 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  last_map = *(int32_t *)ctx->pinned;
+  last_flag = *(int32_t *)((char *)ctx->pinned + 8);
+  hipLaunchKernelGGL(k_colmap_fix, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, ctx->stream, flags, d_colmap, n);
+  LAUNCHCHK();
+  *h_ruse = (int64_t)last_map + last_flag;
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return GRID_OK;
+}
+
+// ------------------------------------------------------ host formatting ----
+int grid_format_hundredths(const int32_t *v, int64_t n, char *out, int64_t cap, int64_t *len) {
+  REQUIRE(v || n == 0, "bad args");
+  REQUIRE(out && len, "bad args");
+  int64_t p = 0;
+  char tmp[24];
+  for (int64_t i = 0; i < n; i++) {
+    if (p + 16 > cap) { grid_set_error("format buffer too small"); return GRID_ERANGE; }
+    if (i) out[p++] = '\t';
+    int32_t x = v[i];
+    if (x == GRID_ZQ_NAN) { out[p++] = 'N'; out[p++] = 'A'; continue; }
+    if (x == GRID_ZQ_NEG0) { memcpy(out + p, "-0.00", 5); p += 5; continue; }
+    int64_t a = x;
+    if (a < 0) { out[p++] = '-'; a = -a; }
+    int64_t ip = a / 100, fp = a % 100;
+    int t = 0;
+    do { tmp[t++] = (char)('0' + ip % 10); ip /= 10; } while (ip);
+    while (t) out[p++] = tmp[--t];
+    out[p++] = '.';
+    out[p++] = (char)('0' + fp / 10);
+    out[p++] = (char)('0' + fp % 10);
+  }
+  *len = p;
+  return GRID_OK;
+}
+
+// Level schedule for the in-place Gauss-Seidel sweep (hi_inference.py:204-224).
+// Sample i reads neighbour j's value of THIS sweep if j < i and of the
+// PREVIOUS sweep if j >= i.  Levels: lvl(i) > lvl(j) for neighbours j < i, and
+// lvl(j) >= lvl(i) for neighbours j > i (j must not be overwritten before i
+// reads it).  Within a level all reads precede all writes, so running levels
+// in order reproduces the sequential sweep exactly.
+int grid_hi_levels(int64_t n, const int64_t *off, const int32_t *nbr, int32_t *order,
+                   int32_t *level_off, int32_t *nlevels) {
+  REQUIRE(n >= 0 && off && order && level_off && nlevels, "bad args");
+  std::vector<int32_t> lvl(n, 0), minl(n, 0);
+  int32_t maxl = -1;
+  for (int64_t i = 0; i < n; i++) {
+    int32_t l = minl[i];
+    for (int h = 0; h < 2; h++)
+      for (int64_t t = off[2 * i + h]; t < off[2 * i + h + 1]; t++) {
+        int64_t j = nbr[t] >> 1;
+        if (j < i && lvl[j] + 1 > l) l = lvl[j] + 1;
+      }
+    lvl[i] = l;
+    for (int h = 0; h < 2; h++)
+      for (int64_t t = off[2 * i + h]; t < off[2 * i + h + 1]; t++) {
+        int64_t j = nbr[t] >> 1;
+        if (j > i && minl[j] < l) minl[j] = l;
+      }
+    if (l > maxl) maxl = l;
+  }
+  int32_t L = maxl + 1;
+  std::vector<int32_t> cnt(L + 1, 0);
+  for (int64_t i = 0; i < n; i++) cnt[lvl[i] + 1]++;
+  for (int32_t l = 0; l < L; l++) cnt[l + 1] += cnt[l];
+  for (int32_t l = 0; l <= L; l++) level_off[l] = cnt[l];
+  for (int64_t i = 0; i < n; i++) order[cnt[lvl[i]]++] = (int32_t)i;
+  *nlevels = L;
+  return GRID_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,195 @@
+// Steps 6 and 7 kernels.
+//   step 6: grid/utils/compute_dipcn.py:62-88 (neighbour-normalised read ratio)
+//   step 7: grid/utils/hi_inference.py:175-250 (_run_phasing + _compute_imp)
+#include "common.hpp"
+
+namespace {
+
+__global__ void k_dipcn(int64_t n, const double *__restrict__ reads, const uint8_t *__restrict__ has,
+                        const double *__restrict__ scale, const int32_t *__restrict__ nbr,
+                        const double *__restrict__ nscale, const int32_t *__restrict__ ncnt, int64_t ld,
+                        int64_t n_nbr, double *__restrict__ out, uint8_t *__restrict__ valid,
+                        int32_t *__restrict__ zerodiv) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  valid[i] = 0;
+  if (!has[i]) return;
+  double total = 0.0;
+  int64_t count = 0;
+  const int64_t c = ncnt[i];
+  for (int64_t t = 0; t < c; t++) {
+    if (count >= n_nbr) break;
+    int32_t j = nbr[i * ld + t];
+    if (j < 0 || !has[j]) continue;
+    double ns = nscale[i * ld + t];
+    if (ns == 0.0) { atomicOr(zerodiv, 1); return; }   // Python: ZeroDivisionError
+    total = total + reads[j] / ns;
+    count++;
+  }
+  if (count == 0) return;
+  double s = scale[i];
+  double mean = total / (double)count;
+  if (s == 0.0 || mean == 0.0) { atomicOr(zerodiv, 1); return; }
+  out[i] = (reads[i] / s) / mean;
+  valid[i] = 1;
+}
+
+__device__ __forceinline__ void nbr_means(int64_t i, const double *hap, const int64_t *off,
+                                          const int32_t *nbr, const double *w, double ws[2],
+                                          double wv[2]) {
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    double s = 1e-9, v = 0.0;
+    const int64_t e = off[2 * i + h + 1];
+    for (int64_t t = off[2 * i + h]; t < e; t++) {
+      double x = hap[nbr[t]];
+      if (x == x) {
+        double wt = w[t];
+        s = s + wt;
+        v = v + wt * x;
+      }
+    }
+    ws[h] = s;
+    wv[h] = v;
+  }
+}
+
+constexpr int PT = 1024;
+
+// One workgroup runs the whole phasing of one locus.  hap lives in LDS when
+// it fits (2n doubles), else in the global output buffer (same workgroup, so
+// __syncthreads orders it).  Iterations run the precomputed level schedule:
+// within a level every sample reads first, then all write.
+template <bool USE_LDS>
+__global__ __launch_bounds__(PT) void k_phase(int64_t n, const double *__restrict__ irr,
+                                              const int64_t *__restrict__ off,
+                                              const int32_t *__restrict__ nbr,
+                                              const double *__restrict__ w, int64_t min_nbr,
+                                              int64_t iters, const int32_t *__restrict__ order,
+                                              const int32_t *__restrict__ loff, int nlev,
+                                              double *hap_g, double *__restrict__ imp,
+                                              double *__restrict__ mean_out) {
+  extern __shared__ __attribute__((aligned(16))) double s_hap[];
+  __shared__ double s_mean;
+  double *hap = USE_LDS ? s_hap : hap_g;
+  const int tid = threadIdx.x;
+  const double qnan = __builtin_nan("");
+  for (int64_t i = tid; i < n; i += PT) {
+    bool ok = (off[2 * i + 1] - off[2 * i] >= min_nbr) && (off[2 * i + 2] - off[2 * i + 1] >= min_nbr);
+    double v = ok ? irr[i] / 2 : qnan;
+    hap[2 * i] = v;
+    hap[2 * i + 1] = v;
+  }
+  if (tid == 0) {
+    double m = 0.0;
+    int64_t c = 0;
+    for (int64_t i = 0; i < n; i++) {
+      bool ok = (off[2 * i + 1] - off[2 * i] >= min_nbr) && (off[2 * i + 2] - off[2 * i + 1] >= min_nbr);
+      if (ok) { m = m + irr[i]; c++; }
+    }
+    if (c > 0) m = m / (double)c;
+    s_mean = m;
+  }
+  __syncthreads();
+  for (int64_t it = 0; it < iters; it++) {
+    for (int l = 0; l < nlev; l++) {
+      const int e0 = loff[l], e1 = loff[l + 1];
+      for (int base = e0; base < e1; base += PT) {
+        const int e = base + tid;
+        bool upd = false;
+        int64_t i = 0;
+        double n0 = 0.0, n1 = 0.0;
+        if (e < e1) {
+          i = order[e];
+          if (hap[2 * i] == hap[2 * i]) {
+            double ws[2], wv[2];
+            nbr_means(i, hap, off, nbr, w, ws, wv);
+            double m0 = wv[0] / ws[0];
+            double m1 = wv[1] / ws[1];
+            double den = m0 + m1;
+            if (den > 0.0) {
+              n0 = irr[i] * m0 / den;
+              n1 = irr[i] * m1 / den;
+              upd = true;
+            }
+          }
+        }
+        __syncthreads();
+        if (upd) {
+          hap[2 * i] = n0;
+          hap[2 * i + 1] = n1;
+        }
+        __syncthreads();
+      }
+    }
+  }
+  const double mean = s_mean;
+  for (int64_t i = tid; i < n; i += PT) {
+    double ws[2], wv[2];
+    nbr_means(i, hap, off, nbr, w, ws, wv);
+    double i0 = wv[0] / ws[0];
+    double i1 = wv[1] / ws[1];
+    if (ws[0] <= 1e-9) i0 = mean / 2;
+    if (ws[1] <= 1e-9) i1 = mean / 2;
+    imp[2 * i] = i0;
+    imp[2 * i + 1] = i1;
+  }
+  if (USE_LDS) {
+    __syncthreads();
+    for (int64_t e = tid; e < 2 * n; e += PT) hap_g[e] = hap[e];
+  }
+  if (tid == 0) *mean_out = mean;
+}
+
+}  // namespace
+
+extern "C" {
+
+int grid_dipcn(grid_ctx *ctx, int64_t n, const double *d_reads, const uint8_t *d_has, const double *d_scale,
+               const int32_t *d_nbr, const double *d_nscale, const int32_t *d_ncnt, int64_t ld, int64_t n_nbr,
+               double *d_out, uint8_t *d_valid, int32_t *h_zerodiv) {
+  REQUIRE(ctx && n >= 0 && ld >= 0, "bad args");
+  if (n == 0) {
+    if (h_zerodiv) *h_zerodiv = 0;
+    return GRID_OK;
+  }
+  void *s = nullptr;
+  int rc = grid_scratch(ctx, 256, &s);
+  if (rc) return rc;
+  int32_t *d_zd = (int32_t *)s;
+  HIPCHK(hipMemsetAsync(d_zd, 0, 4, ctx->stream));
+  hipLaunchKernelGGL(k_dipcn, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, ctx->stream, n, d_reads, d_has,
+                     d_scale, d_nbr, d_nscale, d_ncnt, ld, n_nbr, d_out, d_valid, d_zd);
+  LAUNCHCHK();
+  if (h_zerodiv) {
+    HIPCHK(hipMemcpyAsync(ctx->pinned, d_zd, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    *h_zerodiv = *(int32_t *)ctx->pinned;
+  }
+  return GRID_OK;
+}
+
+int grid_hi_phase(grid_ctx *ctx, int64_t n, const double *d_irr, const int64_t *d_off, const int32_t *d_nbr,
+                  const double *d_w, int64_t min_nbr, int64_t n_iters, const int32_t *d_order,
+                  const int32_t *d_loff, int32_t nlevels, double *d_hap, double *d_imp, double *d_mean) {
+  REQUIRE(ctx && n >= 0 && n_iters >= 0 && nlevels >= 0, "bad args");
+  if (n == 0) return GRID_OK;
+  const size_t lds = (size_t)2 * n * sizeof(double);
+  if (lds <= 120 * 1024) {
+    static bool attr = false;
+    if (!attr) {
+      HIPCHK(hipFuncSetAttribute((const void *)k_phase<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 120 * 1024));
+      attr = true;
+    }
+    hipLaunchKernelGGL(k_phase<true>, dim3(1), dim3(PT), lds, ctx->stream, n, d_irr, d_off, d_nbr, d_w, min_nbr,
+                       n_iters, d_order, d_loff, nlevels, d_hap, d_imp, d_mean);
+  } else {
+    hipLaunchKernelGGL(k_phase<false>, dim3(1), dim3(PT), 0, ctx->stream, n, d_irr, d_off, d_nbr, d_w, min_nbr,
+                       n_iters, d_order, d_loff, nlevels, d_hap, d_imp, d_mean);
+  }
+  LAUNCHCHK();
+  return GRID_OK;
+}
+
+}  // extern "C"

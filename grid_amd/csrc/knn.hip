@@ -1,0 +1,311 @@
+// Step 5 kernels: exact all-pairs k-NN on clipped z-score hundredths.
+//
+// Replaces sklearn NearestNeighbors(brute, euclidean) as called by
+// grid/utils/find_neighbors.py:207-213.  Clipped z values are integers
+// |q| <= qmax <= 256 (hundredths), exactly representable in bf16, so the Gram
+// matrix G = Z Z^T is computed EXACTLY on the bf16 MFMA pipe:
+//   * fp32 MFMA accumulators hold partial sums of at most FS*64 products, kept
+//     below 2^24 so every fp32 partial is an exact integer;
+//   * every FS K-steps they are flushed into int32 accumulators (exact while a
+//     K-slice stays below 2^31 / qmax^2 products);
+//   * each workgroup owns one 128x128 tile of one K-slice and adds its int32
+//     tile into the int64 Gram with integer atomics (order-free, exact).
+// d2(i,j) = G_ii + G_jj - 2 G_ij is then exact, and neighbours are ordered by
+// (d2, j).  That equals sklearn's order wherever exact distances differ.
+#include "common.hpp"
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+constexpr int BM = 128;
+constexpr int BK = 64;              // bf16 elements per K-step (128 B per row)
+constexpr int NT = 256;             // threads per workgroup (4 waves, 2x2)
+constexpr int TILE_BYTES = BM * BK * 2;   // 16 KiB
+
+// LDS image: [row][8 chunks of 16 B], chunk XOR-swizzled by (row>>1)&7 so the
+// ds_read_b128 lane groups of the 32x32x16 fragment reads are conflict-free.
+__device__ __forceinline__ int lds_off(int row, int chunk) {
+  return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
+}
+
+__device__ __forceinline__ bf16x8 as_bf16x8(uint4 v) {
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__global__ __launch_bounds__(NT, 2) void k_gram(const uint16_t *__restrict__ z, int64_t ld, int nt,
+                                                int ntiles, int64_t nsteps, int sps, int fs,
+                                                int64_t np_, unsigned long long *__restrict__ gram) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_BYTES];
+  // XCD-aware bijective remap: workgroups that share an XCD get a contiguous
+  // range of (slice, tile) work items (same K-slice, neighbouring tiles).
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, loc = bid >> 3;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const int slice = wid / ntiles;
+  int t = wid - slice * ntiles;
+  int ti = 0;
+  while (t >= nt - ti) { t -= nt - ti; ti++; }
+  const int tj = ti + t;
+
+  const int64_t s0 = (int64_t)slice * sps;
+  int64_t s1 = s0 + sps;
+  if (s1 > nsteps) s1 = nsteps;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+
+  const uint16_t *za = z + (int64_t)ti * BM * ld;
+  const uint16_t *zb = z + (int64_t)tj * BM * ld;
+
+  f32x16 acc[2][2];
+  int32_t iacc[2][2][16];
+#pragma unroll
+  for (int a = 0; a < 2; a++)
+#pragma unroll
+    for (int b = 0; b < 2; b++) {
+#pragma unroll
+      for (int r = 0; r < 16; r++) { acc[a][b][r] = 0.0f; iacc[a][b][r] = 0; }
+    }
+
+  uint4 ra0, ra1, ra2, ra3, rb0, rb1, rb2, rb3;
+  // global -> registers for K-step `step` (16 B per thread per operand, x4)
+#define GRAM_GLOAD(step)                                                              \
+  do {                                                                                \
+    const int64_t kofs_ = (step) * BK;                                                \
+    ra0 = *reinterpret_cast<const uint4 *>(za + (int64_t)((tid + 0 * NT) >> 3) * ld + kofs_ + ((tid + 0 * NT) & 7) * 8); \
+    ra1 = *reinterpret_cast<const uint4 *>(za + (int64_t)((tid + 1 * NT) >> 3) * ld + kofs_ + ((tid + 1 * NT) & 7) * 8); \
+    ra2 = *reinterpret_cast<const uint4 *>(za + (int64_t)((tid + 2 * NT) >> 3) * ld + kofs_ + ((tid + 2 * NT) & 7) * 8); \
+    ra3 = *reinterpret_cast<const uint4 *>(za + (int64_t)((tid + 3 * NT) >> 3) * ld + kofs_ + ((tid + 3 * NT) & 7) * 8); \
+    rb0 = *reinterpret_cast<const uint4 *>(zb + (int64_t)((tid + 0 * NT) >> 3) * ld + kofs_ + ((tid + 0 * NT) & 7) * 8); \
+    rb1 = *reinterpret_cast<const uint4 *>(zb + (int64_t)((tid + 1 * NT) >> 3) * ld + kofs_ + ((tid + 1 * NT) & 7) * 8); \
+    rb2 = *reinterpret_cast<const uint4 *>(zb + (int64_t)((tid + 2 * NT) >> 3) * ld + kofs_ + ((tid + 2 * NT) & 7) * 8); \
+    rb3 = *reinterpret_cast<const uint4 *>(zb + (int64_t)((tid + 3 * NT) >> 3) * ld + kofs_ + ((tid + 3 * NT) & 7) * 8); \
+  } while (0)
+  // registers -> swizzled LDS image of buffer `b`
+#define GRAM_LSTORE(b)                                                                \
+  do {                                                                                \
+    char *A_ = smem + (b) * 2 * TILE_BYTES;                                           \
+    char *B_ = A_ + TILE_BYTES;                                                       \
+    *reinterpret_cast<uint4 *>(A_ + lds_off((tid + 0 * NT) >> 3, (tid + 0 * NT) & 7)) = ra0; \
+    *reinterpret_cast<uint4 *>(A_ + lds_off((tid + 1 * NT) >> 3, (tid + 1 * NT) & 7)) = ra1; \
+    *reinterpret_cast<uint4 *>(A_ + lds_off((tid + 2 * NT) >> 3, (tid + 2 * NT) & 7)) = ra2; \
+    *reinterpret_cast<uint4 *>(A_ + lds_off((tid + 3 * NT) >> 3, (tid + 3 * NT) & 7)) = ra3; \
+    *reinterpret_cast<uint4 *>(B_ + lds_off((tid + 0 * NT) >> 3, (tid + 0 * NT) & 7)) = rb0; \
+    *reinterpret_cast<uint4 *>(B_ + lds_off((tid + 1 * NT) >> 3, (tid + 1 * NT) & 7)) = rb1; \
+    *reinterpret_cast<uint4 *>(B_ + lds_off((tid + 2 * NT) >> 3, (tid + 2 * NT) & 7)) = rb2; \
+    *reinterpret_cast<uint4 *>(B_ + lds_off((tid + 3 * NT) >> 3, (tid + 3 * NT) & 7)) = rb3; \
+  } while (0)
+
+  if (s0 < s1) {
+    GRAM_GLOAD(s0);
+    GRAM_LSTORE(0);
+  }
+  __syncthreads();
+  int since = 0;
+  int buf = 0;
+  for (int64_t st = s0; st < s1; st++) {
+    const bool more = st + 1 < s1;
+    if (more) GRAM_GLOAD(st + 1);
+    const char *A = smem + buf * 2 * TILE_BYTES;
+    const char *B = A + TILE_BYTES;
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+      const int ch = 2 * s + (lane >> 5);
+      bf16x8 fa[2], fb[2];
+#pragma unroll
+      for (int m = 0; m < 2; m++) {
+        int rowa = wr * 64 + m * 32 + (lane & 31);
+        int rowb = wc * 64 + m * 32 + (lane & 31);
+        fa[m] = as_bf16x8(*reinterpret_cast<const uint4 *>(A + lds_off(rowa, ch)));
+        fb[m] = as_bf16x8(*reinterpret_cast<const uint4 *>(B + lds_off(rowb, ch)));
+      }
+#pragma unroll
+      for (int m = 0; m < 2; m++)
+#pragma unroll
+        for (int nn = 0; nn < 2; nn++)
+          acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[m], fb[nn], acc[m][nn], 0, 0, 0);
+    }
+    if (++since == fs || st + 1 == s1) {
+      since = 0;
+#pragma unroll
+      for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++)
+#pragma unroll
+          for (int r = 0; r < 16; r++) {
+            iacc[a][b][r] += (int32_t)acc[a][b][r];
+            acc[a][b][r] = 0.0f;
+          }
+    }
+    if (more) GRAM_LSTORE(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  // int64 atomics into the Gram tile (exact, order-free)
+#pragma unroll
+  for (int a = 0; a < 2; a++)
+#pragma unroll
+    for (int b = 0; b < 2; b++)
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        int row = ti * BM + wr * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        int col = tj * BM + wc * 64 + b * 32 + (lane & 31);
+        int32_t v = iacc[a][b][r];
+        if (v != 0)
+          atomicAdd(gram + (int64_t)row * np_ + col, (unsigned long long)(long long)v);
+      }
+}
+
+constexpr int SELCAP = 4096;
+
+__device__ __forceinline__ int64_t gram_at(const int64_t *g, int64_t np_, int64_t i, int64_t j) {
+  return ((i >> 7) <= (j >> 7)) ? g[i * np_ + j] : g[j * np_ + i];
+}
+
+__global__ __launch_bounds__(256) void k_topk(const int64_t *__restrict__ g, int64_t n, int64_t np_,
+                                              int64_t k, int64_t row0, int32_t *__restrict__ idx,
+                                              int64_t *__restrict__ d2o, int32_t *__restrict__ cnto) {
+  __shared__ unsigned hist[256];
+  __shared__ unsigned long long s_prefix;
+  __shared__ long long s_rank;
+  __shared__ unsigned long long sel[SELCAP];
+  __shared__ int s_nsel, s_self;
+  const int64_t i = row0 + blockIdx.x;
+  const int tid = threadIdx.x;
+  const int64_t ktake = (k + 1 < n) ? k + 1 : n;
+  const int64_t gii = g[i * np_ + i];
+  auto key = [&](int64_t j) -> unsigned long long {
+    int64_t d2 = gii + g[j * np_ + j] - 2 * gram_at(g, np_, i, j);
+    return ((unsigned long long)d2 << 20) | (unsigned long long)j;
+  };
+  unsigned long long prefix = 0, mask = 0;
+  long long rank = ktake - 1;
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    hist[tid] = 0;
+    __syncthreads();
+    for (int64_t j = tid; j < n; j += 256) {
+      unsigned long long kk = key(j);
+      if ((kk & mask) == prefix) atomicAdd(&hist[(kk >> shift) & 255], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      long long cum = 0;
+      for (int d = 0; d < 256; d++) {
+        if (cum + hist[d] > rank) {
+          s_prefix = prefix | ((unsigned long long)d << shift);
+          s_rank = rank - cum;
+          break;
+        }
+        cum += hist[d];
+      }
+    }
+    __syncthreads();
+    prefix = s_prefix;
+    rank = s_rank;
+    mask |= 0xFFull << shift;
+    __syncthreads();
+  }
+  const unsigned long long T = prefix;   // the ktake-th smallest key (keys unique)
+  if (tid == 0) { s_nsel = 0; s_self = -1; }
+  for (int e = tid; e < SELCAP; e += 256) sel[e] = ~0ull;
+  __syncthreads();
+  for (int64_t j = tid; j < n; j += 256) {
+    unsigned long long kk = key(j);
+    if (kk <= T) {
+      int p = atomicAdd(&s_nsel, 1);
+      if (p < SELCAP) sel[p] = kk;
+    }
+  }
+  __syncthreads();
+  int cap = 1;
+  while (cap < ktake) cap <<= 1;
+  // bitonic sort of sel[0..cap)
+  for (int size = 2; size <= cap; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int e = tid; e < cap; e += 256) {
+        int p = e ^ stride;
+        if (p > e) {
+          bool up = (e & size) == 0;
+          unsigned long long a = sel[e], b = sel[p];
+          if ((a > b) == up) { sel[e] = b; sel[p] = a; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int e = tid; e < ktake; e += 256)
+    if ((int64_t)(sel[e] & 0xFFFFFull) == i) s_self = e;
+  __syncthreads();
+  const int selfpos = s_self;
+  const int64_t orow = i - row0;
+  for (int e = tid; e < ktake; e += 256) {
+    int64_t j = (int64_t)(sel[e] & 0xFFFFFull);
+    if (e == selfpos) continue;
+    int64_t pos = e - ((selfpos >= 0 && e > selfpos) ? 1 : 0);
+    if (pos < k) {
+      idx[orow * k + pos] = (int32_t)j;
+      d2o[orow * k + pos] = (int64_t)(sel[e] >> 20);
+    }
+  }
+  if (tid == 0) {
+    int64_t c = ktake - (selfpos >= 0 ? 1 : 0);
+    cnto[orow] = (int32_t)(c < k ? c : k);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int grid_knn_gram(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t kpad, int64_t ld,
+                  int32_t qmax, int64_t *d_gram) {
+  REQUIRE(ctx && d_zb && d_gram, "bad args");
+  REQUIRE(np_ > 0 && np_ % BM == 0, "np (%lld) must be a positive multiple of %d", (long long)np_, BM);
+  REQUIRE(kpad >= 0 && kpad % BK == 0 && ld >= kpad && ld % 8 == 0, "kpad must be a multiple of %d", BK);
+  REQUIRE(((uintptr_t)d_zb % 16) == 0, "zb must be 16-byte aligned");
+  REQUIRE(qmax >= 0 && qmax <= 256, "qmax must be in [0, 256]");
+  if (kpad == 0) return GRID_OK;
+  const int64_t nsteps = kpad / BK;
+  const int64_t q2 = (int64_t)(qmax > 0 ? qmax : 1) * (qmax > 0 ? qmax : 1);
+  // fp32-exact flush interval and int32-exact slice length, in K-steps
+  int fs = (int)((1ll << 24) / (q2 * BK));
+  if (fs < 1) fs = 1;
+  int64_t sps_max = ((1ll << 31) - 1) / (q2 * BK);
+  const int nt = (int)(np_ / BM);
+  const int ntiles = nt * (nt + 1) / 2;
+  // aim for >= 8 work items per CU (256 CUs) without exceeding the int32 bound
+  int64_t target_slices = ceil_div(2048, ntiles);
+  int64_t sps = ceil_div(nsteps, target_slices);
+  if (sps > sps_max) sps = sps_max;
+  if (sps < 1) sps = 1;
+  const int64_t nslices = ceil_div(nsteps, sps);
+  const int64_t nwg = nslices * ntiles;
+  REQUIRE(nwg < (1ll << 31), "too many work items");
+  hipLaunchKernelGGL(k_gram, dim3((unsigned)nwg), dim3(NT), 0, ctx->stream, d_zb, ld, nt, ntiles, nsteps,
+                     (int)sps, fs, np_, (unsigned long long *)d_gram);
+  LAUNCHCHK();
+  return GRID_OK;
+}
+
+int grid_knn_topk(grid_ctx *ctx, const int64_t *d_gram, int64_t n, int64_t np_, int64_t k, int64_t row0,
+                  int64_t nrows, int32_t *d_idx, int64_t *d_d2, int32_t *d_cnt) {
+  REQUIRE(ctx && d_gram && n > 0 && np_ >= n && k >= 0, "bad args");
+  REQUIRE(n <= (1 << 20), "n > 2^20 samples not supported by the packed key");
+  REQUIRE(k + 1 <= SELCAP, "num_neighbors + 1 must be <= %d", SELCAP);
+  REQUIRE(row0 >= 0 && nrows >= 0 && row0 + nrows <= n, "bad row block");
+  if (nrows == 0 || k == 0) {
+    if (nrows) HIPCHK(hipMemsetAsync(d_cnt, 0, nrows * 4, ctx->stream));
+    return GRID_OK;
+  }
+  hipLaunchKernelGGL(k_topk, dim3((unsigned)nrows), dim3(256), 0, ctx->stream, d_gram, n, np_, k, row0, d_idx,
+                     d_d2, d_cnt);
+  LAUNCHCHK();
+  return GRID_OK;
+}
+
+}  // extern "C"

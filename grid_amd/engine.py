@@ -1,0 +1,201 @@
+"""Array-level driver of the MI355X hot path (steps 4-7).
+
+Each function stages inputs in HBM, launches the HIP kernels of
+libgridhip.so through ``grid_amd._abi`` and returns results.  The scalar
+decision logic the reference performs in Python between its NumPy calls
+(median -> scale, ``sorted(...)[int(top_frac*n)]`` threshold, sigma2 bounds)
+stays here, on a handful of values read back from the device.
+
+Reference correspondence (paths under /root/reference):
+  normalize_stats / select   grid/utils/normalize_mosdepth.py:120, 419-499
+  knn_*                      grid/utils/find_neighbors.py:57-65, 128-227
+  dipcn                      grid/utils/compute_dipcn.py:62-88
+  phase                      grid/utils/hi_inference.py:175-250
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _abi
+from ._abi import BLOCK, Device, DevBuf, GridNativeError, call, ptr
+
+F8, I4, I8, U2, U1 = np.float64, np.int32, np.int64, np.uint16, np.uint8
+
+
+def _read(buf: DevBuf, index: int):
+    out = np.empty(1, dtype=buf.dtype)
+    call("grid_d2h", buf.dev.ctx, out.ctypes.data, buf.ptr + index * buf.dtype.itemsize, buf.dtype.itemsize)
+    return out[0]
+
+
+def py_index(n: int, idx: int) -> int:
+    """Python list indexing semantics (negative wraps, else IndexError)."""
+    if idx < 0:
+        idx += n
+    if idx < 0 or idx >= n:
+        raise IndexError("list index out of range")
+    return idx
+
+
+# ------------------------------------------------------------------ step 4 --
+@dataclass
+class NormStats:
+    n: int
+    m: int
+    rowmean: DevBuf       # [n] f64 (== individual_raw_means)
+    mu: DevBuf            # [m] f64
+    var: DevBuf           # [m] f64
+    ratio: DevBuf         # [m] f64 (NaN where mu <= 0)
+    nvalid: int
+    scale: float
+    sorted_ratio: DevBuf  # [m] f64, first nvalid ascending
+
+
+def row_means(dev: Device, q: DevBuf, n: int, m: int, ld: int) -> DevBuf:
+    nblk = -(-m // BLOCK)
+    bsum = dev.alloc((max(n, 1), max(nblk, 1)), F8)
+    bcnt = dev.alloc((max(n, 1), max(nblk, 1)), I4)
+    call("grid_norm_row_blocks", dev.ctx, ptr(q), n, m, ld, bsum.ptr, bcnt.ptr)
+    rm = dev.alloc(max(n, 1), F8)
+    call("grid_norm_row_means", dev.ctx, bsum.ptr, bcnt.ptr, n, nblk, rm.ptr)
+    return rm
+
+
+def median_scale(sorted_ratio: DevBuf, nvalid: int) -> float:
+    """normalize_mosdepth.py:460-468 from the device-sorted valid ratios."""
+    if nvalid == 0:
+        return 1.0
+    if nvalid % 2:
+        med = float(_read(sorted_ratio, nvalid // 2))
+    else:
+        med = (float(_read(sorted_ratio, nvalid // 2 - 1)) + float(_read(sorted_ratio, nvalid // 2))) / 2.0
+    if med > 0:
+        return 1.0 / math.sqrt(med / 100.0)
+    return 1.0
+
+
+def normalize_stats(dev: Device, q: DevBuf, n: int, m: int, ld: int) -> NormStats:
+    rm = row_means(dev, q, n, m, ld)
+    mu, var, ratio = dev.alloc(max(m, 1), F8), dev.alloc(max(m, 1), F8), dev.alloc(max(m, 1), F8)
+    call("grid_norm_col_means", dev.ctx, ptr(q), n, m, ld, rm.ptr, mu.ptr)
+    call("grid_norm_col_vars", dev.ctx, ptr(q), n, m, ld, rm.ptr, mu.ptr, var.ptr, ratio.ptr)
+    srt = dev.alloc(max(m, 1), F8)
+    nv = C.c_int64()
+    call("grid_sort_valid", dev.ctx, ratio.ptr, m, srt.ptr, C.byref(nv))
+    scale = median_scale(srt, nv.value)
+    return NormStats(n, m, rm, mu, var, ratio, nv.value, scale, srt)
+
+
+def select_regions(dev: Device, st: NormStats, top_frac: float):
+    """select_high_variance_regions (normalize_mosdepth.py:492-499)."""
+    if st.nvalid == 0:
+        return dev.alloc(1, I4), 0
+    k = py_index(st.nvalid, int(top_frac * st.nvalid))
+    thr = float(_read(st.sorted_ratio, k))
+    sel = dev.alloc(max(st.m, 1), I4)
+    cnt = C.c_int64()
+    call("grid_select_gt", dev.ctx, st.ratio.ptr, st.m, thr, sel.ptr, C.byref(cnt))
+    return sel, cnt.value
+
+
+def zquant(dev: Device, q, n, ld, sel: DevBuf, r: int, st: NormStats, zq: DevBuf | None = None,
+           colmap: DevBuf | None = None, qmax: int = 0, zb: DevBuf | None = None, ld_zb: int = 0):
+    of = C.c_int32()
+    call("grid_norm_zquant", dev.ctx, ptr(q), n, ld, sel.ptr, r, st.rowmean.ptr, st.mu.ptr, st.scale,
+         ptr(zq), r, ptr(colmap), qmax, ptr(zb), ld_zb, C.byref(of))
+    if of.value:
+        raise GridNativeError("normalised z-score exceeds the int32 hundredths range")
+
+
+# ------------------------------------------------------------------ step 5 --
+def qmax_for_zmax(zmax: float) -> int:
+    """Clip bound in hundredths for the exact integer path, or raise."""
+    q = int(round(zmax * 100))
+    if q / 100.0 != zmax or not (0 <= q <= 256):
+        raise GridNativeError(f"zmax={zmax!r}: the exact bf16 k-NN path needs zmax = k/100 with 0 <= k <= 256")
+    return q
+
+
+def pad_to(x: int, a: int) -> int:
+    return -(-x // a) * a
+
+
+def sigma2_min(dev: Device, r3: DevBuf, r: int, frac_r: float):
+    """find_neighbors.py:148-161 on device-resident ratios; None if no finite."""
+    srt = dev.alloc(max(r, 1), F8)
+    nv = C.c_int64()
+    call("grid_sort_valid", dev.ctx, r3.ptr, r, srt.ptr, C.byref(nv))
+    if nv.value == 0:
+        return None
+    lo = min(int(r * (1.0 - frac_r)), nv.value - 1)
+    return float(_read(srt, lo))
+
+
+def knn(dev: Device, zb: DevBuf, n: int, np_: int, kpad: int, ld: int, qmax: int, k: int,
+        r_use: int):
+    """Exact k-NN on the bf16 hundredths panel: returns (idx, d2, cnt) numpy."""
+    if 4 * qmax * qmax * max(r_use, 1) >= 2 ** 44:
+        raise GridNativeError("R_use too large for the packed distance key")
+    gram = dev.zeros((np_, np_), I8)
+    call("grid_knn_gram", dev.ctx, zb.ptr, np_, kpad, ld, qmax, gram.ptr)
+    kk = max(k, 1)
+    idx, d2, cnt = dev.alloc((n, kk), I4), dev.alloc((n, kk), I8), dev.alloc(n, I4)
+    call("grid_knn_topk", dev.ctx, gram.ptr, n, np_, k, 0, n, idx.ptr, d2.ptr, cnt.ptr)
+    return idx.numpy(), d2.numpy(), cnt.numpy()
+
+
+def knn_from_hundredths(dev: Device, zq: np.ndarray, k: int, qmax: int):
+    """Host (n x R_use) int hundredths, already clipped, NaN -> 0."""
+    n, r = zq.shape
+    np_ = pad_to(max(n, 1), 128)
+    kpad = pad_to(max(r, 1), 64)
+    zf = np.zeros((np_, kpad), dtype=np.float32)
+    zf[:n, :r] = zq
+    zbits = (zf.view(np.uint32) >> 16).astype(np.uint16)     # exact for |v| <= 256
+    zb = dev.upload(zbits)
+    return knn(dev, zb, n, np_, kpad, kpad, qmax, k, r)
+
+
+# ------------------------------------------------------------------ step 6 --
+def dipcn(dev: Device, reads: np.ndarray, has: np.ndarray, scale: np.ndarray, nbr: np.ndarray,
+          nscale: np.ndarray, ncnt: np.ndarray, n_nbr: int):
+    n = len(reads)
+    ld = nbr.shape[1] if nbr.ndim == 2 else 0
+    d = [dev.upload(np.ascontiguousarray(a)) for a in
+         (reads.astype(F8), has.astype(U1), scale.astype(F8), nbr.astype(I4), nscale.astype(F8), ncnt.astype(I4))]
+    out, valid = dev.alloc(max(n, 1), F8), dev.alloc(max(n, 1), U1)
+    zd = C.c_int32()
+    call("grid_dipcn", dev.ctx, n, d[0].ptr, d[1].ptr, d[2].ptr, d[3].ptr, d[4].ptr, d[5].ptr, ld, n_nbr,
+         out.ptr, valid.ptr, C.byref(zd))
+    if zd.value:
+        raise ZeroDivisionError("float division by zero")
+    return out.numpy()[:n], valid.numpy()[:n].astype(bool)
+
+
+# ------------------------------------------------------------------ step 7 --
+def csr_from_lists(hap_nbrs):
+    off = np.zeros(len(hap_nbrs) + 1, dtype=I8)
+    for h, lst in enumerate(hap_nbrs):
+        off[h + 1] = off[h] + len(lst)
+    nbr = np.fromiter((a for lst in hap_nbrs for a, _ in lst), dtype=I4, count=int(off[-1]))
+    w = np.fromiter((b for lst in hap_nbrs for _, b in lst), dtype=F8, count=int(off[-1]))
+    return off, nbr, w
+
+
+def phase(dev: Device, irr: np.ndarray, off: np.ndarray, nbr: np.ndarray, w: np.ndarray, min_nbr: int,
+          n_iters: int):
+    n = len(irr)
+    if n == 0:
+        return np.zeros(0), np.zeros(0), 0.0
+    order, loff, nl = _abi.hi_levels(off, nbr)
+    bufs = [dev.upload(np.ascontiguousarray(a)) for a in
+            (np.asarray(irr, F8), off.astype(I8), (nbr if nbr.size else np.zeros(1, I4)).astype(I4),
+             (w if w.size else np.zeros(1, F8)).astype(F8), order.astype(I4), loff.astype(I4))]
+    hap, imp, mean = dev.alloc(2 * n, F8), dev.alloc(2 * n, F8), dev.alloc(1, F8)
+    call("grid_hi_phase", dev.ctx, n, bufs[0].ptr, bufs[1].ptr, bufs[2].ptr, bufs[3].ptr, min_nbr, n_iters,
+         bufs[4].ptr, bufs[5].ptr, nl, hap.ptr, imp.ptr, mean.ptr)
+    return hap.numpy(), imp.numpy(), float(mean.numpy()[0])

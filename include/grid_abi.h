@@ -1,0 +1,176 @@
+/*
+ * grid_abi.h -- C ABI of libgridhip.so, the MI355X (gfx950) implementation of
+ * GRiD pipeline steps 4-7 (depth normalisation -> nearest neighbours ->
+ * diploid CN -> haploid inference).
+ *
+ * The reference (caterer-z-t/GRiD) is pure Python; its "FFI" for this path is
+ * the set of step functions the orchestrator calls
+ * (grid/pipeline.py:66-103).  Our Python step modules (grid_amd/utils/ step modules)
+ * keep those signatures and bind THIS header through ctypes
+ * (grid_amd/_abi.py).  Each entry point below cites the reference code it
+ * replaces.  Plain C: pointers + sizes, no torch types.
+ *
+ * Conventions
+ *  - Every function returns int: GRID_OK (0) or an error code; the message is
+ *    in grid_last_error() (thread-local).  No C++ exception crosses the ABI.
+ *  - "d_" pointers are DEVICE pointers (from grid_dev_alloc, or any HIP
+ *    allocation of the same runtime, e.g. a torch tensor's data_ptr()).
+ *    "h_" pointers are host pointers.  Caller owns every buffer.
+ *  - Work is enqueued on the context's stream; results are ready after
+ *    grid_sync(ctx) (or a later blocking grid_d2h).
+ *  - Depth matrices hold mosdepth depths as int32 HUNDREDTHS (the reference
+ *    parses "%.2f" text with float(); q/100.0 in IEEE fp64 is that same
+ *    double).  GRID_MISSING marks a NaN cell.
+ *  - All fp64 statistics reproduce the reference's NumPy operation order
+ *    bit for bit (kernels are built with -ffp-contract=off).
+ */
+#ifndef GRID_ABI_H
+#define GRID_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GRID_OK 0
+#define GRID_EINVAL 1
+#define GRID_EHIP 2
+#define GRID_EZERODIV 3
+#define GRID_EUNSUPPORTED 4
+#define GRID_ERANGE 5
+
+#define GRID_MISSING ((int32_t)0x80000000)   /* NaN depth cell            */
+#define GRID_ZQ_NAN ((int32_t)0x80000000)    /* z printed as "NA"         */
+#define GRID_ZQ_NEG0 ((int32_t)0x80000001)   /* z printed as "-0.00"      */
+#define GRID_BLOCK 8192                      /* NumPy reduction buffer    */
+
+typedef struct grid_ctx grid_ctx;
+
+/* ---------------------------------------------------------------- runtime */
+const char *grid_last_error(void);
+int grid_abi_version(void);
+int grid_device_count(int *n);
+int grid_ctx_create(int device, grid_ctx **out);
+int grid_ctx_destroy(grid_ctx *ctx);
+/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream);
+ * NULL restores the context's own stream. */
+int grid_ctx_set_stream(grid_ctx *ctx, void *hip_stream);
+int grid_sync(grid_ctx *ctx);
+int grid_dev_alloc(grid_ctx *ctx, size_t bytes, void **d_ptr);
+int grid_dev_free(grid_ctx *ctx, void *d_ptr);
+int grid_h2d(grid_ctx *ctx, void *d_dst, const void *h_src, size_t bytes);
+int grid_d2h(grid_ctx *ctx, void *h_dst, const void *d_src, size_t bytes);
+int grid_d2d(grid_ctx *ctx, void *d_dst, const void *d_src, size_t bytes);
+int grid_memset(grid_ctx *ctx, void *d_dst, int value, size_t bytes);
+/* Event timing on the context stream (for bench.py): returns ms between two
+ * recorded markers. */
+int grid_event_record(grid_ctx *ctx, int slot);
+int grid_event_elapsed(grid_ctx *ctx, int slot_a, int slot_b, float *ms);
+
+/* --------------------------------------------------------- step 4: normalize
+ * Replaces grid/utils/normalize_mosdepth.py normalize_matrix :419-476 and
+ * individual_raw_means :120 (np.nanmean(axis=1) -> 8192-block pairwise sums;
+ * np.nanmean/np.nansum(axis=0) -> sequential over rows).
+ *
+ * d_q: [n][ld] int32 hundredths, columns [0, m) are this shard, whose first
+ * column sits at a GLOBAL offset that is a multiple of GRID_BLOCK. */
+
+/* Per-row, per-8192-block pairwise sums of q/100 (NaN->0) and counts.
+ * d_blocksum/d_blockcnt: [n][ceil(m/8192)]. */
+int grid_norm_row_blocks(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t m, int64_t ld,
+                         double *d_blocksum, int32_t *d_blockcnt);
+/* rowmean[i] = (((0 + b0) + b1) + ...) / count  (np.nanmean axis=1). */
+int grid_norm_row_means(grid_ctx *ctx, const double *d_blocksum, const int32_t *d_blockcnt,
+                        int64_t n, int64_t nblk, double *d_rowmean);
+/* mu[j] = nanmean_i(q_ij/100/rm_i); cnt; (normalize_mosdepth.py:442-445) */
+int grid_norm_col_means(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t m, int64_t ld,
+                        const double *d_rowmean, double *d_mu);
+/* var[j] = nansum_i((y_ij-mu_j)^2)/(n-1); ratio = mu>0 ? 100*var/mu : NaN  (:446-451) */
+int grid_norm_col_vars(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t m, int64_t ld,
+                       const double *d_rowmean, const double *d_mu, double *d_var,
+                       double *d_ratio);
+/* Ascending sort of the non-NaN values of d_v; *h_nvalid receives the count.
+ * d_sorted must hold n doubles.  (np.median :462 / sorted() :495) */
+int grid_sort_valid(grid_ctx *ctx, const double *d_v, int64_t n, double *d_sorted,
+                    int64_t *h_nvalid);
+/* Stable compaction of indices j with v[j] > thr (NaN never kept). (:499) */
+int grid_select_gt(grid_ctx *ctx, const double *d_v, int64_t n, double thr, int32_t *d_idx,
+                   int64_t *h_count);
+/* out[i] = float("%.{decimals}f" % v[i]) (exact decimal rounding, half-even on
+ * the binary value; NaN/inf pass through). */
+int grid_round_decimals(grid_ctx *ctx, const double *d_v, int64_t n, int decimals,
+                        double *d_out);
+/* Gather: out[i] = v[idx[i]]. */
+int grid_gather_f64(grid_ctx *ctx, const double *d_v, const int32_t *d_idx, int64_t n,
+                    double *d_out);
+/* find_neighbors.py:171 keep-mask -> column map: colmap[s] = rank among kept
+ * (or -1); *h_ruse = number kept.  keep = finite(r) && r>=smin && r<=smax. */
+int grid_colmap_range(grid_ctx *ctx, const double *d_r, int64_t n, double smin, double smax,
+                      int32_t *d_colmap, int64_t *h_ruse);
+/* z_{i,s} = ((q/100/rm_i - mu_j)/sqrt(mu_j))*scale for j = sel[s]
+ * (normalize_mosdepth.py:458,470), quantised exactly as "%.2f" into
+ * d_zq[i*ld_zq + s] (GRID_ZQ_NAN / GRID_ZQ_NEG0 sentinels; may be NULL), and,
+ * for colmap[s] >= 0, clip(., -qmax, qmax) hundredths stored as bf16 into
+ * d_zb[i*ld_zb + colmap[s]] (find_neighbors.py:57-58,65; may be NULL).
+ * *h_overflow (may be NULL) reports |z*100| >= 2^31. */
+int grid_norm_zquant(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t ld,
+                     const int32_t *d_sel, int64_t r, const double *d_rowmean,
+                     const double *d_mu, double scale, int32_t *d_zq, int64_t ld_zq,
+                     const int32_t *d_colmap, int32_t qmax, uint16_t *d_zb, int64_t ld_zb,
+                     int32_t *h_overflow);
+
+/* ---------------------------------------------------- step 5: neighbours
+ * Replaces grid/utils/find_neighbors.py find_neighbors_sklearn :179-227
+ * (sklearn NearestNeighbors brute Euclidean ArgKmin).
+ *
+ * d_zb: [np][kpad] bf16 integer hundredths (|v| <= qmax <= 256), rows >= n
+ * and columns >= R_use zero.  np % 128 == 0, kpad % 64 == 0.
+ * Gram G = Zb Zb^T exactly: bf16 MFMA with fp32 partial sums flushed to
+ * integers every <= 2^24/qmax^2 products, int64 atomics across K-slices.
+ * d_gram: [np][np] int64, must be zeroed; only tiles (ti <= tj) are written. */
+int grid_knn_gram(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t kpad, int64_t ld,
+                  int32_t qmax, int64_t *d_gram);
+/* Per row i < n: the min(k+1, n) smallest (d2, j) with
+ * d2 = G_ii + G_jj - 2 G_ij, self dropped, first k kept (find_neighbors.py
+ * :205-225).  d_idx/d_d2: [n][k]; d_cnt[i] = entries written.
+ * row0/nrows select a row block (multi-GPU); n is the total sample count. */
+int grid_knn_topk(grid_ctx *ctx, const int64_t *d_gram, int64_t n, int64_t np_, int64_t k,
+                  int64_t row0, int64_t nrows, int32_t *d_idx, int64_t *d_d2, int32_t *d_cnt);
+
+/* ---------------------------------------------------- step 6: diploid CN
+ * Replaces grid/utils/compute_dipcn.py :62-88.
+ * For each sample i: if has_reads[i] and scale[i] known: over nbr list
+ * d_nbr[i*ld + t] (t < nbr_cnt[i]; -1 = neighbour absent from the counts)
+ * take the first n_nbr present, total += reads[j]/nbr_scale[i*ld+t];
+ * out[i] = (reads[i]/scale[i])/(total/count); valid[i] = 1 if written.
+ * *h_zerodiv = 1 if the reference would raise ZeroDivisionError. */
+int grid_dipcn(grid_ctx *ctx, int64_t n, const double *d_reads, const uint8_t *d_has_reads,
+               const double *d_scale, const int32_t *d_nbr, const double *d_nbr_scale,
+               const int32_t *d_nbr_cnt, int64_t ld, int64_t n_nbr, double *d_out,
+               uint8_t *d_valid, int32_t *h_zerodiv);
+
+/* ---------------------------------------------------- step 7: haploid
+ * Replaces grid/utils/hi_inference.py _run_phasing :175-226 and _compute_imp
+ * :229-250.  Hap-neighbour lists in CSR over 2n haplotypes (d_off[2n+1],
+ * d_nbr hap indices, d_w weights).  The in-place Gauss-Seidel sweep is run
+ * as a level schedule (grid_hi_levels) that is bit-identical to the
+ * sequential order.  Outputs hap[2n] (NaN = unphased), imp[2n], *h_mean. */
+int grid_hi_levels(int64_t n, const int64_t *h_off, const int32_t *h_nbr, int32_t *h_order,
+                   int32_t *h_level_off, int32_t *h_nlevels);
+int grid_hi_phase(grid_ctx *ctx, int64_t n, const double *d_irr, const int64_t *d_off,
+                  const int32_t *d_nbr, const double *d_w, int64_t min_nbr, int64_t n_iters,
+                  const int32_t *d_order, const int32_t *d_level_off, int32_t nlevels,
+                  double *d_hap, double *d_imp, double *d_mean);
+
+/* ---------------------------------------------------- host formatting
+ * Exact "%.2f" text for integer hundredths (GRID_ZQ_* sentinels -> "NA",
+ * "-0.00"), tab-joined.  Returns bytes written in *h_len (no terminator). */
+int grid_format_hundredths(const int32_t *h_v, int64_t n, char *h_out, int64_t cap,
+                           int64_t *h_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

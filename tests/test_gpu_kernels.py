@@ -1,0 +1,201 @@
+"""Kernel-level parity of the HIP path against the CPU oracle (MI355X only).
+
+Bar: bit-exact for every fp64 statistic, index and integer; printed text
+identical.  Sizes are small enough for the oracle to finish in seconds.
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+from oracle import steps
+from oracle.npsum import nanmean_rows
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    from grid_amd._abi import Device
+    d = Device(0)
+    yield d
+    d.close()
+
+
+def to_q(mat):
+    from grid_amd._abi import MISSING
+    q = np.where(np.isnan(mat), 0, np.rint(mat * 100)).astype(np.int64)
+    assert np.array_equal(np.where(np.isnan(mat), 0, q / 100.0), np.where(np.isnan(mat), 0, mat))
+    q = np.where(np.isnan(mat), MISSING, q).astype(np.int32)
+    return np.ascontiguousarray(q)
+
+
+def run_normalize(dev, mat, top_frac=0.1):
+    from grid_amd import engine
+    q = to_q(mat)
+    n, m = q.shape
+    qd = dev.upload(q)
+    st = engine.normalize_stats(dev, qd, n, m, m)
+    sel, r = engine.select_regions(dev, st, top_frac)
+    zq = dev.alloc((n, max(r, 1)), np.int32)
+    if r:
+        engine.zquant(dev, qd, n, m, sel, r, st, zq=zq)
+    return st, sel.numpy()[:r], zq.numpy()[:, :r]
+
+
+def check_normalize(dev, mat, top_frac=0.1):
+    from grid_amd import _abi
+    st, sel, zq = run_normalize(dev, mat, top_frac)
+    with np.errstate(all="ignore"):
+        z, ratios, mu, var, scale = steps.normalize_matrix(mat)
+        raw = nanmean_rows(mat)
+    assert np.array_equal(st.rowmean.numpy()[: len(raw)], raw, equal_nan=True)
+    assert np.array_equal(st.mu.numpy()[: len(mu)], mu, equal_nan=True)
+    assert np.array_equal(st.var.numpy()[: len(var)], var, equal_nan=True)
+    r_ref = np.full(len(mu), np.nan)
+    for k, v in ratios.items():
+        r_ref[k] = v
+    assert np.array_equal(st.ratio.numpy()[: len(mu)], r_ref, equal_nan=True)
+    assert st.scale == scale
+    exp_sel = steps.select_high_variance_regions(ratios, top_frac)
+    assert sel.tolist() == exp_sel
+    for i in range(mat.shape[0]):
+        exp = "\t".join("NA" if np.isnan(z[i, j]) else f"{z[i, j]:.2f}" for j in exp_sel)
+        assert _abi.format_hundredths(zq[i]) == exp, f"row {i}"
+
+
+def test_normalize_golden_g2(dev):
+    d = np.load(os.path.join(G, "g2.npz"))
+    n_cases = len([k for k in d.files if k.endswith("_in")])
+    for ci in range(n_cases):
+        check_normalize(dev, d[f"c{ci}_in"])
+
+
+@pytest.mark.parametrize("n,m,seed", [(37, 20000, 1), (5, 8192 * 3, 2), (130, 1000, 3), (2, 7, 4)])
+def test_normalize_random(dev, n, m, seed):
+    rng = np.random.default_rng(seed)
+    q = rng.integers(1, 20000, size=(n, m))
+    mat = q / 100.0
+    mat[rng.random((n, m)) < 0.03] = np.nan
+    check_normalize(dev, mat, top_frac=[0.1, 0.0, 0.5, 0.9][seed % 4])
+
+
+def test_round_decimals_g5(dev):
+    cases = json.load(open(os.path.join(G, "g5.json")))
+    v = np.array([float.fromhex(c[0]) for c in cases])
+    vd = dev.upload(v)
+    for dec, col in ((2, 1), (3, 2)):
+        out = dev.alloc(len(v), np.float64)
+        from grid_amd._abi import call
+        call("grid_round_decimals", dev.ctx, vd.ptr, len(v), dec, out.ptr)
+        got = out.numpy()
+        exp = np.array([float(c[col]) for c in cases])
+        assert np.array_equal(got, exp), [(c, g) for c, g, e in zip(cases, got, exp) if g != e][:5]
+        # sign of zero as printed
+        assert [math.copysign(1, g) for g in got] == [math.copysign(1, e) for e in exp]
+
+
+def test_knn_golden_g3(dev):
+    from grid_amd import engine
+    for case in json.load(open(os.path.join(G, "g3.json"))):
+        q = np.array(case["q"], dtype=np.int64)
+        k = case["k"]
+        idx, d2, cnt = engine.knn_from_hundredths(dev, q, k, 200)
+        exp = steps.knn_exact(q, k)
+        for i in range(q.shape[0]):
+            assert cnt[i] == len(exp[i])
+            assert idx[i, : cnt[i]].tolist() == [j for j, _ in exp[i]]
+            assert d2[i, : cnt[i]].tolist() == [s for _, s in exp[i]]
+
+
+@pytest.mark.parametrize("n,r,k,qmax,seed", [(300, 5000, 10, 200, 1), (129, 64, 5, 256, 2),
+                                             (700, 3000, 40, 200, 3), (1, 10, 3, 200, 4)])
+def test_knn_random(dev, n, r, k, qmax, seed):
+    from grid_amd import engine
+    rng = np.random.default_rng(seed)
+    q = rng.integers(-qmax, qmax + 1, size=(n, r))
+    idx, d2, cnt = engine.knn_from_hundredths(dev, q, k, qmax)
+    exp = steps.knn_exact(q, k)
+    for i in range(n):
+        assert idx[i, : cnt[i]].tolist() == [j for j, _ in exp[i]]
+        assert d2[i, : cnt[i]].tolist() == [s for _, s in exp[i]]
+
+
+def test_gram_exact_worst_case(dev):
+    """bf16 MFMA + fp32 partials are exact at the integer bounds (all |q| = qmax)."""
+    from grid_amd import engine
+    from grid_amd._abi import call
+    for qmax in (200, 256):
+        rng = np.random.default_rng(qmax)
+        n, r = 256, 64 * 700
+        q = np.where(rng.random((n, r)) < 0.5, -qmax, qmax).astype(np.int64)
+        q[:3] = qmax                     # rows with maximal positive sums
+        zf = (q.astype(np.float32).view(np.uint32) >> 16).astype(np.uint16)
+        zb = dev.upload(zf)
+        g = dev.zeros((n, n), np.int64)
+        call("grid_knn_gram", dev.ctx, zb.ptr, n, r, r, qmax, g.ptr)
+        got = g.numpy()
+        ref = q @ q.T
+        for ti in range(2):
+            for tj in range(ti, 2):
+                assert np.array_equal(got[ti*128:(ti+1)*128, tj*128:(tj+1)*128],
+                                      ref[ti*128:(ti+1)*128, tj*128:(tj+1)*128])
+
+
+def test_dipcn_random(dev):
+    from grid_amd import engine
+    rng = np.random.default_rng(7)
+    n, k = 200, 12
+    ids = [f"S{i:04d}" for i in range(n)]
+    reads = {ids[i]: float(rng.integers(0, 5000)) for i in range(n) if i % 17}
+    reads[ids[5]] = 0.0
+    scale = np.round(rng.uniform(5, 60, n), 2)
+    nbr = np.array([rng.choice(n, k, replace=False) for _ in range(n)], dtype=np.int32)
+    nbrs = {ids[i]: [(ids[j], float(scale[j])) for j in nbr[i]] for i in range(n)}
+    sc = {ids[i]: float(scale[i]) for i in range(n)}
+    exp = dict(steps.dipcn(nbrs, sc, reads, 7))
+    has = np.array([ids[i] in reads for i in range(n)])
+    rd = np.array([reads.get(ids[i], 0.0) for i in range(n)])
+    out, valid = engine.dipcn(dev, rd, has, scale, nbr, scale[nbr], np.full(n, k, np.int32), 7)
+    assert {ids[i] for i in range(n) if valid[i]} == set(exp)
+    for i in range(n):
+        if valid[i]:
+            assert out[i] == exp[ids[i]]
+
+
+def test_phasing_golden_g4(dev):
+    from grid_amd import engine
+    for case in json.load(open(os.path.join(G, "g4.json"))):
+        irr = np.array([float.fromhex(x) for x in case["irr"]])
+        hn = [[(a, float.fromhex(b)) for a, b in l] for l in case["nbrs"]]
+        off, nbr, w = engine.csr_from_lists(hn)
+        hap, imp, mean = engine.phase(dev, irr, off, nbr, w, case["min_nbr"], case["iters"])
+        assert [float(x).hex() for x in hap] == case["hap"]
+        assert float(mean).hex() == case["mean"]
+        assert [[float(imp[2*i]).hex(), float(imp[2*i+1]).hex()] for i in range(len(irr))] == case["imp"]
+
+
+@pytest.mark.parametrize("n,seed", [(500, 1), (3000, 2), (9000, 3)])
+def test_phasing_random(dev, n, seed):
+    from grid_amd import engine
+    rng = np.random.default_rng(seed)
+    irr = rng.uniform(0.1, 4.0, n)
+    hn = []
+    for h in range(2 * n):
+        c = (h // 2) % 26
+        lst = []
+        for _ in range(int(rng.integers(0, 11))):
+            j = int(rng.integers(0, n // 26)) * 26 + c
+            lst.append((min(2 * j + int(rng.integers(0, 2)), 2 * n - 1), 1.0))
+        hn.append(lst)
+    off, nbr, w = engine.csr_from_lists(hn)
+    iters = 20
+    hap, imp, mean = engine.phase(dev, irr, off, nbr, w, 1, iters)
+    eh, em = steps.run_phasing(list(irr), hn, 1, iters)
+    assert np.array_equal(hap, np.array(eh), equal_nan=True)
+    assert mean == em
+    ei = [steps.compute_imp(i, eh, hn, em) for i in range(n)]
+    assert np.array_equal(imp, np.array(ei).reshape(-1))
