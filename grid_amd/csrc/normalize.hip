@@ -298,9 +298,38 @@ __global__ __launch_bounds__(256) void k_zquant(const int32_t *__restrict__ q, i
   }
 }
 
+// Full fp64 z matrix (normalize_matrix's returned array, :458 and :470):
+// transformed where mu > 0, x/rm*scale elsewhere, NaN for missing cells.
+__global__ __launch_bounds__(256) void k_zfull(const int32_t *__restrict__ q, int64_t n, int64_t m, int64_t ld,
+                                               const double *__restrict__ rm, const double *__restrict__ mu,
+                                               double scale, double *__restrict__ z) {
+  int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t i = blockIdx.y;
+  if (j >= m) return;
+  int32_t qv = q[i * ld + j];
+  double rmi = rm[i];
+  double x = (qv == GRID_MISSING) ? __builtin_nan("") : (double)qv / 100.0;
+  double rs = (rmi == 0.0) ? __builtin_nan("") : rmi;
+  double y = x / rs;
+  double mj = mu[j];
+  if (mj > 0.0) y = (y - mj) / sqrt(mj);
+  z[i * m + j] = y * scale;
+}
+
 }  // namespace
 
 extern "C" {
+
+int grid_norm_zfull(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t m, int64_t ld, const double *d_rm,
+                    const double *d_mu, double scale, double *d_z) {
+  REQUIRE(ctx && n >= 0 && m >= 0 && ld >= m && n <= 65535, "bad args");
+  if (n == 0 || m == 0) return GRID_OK;
+  hipLaunchKernelGGL(k_zfull, dim3((unsigned)ceil_div(m, 256), (unsigned)n), dim3(256), 0, ctx->stream, d_q, n, m,
+                     ld, d_rm, d_mu, scale, d_z);
+  LAUNCHCHK();
+  return GRID_OK;
+}
+
 
 int grid_norm_row_blocks(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t m, int64_t ld,
                          double *d_bsum, int32_t *d_bcnt) {

@@ -151,6 +151,8 @@ def knn(dev: Device, zb: DevBuf, n: int, np_: int, kpad: int, ld: int, qmax: int
 def knn_from_hundredths(dev: Device, zq: np.ndarray, k: int, qmax: int):
     """Host (n x R_use) int hundredths, already clipped, NaN -> 0."""
     n, r = zq.shape
+    if n == 0:
+        return np.zeros((0, max(k, 1)), I4), np.zeros((0, max(k, 1)), I8), np.zeros(0, I4)
     np_ = pad_to(max(n, 1), 128)
     kpad = pad_to(max(r, 1), 64)
     zf = np.zeros((np_, kpad), dtype=np.float32)
@@ -162,8 +164,10 @@ def knn_from_hundredths(dev: Device, zq: np.ndarray, k: int, qmax: int):
 
 # ------------------------------------------------------------------ step 6 --
 def dipcn(dev: Device, reads: np.ndarray, has: np.ndarray, scale: np.ndarray, nbr: np.ndarray,
-          nscale: np.ndarray, ncnt: np.ndarray, n_nbr: int):
-    n = len(reads)
+          nscale: np.ndarray, ncnt: np.ndarray, n_nbr: int, n_rows: int | None = None):
+    """reads/has/scale are indexed by sample id over a universe that starts
+    with the ``n_rows`` neighbour-file rows; nbr holds universe indices."""
+    n = len(ncnt) if n_rows is None else n_rows
     ld = nbr.shape[1] if nbr.ndim == 2 else 0
     d = [dev.upload(np.ascontiguousarray(a)) for a in
          (reads.astype(F8), has.astype(U1), scale.astype(F8), nbr.astype(I4), nscale.astype(F8), ncnt.astype(I4))]

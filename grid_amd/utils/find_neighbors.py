@@ -1,0 +1,143 @@
+"""Step 5 -- nearest neighbours on normalised coverage, MI355X path.
+
+Drop-in for grid/utils/find_neighbors.py.  The reference calls scikit-learn's
+brute-force Euclidean ArgKmin (:207-213).  Here the clipped z-scores, which
+the normalised file holds as exact hundredths, become an integer bf16 panel
+in HBM; the Gram matrix is computed exactly on the MFMA pipe and the k+1
+nearest are selected per row on the GPU (grid_amd/csrc/knn.hip).  Neighbour
+order equals sklearn's wherever exact distances differ.
+"""
+from __future__ import annotations
+
+import gzip
+from pathlib import Path
+
+import numpy as np
+
+from .. import _abi, engine
+from ..device import get_device
+from .utils import log, progress_bar
+
+
+def _hundredths(tok: str) -> int:
+    """"%.2f" text -> integer hundredths (NA -> missing)."""
+    if tok in ("NA", "nan"):
+        return _abi.MISSING
+    neg = tok.startswith("-")
+    t = tok[1:] if neg else tok
+    ip, _, fp = t.partition(".")
+    if len(fp) != 2 or not ip.isdigit() or not fp.isdigit():
+        v = float(tok)
+        k = round(v * 100)
+        if k / 100.0 != v:
+            raise ValueError(f"z value {tok!r} is not a 2-decimal number")
+        return k
+    k = int(ip) * 100 + int(fp)
+    return -k if neg else k
+
+
+def read_normalized_data(input_file):
+    """:81-124 -> (individuals, sigma2ratios, data_matrix float64, scales)."""
+    ids, scales, zq, ratios = _read_normalized_q(input_file)
+    data = np.where(zq == _abi.MISSING, np.nan, zq / 100.0)
+    return ids, ratios, data, scales
+
+
+def _read_normalized_q(input_file):
+    ids, scales, rows = [], {}, []
+    with gzip.open(input_file, "rt") as f:
+        f.readline()
+        parts = f.readline().strip().split("\t")
+        ratios = np.array([np.nan if v in ("NA", "nan") else float(v) for v in parts[2:]])
+        for line in f:
+            p = line.strip().split("\t")
+            ids.append(p[0])
+            scales[p[0]] = float(p[1])
+            rows.append([_hundredths(v) for v in p[2:]])
+    r = len(rows[0]) if rows else 0
+    zq = np.array(rows, dtype=np.int64).reshape(len(rows), r) if rows else np.zeros((0, 0), np.int64)
+    return ids, scales, zq, ratios
+
+
+def filter_regions_by_variance(sigma2ratios, frac_r: float = 1.0, sigma2_max: float = 1000.0, console=None):
+    """:128-175 (host; R values)."""
+    sigma2ratios = np.asarray(sigma2ratios, dtype=np.float64)
+    R = len(sigma2ratios)
+    finite = np.isfinite(sigma2ratios)
+    fv = np.sort(sigma2ratios[finite])
+    if len(fv) == 0:
+        log(console, "Warning: no finite variance ratios — keeping all regions", style="warning")
+        return np.arange(R), R
+    lo = min(int(R * (1.0 - frac_r)), len(fv) - 1)
+    smin = float(fv[lo])
+    extreme = int(np.sum(sigma2ratios > sigma2_max))
+    if extreme and console:
+        log(console, f"Removed {extreme} / {R} regions with sigma2ratio > {sigma2_max}", style="warning")
+    keep = finite & (sigma2ratios >= smin) & (sigma2ratios <= sigma2_max)
+    idx = np.where(keep)[0]
+    return idx, len(idx)
+
+
+def find_neighbors_sklearn(data_matrix, individuals, n_neighbors: int = 500, zmax: float = 2.0):
+    """:179-227 API: {id: [(neighbour_id, squared distance), ...]} computed on
+    the GPU.  ``data_matrix`` must hold exact hundredths within +-zmax (the
+    state after find_neighbors' clip, :57-58)."""
+    data = np.asarray(data_matrix, dtype=np.float64)
+    q = np.rint(data * 100.0)
+    if not np.array_equal(q / 100.0, data):
+        raise _abi.GridNativeError("find_neighbors_sklearn: values must be exact hundredths")
+    qmax = int(np.max(np.abs(q))) if q.size else 0
+    qmax = max(qmax, engine.qmax_for_zmax(zmax))
+    if qmax > 256:
+        raise _abi.GridNativeError("values exceed the exact bf16 range (|v| <= 2.56)")
+    idx, d2, cnt = engine.knn_from_hundredths(get_device(), q.astype(np.int64), n_neighbors, qmax)
+    return {ind: [(individuals[int(idx[i, t])], int(d2[i, t]) / 10000.0) for t in range(cnt[i])]
+            for i, ind in enumerate(individuals)}
+
+
+def save_neighbors(neighbors_dict, scales, output_file, zmax, R_use) -> None:
+    """:231-267"""
+    if R_use == 0:
+        R_use = 1
+    with gzip.open(output_file, "wt", compresslevel=6) as out:
+        for ind, nbrs in neighbors_dict.items():
+            line = f"{ind}\t{scales.get(ind, 1.0):.2f}"
+            for nid, sq in nbrs:
+                line += f"\t{nid}\t{scales.get(nid, 1.0):.2f}\t{sq / (2 * R_use):.2f}"
+            out.write(line + "\n")
+
+
+def find_neighbors(config, console):
+    """Step entry point (:11-77)."""
+    try:
+        zmax = config["mosdepth"]["neighbors"].get("zmax", 2.0)
+        sigma2_max = config["mosdepth"]["neighbors"].get("sigma2_max", 1000.0)
+        n_neighbors = config["mosdepth"]["neighbors"].get("num_neighbors", 500)
+        frac_r = config["mosdepth"]["neighbors"].get("frac_r", 1.0)
+        in_prefix = config["mosdepth"]["normalize"].get("output_file_prefix")
+        ftype = config.get("output_file_type", "tsv")
+        output_dir = config.get("output_dir", ".")
+        input_file = Path(f"{output_dir}/{in_prefix}.{ftype}.gz")
+        out_prefix = config["mosdepth"]["neighbors"].get("output_file_prefix", "neighbor_coverage")
+        output_file = Path(output_dir) / f"{out_prefix}.zMax{zmax:.1f}.{ftype}.gz"
+    except Exception as e:
+        log(console, f"Config error: {e}", style="danger")
+        return
+    output_file.parent.mkdir(parents=True, exist_ok=True)
+
+    ids, scales, zq, ratios = _read_normalized_q(input_file)
+    N = len(ids)
+    qmax = engine.qmax_for_zmax(float(zmax))
+    # clip (:57) and NaN -> 0 (:58), on exact hundredths
+    zc = np.where(zq == _abi.MISSING, 0, np.clip(zq, -qmax, qmax))
+    valid, R_use = filter_regions_by_variance(ratios, frac_r=frac_r, sigma2_max=sigma2_max, console=console)
+    zc = zc[:, valid] if zc.size else zc.reshape(N, 0)
+
+    with progress_bar(console, total=N, description="Finding neighbors...") as (progress, task):
+        idx, d2, cnt = engine.knn_from_hundredths(get_device(config), zc, int(n_neighbors), qmax)
+        progress.advance(task, N)
+
+    nbrs = {ind: [(ids[int(idx[i, t])], int(d2[i, t]) / 10000.0) for t in range(cnt[i])]
+            for i, ind in enumerate(ids)}
+    save_neighbors(nbrs, scales, output_file, zmax, R_use)
+    log(console, f"Saved neighbors to {output_file}", style="success")

@@ -1,0 +1,210 @@
+"""Step 7 -- haplotype inference (IBS / IBD-constrained phasing), MI355X path.
+
+Drop-in for grid/utils/hi_inference.py.  The file readers keep the
+reference's parsing rules; the Gauss-Seidel proportional phasing
+(_run_phasing :175-226) and the imputation (_compute_imp :229-250) run on the
+GPU (grid_amd/csrc/dipcn_phase.hip).  The in-place sweep is executed as a
+level schedule computed from the neighbour graph (grid_hi_levels): samples
+in one level read, then write, and the result is bit-identical to the
+sequential in-place order.
+"""
+from __future__ import annotations
+
+from collections import defaultdict
+from pathlib import Path
+
+import numpy as np
+
+from .. import engine
+from ..device import get_device
+from .utils import log, open_maybe_gz
+
+
+def _read_dip_cn_file(dip_cn_file):
+    """:10-31"""
+    ids, irrs, idx = [], [], {}
+    with open_maybe_gz(dip_cn_file) as f:
+        for line in f:
+            line = line.strip()
+            if not line:
+                continue
+            parts = line.split()
+            if len(parts) < 2:
+                continue
+            try:
+                v = float(parts[1])
+            except ValueError:
+                continue
+            idx[parts[0]] = len(irrs)
+            ids.append(parts[0])
+            irrs.append(v)
+    return ids, irrs, idx
+
+
+def _load_ibs_neighbors(neighbors_file, IDtoInd, MAX_NBR):
+    """:34-74 (computeIBSpbwt: header + ID hap nbrInd cMlen cMedge IDnbr hapNbr)."""
+    hap_nbrs = [[] for _ in range(2 * len(IDtoInd))]
+    with open_maybe_gz(neighbors_file) as f:
+        next(f)
+        for line in f:
+            line = line.strip()
+            if not line:
+                continue
+            p = line.split()
+            if len(p) < 7:
+                continue
+            try:
+                hap, hap_nbr = int(p[1]), int(p[6])
+            except ValueError:
+                continue
+            if hap not in (1, 2) or hap_nbr not in (1, 2):
+                continue
+            i, j = IDtoInd.get(p[0]), IDtoInd.get(p[5])
+            if i is not None and j is not None:
+                h = 2 * i + hap - 1
+                if len(hap_nbrs[h]) < MAX_NBR:
+                    hap_nbrs[h].append((2 * j + hap_nbr - 1, 1.0))
+    return hap_nbrs
+
+
+def _segment_distance(bp1, bp2, region_start, region_end):
+    """:77-83"""
+    if bp2 < region_start:
+        return float(region_start - bp2)
+    if bp1 > region_end:
+        return float(bp1 - region_end)
+    return 0.0
+
+
+def _load_ibd_neighbors(ilash_file, IDtoInd, MAX_NBR, region_start, region_end, min_length=0.5,
+                        min_match=0.70, weighted=False, weight_scale=1_000_000):
+    """:86-172 (iLASH, 11 columns; symmetric; sorted by cM desc; optional
+    Lorentzian distance x match weight)."""
+    raw = defaultdict(list)
+    with open_maybe_gz(ilash_file) as f:
+        for line in f:
+            line = line.strip()
+            if not line:
+                continue
+            p = line.split("\t")
+            if len(p) < 11:
+                p = line.split()
+            if len(p) < 11:
+                continue
+            try:
+                bp1, bp2 = int(p[5]), int(p[6])
+                length, match = float(p[9]), float(p[10])
+            except (ValueError, IndexError):
+                continue
+            if length < min_length or match < min_match:
+                continue
+            try:
+                h1 = int(p[1].rsplit("_", 1)[-1])
+                h2 = int(p[3].rsplit("_", 1)[-1])
+            except ValueError:
+                continue
+            if h1 not in (0, 1) or h2 not in (0, 1):
+                continue
+            i, j = IDtoInd.get(p[0]), IDtoInd.get(p[2])
+            if i is None or j is None:
+                continue
+            if weighted:
+                w = (weight_scale / (_segment_distance(bp1, bp2, region_start, region_end) + weight_scale)) * match
+            else:
+                w = 1.0
+            a, b = 2 * i + h1, 2 * j + h2
+            raw[a].append((b, w, length))
+            raw[b].append((a, w, length))
+    hap_nbrs = [[] for _ in range(2 * len(IDtoInd))]
+    for h, segs in raw.items():
+        segs.sort(key=lambda x: -x[2])
+        hap_nbrs[h] = [(nb, w) for nb, w, _ in segs[:MAX_NBR]]
+    return hap_nbrs
+
+
+def _run_phasing(IRRs, hap_nbrs, MIN_NBR, N_ITERS, console=None):
+    """:175-226 on the GPU.  Returns (hap_IRRs list, mean_IRRs)."""
+    hap, _, mean = _phase_device(IRRs, hap_nbrs, MIN_NBR, N_ITERS, console)
+    return [float(x) for x in hap], mean
+
+
+def _phase_device(IRRs, hap_nbrs, MIN_NBR, N_ITERS, console=None, dev=None):
+    n = len(IRRs)
+    off, nbr, w = engine.csr_from_lists(hap_nbrs)
+    n_ph = sum(1 for i in range(n) if off[2 * i + 1] - off[2 * i] >= MIN_NBR
+               and off[2 * i + 2] - off[2 * i + 1] >= MIN_NBR)
+    log(console, f"Phasing {n_ph} samples with >={MIN_NBR} neighbors for both haps")
+    if n_ph > 0:
+        tot = sum(int(off[2 * i + 2] - off[2 * i]) for i in range(n)
+                  if off[2 * i + 1] - off[2 * i] >= MIN_NBR and off[2 * i + 2] - off[2 * i + 1] >= MIN_NBR)
+        log(console, f"Avg neighbors per hap: {tot / (2.0 * n_ph):.2f}")
+    return engine.phase(dev or get_device(), np.asarray(IRRs, dtype=np.float64), off, nbr, w, MIN_NBR, N_ITERS)
+
+
+def _compute_imp(i, hap_IRRs, hap_nbrs, mean_IRRs):
+    """:229-250 (single-sample API; the step computes all samples on the GPU)."""
+    import math
+    ws, wv = [1e-9, 1e-9], [0.0, 0.0]
+    for h in range(2):
+        for nb, w in hap_nbrs[2 * i + h]:
+            v = hap_IRRs[nb]
+            if not math.isnan(v):
+                ws[h] += w
+                wv[h] += w * v
+    i0, i1 = wv[0] / ws[0], wv[1] / ws[1]
+    if ws[0] <= 1e-9:
+        i0 = mean_IRRs / 2
+    if ws[1] <= 1e-9:
+        i1 = mean_IRRs / 2
+    return i0, i1
+
+
+def hi_inference(config, console):
+    """Step entry point (:253-339)."""
+    try:
+        hc = config.get("compute_haploid_genotypes", {})
+        prefix = hc.get("output_file_prefix", "haploid_genotypes")
+        ftype = config.get("output_file_type", "tsv")
+        output_dir = config.get("output_dir", ".")
+        output_file = Path(f"{output_dir}/{prefix}.{ftype}")
+        dip_prefix = config["compute_diploid_genotypes"].get("output_file_prefix")
+        dip_file = Path(f"{output_dir}/{dip_prefix}.{ftype}")
+        method = hc.get("method", "ibs").lower()
+        MIN_NBR = hc.get("min_neighbors", 1)
+        MAX_NBR = hc.get("max_neighbors", 10)
+        N_ITERS = hc.get("n_iters", 100)
+    except Exception as e:
+        log(console, f"Config error: {e}", style="danger")
+        return
+
+    IDs, IRRs, IDtoInd = _read_dip_cn_file(dip_file)
+    N = len(IRRs)
+    log(console, f"Read diploid IRR data for {N} samples", style="success")
+    if method == "ibs":
+        ibs = hc.get("ibs_output")
+        if not ibs:
+            log(console, "Config error: ibs_output required for method='ibs'", style="danger")
+            return
+        log(console, f"Loading IBS neighbors from {ibs}")
+        hap_nbrs = _load_ibs_neighbors(ibs, IDtoInd, MAX_NBR)
+    elif method == "ibd":
+        ibd = hc.get("ibd_output")
+        if not ibd:
+            log(console, "Config error: ibd_output required for method='ibd'", style="danger")
+            return
+        weighted = hc.get("weighted", False)
+        log(console, f"Loading IBD neighbors from {ibd} (weighted={weighted})")
+        hap_nbrs = _load_ibd_neighbors(ibd, IDtoInd, MAX_NBR, config.get("start_bp"), config.get("end_bp"),
+                                       min_length=hc.get("min_length", 0.5), min_match=hc.get("min_match", 0.70),
+                                       weighted=weighted, weight_scale=hc.get("weight_scale", 1_000_000))
+    else:
+        log(console, f"Config error: unknown method '{method}', must be 'ibs' or 'ibd'", style="danger")
+        return
+
+    hap, imp, _ = _phase_device(IRRs, hap_nbrs, MIN_NBR, N_ITERS, console, get_device(config))
+    with open_maybe_gz(output_file, "wt") as fout:
+        fout.write("ID\tIRRs\thap1phased\thap2phased\thap1imp\thap2imp\n")
+        for i in range(N):
+            fout.write(f"{IDs[i]}\t{IRRs[i]:.2f}\t{hap[2*i]:.2f}\t{hap[2*i+1]:.2f}\t"
+                       f"{imp[2*i]:.2f}\t{imp[2*i+1]:.2f}\n")
+    log(console, f"Haploid genotypes written to {output_file}", style="success")

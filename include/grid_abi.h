@@ -121,6 +121,11 @@ int grid_norm_zquant(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t ld,
                      const int32_t *d_colmap, int32_t qmax, uint16_t *d_zb, int64_t ld_zb,
                      int32_t *h_overflow);
 
+/* The full fp64 matrix normalize_matrix returns (:458, :470): z[i*m+j] =
+ * ((y-mu)/sqrt(mu))*scale where mu > 0, y*scale elsewhere, NaN if missing. */
+int grid_norm_zfull(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t m, int64_t ld,
+                    const double *d_rowmean, const double *d_mu, double scale, double *d_z);
+
 /* ---------------------------------------------------- step 5: neighbours
  * Replaces grid/utils/find_neighbors.py find_neighbors_sklearn :179-227
  * (sklearn NearestNeighbors brute Euclidean ArgKmin).
