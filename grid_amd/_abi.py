@@ -31,6 +31,7 @@ _SIGS = {
     "grid_ctx_create": [C.c_int, C.POINTER(_vp)],
     "grid_ctx_destroy": [_vp],
     "grid_ctx_set_stream": [_vp, _vp],
+    "grid_ctx_own_stream": [_vp],
     "grid_sync": [_vp],
     "grid_dev_alloc": [_vp, C.c_size_t, C.POINTER(_vp)],
     "grid_dev_free": [_vp, _vp],
@@ -57,6 +58,7 @@ _SIGS = {
     "grid_dipcn": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, C.POINTER(_i32)],
     "grid_hi_levels": [_i64, _vp, _vp, _vp, _vp, C.POINTER(_i32)],
     "grid_hi_phase": [_vp, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _i32, _vp, _vp, _vp],
+    "grid_synth_depth": [_vp, C.c_uint64, _i64, _i64, _i64, _i64, _i32, _vp],
     "grid_format_hundredths": [_vp, _i64, _vp, _i64, C.POINTER(_i64)],
 }
 EXPORTS = tuple(_SIGS) + ("grid_last_error",)
@@ -131,8 +133,10 @@ class Device:
             self.set_stream(stream)
 
     def set_stream(self, stream):
+        """Enqueue on ``stream`` (a torch.cuda.Stream, a raw handle, or
+        None/0 for the default stream)."""
         s = stream if isinstance(stream, int) or stream is None else stream.cuda_stream
-        call("grid_ctx_set_stream", self.ctx, s)
+        call("grid_ctx_set_stream", self.ctx, s or None)
 
     def sync(self):
         call("grid_sync", self.ctx)

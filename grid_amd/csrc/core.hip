@@ -77,7 +77,13 @@ int grid_ctx_destroy(grid_ctx *ctx) {
 
 int grid_ctx_set_stream(grid_ctx *ctx, void *s) {
   REQUIRE(ctx, "ctx is NULL");
-  ctx->stream = s ? (hipStream_t)s : ctx->own;
+  ctx->stream = (hipStream_t)s;   // NULL = the default (null) stream
+  return GRID_OK;
+}
+
+int grid_ctx_own_stream(grid_ctx *ctx) {
+  REQUIRE(ctx, "ctx is NULL");
+  ctx->stream = ctx->own;
   return GRID_OK;
 }
 
@@ -168,7 +174,7 @@ __global__ void k_round_dec(const double *v, int64_t n, double s, double *out) {
 
 __global__ void k_gather(const double *v, const int32_t *idx, int64_t n, double *out) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = v[idx[i]];
+  if (i < n) out[i] = idx[i] >= 0 ? v[idx[i]] : __builtin_nan("");
 }
 
 __global__ void k_keep_flags(const double *r, int64_t n, double smin, double smax, int32_t *f) {

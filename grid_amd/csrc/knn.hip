@@ -252,9 +252,14 @@ __global__ __launch_bounds__(256) void k_topk(const int64_t *__restrict__ g, int
       d2o[orow * k + pos] = (int64_t)(sel[e] >> 20);
     }
   }
-  if (tid == 0) {
+  {
     int64_t c = ktake - (selfpos >= 0 ? 1 : 0);
-    cnto[orow] = (int32_t)(c < k ? c : k);
+    c = c < k ? c : k;
+    for (int64_t e = c + tid; e < k; e += 256) {   // unused slots: idx -1, d2 0
+      idx[orow * k + e] = -1;
+      d2o[orow * k + e] = 0;
+    }
+    if (tid == 0) cnto[orow] = (int32_t)c;
   }
 }
 

@@ -54,9 +54,11 @@ int grid_abi_version(void);
 int grid_device_count(int *n);
 int grid_ctx_create(int device, grid_ctx **out);
 int grid_ctx_destroy(grid_ctx *ctx);
-/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream);
- * NULL restores the context's own stream. */
+/* Enqueue on an external hipStream_t (e.g. torch.cuda.current_stream()
+ * .cuda_stream); NULL selects the default (null) stream.
+ * grid_ctx_own_stream restores the context's private non-blocking stream. */
 int grid_ctx_set_stream(grid_ctx *ctx, void *hip_stream);
+int grid_ctx_own_stream(grid_ctx *ctx);
 int grid_sync(grid_ctx *ctx);
 int grid_dev_alloc(grid_ctx *ctx, size_t bytes, void **d_ptr);
 int grid_dev_free(grid_ctx *ctx, void *d_ptr);
@@ -102,7 +104,7 @@ int grid_select_gt(grid_ctx *ctx, const double *d_v, int64_t n, double thr, int3
  * the binary value; NaN/inf pass through). */
 int grid_round_decimals(grid_ctx *ctx, const double *d_v, int64_t n, int decimals,
                         double *d_out);
-/* Gather: out[i] = v[idx[i]]. */
+/* Gather: out[i] = v[idx[i]] (NaN where idx[i] < 0). */
 int grid_gather_f64(grid_ctx *ctx, const double *d_v, const int32_t *d_idx, int64_t n,
                     double *d_out);
 /* find_neighbors.py:171 keep-mask -> column map: colmap[s] = rank among kept
@@ -139,7 +141,8 @@ int grid_knn_gram(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t kpad
                   int32_t qmax, int64_t *d_gram);
 /* Per row i < n: the min(k+1, n) smallest (d2, j) with
  * d2 = G_ii + G_jj - 2 G_ij, self dropped, first k kept (find_neighbors.py
- * :205-225).  d_idx/d_d2: [n][k]; d_cnt[i] = entries written.
+ * :205-225).  d_idx/d_d2: [n][k]; d_cnt[i] = entries written; unused
+ * slots hold idx -1, d2 0.
  * row0/nrows select a row block (multi-GPU); n is the total sample count. */
 int grid_knn_topk(grid_ctx *ctx, const int64_t *d_gram, int64_t n, int64_t np_, int64_t k,
                   int64_t row0, int64_t nrows, int32_t *d_idx, int64_t *d_d2, int32_t *d_cnt);
@@ -168,6 +171,12 @@ int grid_hi_phase(grid_ctx *ctx, int64_t n, const double *d_irr, const int64_t *
                   const int32_t *d_nbr, const double *d_w, int64_t min_nbr, int64_t n_iters,
                   const int32_t *d_order, const int32_t *d_level_off, int32_t nlevels,
                   double *d_hap, double *d_imp, double *d_mean);
+
+/* ---------------------------------------------------- synthetic input
+ * Counter-based synthetic cohort (bench/smoke input, not a product path):
+ * d_q[i*ld + j] = hundredths depth of sample i at GLOBAL bin col0 + j. */
+int grid_synth_depth(grid_ctx *ctx, uint64_t seed, int64_t n, int64_t m, int64_t ld, int64_t col0,
+                     int32_t nclusters, int32_t *d_q);
 
 /* ---------------------------------------------------- host formatting
  * Exact "%.2f" text for integer hundredths (GRID_ZQ_* sentinels -> "NA",
