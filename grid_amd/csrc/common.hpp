@@ -64,3 +64,25 @@ __host__ __device__ inline double round_dec_k(double v, double s) {
 }
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// ---- exact fast division (bit-identical to IEEE division) ------------------
+// fl(q/100) for any int32 q: y0 = q*RN(0.01) is corrected once with the exact
+// FMA remainder.  Verified EXHAUSTIVELY over all 2^32 int32 values
+// (tests/test_exact_division.py compiles and runs the check).
+__host__ __device__ inline double div100_exact(int32_t q) {
+  const double a = (double)q;
+  const double y0 = a * 0.01;
+  const double e = fma(-y0, 100.0, a);
+  return fma(e, 0.01, y0);
+}
+// fl(x/b) given r = fl(1/b): Markstein's correction (r correctly rounded,
+// remainders exact via FMA) applied twice; the second step is a no-op when
+// the first is already correctly rounded.  Valid for normal-range operands
+// (no overflow/underflow), which depth ratios and z-scores are.
+__host__ __device__ inline double div_exact(double x, double b, double r) {
+  double y = x * r;
+  double e = fma(-y, b, x);
+  y = fma(e, r, y);
+  e = fma(-y, b, x);
+  return fma(e, r, y);
+}

@@ -54,7 +54,51 @@ __device__ __forceinline__ void nbr_means(int64_t i, const double *hap, const in
   }
 }
 
-constexpr int PT = 1024;
+constexpr int PT = 256;
+constexpr int CAP = 16;   // neighbours per haplotype held in registers (longer lists: loop)
+
+// Weighted neighbour means of sample i with all list loads issued up front
+// (independent) so one level costs ~one memory latency; the accumulation is
+// the reference's sequential order (hi_inference.py:212-217).
+__device__ __forceinline__ void nbr_means_fast(int64_t i, const double *hap, const int64_t *off,
+                                               const int32_t *nbr, const double *w, double ws[2],
+                                               double wv[2]) {
+  const int64_t o0 = off[2 * i], o1 = off[2 * i + 1], o2 = off[2 * i + 2];
+  const int64_t c0 = o1 - o0, c1 = o2 - o1;
+  if (c0 > CAP || c1 > CAP) {
+    nbr_means(i, hap, off, nbr, w, ws, wv);
+    return;
+  }
+  int32_t nb[2][CAP];
+  double wt[2][CAP];
+#pragma unroll
+  for (int t = 0; t < CAP; t++) {
+    nb[0][t] = t < c0 ? nbr[o0 + t] : 0;
+    wt[0][t] = t < c0 ? w[o0 + t] : 0.0;
+    nb[1][t] = t < c1 ? nbr[o1 + t] : 0;
+    wt[1][t] = t < c1 ? w[o1 + t] : 0.0;
+  }
+  double x[2][CAP];
+#pragma unroll
+  for (int t = 0; t < CAP; t++) {
+    x[0][t] = hap[nb[0][t]];
+    x[1][t] = hap[nb[1][t]];
+  }
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const int64_t c = h ? c1 : c0;
+    double s = 1e-9, v = 0.0;
+#pragma unroll
+    for (int t = 0; t < CAP; t++) {
+      if (t < c && x[h][t] == x[h][t]) {
+        s = s + wt[h][t];
+        v = v + wt[h][t] * x[h][t];
+      }
+    }
+    ws[h] = s;
+    wv[h] = v;
+  }
+}
 
 // One workgroup runs the whole phasing of one locus.  hap lives in LDS when
 // it fits (2n doubles), else in the global output buffer (same workgroup, so
@@ -103,7 +147,7 @@ __global__ __launch_bounds__(PT) void k_phase(int64_t n, const double *__restric
           i = order[e];
           if (hap[2 * i] == hap[2 * i]) {
             double ws[2], wv[2];
-            nbr_means(i, hap, off, nbr, w, ws, wv);
+            nbr_means_fast(i, hap, off, nbr, w, ws, wv);
             double m0 = wv[0] / ws[0];
             double m1 = wv[1] / ws[1];
             double den = m0 + m1;

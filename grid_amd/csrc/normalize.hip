@@ -17,7 +17,7 @@ constexpr int LEAF = 128;
 constexpr int LEAF_PAD = 136;         // LDS row stride (ints) per leaf: conflict-free chains
 
 __device__ __forceinline__ double qval(int32_t q) {
-  return q == GRID_MISSING ? 0.0 : (double)q / 100.0;
+  return q == GRID_MISSING ? 0.0 : div100_exact(q);
 }
 
 // ---- full 8192-element blocks: one 256-thread workgroup per (row, block) ----
@@ -178,124 +178,235 @@ __global__ void k_row_means(const double *__restrict__ bsum, const int32_t *__re
   rm[row] = acc / (double)c;
 }
 
-// y = (q/100) / rm_safe ; rm_safe = NaN where rm == 0 (normalize_mosdepth.py:441)
-__device__ __forceinline__ bool yval(int32_t qv, double rm, double &y) {
+// y = (q/100) / rm_safe ; rm_safe = NaN where rm == 0 (normalize_mosdepth.py:441).
+// rinv[i] = 1/rm[i] (IEEE) makes each division an exact FMA correction.
+__device__ __forceinline__ bool yval(int32_t qv, double rm, double ri, double &y) {
   if (qv == GRID_MISSING || rm == 0.0 || !(rm == rm)) return false;
-  y = ((double)qv / 100.0) / rm;
+  y = div_exact(div100_exact(qv), rm, ri);
   return true;
+}
+
+__global__ void k_recip(const double *__restrict__ v, int64_t n, double *__restrict__ r) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) r[i] = 1.0 / v[i];
 }
 
 constexpr int CU = 8;   // rows unrolled per iteration in the column kernels
 
+// VW adjacent columns per thread (int4 loads when VW == 4), sequential over rows.
+template <int VW>
+__device__ __forceinline__ void load_cols(const int32_t *p, int32_t (&v)[VW]) {
+  if constexpr (VW == 4) {
+    int4 t = *reinterpret_cast<const int4 *>(p);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  } else {
+#pragma unroll
+    for (int c = 0; c < VW; c++) v[c] = p[c];
+  }
+}
+
+template <int VW>
 __global__ __launch_bounds__(256) void k_col_means(const int32_t *__restrict__ q, int64_t n, int64_t m,
                                                    int64_t ld, const double *__restrict__ rm,
-                                                   double *__restrict__ mu) {
-  int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= m) return;
-  const int32_t *col = q + j;
-  double acc = 0.0;
-  int64_t c = 0;
+                                                   const double *__restrict__ rinv, double *__restrict__ mu) {
+  const int64_t j0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * VW;
+  if (j0 >= m) return;
+  if (VW > 1 && j0 + VW > m) {   // ragged tail: scalar path
+    for (int64_t j = j0; j < m; j++) {
+      double acc = 0.0;
+      int64_t c = 0;
+      for (int64_t i = 0; i < n; i++) {
+        double y;
+        if (yval(q[i * ld + j], rm[i], rinv[i], y)) { acc = acc + y; c++; }
+      }
+      mu[j] = acc / (double)c;
+    }
+    return;
+  }
+  double acc[VW];
+  int64_t cnt[VW];
+#pragma unroll
+  for (int c = 0; c < VW; c++) { acc[c] = 0.0; cnt[c] = 0; }
+  const int32_t *col = q + j0;
   int64_t i = 0;
   for (; i + CU <= n; i += CU) {
-    int32_t v[CU];
+    int32_t v[CU][VW];
 #pragma unroll
-    for (int u = 0; u < CU; u++) v[u] = col[(i + u) * ld];
+    for (int u = 0; u < CU; u++) load_cols<VW>(col + (i + u) * ld, v[u]);
 #pragma unroll
     for (int u = 0; u < CU; u++) {
-      double y;
-      if (yval(v[u], rm[i + u], y)) { acc = acc + y; c++; }
+      const double r = rm[i + u], ri = rinv[i + u];
+#pragma unroll
+      for (int c = 0; c < VW; c++) {
+        double y;
+        if (yval(v[u][c], r, ri, y)) { acc[c] = acc[c] + y; cnt[c]++; }
+      }
     }
   }
   for (; i < n; i++) {
-    double y;
-    if (yval(col[i * ld], rm[i], y)) { acc = acc + y; c++; }
+    int32_t v[VW];
+    load_cols<VW>(col + i * ld, v);
+#pragma unroll
+    for (int c = 0; c < VW; c++) {
+      double y;
+      if (yval(v[c], rm[i], rinv[i], y)) { acc[c] = acc[c] + y; cnt[c]++; }
+    }
   }
-  mu[j] = acc / (double)c;       // 0/0 -> NaN for an all-NaN column (numpy)
+#pragma unroll
+  for (int c = 0; c < VW; c++) mu[j0 + c] = acc[c] / (double)cnt[c];   // 0/0 -> NaN (numpy)
 }
 
+template <int VW>
 __global__ __launch_bounds__(256) void k_col_vars(const int32_t *__restrict__ q, int64_t n, int64_t m,
                                                   int64_t ld, const double *__restrict__ rm,
-                                                  const double *__restrict__ mu,
-                                                  double *__restrict__ var,
+                                                  const double *__restrict__ rinv,
+                                                  const double *__restrict__ mu, double *__restrict__ var,
                                                   double *__restrict__ ratio) {
-  int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= m) return;
-  const int32_t *col = q + j;
-  const double mj = mu[j];
-  double acc = 0.0;
+  const int64_t j0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * VW;
+  if (j0 >= m) return;
+  const double qnan = __builtin_nan("");
+  if (VW > 1 && j0 + VW > m) {
+    for (int64_t j = j0; j < m; j++) {
+      const double mj = mu[j];
+      double acc = 0.0;
+      for (int64_t i = 0; i < n; i++) {
+        double y;
+        if (yval(q[i * ld + j], rm[i], rinv[i], y)) {
+          double d = y - mj, dd = d * d;
+          if (dd == dd) acc = acc + dd;
+        }
+      }
+      double vv = acc / (double)(n - 1);
+      var[j] = vv;
+      ratio[j] = (mj > 0.0) ? (100.0 * vv) / mj : qnan;
+    }
+    return;
+  }
+  double acc[VW], mj[VW];
+#pragma unroll
+  for (int c = 0; c < VW; c++) { acc[c] = 0.0; mj[c] = mu[j0 + c]; }
+  const int32_t *col = q + j0;
   int64_t i = 0;
   for (; i + CU <= n; i += CU) {
-    int32_t v[CU];
+    int32_t v[CU][VW];
 #pragma unroll
-    for (int u = 0; u < CU; u++) v[u] = col[(i + u) * ld];
+    for (int u = 0; u < CU; u++) load_cols<VW>(col + (i + u) * ld, v[u]);
 #pragma unroll
     for (int u = 0; u < CU; u++) {
-      double y;
-      if (yval(v[u], rm[i + u], y)) {
-        double d = y - mj;
-        double dd = d * d;
-        if (dd == dd) acc = acc + dd;      // nansum: NaN (mu NaN) -> 0
+      const double r = rm[i + u], ri = rinv[i + u];
+#pragma unroll
+      for (int c = 0; c < VW; c++) {
+        double y;
+        if (yval(v[u][c], r, ri, y)) {
+          double d = y - mj[c], dd = d * d;
+          if (dd == dd) acc[c] = acc[c] + dd;      // nansum: NaN (mu NaN) -> 0
+        }
       }
     }
   }
   for (; i < n; i++) {
-    double y;
-    if (yval(col[i * ld], rm[i], y)) {
-      double d = y - mj;
-      double dd = d * d;
-      if (dd == dd) acc = acc + dd;
+    int32_t v[VW];
+    load_cols<VW>(col + i * ld, v);
+#pragma unroll
+    for (int c = 0; c < VW; c++) {
+      double y;
+      if (yval(v[c], rm[i], rinv[i], y)) {
+        double d = y - mj[c], dd = d * d;
+        if (dd == dd) acc[c] = acc[c] + dd;
+      }
     }
   }
-  double vv = acc / (double)(n - 1);
-  var[j] = vv;
-  ratio[j] = (mj > 0.0) ? (100.0 * vv) / mj : __builtin_nan("");
+#pragma unroll
+  for (int c = 0; c < VW; c++) {
+    double vv = acc[c] / (double)(n - 1);
+    var[j0 + c] = vv;
+    ratio[j0 + c] = (mj[c] > 0.0) ? (100.0 * vv) / mj[c] : qnan;
+  }
 }
 
-__global__ __launch_bounds__(256) void k_zquant(const int32_t *__restrict__ q, int64_t n, int64_t ld,
-                                                const int32_t *__restrict__ sel, int64_t r,
-                                                const double *__restrict__ rm,
-                                                const double *__restrict__ mu, double scale,
-                                                int32_t *__restrict__ zq, int64_t ld_zq,
-                                                const int32_t *__restrict__ colmap, int32_t qmax,
-                                                uint16_t *__restrict__ zb, int64_t ld_zb,
-                                                int32_t *__restrict__ overflow) {
+// Per selected column s: j = sel[s], mu_j, sqrt(mu_j), 1/sqrt(mu_j).
+__global__ void k_zprep(const int32_t *__restrict__ sel, int64_t r, const double *__restrict__ mu,
+                        double *__restrict__ mus, double *__restrict__ sq, double *__restrict__ rsq) {
   int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  int64_t i = blockIdx.y;
   if (s >= r) return;
-  int32_t j = sel[s];
-  int32_t qv = q[i * ld + j];
-  double rmi = rm[i];
-  int32_t out;
-  double y;
-  if (!yval(qv, rmi, y)) {
-    out = GRID_ZQ_NAN;
-  } else {
-    double mj = mu[j];
-    double z = ((y - mj) / sqrt(mj)) * scale;
-    if (!(z == z)) {
-      out = GRID_ZQ_NAN;
-    } else {
-      double k = round_dec_k(z, 100.0);
-      if (fabs(k) >= 2147483000.0) {
-        atomicOr(overflow, 1);
-        k = 0.0;
+  double m = mu[sel[s]];
+  double t = sqrt(m);
+  mus[s] = m;
+  sq[s] = t;
+  rsq[s] = 1.0 / t;
+}
+
+constexpr int ZR = 8;    // rows per zquant block
+
+// 4 consecutive selected columns x ZR rows per thread.
+__global__ __launch_bounds__(256) void k_zquant4(const int32_t *__restrict__ q, int64_t n, int64_t ld,
+                                                 const int32_t *__restrict__ sel, int64_t r,
+                                                 const double *__restrict__ rm, const double *__restrict__ rinv,
+                                                 const double *__restrict__ mus, const double *__restrict__ sq,
+                                                 const double *__restrict__ rsq, double scale,
+                                                 int32_t *__restrict__ zq, int64_t ld_zq,
+                                                 const int32_t *__restrict__ colmap, int32_t qmax,
+                                                 uint16_t *__restrict__ zb, int64_t ld_zb,
+                                                 int32_t *__restrict__ overflow) {
+  const int64_t s0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const int64_t i0 = (int64_t)blockIdx.y * ZR;
+  if (s0 >= r) return;
+  const int w = (int)((r - s0) < 4 ? (r - s0) : 4);
+  int32_t js[4], cm[4];
+  double m_[4], sq_[4], rs_[4];
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const bool ok = c < w;
+    js[c] = ok ? sel[s0 + c] : 0;
+    cm[c] = (ok && colmap) ? colmap[s0 + c] : (ok ? (int32_t)(s0 + c) : -1);
+    m_[c] = ok ? mus[s0 + c] : 1.0;
+    sq_[c] = ok ? sq[s0 + c] : 1.0;
+    rs_[c] = ok ? rsq[s0 + c] : 1.0;
+  }
+  const bool vec_zq = zq && w == 4 && ((ld_zq & 3) == 0) && ((s0 & 3) == 0);
+  int of = 0;
+  const int64_t i1 = (i0 + ZR < n) ? i0 + ZR : n;
+  for (int64_t i = i0; i < i1; i++) {
+    const int32_t *row = q + i * ld;
+    const double rmi = rm[i], rii = rinv[i];
+    int32_t out[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      out[c] = GRID_ZQ_NAN;
+      if (c < w) {
+        double y;
+        if (yval(row[js[c]], rmi, rii, y)) {
+          double z = div_exact(y - m_[c], sq_[c], rs_[c]) * scale;
+          if (z == z) {
+            double k = round_dec_k(z, 100.0);
+            if (fabs(k) >= 2147483000.0) { of = 1; k = 0.0; }
+            out[c] = (int32_t)k;
+            if (out[c] == 0 && signbit(z)) out[c] = GRID_ZQ_NEG0;
+          }
+        }
       }
-      out = (int32_t)k;
-      if (out == 0 && signbit(z)) out = GRID_ZQ_NEG0;
+    }
+    if (zq) {
+      if (vec_zq) {
+        *reinterpret_cast<int4 *>(zq + i * ld_zq + s0) = make_int4(out[0], out[1], out[2], out[3]);
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+          if (c < w) zq[i * ld_zq + s0 + c] = out[c];
+      }
+    }
+    if (zb) {
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        if (cm[c] >= 0) {
+          int32_t v = (out[c] == GRID_ZQ_NAN || out[c] == GRID_ZQ_NEG0) ? 0 : out[c];
+          v = v > qmax ? qmax : (v < -qmax ? -qmax : v);
+          zb[i * ld_zb + cm[c]] = (uint16_t)(__float_as_uint((float)v) >> 16);
+        }
+      }
     }
   }
-  if (zq) zq[i * ld_zq + s] = out;
-  if (zb) {
-    int32_t c = colmap ? colmap[s] : (int32_t)s;
-    if (c >= 0) {
-      int32_t v = (out == GRID_ZQ_NAN || out == GRID_ZQ_NEG0) ? 0 : out;
-      v = v > qmax ? qmax : (v < -qmax ? -qmax : v);
-      // exact bf16 of a small integer (|v| <= 256): float bits >> 16
-      float f = (float)v;
-      uint32_t bits = __float_as_uint(f);
-      zb[i * ld_zb + c] = (uint16_t)(bits >> 16);
-    }
-  }
+  if (of) atomicOr(overflow, 1);
 }
 
 // Full fp64 z matrix (normalize_matrix's returned array, :458 and :470):
@@ -364,12 +475,36 @@ int grid_norm_row_means(grid_ctx *ctx, const double *d_bsum, const int32_t *d_bc
   return GRID_OK;
 }
 
+static int recip_rows(grid_ctx *ctx, const double *d_rm, int64_t n, size_t extra, double **rinv, char **rest) {
+  void *s = nullptr;
+  size_t nb = (((size_t)n * 8 + 255) & ~size_t(255));
+  int rc = grid_scratch(ctx, 256 + nb + extra, &s);
+  if (rc) return rc;
+  *rinv = (double *)((char *)s + 256);
+  *rest = (char *)s + 256 + nb;
+  if (n > 0) {
+    hipLaunchKernelGGL(k_recip, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, ctx->stream, d_rm, n, *rinv);
+    LAUNCHCHK();
+  }
+  return GRID_OK;
+}
+
+static bool vec4_ok(const void *p, int64_t ld) { return ((uintptr_t)p % 16) == 0 && ld % 4 == 0; }
+
 int grid_norm_col_means(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t m, int64_t ld,
                         const double *d_rm, double *d_mu) {
   REQUIRE(ctx && n >= 0 && m >= 0 && ld >= m, "bad args");
   if (m == 0) return GRID_OK;
-  hipLaunchKernelGGL(k_col_means, dim3((unsigned)ceil_div(m, 256)), dim3(256), 0, ctx->stream, d_q, n, m,
-                     ld, d_rm, d_mu);
+  double *rinv;
+  char *rest;
+  int rc = recip_rows(ctx, d_rm, n, 0, &rinv, &rest);
+  if (rc) return rc;
+  if (vec4_ok(d_q, ld))
+    hipLaunchKernelGGL(k_col_means<4>, dim3((unsigned)ceil_div(ceil_div(m, 4), 256)), dim3(256), 0, ctx->stream,
+                       d_q, n, m, ld, d_rm, rinv, d_mu);
+  else
+    hipLaunchKernelGGL(k_col_means<1>, dim3((unsigned)ceil_div(m, 256)), dim3(256), 0, ctx->stream, d_q, n, m,
+                       ld, d_rm, rinv, d_mu);
   LAUNCHCHK();
   return GRID_OK;
 }
@@ -378,8 +513,16 @@ int grid_norm_col_vars(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t m, 
                        const double *d_rm, const double *d_mu, double *d_var, double *d_ratio) {
   REQUIRE(ctx && n >= 0 && m >= 0 && ld >= m, "bad args");
   if (m == 0) return GRID_OK;
-  hipLaunchKernelGGL(k_col_vars, dim3((unsigned)ceil_div(m, 256)), dim3(256), 0, ctx->stream, d_q, n, m,
-                     ld, d_rm, d_mu, d_var, d_ratio);
+  double *rinv;
+  char *rest;
+  int rc = recip_rows(ctx, d_rm, n, 0, &rinv, &rest);
+  if (rc) return rc;
+  if (vec4_ok(d_q, ld))
+    hipLaunchKernelGGL(k_col_vars<4>, dim3((unsigned)ceil_div(ceil_div(m, 4), 256)), dim3(256), 0, ctx->stream,
+                       d_q, n, m, ld, d_rm, rinv, d_mu, d_var, d_ratio);
+  else
+    hipLaunchKernelGGL(k_col_vars<1>, dim3((unsigned)ceil_div(m, 256)), dim3(256), 0, ctx->stream, d_q, n, m,
+                       ld, d_rm, rinv, d_mu, d_var, d_ratio);
   LAUNCHCHK();
   return GRID_OK;
 }
@@ -390,19 +533,25 @@ int grid_norm_zquant(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t ld, c
                      int64_t ld_zb, int32_t *h_overflow) {
   REQUIRE(ctx && n >= 0 && r >= 0, "bad args");
   REQUIRE(qmax >= 0 && qmax <= 256, "qmax %d outside the exact-bf16 range [0, 256]", qmax);
-  REQUIRE(n <= 65535, "n > 65535 rows per launch");
   if (n == 0 || r == 0) {
     if (h_overflow) *h_overflow = 0;
     return GRID_OK;
   }
-  int32_t *d_of = nullptr;
-  void *s = nullptr;
-  int rc = grid_scratch(ctx, 256, &s);
+  REQUIRE(ceil_div(n, ZR) <= 65535, "n too large for one launch");
+  double *rinv;
+  char *rest;
+  size_t rb = (((size_t)r * 8 + 255) & ~size_t(255));
+  int rc = recip_rows(ctx, d_rm, n, 3 * rb, &rinv, &rest);
   if (rc) return rc;
-  d_of = (int32_t *)s;
+  double *mus = (double *)rest, *sq = (double *)(rest + rb), *rsq = (double *)(rest + 2 * rb);
+  int32_t *d_of = (int32_t *)ctx->scratch;
   HIPCHK(hipMemsetAsync(d_of, 0, 4, ctx->stream));
-  hipLaunchKernelGGL(k_zquant, dim3((unsigned)ceil_div(r, 256), (unsigned)n), dim3(256), 0, ctx->stream,
-                     d_q, n, ld, d_sel, r, d_rm, d_mu, scale, d_zq, ld_zq, d_colmap, qmax, d_zb, ld_zb, d_of);
+  hipLaunchKernelGGL(k_zprep, dim3((unsigned)ceil_div(r, 256)), dim3(256), 0, ctx->stream, d_sel, r, d_mu, mus, sq,
+                     rsq);
+  LAUNCHCHK();
+  hipLaunchKernelGGL(k_zquant4, dim3((unsigned)ceil_div(ceil_div(r, 4), 256), (unsigned)ceil_div(n, ZR)), dim3(256), 0,
+                     ctx->stream, d_q, n, ld, d_sel, r, d_rm, rinv, mus, sq, rsq, scale, d_zq, ld_zq, d_colmap, qmax,
+                     d_zb, ld_zb, d_of);
   LAUNCHCHK();
   if (h_overflow) {
     HIPCHK(hipMemcpyAsync(ctx->pinned, d_of, 4, hipMemcpyDeviceToHost, ctx->stream));
