@@ -136,7 +136,7 @@ def main():
         comm = TorchComm(dist)
 
     from grid_amd import _abi
-    from grid_amd.fused import Steps47, TorchAlloc, shard_range
+    from grid_amd.fused import HipOps, Steps47, TorchAlloc, shard_range
 
     dev = _abi.Device(local)
     dev.set_stream(torch.cuda.current_stream())
@@ -146,7 +146,7 @@ def main():
     q = torch.empty((n, max(ml, 1)), dtype=torch.int32, device="cuda")
     _abi.call("grid_synth_depth", dev.ctx, SEED, n, ml, ml, c0, NCL, q.data_ptr())
     reads, off, nbr, w = synth_reads_and_ibs(n)
-    st = Steps47(dev, TorchAlloc(local), n, m, c0, ml, k=args.k, n_nbr=300, top_frac=0.1, zmax=2.0,
+    st = Steps47(HipOps(dev), TorchAlloc(local), n, m, c0, ml, k=args.k, n_nbr=300, top_frac=0.1, zmax=2.0,
                  sigma2_max=1000.0, frac_r=1.0, min_nbr=1, n_iters=args.n_iters, comm=comm)
     st.set_reads(reads)
     st.set_phasing_graph(off, nbr, w)

@@ -100,10 +100,41 @@ __device__ __forceinline__ void nbr_means_fast(int64_t i, const double *hap, con
   }
 }
 
+struct PhItem {
+  int64_t i;
+  int64_t c0, c1;
+  int32_t nb[2][CAP];
+  double wt[2][CAP];
+};
+
+// Fetch the schedule item e (sample order[e] and its neighbour lists) into
+// registers; lists longer than CAP are read later by the loop fallback.
+__device__ __forceinline__ void ph_fetch(int e, int e1, const int32_t *__restrict__ order,
+                                         const int64_t *__restrict__ off, const int32_t *__restrict__ nbr,
+                                         const double *__restrict__ w, PhItem &it) {
+  it.i = -1;
+  if (e >= e1) return;
+  const int64_t i = order[e];
+  const int64_t o0 = off[2 * i], o1 = off[2 * i + 1], o2 = off[2 * i + 2];
+  it.i = i;
+  it.c0 = o1 - o0;
+  it.c1 = o2 - o1;
+  if (it.c0 > CAP || it.c1 > CAP) return;
+#pragma unroll
+  for (int t = 0; t < CAP; t++) {
+    it.nb[0][t] = t < it.c0 ? nbr[o0 + t] : 0;
+    it.wt[0][t] = t < it.c0 ? w[o0 + t] : 0.0;
+    it.nb[1][t] = t < it.c1 ? nbr[o1 + t] : 0;
+    it.wt[1][t] = t < it.c1 ? w[o1 + t] : 0.0;
+  }
+}
+
 // One workgroup runs the whole phasing of one locus.  hap lives in LDS when
 // it fits (2n doubles), else in the global output buffer (same workgroup, so
-// __syncthreads orders it).  Iterations run the precomputed level schedule:
-// within a level every sample reads first, then all write.
+// __syncthreads orders it).  Iterations run the precomputed level schedule,
+// flattened into chunks of PT samples: within a chunk every sample reads, then
+// all write.  The next chunk's neighbour lists are prefetched into registers
+// while the current chunk computes, so a chunk costs ~LDS latency + barriers.
 template <bool USE_LDS>
 __global__ __launch_bounds__(PT) void k_phase(int64_t n, const double *__restrict__ irr,
                                               const int64_t *__restrict__ off,
@@ -135,36 +166,71 @@ __global__ __launch_bounds__(PT) void k_phase(int64_t n, const double *__restric
     s_mean = m;
   }
   __syncthreads();
-  for (int64_t it = 0; it < iters; it++) {
-    for (int l = 0; l < nlev; l++) {
-      const int e0 = loff[l], e1 = loff[l + 1];
-      for (int base = e0; base < e1; base += PT) {
-        const int e = base + tid;
-        bool upd = false;
-        int64_t i = 0;
-        double n0 = 0.0, n1 = 0.0;
-        if (e < e1) {
-          i = order[e];
-          if (hap[2 * i] == hap[2 * i]) {
-            double ws[2], wv[2];
-            nbr_means_fast(i, hap, off, nbr, w, ws, wv);
-            double m0 = wv[0] / ws[0];
-            double m1 = wv[1] / ws[1];
-            double den = m0 + m1;
-            if (den > 0.0) {
-              n0 = irr[i] * m0 / den;
-              n1 = irr[i] * m1 / den;
-              upd = true;
+  if (iters > 0 && nlev > 0) {
+    // chunk cursor: (level l, base) ; advance = next PT samples of the level, else next level (wrapping)
+    int l = 0, base = loff[0];
+    while (base >= loff[l + 1] && l + 1 < nlev) { l++; base = loff[l]; }
+    PhItem cur, nxt;
+    ph_fetch(base + tid, loff[l + 1], order, off, nbr, w, cur);
+    int64_t it = 0;
+    while (it < iters) {
+      // next chunk position
+      int nl = l, nb = base + PT;
+      int64_t nit = it;
+      if (nb >= loff[nl + 1]) {
+        do {
+          nl++;
+          if (nl == nlev) { nl = 0; nit++; }
+          nb = loff[nl];
+        } while (nb >= loff[nl + 1]);
+      }
+      if (nit < iters) ph_fetch(nb + tid, loff[nl + 1], order, off, nbr, w, nxt);
+      // compute the current chunk
+      bool upd = false;
+      double n0 = 0.0, n1 = 0.0;
+      const int64_t i = cur.i;
+      if (i >= 0 && hap[2 * i] == hap[2 * i]) {
+        double ws[2], wv[2];
+        if (cur.c0 > CAP || cur.c1 > CAP) {
+          nbr_means(i, hap, off, nbr, w, ws, wv);
+        } else {
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            const int64_t c = h ? cur.c1 : cur.c0;
+            double x[CAP];
+#pragma unroll
+            for (int t = 0; t < CAP; t++) x[t] = hap[cur.nb[h][t]];
+            double sw = 1e-9, sv = 0.0;
+#pragma unroll
+            for (int t = 0; t < CAP; t++) {
+              if (t < c && x[t] == x[t]) {
+                sw = sw + cur.wt[h][t];
+                sv = sv + cur.wt[h][t] * x[t];
+              }
             }
+            ws[h] = sw;
+            wv[h] = sv;
           }
         }
-        __syncthreads();
-        if (upd) {
-          hap[2 * i] = n0;
-          hap[2 * i + 1] = n1;
+        double m0 = wv[0] / ws[0];
+        double m1 = wv[1] / ws[1];
+        double den = m0 + m1;
+        if (den > 0.0) {
+          n0 = irr[i] * m0 / den;
+          n1 = irr[i] * m1 / den;
+          upd = true;
         }
-        __syncthreads();
       }
+      __syncthreads();
+      if (upd) {
+        hap[2 * i] = n0;
+        hap[2 * i + 1] = n1;
+      }
+      __syncthreads();
+      l = nl;
+      base = nb;
+      it = nit;
+      cur = nxt;
     }
   }
   const double mean = s_mean;

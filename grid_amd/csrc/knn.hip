@@ -14,6 +14,8 @@
 // (d2, j).  That equals sklearn's order wherever exact distances differ.
 #include "common.hpp"
 
+#include <cstdlib>
+
 namespace {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
@@ -161,6 +163,264 @@ __global__ __launch_bounds__(NT, 2) void k_gram(const uint16_t *__restrict__ z, 
       }
 }
 
+// Variant 2: LDS-DMA staging (global_load_lds_dwordx4, 1 KiB per wave
+// instruction written lane-linearly).  The XOR swizzle moves to the per-lane
+// SOURCE address: lane L of an 8-row piece loads chunk (L&7)^((row>>1)&7) of
+// row r0+L/8, so the lane-linear LDS image equals lds_off() layout.
+typedef __attribute__((address_space(1))) const void *gptr_t;
+typedef __attribute__((address_space(3))) void *lptr_t;
+
+__global__ __launch_bounds__(NT, 2) void k_gram_dma(const uint16_t *__restrict__ z, int64_t ld, int nt,
+                                                    int ntiles, int64_t nsteps, int sps, int fs,
+                                                    int64_t np_, unsigned long long *__restrict__ gram) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_BYTES];
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, loc = bid >> 3;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const int slice = wid / ntiles;
+  int t = wid - slice * ntiles;
+  int ti = 0;
+  while (t >= nt - ti) { t -= nt - ti; ti++; }
+  const int tj = ti + t;
+  const int64_t s0 = (int64_t)slice * sps;
+  int64_t s1 = s0 + sps;
+  if (s1 > nsteps) s1 = nsteps;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+
+  // this lane's source rows/chunks for its wave's 4 pieces (rows wave*32 + u*8 + lane/8)
+  const int prow = wave * 32 + (lane >> 3);          // + u*8
+  const uint16_t *za = z + (int64_t)ti * BM * ld;
+  const uint16_t *zb = z + (int64_t)tj * BM * ld;
+  int64_t srcoff[4];
+#pragma unroll
+  for (int u = 0; u < 4; u++) {
+    const int row = prow + u * 8;
+    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    srcoff[u] = (int64_t)row * ld + c * 8;
+  }
+
+  f32x16 acc[2][2];
+  int32_t iacc[2][2][16];
+#pragma unroll
+  for (int a = 0; a < 2; a++)
+#pragma unroll
+    for (int b = 0; b < 2; b++)
+#pragma unroll
+      for (int r = 0; r < 16; r++) { acc[a][b][r] = 0.0f; iacc[a][b][r] = 0; }
+
+#define GRAM_DMA(step, b)                                                                       \
+  do {                                                                                          \
+    char *A_ = smem + (b) * 2 * TILE_BYTES;                                                     \
+    char *B_ = A_ + TILE_BYTES;                                                                 \
+    const int64_t k_ = (step) * BK;                                                             \
+    _Pragma("unroll") for (int u = 0; u < 4; u++) {                                             \
+      __builtin_amdgcn_global_load_lds((gptr_t)(za + srcoff[u] + k_),                           \
+                                       (lptr_t)(A_ + (wave * 32 + u * 8) * 128), 16, 0, 0);      \
+      __builtin_amdgcn_global_load_lds((gptr_t)(zb + srcoff[u] + k_),                           \
+                                       (lptr_t)(B_ + (wave * 32 + u * 8) * 128), 16, 0, 0);      \
+    }                                                                                           \
+  } while (0)
+
+  // one K-step of MFMAs on LDS buffer `b_`; ZERO_ starts a new fp32 chunk by
+  // feeding a zero accumulator to the first MFMA (no separate clearing pass)
+#define GRAM_COMPUTE(b_, ZERO_)                                                                \
+  do {                                                                                         \
+    const char *A = smem + (b_) * 2 * TILE_BYTES;                                              \
+    const char *B = A + TILE_BYTES;                                                            \
+    _Pragma("unroll") for (int s = 0; s < 4; s++) {                                            \
+      const int ch = 2 * s + (lane >> 5);                                                      \
+      bf16x8 fa[2], fb[2];                                                                     \
+      _Pragma("unroll") for (int m = 0; m < 2; m++) {                                          \
+        fa[m] = as_bf16x8(*reinterpret_cast<const uint4 *>(A + lds_off(wr * 64 + m * 32 + (lane & 31), ch))); \
+        fb[m] = as_bf16x8(*reinterpret_cast<const uint4 *>(B + lds_off(wc * 64 + m * 32 + (lane & 31), ch))); \
+      }                                                                                        \
+      _Pragma("unroll") for (int m = 0; m < 2; m++)                                            \
+        _Pragma("unroll") for (int nn = 0; nn < 2; nn++)                                       \
+          acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[m], fb[nn],                  \
+                                                               (ZERO_ && s == 0) ? zero16 : acc[m][nn], 0, 0, 0); \
+    }                                                                                          \
+  } while (0)
+
+  const f32x16 zero16 = {};
+  if (s0 < s1) GRAM_DMA(s0, 0);
+  __syncthreads();
+  int buf = 0;
+  for (int64_t cs = s0; cs < s1; cs += fs) {
+    const int64_t ce = (cs + fs < s1) ? cs + fs : s1;
+    // first step of the chunk: fresh fp32 partials
+    if (cs + 1 < s1) GRAM_DMA(cs + 1, buf ^ 1);
+    GRAM_COMPUTE(buf, true);
+    __syncthreads();
+    buf ^= 1;
+    for (int64_t st = cs + 1; st < ce; st++) {
+      if (st + 1 < s1) GRAM_DMA(st + 1, buf ^ 1);
+      GRAM_COMPUTE(buf, false);
+      __syncthreads();     // drains this wave's DMA (vmcnt) and orders all reads of buf
+      buf ^= 1;
+    }
+    // flush: exact fp32 partials (< 2^24) into int32
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+      for (int b = 0; b < 2; b++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) iacc[a][b][r] += (int32_t)acc[a][b][r];
+  }
+#undef GRAM_COMPUTE
+#undef GRAM_DMA
+#pragma unroll
+  for (int a = 0; a < 2; a++)
+#pragma unroll
+    for (int b = 0; b < 2; b++)
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        int row = ti * BM + wr * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        int col = tj * BM + wc * 64 + b * 32 + (lane & 31);
+        int32_t v = iacc[a][b][r];
+        if (v != 0) atomicAdd(gram + (int64_t)row * np_ + col, (unsigned long long)(long long)v);
+      }
+}
+
+// Variant 3: one 256-thread workgroup per CU (1 wave per SIMD, up to 512
+// VGPRs), 256x128 output tile (4 waves x 128x64 = 4x2 MFMA 32x32 blocks),
+// 3-slot LDS-DMA ring (48 KiB per slot) with two K-steps in flight: counted
+// `s_waitcnt vmcnt(12)` + raw s_barrier, so the DMA stream never drains in the
+// main loop.  Tiles (I, j): rows [256I, 256I+256) x cols [128j, 128j+128) with
+// j >= 2I (the upper triangle at 128-granularity; the strictly-lower half of
+// the diagonal tiles is computed and ignored).
+constexpr int BM3 = 256, BN3 = 128;
+constexpr int SLOT3 = (BM3 + BN3) * BK * 2;     // 48 KiB
+constexpr int DMA3 = (BM3 + BN3) / 8 / 4;       // 1-KiB DMA instructions per wave per K-step (12)
+
+__device__ __forceinline__ uint4 lds_read_b128(uint32_t addr) {
+  uint4 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+
+__global__ __launch_bounds__(NT, 1) void k_gram3(const uint16_t *__restrict__ z, int64_t ld, int nt, int ni,
+                                                 int ntiles, int64_t nsteps, int sps, int fs, int64_t np_,
+                                                 unsigned long long *__restrict__ gram) {
+  __shared__ __attribute__((aligned(16))) char smem[3 * SLOT3];
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, loc = bid >> 3;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const int slice = wid / ntiles;
+  int t = wid - slice * ntiles;
+  int I = 0;
+  while (t >= nt - 2 * I) { t -= nt - 2 * I; I++; }
+  const int tj = 2 * I + t;
+  const int64_t s0 = (int64_t)slice * sps;
+  int64_t s1 = s0 + sps;
+  if (s1 > nsteps) s1 = nsteps;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const uint16_t *za = z + (int64_t)I * BM3 * ld;
+  const uint16_t *zb = z + (int64_t)tj * BN3 * ld;
+  const int rl = lane >> 3;
+  const int64_t abase = (int64_t)(wave * 64 + rl) * ld, bbase = (int64_t)(wave * 32 + rl) * ld;
+  const int64_t ld8 = 8 * ld;
+  const int cx = lane & 7;
+  // swizzle term (row>>1)&7 for rows wave*64 + u*8 + rl is ((u*4 + (wave*64+rl)/2) & 7) -> depends on u only via u*4&7
+  const int sa = ((wave * 64 + rl) >> 1) & 7, sb = ((wave * 32 + rl) >> 1) & 7;
+  // LDS byte addresses of this lane's fragment rows (chunk 0); chunk c adds ((c ^ swz) << 4) - swz already
+  // folded: lds_off(row, c) = row*128 + ((c ^ ((row>>1)&7)) << 4)
+  const uint32_t sbase = (uint32_t)(uintptr_t)smem;
+  int rowa[4], rowb[2];
+#pragma unroll
+  for (int m = 0; m < 4; m++) rowa[m] = wr * 128 + m * 32 + (lane & 31);
+#pragma unroll
+  for (int nn = 0; nn < 2; nn++) rowb[nn] = wc * 64 + nn * 32 + (lane & 31);
+
+  f32x16 acc[4][2];
+  int32_t iacc[4][2][16];
+#pragma unroll
+  for (int a = 0; a < 4; a++)
+#pragma unroll
+    for (int b = 0; b < 2; b++)
+#pragma unroll
+      for (int r = 0; r < 16; r++) { acc[a][b][r] = 0.0f; iacc[a][b][r] = 0; }
+
+  auto issue = [&](int64_t step, int slot) __attribute__((always_inline)) {
+    char *A_ = smem + slot * SLOT3;
+    const int64_t k_ = step * BK;
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+      __builtin_amdgcn_global_load_lds((gptr_t)(za + abase + u * ld8 + k_ + ((cx ^ ((sa + 4 * u) & 7)) * 8)),
+                                       (lptr_t)(A_ + (wave * 64 + u * 8) * 128), 16, 0, 0);
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+      __builtin_amdgcn_global_load_lds((gptr_t)(zb + bbase + u * ld8 + k_ + ((cx ^ ((sb + 4 * u) & 7)) * 8)),
+                                       (lptr_t)(A_ + BM3 * 128 + (wave * 32 + u * 8) * 128), 16, 0, 0);
+  };
+
+  if (s0 < s1) issue(s0, 0);
+  if (s0 + 1 < s1) {
+    issue(s0 + 1, 1);
+    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  int slot = 0, phase = 0;
+  for (int64_t st = s0; st < s1; st++) {
+    if (st + 2 < s1) issue(st + 2, slot == 0 ? 2 : slot - 1);
+    const uint32_t A = sbase + slot * SLOT3, B = A + BM3 * 128;
+#pragma unroll
+    for (int s = 0; s < 4; s++) {
+      const int ch = 2 * s + (lane >> 5);
+      uint4 fa[4], fb[2];
+#pragma unroll
+      for (int m = 0; m < 4; m++) fa[m] = lds_read_b128(A + lds_off(rowa[m], ch));
+#pragma unroll
+      for (int nn = 0; nn < 2; nn++) fb[nn] = lds_read_b128(B + lds_off(rowb[nn], ch));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int m = 0; m < 4; m++)
+#pragma unroll
+        for (int nn = 0; nn < 2; nn++)
+          acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(fa[m]), as_bf16x8(fb[nn]), acc[m][nn], 0, 0, 0);
+    }
+    if (++phase == fs || st + 1 == s1) {
+      phase = 0;
+#pragma unroll
+      for (int a = 0; a < 4; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++)
+#pragma unroll
+          for (int r = 0; r < 16; r++) {
+            iacc[a][b][r] += (int32_t)acc[a][b][r];
+            acc[a][b][r] = 0.0f;
+          }
+    }
+    if (st + 2 < s1) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    slot = slot == 2 ? 0 : slot + 1;
+  }
+#pragma unroll
+  for (int a = 0; a < 4; a++)
+#pragma unroll
+    for (int b = 0; b < 2; b++)
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        int row = I * BM3 + wr * 128 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        int col = tj * BN3 + wc * 64 + b * 32 + (lane & 31);
+        int32_t v = iacc[a][b][r];
+        if (v != 0) atomicAdd(gram + (int64_t)row * np_ + col, (unsigned long long)(long long)v);
+      }
+}
+
 constexpr int SELCAP = 4096;
 
 __device__ __forceinline__ int64_t gram_at(const int64_t *g, int64_t np_, int64_t i, int64_t j) {
@@ -291,8 +551,21 @@ int grid_knn_gram(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t kpad
   const int64_t nslices = ceil_div(nsteps, sps);
   const int64_t nwg = nslices * ntiles;
   REQUIRE(nwg < (1ll << 31), "too many work items");
-  hipLaunchKernelGGL(k_gram, dim3((unsigned)nwg), dim3(NT), 0, ctx->stream, d_zb, ld, nt, ntiles, nsteps,
-                     (int)sps, fs, np_, (unsigned long long *)d_gram);
+  const char *ve = getenv("GRID_GRAM_VARIANT");   // A/B switch for tools/bench_gram.py
+  const int variant = ve ? atoi(ve) : 2;
+  if (variant == 3 && np_ % BM3 == 0) {
+    const int ni = (int)(np_ / BM3);
+    int nt3 = 0;
+    for (int i = 0; i < ni; i++) nt3 += nt - 2 * i;
+    const int64_t nwg3 = nslices * nt3;
+    hipLaunchKernelGGL(k_gram3, dim3((unsigned)nwg3), dim3(NT), 0, ctx->stream, d_zb, ld, nt, ni, nt3, nsteps,
+                       (int)sps, fs, np_, (unsigned long long *)d_gram);
+  } else if (variant == 1)
+    hipLaunchKernelGGL(k_gram, dim3((unsigned)nwg), dim3(NT), 0, ctx->stream, d_zb, ld, nt, ntiles, nsteps,
+                       (int)sps, fs, np_, (unsigned long long *)d_gram);
+  else
+    hipLaunchKernelGGL(k_gram_dma, dim3((unsigned)nwg), dim3(NT), 0, ctx->stream, d_zb, ld, nt, ntiles, nsteps,
+                       (int)sps, fs, np_, (unsigned long long *)d_gram);
   LAUNCHCHK();
   return GRID_OK;
 }

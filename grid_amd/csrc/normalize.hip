@@ -364,10 +364,21 @@ __global__ __launch_bounds__(256) void k_zquant4(const int32_t *__restrict__ q, 
     rs_[c] = ok ? rsq[s0 + c] : 1.0;
   }
   const bool vec_zq = zq && w == 4 && ((ld_zq & 3) == 0) && ((s0 & 3) == 0);
+  const bool vec_zb = zb && w == 4 && cm[0] >= 0 && cm[1] == cm[0] + 1 && cm[2] == cm[0] + 2 &&
+                      cm[3] == cm[0] + 3 && ((cm[0] & 3) == 0) && ((ld_zb & 3) == 0);
   int of = 0;
   const int64_t i1 = (i0 + ZR < n) ? i0 + ZR : n;
-  for (int64_t i = i0; i < i1; i++) {
-    const int32_t *row = q + i * ld;
+  // all loads of the block's rows first (32 independent gathers in flight)
+  int32_t qv[ZR][4];
+#pragma unroll
+  for (int u = 0; u < ZR; u++)
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+      qv[u][c] = (i0 + u < i1 && c < w) ? q[(i0 + u) * ld + js[c]] : GRID_MISSING;
+#pragma unroll
+  for (int u = 0; u < ZR; u++) {
+    const int64_t i = i0 + u;
+    if (i >= i1) break;
     const double rmi = rm[i], rii = rinv[i];
     int32_t out[4];
 #pragma unroll
@@ -375,7 +386,7 @@ __global__ __launch_bounds__(256) void k_zquant4(const int32_t *__restrict__ q, 
       out[c] = GRID_ZQ_NAN;
       if (c < w) {
         double y;
-        if (yval(row[js[c]], rmi, rii, y)) {
+        if (yval(qv[u][c], rmi, rii, y)) {
           double z = div_exact(y - m_[c], sq_[c], rs_[c]) * scale;
           if (z == z) {
             double k = round_dec_k(z, 100.0);
@@ -396,13 +407,19 @@ __global__ __launch_bounds__(256) void k_zquant4(const int32_t *__restrict__ q, 
       }
     }
     if (zb) {
+      uint32_t bv[4];
 #pragma unroll
       for (int c = 0; c < 4; c++) {
-        if (cm[c] >= 0) {
-          int32_t v = (out[c] == GRID_ZQ_NAN || out[c] == GRID_ZQ_NEG0) ? 0 : out[c];
-          v = v > qmax ? qmax : (v < -qmax ? -qmax : v);
-          zb[i * ld_zb + cm[c]] = (uint16_t)(__float_as_uint((float)v) >> 16);
-        }
+        int32_t v = (out[c] == GRID_ZQ_NAN || out[c] == GRID_ZQ_NEG0) ? 0 : out[c];
+        v = v > qmax ? qmax : (v < -qmax ? -qmax : v);
+        bv[c] = __float_as_uint((float)v) >> 16;      // exact bf16 of |v| <= 256
+      }
+      if (vec_zb) {
+        *reinterpret_cast<uint2 *>(zb + i * ld_zb + cm[0]) = make_uint2(bv[0] | (bv[1] << 16), bv[2] | (bv[3] << 16));
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+          if (cm[c] >= 0) zb[i * ld_zb + cm[c]] = (uint16_t)bv[c];
       }
     }
   }

@@ -1,22 +1,27 @@
 """Device-resident chain of steps 4-7 with preallocated HBM buffers.
 
-This is the same arithmetic as the drop-in step modules, without the text
-files in between: the normalised matrix stays in HBM as exact hundredths
-(int32, the step-4 output) plus the clipped bf16 panel that step 5 reads,
-the neighbour lists feed the dipCN kernel directly, and the dipCN values
-feed phasing.  ``bench.py`` and ``__graft_entry__.smoke()`` drive it.
+Same arithmetic as the drop-in step modules, without the text files in
+between: the normalised matrix stays in HBM as exact hundredths (int32, the
+step-4 output) plus the clipped bf16 panel that step 5 reads, the neighbour
+lists feed the dipCN kernel directly, and the dipCN values feed phasing.
+``bench.py`` and ``__graft_entry__.smoke()`` drive it.
 
 Multi-GPU: the bin (column) axis is sharded in 8192-aligned ranges
-(``shard_range``).  Exactness across shards rests on three facts:
-  * row means: every rank computes 8192-block pairwise sums of its columns;
-    the blocks are all-gathered and every rank runs the same sequential chain
-    (padding blocks are exact zeros);
-  * column statistics need no communication (sequential over all rows
-    locally); medians/thresholds come from all-gathered ratio vectors;
+(``shard_range``), strong scaling of one cohort.  Exactness across shards:
+  * row means: each rank computes 8192-block pairwise sums of its columns;
+    blocks are all-gathered and every rank runs the same sequential chain
+    (padding blocks are exact zeros, and acc + 0.0 == acc);
+  * column statistics need no communication (sequential over all rows,
+    locally); the median and the selection threshold come from all-gathered
+    ratio vectors, sorted identically on every rank;
   * the Gram matrix is an integer sum over bins: per-rank partials are
-    combined with one all-reduce (int64 sum, order-free, exact).
-``comm`` is None for one GPU, else a torch.distributed wrapper
-(``TorchComm``).
+    combined with ONE all-reduce (int64 sum: order-free, exact);
+  * top-k by row blocks, then an all-gather of the neighbour lists; dipCN and
+    phasing are replicated (tiny / sequential per locus).
+
+The chain is written against an ``ops`` object.  The product always uses
+``HipOps`` (libgridhip.so kernels); tests substitute a CPU restatement to
+check the sharding logic under torch.distributed/gloo.
 """
 from __future__ import annotations
 
@@ -41,58 +46,31 @@ def shard_range(m: int, rank: int, world: int):
 
 
 class TorchAlloc:
-    """Device buffers as torch tensors (so torch.distributed can use them)."""
+    """Buffers as torch tensors (device "cuda:i", or "cpu" in tests)."""
 
-    def __init__(self, device_index: int):
+    def __init__(self, device):
         import torch
         self.torch = torch
-        self.device = torch.device("cuda", device_index)
+        self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
         self._dt = {np.dtype(F8): torch.float64, np.dtype(I4): torch.int32, np.dtype(I8): torch.int64,
                     np.dtype(U2): torch.int16, np.dtype(U1): torch.uint8}
 
     def empty(self, shape, dtype):
         return self.torch.empty(shape, dtype=self._dt[np.dtype(dtype)], device=self.device)
 
-    def zero_(self, t):
-        t.zero_()
-
-    @staticmethod
-    def numpy(t):
-        a = t.cpu().numpy()
-        return a.view(np.uint16) if a.dtype == np.int16 else a
+    def upload(self, arr):
+        arr = np.ascontiguousarray(arr)
+        src = self.torch.from_numpy(arr.view(np.int16) if arr.dtype == np.uint16 else arr)
+        return src.to(self.device).clone()
 
     @staticmethod
     def read(t, i):
         return t.view(-1)[i].item()
 
 
-class AbiAlloc:
-    """Device buffers from libgridhip (no torch)."""
-
-    def __init__(self, dev):
-        self.dev = dev
-
-    def empty(self, shape, dtype):
-        return self.dev.alloc(shape, dtype)
-
-    @staticmethod
-    def zero_(b):
-        b.zero()
-
-    @staticmethod
-    def numpy(b):
-        return b.numpy()
-
-    @staticmethod
-    def read(b, i):
-        out = np.empty(1, dtype=b.dtype)
-        call("grid_d2h", b.dev.ctx, out.ctypes.data, b.ptr + i * b.dtype.itemsize, b.dtype.itemsize)
-        return out[0].item()
-
-
 class TorchComm:
-    """The three collectives the sharded chain needs, over torch.distributed
-    (backend "nccl" = RCCL over xGMI on MI355X, "gloo" on CPU)."""
+    """The collectives the sharded chain needs, over torch.distributed
+    (backend "nccl" = RCCL over xGMI on MI355X; "gloo" in CPU tests)."""
 
     def __init__(self, dist):
         self.dist = dist
@@ -101,43 +79,107 @@ class TorchComm:
 
     def all_gather(self, t):
         import torch
-        out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
-        self.dist.all_gather_into_tensor(out, t.contiguous())
-        return out
+        t = t.contiguous()
+        parts = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(parts, t)
+        return torch.stack(parts)
 
     def all_reduce_sum(self, t):
         self.dist.all_reduce(t)
         return t
 
-    def all_reduce_min(self, t):
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
-        return t
+
+class HipOps:
+    """The chain's compute steps as libgridhip.so kernels (include/grid_abi.h)."""
+
+    def __init__(self, dev):
+        self.dev = dev
+        self.ctx = dev.ctx
+        self.zerodiv = C.c_int32()
+
+    def row_blocks(self, q, n, m, ld, bsum, bcnt):
+        call("grid_norm_row_blocks", self.ctx, ptr(q), n, m, ld, ptr(bsum), ptr(bcnt))
+
+    def row_means(self, bsum, bcnt, n, nblk, rm):
+        call("grid_norm_row_means", self.ctx, ptr(bsum), ptr(bcnt), n, nblk, ptr(rm))
+
+    def col_means(self, q, n, m, ld, rm, mu):
+        call("grid_norm_col_means", self.ctx, ptr(q), n, m, ld, ptr(rm), ptr(mu))
+
+    def col_vars(self, q, n, m, ld, rm, mu, var, ratio):
+        call("grid_norm_col_vars", self.ctx, ptr(q), n, m, ld, ptr(rm), ptr(mu), ptr(var), ptr(ratio))
+
+    def sort_valid(self, v, n, out):
+        nv = C.c_int64()
+        call("grid_sort_valid", self.ctx, ptr(v), n, ptr(out), C.byref(nv))
+        return nv.value
+
+    def select_gt(self, v, n, thr, idx):
+        c = C.c_int64()
+        call("grid_select_gt", self.ctx, ptr(v), n, thr, ptr(idx), C.byref(c))
+        return c.value
+
+    def gather(self, v, idx, n, out):
+        call("grid_gather_f64", self.ctx, ptr(v), ptr(idx), n, ptr(out))
+
+    def round_decimals(self, v, n, dec, out):
+        call("grid_round_decimals", self.ctx, ptr(v), n, dec, ptr(out))
+
+    def colmap_range(self, r, n, smin, smax, colmap):
+        c = C.c_int64()
+        call("grid_colmap_range", self.ctx, ptr(r), n, smin, smax, ptr(colmap), C.byref(c))
+        return c.value
+
+    def zquant(self, q, n, ld, sel, r, rm, mu, scale, zq, ld_zq, colmap, qmax, zb, ld_zb):
+        of = C.c_int32()
+        call("grid_norm_zquant", self.ctx, ptr(q), n, ld, ptr(sel), r, ptr(rm), ptr(mu), scale, ptr(zq), ld_zq,
+             ptr(colmap), qmax, ptr(zb), ld_zb, C.byref(of))
+        return of.value
+
+    def gram(self, zb, np_, kpad, ld, qmax, gram):
+        call("grid_knn_gram", self.ctx, ptr(zb), np_, kpad, ld, qmax, ptr(gram))
+
+    def topk(self, gram, n, np_, k, row0, nrows, idx, d2, cnt):
+        call("grid_knn_topk", self.ctx, ptr(gram), n, np_, k, row0, nrows, ptr(idx), ptr(d2), ptr(cnt))
+
+    def dipcn(self, n, reads, has, scale, nbr, nscale, ncnt, ld, n_nbr, out, valid):
+        call("grid_dipcn", self.ctx, n, ptr(reads), ptr(has), ptr(scale), ptr(nbr), ptr(nscale), ptr(ncnt), ld,
+             n_nbr, ptr(out), ptr(valid), C.byref(self.zerodiv))
+        return self.zerodiv.value
+
+    def phase(self, n, irr, off, nbr, w, min_nbr, iters, order, loff, nlev, hap, imp, mean):
+        call("grid_hi_phase", self.ctx, n, ptr(irr), ptr(off), ptr(nbr), ptr(w), min_nbr, iters, ptr(order),
+             ptr(loff), nlev, ptr(hap), ptr(imp), ptr(mean))
+
+    def levels(self, off, nbr):
+        return _abi.hi_levels(off, nbr)
 
 
 class Steps47:
-    """One GPU's share of the steps 4-7 chain for an n x m cohort.
+    """One rank's share of the steps 4-7 chain for an n x m cohort.
 
-    Inputs (device): q [n][ld] int32 hundredths of this rank's columns,
-    reads [n] f64 (read counts of every sample), the IBS hap-neighbour CSR of
-    the cohort and its GS level schedule.
+    Inputs: q [n][ld] int32 hundredths of this rank's columns (global offset
+    col0, a multiple of 8192), reads [n] f64 for every sample, and the IBS
+    hap-neighbour CSR of the cohort (its GS level schedule is derived once).
     """
 
-    def __init__(self, dev, alloc, n, m_total, col0, m_local, *, k=10, n_nbr=300, top_frac=0.1, zmax=2.0,
+    def __init__(self, ops, alloc, n, m_total, col0, m_local, *, k=10, n_nbr=300, top_frac=0.1, zmax=2.0,
                  sigma2_max=1000.0, frac_r=1.0, min_nbr=1, n_iters=100, comm=None):
-        self.dev, self.A, self.comm = dev, alloc, comm
+        self.ops, self.A, self.comm = ops, alloc, comm
         self.rank = comm.rank if comm else 0
         self.world = comm.world if comm else 1
         self.n, self.m, self.col0, self.ml = n, m_total, col0, m_local
         assert col0 % BLOCK == 0
         self.k, self.n_nbr, self.top_frac = k, n_nbr, top_frac
-        self.zmax, self.sigma2_max, self.frac_r = zmax, sigma2_max, frac_r
+        self.sigma2_max, self.frac_r = sigma2_max, frac_r
         self.min_nbr, self.n_iters = min_nbr, n_iters
         self.qmax = qmax_for_zmax(zmax)
         a = alloc
         n1 = max(n, 1)
+        widths = [shard_range(m_total, r, self.world) for r in range(self.world)]
+        self.mlmax = max(c1 - c0 for c0, c1 in widths)
         self.nblk_l = -(-m_local // BLOCK)
-        self.nblk_max = max(-(-(shard_range(m_total, r, self.world)[1] - shard_range(m_total, r, self.world)[0])
-                              // BLOCK) for r in range(self.world))
+        self.nblk_max = -(-self.mlmax // BLOCK)
         self.bsum = a.empty((n1, max(self.nblk_l, 1)), F8)
         self.bcnt = a.empty((n1, max(self.nblk_l, 1)), I4)
         if self.world > 1:
@@ -145,29 +187,23 @@ class Steps47:
             self.bcnt_pad = a.empty((n1, max(self.nblk_max, 1)), I4)
         self.rm = a.empty(n1, F8)
         ml1 = max(m_local, 1)
-        self.mlmax = max(shard_range(m_total, r, self.world)[1] - shard_range(m_total, r, self.world)[0]
-                         for r in range(self.world))
         self.mu, self.var = a.empty(ml1, F8), a.empty(ml1, F8)
         self.ratio = a.empty(max(self.mlmax, 1), F8)
-        self.ratio_all = a.empty(max(self.mlmax * self.world, 1), F8)
         self.sorted = a.empty(max(self.mlmax * self.world, 1), F8)
         self.sel = a.empty(ml1, I4)
         self.r3 = a.empty(max(self.mlmax, 1), F8)
         self.colmap = a.empty(ml1, I4)
-        self.zq = a.empty((n1, ml1), I4)                       # step-4 output: exact hundredths
-        self.np_ = pad_to(n1, 128)
+        self.zq = a.empty((n1, ml1), I4)                 # step-4 output: exact hundredths
+        self.np_ = pad_to(n1, 256)
         self.kpad = pad_to(ml1, 64)
-        self.zb = a.empty((self.np_, self.kpad), U2)          # step-5 input panel (bf16)
-        a.zero_(self.zb)                                       # pad rows/cols stay zero
+        self.zb = a.empty((self.np_, self.kpad), U2)    # step-5 input panel (bf16)
+        self.zb.zero_()                                  # pad rows stay zero
         self.gram = a.empty((self.np_, self.np_), I8)
         kk = max(k, 1)
         self.rows_per = -(-n // self.world)
         self.idx_l = a.empty((self.rows_per, kk), I4)
         self.d2_l = a.empty((self.rows_per, kk), I8)
         self.cnt_l = a.empty(self.rows_per, I4)
-        self.idx = a.empty((n1, kk), I4)
-        self.d2 = a.empty((n1, kk), I8)
-        self.cnt = a.empty(n1, I4)
         self.scale2 = a.empty(n1, F8)
         self.nscale = a.empty((n1, kk), F8)
         self.dip = a.empty(n1, F8)
@@ -175,31 +211,22 @@ class Steps47:
         self.hap = a.empty(2 * n1, F8)
         self.imp = a.empty(2 * n1, F8)
         self.mean = a.empty(1, F8)
-        self.zerodiv = C.c_int32()
-        self.events = None
+        self.marks = None
 
-    # ------------------------------------------------------------------
+    # ------------------------------------------------------------------ inputs
     def set_phasing_graph(self, off, nbr, w):
-        order, loff, nl = _abi.hi_levels(off, nbr)
-        up = lambda x, dt: self._upload(np.ascontiguousarray(x, dtype=dt))  # noqa: E731
-        self.off, self.nbr, self.w = up(off, I8), up(nbr if nbr.size else np.zeros(1), I4), \
-            up(w if w.size else np.zeros(1), F8)
-        self.order, self.loff, self.nlev = up(order, I4), up(loff, I4), nl
+        order, loff, nl = self.ops.levels(off, nbr)
+        up = self.A.upload
+        self.off = up(np.asarray(off, I8))
+        self.nbr = up(np.asarray(nbr if len(nbr) else np.zeros(1), I4))
+        self.w = up(np.asarray(w if len(w) else np.zeros(1), F8))
+        self.order, self.loff, self.nlev = up(np.asarray(order, I4)), up(np.asarray(loff, I4)), nl
 
     def set_reads(self, reads):
-        self.reads = self._upload(np.ascontiguousarray(reads, dtype=F8))
-        self.has = self._upload(np.ones(max(self.n, 1), dtype=U1))
+        self.reads = self.A.upload(np.asarray(reads, F8))
+        self.has = self.A.upload(np.ones(max(self.n, 1), dtype=U1))
 
-    def _upload(self, arr):
-        b = self.A.empty(arr.shape, arr.dtype)
-        if hasattr(b, "copy_"):
-            import torch
-            src = torch.from_numpy(arr.view(np.int16) if arr.dtype == np.uint16 else arr)
-            b.copy_(src)
-        else:
-            b.copy_from(arr)
-        return b
-
+    # ---------------------------------------------------------------- helpers
     def _read(self, b, i):
         return self.A.read(b, i)
 
@@ -208,13 +235,17 @@ class Steps47:
         every rank (padded with ``fill``); returns (buffer, total length)."""
         if self.comm is None:
             return b, count
-        import torch
         if count < maxcount:
             b.view(-1)[count:maxcount].fill_(fill)
         g = self.comm.all_gather(b.view(-1)[:maxcount])
         return g.view(-1), self.world * maxcount
 
-    # ------------------------------------------------------------------
+    def _sum_int(self, v):
+        import torch
+        t = torch.tensor([v], dtype=torch.int64, device=self.gram.device)
+        self.comm.all_reduce_sum(t)
+        return int(t.item())
+
     def _mark(self, name):
         if self.marks is not None:
             import torch
@@ -229,41 +260,36 @@ class Steps47:
             out[name] = out.get(name, 0.0) + a.elapsed_time(b)
         return out
 
+    # -------------------------------------------------------------------- run
     def run(self, q, ld, gram_events=None, profile=False):
-        """One pass of steps 4-7.  ``q``: device pointer/buffer [n][ld] int32.
+        """One pass of steps 4-7.  ``q``: buffer [n][ld] int32 (this shard).
         ``gram_events``: optional (start, end) torch.cuda.Event pair recorded
         around the Gram kernel (same stream as every kernel here)."""
-        d, ctx, n, ml = self.dev, self.dev.ctx, self.n, self.ml
-        ev = gram_events
+        o, n, ml = self.ops, self.n, self.ml
         self.marks = [] if profile else None
         self._mark("start")
-        # ---- step 4: row means (8192-block pairwise partials, gathered) ----
-        call("grid_norm_row_blocks", ctx, ptr(q), n, ml, ld, ptr(self.bsum), ptr(self.bcnt))
-        nblk_tot = self.nblk_l
-        bsum, bcnt = self.bsum, self.bcnt
+        # ---- step 4: row means from 8192-block pairwise partials ----
+        o.row_blocks(q, n, ml, ld, self.bsum, self.bcnt)
+        nblk_tot, bsum, bcnt = self.nblk_l, self.bsum, self.bcnt
         if self.comm is not None:
-            import torch
             self.bsum_pad.zero_()
             self.bcnt_pad.zero_()
             self.bsum_pad[:, : self.nblk_l].copy_(self.bsum)
             self.bcnt_pad[:, : self.nblk_l].copy_(self.bcnt)
-            gs = self.comm.all_gather(self.bsum_pad)        # [world][n][nblk_max]
-            gc = self.comm.all_gather(self.bcnt_pad)
-            bsum = gs.permute(1, 0, 2).contiguous()
-            bcnt = gc.permute(1, 0, 2).contiguous()
+            rows = self.bsum_pad.shape[0]
+            bsum = self.comm.all_gather(self.bsum_pad).permute(1, 0, 2).reshape(rows, -1).contiguous()
+            bcnt = self.comm.all_gather(self.bcnt_pad).permute(1, 0, 2).reshape(rows, -1).contiguous()
             nblk_tot = self.world * self.nblk_max
-        call("grid_norm_row_means", ctx, ptr(bsum), ptr(bcnt), n, nblk_tot, ptr(self.rm))
+        o.row_means(bsum, bcnt, n, nblk_tot, self.rm)
         self._mark("row_means")
         # ---- column statistics (local, exact) ----
-        call("grid_norm_col_means", ctx, ptr(q), n, ml, ld, ptr(self.rm), ptr(self.mu))
-        call("grid_norm_col_vars", ctx, ptr(q), n, ml, ld, ptr(self.rm), ptr(self.mu), ptr(self.var),
-             ptr(self.ratio))
+        o.col_means(q, n, ml, ld, self.rm, self.mu)
+        o.col_vars(q, n, ml, ld, self.rm, self.mu, self.var, self.ratio)
         self._mark("col_stats")
+        # ---- median -> scale; sorted(...)[int(top_frac*n)] -> selection ----
         rall, rlen = self._gather_padded(self.ratio, ml, self.mlmax, float("nan"))
-        nv = C.c_int64()
-        call("grid_sort_valid", ctx, ptr(rall), rlen, ptr(self.sorted), C.byref(nv))
-        nvalid = nv.value
-        scale = 1.0
+        nvalid = o.sort_valid(rall, rlen, self.sorted)
+        scale, r_loc = 1.0, 0
         if nvalid:
             if nvalid % 2:
                 med = self._read(self.sorted, nvalid // 2)
@@ -272,79 +298,61 @@ class Steps47:
             if med > 0:
                 scale = 1.0 / math.sqrt(med / 100.0)
             thr = self._read(self.sorted, py_index(nvalid, int(self.top_frac * nvalid)))
-            cnt = C.c_int64()
-            call("grid_select_gt", ctx, ptr(self.ratio), ml, thr, ptr(self.sel), C.byref(cnt))
-            r_loc = cnt.value
-        else:
-            r_loc = 0
+            r_loc = o.select_gt(self.ratio, ml, thr, self.sel)
         self.scale, self.r_loc = scale, r_loc
         # ---- step 5 region filter on the "%.3f" ratios (find_neighbors.py:148-171) ----
-        call("grid_gather_f64", ctx, ptr(self.ratio), ptr(self.sel), r_loc, ptr(self.r3))
-        call("grid_round_decimals", ctx, ptr(self.r3), r_loc, 3, ptr(self.r3))
+        o.gather(self.ratio, self.sel, r_loc, self.r3)
+        o.round_decimals(self.r3, r_loc, 3, self.r3)
         r3all, r3len = self._gather_padded(self.r3, r_loc, self.mlmax, float("nan"))
         r_tot = r_loc if self.comm is None else self._sum_int(r_loc)
-        call("grid_sort_valid", ctx, ptr(r3all), r3len, ptr(self.sorted), C.byref(nv))
-        if nv.value:
-            smin = self._read(self.sorted, min(int(r_tot * (1.0 - self.frac_r)), nv.value - 1))
+        self.r_tot = r_tot
+        nv = o.sort_valid(r3all, r3len, self.sorted)
+        if nv:
+            smin = self._read(self.sorted, min(int(r_tot * (1.0 - self.frac_r)), nv - 1))
             smax = float(self.sigma2_max)
         else:
             smin, smax = -math.inf, math.inf
-        ruse = C.c_int64()
-        call("grid_colmap_range", ctx, ptr(self.r3), r_loc, smin, smax, ptr(self.colmap), C.byref(ruse))
-        self.ruse_loc = ruse.value
+        self.ruse_loc = o.colmap_range(self.r3, r_loc, smin, smax, self.colmap)
         self._mark("select_sort")
         # ---- z-scores: exact hundredths (step-4 output) + clipped bf16 panel ----
-        of = C.c_int32()
-        call("grid_norm_zquant", ctx, ptr(q), n, ld, ptr(self.sel), r_loc, ptr(self.rm), ptr(self.mu), scale,
-             ptr(self.zq), max(ml, 1), ptr(self.colmap), self.qmax, ptr(self.zb), self.kpad, C.byref(of))
-        if of.value:
+        if o.zquant(q, n, ld, self.sel, r_loc, self.rm, self.mu, scale, self.zq, max(ml, 1), self.colmap,
+                    self.qmax, self.zb, self.kpad):
             raise _abi.GridNativeError("z-score outside the int32 hundredths range")
         self._mark("zquant")
         # ---- step 5: exact Gram (MFMA) -> all-reduce -> top-k ----
-        self.A.zero_(self.gram)
+        self.gram.zero_()
         kpad_used = pad_to(max(self.ruse_loc, 1), 64)
         if kpad_used > self.ruse_loc and n > 0:
             self.zb[:n, self.ruse_loc:kpad_used].zero_()      # columns colmap did not write this pass
-        if ev:
-            ev[0].record()
-        call("grid_knn_gram", ctx, ptr(self.zb), self.np_, kpad_used, self.kpad, self.qmax, ptr(self.gram))
-        if ev:
-            ev[1].record()
+        if gram_events:
+            gram_events[0].record()
+        o.gram(self.zb, self.np_, kpad_used, self.kpad, self.qmax, self.gram)
+        if gram_events:
+            gram_events[1].record()
         self._mark("gram")
         if self.comm is not None:
             self.comm.all_reduce_sum(self.gram)
             self._mark("allreduce")
         r0 = min(self.rank * self.rows_per, n)
         nr = max(min(n - r0, self.rows_per), 0)
-        call("grid_knn_topk", ctx, ptr(self.gram), n, self.np_, self.k, r0, nr, ptr(self.idx_l), ptr(self.d2_l),
-             ptr(self.cnt_l))
+        o.topk(self.gram, n, self.np_, self.k, r0, nr, self.idx_l, self.d2_l, self.cnt_l)
         if self.comm is not None:
-            gi = self.comm.all_gather(self.idx_l).view(-1, max(self.k, 1))[:n]
-            gd = self.comm.all_gather(self.d2_l).view(-1, max(self.k, 1))[:n]
-            gc = self.comm.all_gather(self.cnt_l).view(-1)[:n]
-            self.idx[:n].copy_(gi)
-            self.d2[:n].copy_(gd)
-            self.cnt[:n].copy_(gc)
-            idx, cntb = self.idx, self.cnt
+            kk = max(self.k, 1)
+            idx = self.comm.all_gather(self.idx_l).view(-1, kk)[:n].contiguous()
+            self.d2 = self.comm.all_gather(self.d2_l).view(-1, kk)[:n].contiguous()
+            cnt = self.comm.all_gather(self.cnt_l).view(-1)[:n].contiguous()
         else:
-            idx, cntb = self.idx_l, self.cnt_l
+            idx, self.d2, cnt = self.idx_l, self.d2_l, self.cnt_l
         self._mark("topk")
         # ---- step 6: dipCN (scales as printed "%.2f", neighbour gather) ----
-        call("grid_round_decimals", ctx, ptr(self.rm), n, 2, ptr(self.scale2))
-        call("grid_gather_f64", ctx, ptr(self.scale2), ptr(idx), n * max(self.k, 1), ptr(self.nscale))
-        call("grid_dipcn", ctx, n, ptr(self.reads), ptr(self.has), ptr(self.scale2), ptr(idx), ptr(self.nscale),
-             ptr(cntb), max(self.k, 1), self.n_nbr, ptr(self.dip), ptr(self.valid), C.byref(self.zerodiv))
-        if self.zerodiv.value:
+        o.round_decimals(self.rm, n, 2, self.scale2)
+        o.gather(self.scale2, idx, n * max(self.k, 1), self.nscale)
+        if o.dipcn(n, self.reads, self.has, self.scale2, idx, self.nscale, cnt, max(self.k, 1), self.n_nbr,
+                   self.dip, self.valid):
             raise ZeroDivisionError("float division by zero")
         self._mark("dipcn")
         # ---- step 7: level-scheduled Gauss-Seidel phasing + imputation ----
-        call("grid_hi_phase", ctx, n, ptr(self.dip), ptr(self.off), ptr(self.nbr), ptr(self.w), self.min_nbr,
-             self.n_iters, ptr(self.order), ptr(self.loff), self.nlev, ptr(self.hap), ptr(self.imp), ptr(self.mean))
+        o.phase(n, self.dip, self.off, self.nbr, self.w, self.min_nbr, self.n_iters, self.order, self.loff,
+                self.nlev, self.hap, self.imp, self.mean)
         self._mark("phase")
-        self.idx_out, self.cnt_out = idx, cntb
-
-    def _sum_int(self, v):
-        import torch
-        t = torch.tensor([v], dtype=torch.int64, device=self.gram.device)
-        self.comm.all_reduce_sum(t)
-        return int(t.item())
+        self.idx_out, self.cnt_out = idx, cnt

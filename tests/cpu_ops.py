@@ -1,0 +1,170 @@
+"""CPU restatement of ``grid_amd.fused.HipOps`` for tests (uses the oracle's
+arithmetic on CPU torch tensors).  Lets the sharded chain (fused.Steps47)
+run under torch.distributed/gloo without a GPU, so the sharding logic --
+8192-aligned shards, padded all-gathers, global thresholds, the Gram
+all-reduce -- is checked on CPU.  TEST INFRASTRUCTURE ONLY."""
+import math
+
+import numpy as np
+
+from oracle import steps
+from oracle.npsum import col_sum, row_block_sums
+
+MISSING = -(2 ** 31)
+NEG0 = -(2 ** 31) + 1
+
+
+def _np(t):
+    return t.numpy()
+
+
+class NumpyOps:
+    def row_blocks(self, q, n, m, ld, bsum, bcnt):
+        qa = _np(q)[:n, :m]
+        x = np.where(qa == MISSING, 0.0, qa / 100.0)
+        for b, s in enumerate(row_block_sums(x)):
+            _np(bsum)[:n, b] = s
+            _np(bcnt)[:n, b] = (qa[:, b * 8192:(b + 1) * 8192] != MISSING).sum(axis=1)
+
+    def row_means(self, bsum, bcnt, n, nblk, rm):
+        bs, bc = _np(bsum)[:n, :nblk], _np(bcnt)[:n, :nblk]
+        acc = np.zeros(n)
+        for b in range(nblk):
+            acc = acc + bs[:, b]
+        with np.errstate(all="ignore"):
+            _np(rm)[:n] = acc / bc.sum(axis=1).astype(np.float64)
+
+    def _y(self, q, n, m, rm):
+        qa = _np(q)[:n, :m]
+        r = _np(rm)[:n]
+        rs = np.where(r == 0, np.nan, r)
+        with np.errstate(all="ignore"):
+            return np.where(qa == MISSING, np.nan, (qa / 100.0) / rs[:, None])
+
+    def col_means(self, q, n, m, ld, rm, mu):
+        y = self._y(q, n, m, rm)
+        with np.errstate(all="ignore"):
+            _np(mu)[:m] = col_sum(np.nan_to_num(y, nan=0.0)) / (~np.isnan(y)).sum(axis=0)
+
+    def col_vars(self, q, n, m, ld, rm, mu, var, ratio):
+        y = self._y(q, n, m, rm)
+        mj = _np(mu)[:m]
+        with np.errstate(all="ignore"):
+            d = y - mj[None, :]
+            v = col_sum(np.nan_to_num(d * d, nan=0.0)) / (n - 1)
+            _np(var)[:m] = v
+            _np(ratio)[:m] = np.where(mj > 0, (100.0 * v) / mj, np.nan)
+
+    def sort_valid(self, v, n, out):
+        a = _np(v).reshape(-1)[:n]
+        s = np.sort(a[~np.isnan(a)])
+        _np(out).reshape(-1)[: len(s)] = s
+        return len(s)
+
+    def select_gt(self, v, n, thr, idx):
+        a = _np(v).reshape(-1)[:n]
+        with np.errstate(invalid="ignore"):
+            sel = np.where(a > thr)[0]
+        _np(idx)[: len(sel)] = sel
+        return len(sel)
+
+    def gather(self, v, idx, n, out):
+        src = _np(v).reshape(-1)
+        ix = _np(idx).reshape(-1)[:n]
+        _np(out).reshape(-1)[:n] = np.where(ix >= 0, src[np.clip(ix, 0, None)], np.nan)
+
+    def round_decimals(self, v, n, dec, out):
+        a = _np(v).reshape(-1)[:n].copy()
+        _np(out).reshape(-1)[:n] = [x if (math.isnan(x) or math.isinf(x)) else float(f"{x:.{dec}f}") for x in a]
+
+    def colmap_range(self, r, n, smin, smax, colmap):
+        a = _np(r).reshape(-1)[:n]
+        keep = np.isfinite(a) & (a >= smin) & (a <= smax)
+        cm = np.cumsum(keep) - 1
+        _np(colmap)[:n] = np.where(keep, cm, -1)
+        return int(keep.sum())
+
+    def zquant(self, q, n, ld, sel, r, rm, mu, scale, zq, ld_zq, colmap, qmax, zb, ld_zb):
+        if r == 0:
+            return 0
+        js = _np(sel)[:r]
+        qa = _np(q)[:n][:, js]
+        rr = _np(rm)[:n]
+        mj = _np(mu)[js]
+        with np.errstate(all="ignore"):
+            y = np.where(qa == MISSING, np.nan, (qa / 100.0) / np.where(rr == 0, np.nan, rr)[:, None])
+            z = ((y - mj[None, :]) / np.sqrt(mj)[None, :]) * scale
+        out = np.empty((n, r), dtype=np.int64)
+        for i in range(n):
+            for s in range(r):
+                v = z[i, s]
+                if np.isnan(v):
+                    out[i, s] = MISSING
+                else:
+                    t = f"{v:.2f}"
+                    k = int(t.replace(".", ""))
+                    out[i, s] = NEG0 if (k == 0 and t.startswith("-")) else k
+        zqa = _np(zq)
+        zqa[:n, :r] = out
+        cm = _np(colmap)[:r]
+        clip = np.where((out == MISSING) | (out == NEG0), 0, np.clip(out, -qmax, qmax)).astype(np.float32)
+        bits = (clip.view(np.uint32) >> 16).astype(np.uint16).view(np.int16)
+        zba = _np(zb)
+        for s in range(r):
+            if cm[s] >= 0:
+                zba[:n, cm[s]] = bits[:, s]
+        return 0
+
+    def gram(self, zb, np_, kpad, ld, qmax, gram):
+        bits = _np(zb)[:np_, :kpad].view(np.uint16).astype(np.uint32) << 16
+        z = bits.view(np.float32).astype(np.float64)
+        _np(gram)[:np_, :np_] += (z @ z.T).astype(np.int64)
+
+    def topk(self, gram, n, np_, k, row0, nrows, idx, d2, cnt):
+        g = _np(gram)
+        dg = np.diag(g)[:n]
+        for r in range(nrows):
+            i = row0 + r
+            d = dg[i] + dg - 2 * g[i, :n]
+            order = np.lexsort((np.arange(n), d))[: min(k + 1, n)]
+            lst = [(int(j), int(d[j])) for j in order if j != i][:k]
+            _np(idx)[r, :] = -1
+            _np(d2)[r, :] = 0
+            for t, (j, dd) in enumerate(lst):
+                _np(idx)[r, t] = j
+                _np(d2)[r, t] = dd
+            _np(cnt)[r] = len(lst)
+
+    def dipcn(self, n, reads, has, scale, nbr, nscale, ncnt, ld, n_nbr, out, valid):
+        rd, hs, sc = _np(reads), _np(has), _np(scale)
+        nb, ns, nc = _np(nbr), _np(nscale), _np(ncnt)
+        for i in range(n):
+            _np(valid)[i] = 0
+            if not hs[i]:
+                continue
+            tot, c = 0.0, 0
+            for t in range(nc[i]):
+                if c >= n_nbr:
+                    break
+                j = nb[i, t]
+                if j < 0 or not hs[j]:
+                    continue
+                tot += rd[j] / ns[i, t]
+                c += 1
+            if c:
+                _np(out)[i] = (rd[i] / sc[i]) / (tot / c)
+                _np(valid)[i] = 1
+        return 0
+
+    def phase(self, n, irr, off, nbr, w, min_nbr, iters, order, loff, nlev, hap, imp, mean):
+        o, nb, ww = _np(off), _np(nbr), _np(w)
+        hn = [[(int(nb[t]), float(ww[t])) for t in range(o[h], o[h + 1])] for h in range(2 * n)]
+        hp, mn = steps.run_phasing([float(x) for x in _np(irr)[:n]], hn, min_nbr, iters)
+        _np(hap)[: 2 * n] = hp
+        for i in range(n):
+            _np(imp)[2 * i: 2 * i + 2] = steps.compute_imp(i, hp, hn, mn)
+        _np(mean)[0] = mn
+
+    def levels(self, off, nbr):
+        from grid_amd import _abi
+        return _abi.hi_levels(off, nbr)

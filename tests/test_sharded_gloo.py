@@ -1,0 +1,110 @@
+"""Multi-GPU path on CPU: the bin-sharded steps 4-7 chain (grid_amd/fused.py)
+run under torch.distributed with the gloo backend at world sizes 2 and 3
+must give bit-identical results to one rank, and to the oracle.
+
+The compute ops are the CPU restatement in tests/cpu_ops.py (the product
+always uses HipOps); what is under test is the sharding: 8192-aligned
+ranges, padded all-gathers of row-block partials and ratios, the global
+selection threshold and sigma2 bound, the int64 Gram all-reduce, the
+row-block top-k and its all-gather."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+N, M, K, ITERS = 20, 3 * 8192 + 517, 4, 6
+
+
+def cohort():
+    rng = np.random.default_rng(11)
+    base = rng.uniform(25, 55, M)
+    clus = rng.integers(0, 3, N)
+    off = rng.uniform(-0.08, 0.08, (3, M))
+    scale = rng.uniform(0.6, 1.4, N)
+    q = np.rint(base[None, :] * (1 + off[clus]) * scale[:, None] * rng.uniform(0.8, 1.2, (N, M)) * 100)
+    q = q.astype(np.int32)
+    q[rng.random((N, M)) < 0.01] = -(2 ** 31)          # a few missing cells
+    reads = np.rint(rng.uniform(200, 900, N))
+    offs = np.zeros(2 * N + 1, dtype=np.int64)
+    nbr = []
+    for h in range(2 * N):
+        js = rng.integers(0, 2 * N, int(rng.integers(0, 5)))
+        nbr += js.tolist()
+        offs[h + 1] = offs[h] + len(js)
+    return q, reads, offs, np.array(nbr, dtype=np.int32), np.ones(len(nbr))
+
+
+def run_chain(rank, world, comm):
+    from grid_amd.fused import Steps47, TorchAlloc, shard_range
+    from tests.cpu_ops import NumpyOps
+    q, reads, off, nbr, w = cohort()
+    c0, c1 = shard_range(M, rank, world)
+    qs = torch.from_numpy(np.ascontiguousarray(q[:, c0:c1]))
+    st = Steps47(NumpyOps(), TorchAlloc("cpu"), N, M, c0, c1 - c0, k=K, n_nbr=3, n_iters=ITERS, comm=comm)
+    st.set_reads(reads)
+    st.set_phasing_graph(off, nbr, w)
+    st.run(qs, c1 - c0)
+    ml = c1 - c0
+    return {
+        "rm": st.rm.numpy()[:N].copy(), "mu": st.mu.numpy()[:ml].copy(), "var": st.var.numpy()[:ml].copy(),
+        "sel": (st.sel.numpy()[: st.r_loc] + c0).copy(), "zq": st.zq.numpy()[:N, : st.r_loc].copy(),
+        "idx": st.idx_out.numpy()[:N].copy(), "d2": st.d2.numpy()[:N].copy(), "dip": st.dip.numpy()[:N].copy(),
+        "hap": st.hap.numpy()[: 2 * N].copy(), "imp": st.imp.numpy()[: 2 * N].copy(), "scale": st.scale,
+        "ruse": st.ruse_loc,
+    }
+
+
+def _worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from grid_amd.fused import TorchComm
+    res = run_chain(rank, world, TorchComm(dist))
+    np.savez(f"{out_path}.{rank}.npz", **{k: np.asarray(v) for k, v in res.items()})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture(scope="module")
+def single():
+    return run_chain(0, 1, None)
+
+
+def test_single_rank_matches_oracle(single):
+    from oracle import steps
+    from oracle.npsum import nanmean_rows
+    q = cohort()[0]
+    mat = np.where(q == -(2 ** 31), np.nan, q / 100.0)
+    z, ratios, mu, var, scale = steps.normalize_matrix(mat)
+    assert np.array_equal(single["rm"], nanmean_rows(mat))
+    assert np.array_equal(single["mu"], mu, equal_nan=True)
+    assert single["scale"] == scale
+    assert single["sel"].tolist() == steps.select_high_variance_regions(ratios, 0.1)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_equals_single(single, world, tmp_path):
+    port = _free_port()
+    out = str(tmp_path / "res")
+    mp.start_processes(_worker, args=(world, port, out), nprocs=world, join=True, start_method="spawn")
+    parts = [dict(np.load(f"{out}.{r}.npz")) for r in range(world)]
+    for key in ("rm", "idx", "d2", "dip", "hap", "imp"):
+        for p in parts:
+            assert np.array_equal(p[key], single[key], equal_nan=True), key
+    assert np.array_equal(np.concatenate([p["mu"] for p in parts]), single["mu"], equal_nan=True)
+    assert np.array_equal(np.concatenate([p["var"] for p in parts]), single["var"], equal_nan=True)
+    assert np.concatenate([p["sel"] for p in parts]).tolist() == single["sel"].tolist()
+    assert np.array_equal(np.concatenate([p["zq"] for p in parts], axis=1), single["zq"])
+    assert sum(int(p["ruse"]) for p in parts) == int(single["ruse"])
+    assert all(float(p["scale"]) == single["scale"] for p in parts)

@@ -1,0 +1,56 @@
+"""A/B microbenchmark of the exact Gram kernel variants at the bench shape
+(interleaved in one process, random integer data in [-qmax, qmax]).
+
+    python tools/bench_gram.py [--n 3202] [--k 2700000] [--reps 3]
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from grid_amd import _abi  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--n", type=int, default=3202)
+ap.add_argument("--k", type=int, default=2_700_000)
+ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--variants", default="1,2")
+ap.add_argument("--qmax", type=int, default=200)
+a = ap.parse_args()
+
+np_ = -(-a.n // 128) * 128
+kpad = -(-a.k // 64) * 64
+dev = _abi.Device(0)
+dev.set_stream(torch.cuda.current_stream())
+g = torch.Generator(device="cuda").manual_seed(1)
+zi = torch.randint(-a.qmax, a.qmax + 1, (np_, kpad), device="cuda", dtype=torch.int32, generator=g)
+zi[a.n:] = 0
+zb = zi.to(torch.bfloat16).view(torch.int16)
+del zi
+gram = torch.zeros((np_, np_), dtype=torch.int64, device="cuda")
+res = {}
+flops = 2.0 * a.n * a.n * a.k
+for rep in range(a.reps):
+    for v in a.variants.split(","):
+        os.environ["GRID_GRAM_VARIANT"] = v
+        gram.zero_()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        _abi.call("grid_knn_gram", dev.ctx, zb.data_ptr(), np_, kpad, kpad, a.qmax, gram.data_ptr())
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1)
+        res.setdefault(v, []).append(ms)
+        if rep == 0:
+            # check a few upper-triangle tiles against a float64 product on the GPU
+            ref = (zb[:256].view(torch.bfloat16).double() @ zb[:256].view(torch.bfloat16).double().T).long()
+            ok = torch.equal(gram[:128, :256], ref[:128, :256])
+            print(f"variant {v}: tile check {'OK' if ok else 'MISMATCH'}", flush=True)
+for v, t in res.items():
+    ms = min(t)
+    print(f"variant {v}: min {ms:.2f} ms  median {np.median(t):.2f} ms  "
+          f"-> {flops / ms / 1e9:.0f} TFLOP/s (2N^2K), {flops / ms / 1e9 / 2516.6 * 100:.1f}% of bf16 peak",
+          flush=True)
