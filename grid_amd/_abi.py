@@ -57,7 +57,8 @@ _SIGS = {
     "grid_knn_topk": [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _vp, _vp, _vp],
     "grid_dipcn": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, C.POINTER(_i32)],
     "grid_hi_levels": [_i64, _vp, _vp, _vp, _vp, C.POINTER(_i32)],
-    "grid_hi_phase": [_vp, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _i32, _vp, _vp, _vp],
+    "grid_hi_pack": [_i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp],
+    "grid_hi_phase": [_vp, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp],
     "grid_synth_depth": [_vp, C.c_uint64, _i64, _i64, _i64, _i64, _i32, _vp],
     "grid_format_hundredths": [_vp, _i64, _vp, _i64, C.POINTER(_i64)],
 }
@@ -246,3 +247,21 @@ def hi_levels(off: np.ndarray, nbr: np.ndarray):
     call("grid_hi_levels", n, off.ctypes.data, nbr.ctypes.data if nbr.size else None, order.ctypes.data,
          loff.ctypes.data, C.byref(nl))
     return order[:n], loff[: nl.value + 1], nl.value
+
+
+PACK_CAP = 16
+
+
+def hi_schedule(off: np.ndarray, nbr: np.ndarray, w: np.ndarray):
+    """Level schedule + schedule-ordered packed neighbour lists (host C++)."""
+    order, loff, nl = hi_levels(off, nbr)
+    n = len(order)
+    off = np.ascontiguousarray(off, dtype=np.int64)
+    nbr = np.ascontiguousarray(nbr if len(nbr) else np.zeros(1), dtype=np.int32)
+    w = np.ascontiguousarray(w if len(w) else np.zeros(1), dtype=np.float64)
+    pk_nbr = np.zeros((max(n, 1), 2, PACK_CAP), dtype=np.int32)
+    pk_w = np.zeros((max(n, 1), 2, PACK_CAP), dtype=np.float64)
+    pk_cnt = np.zeros((max(n, 1), 2), dtype=np.int32)
+    call("grid_hi_pack", n, off.ctypes.data, nbr.ctypes.data, w.ctypes.data, order.ctypes.data if n else None,
+         PACK_CAP, pk_nbr.ctypes.data, pk_w.ctypes.data, pk_cnt.ctypes.data)
+    return order, loff, nl, pk_nbr, pk_w, pk_cnt

@@ -100,6 +100,19 @@ __device__ __forceinline__ void nbr_means_fast(int64_t i, const double *hap, con
   }
 }
 
+// Workgroup barrier for the level loop.  With hap in LDS only LDS traffic must
+// be ordered, so a raw s_barrier after lgkmcnt(0) keeps the prefetched global
+// loads of the next chunk in flight (__syncthreads would drain them with
+// vmcnt(0)).  With hap in global memory keep the full __syncthreads.
+template <bool USE_LDS>
+__device__ __forceinline__ void wg_barrier() {
+  if (USE_LDS) {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  } else {
+    __syncthreads();
+  }
+}
+
 struct PhItem {
   int64_t i;
   int64_t c0, c1;
@@ -107,25 +120,32 @@ struct PhItem {
   double wt[2][CAP];
 };
 
-// Fetch the schedule item e (sample order[e] and its neighbour lists) into
-// registers; lists longer than CAP are read later by the loop fallback.
+// Fetch schedule item e into registers from the schedule-ordered packed
+// lists (one level of independent loads; grid_hi_pack builds them).  Lists
+// longer than CAP are marked -1 and read later by the loop fallback.
 __device__ __forceinline__ void ph_fetch(int e, int e1, const int32_t *__restrict__ order,
-                                         const int64_t *__restrict__ off, const int32_t *__restrict__ nbr,
-                                         const double *__restrict__ w, PhItem &it) {
+                                         const int32_t *__restrict__ pk_nbr, const double *__restrict__ pk_w,
+                                         const int32_t *__restrict__ pk_cnt, PhItem &it) {
   it.i = -1;
   if (e >= e1) return;
-  const int64_t i = order[e];
-  const int64_t o0 = off[2 * i], o1 = off[2 * i + 1], o2 = off[2 * i + 2];
-  it.i = i;
-  it.c0 = o1 - o0;
-  it.c1 = o2 - o1;
-  if (it.c0 > CAP || it.c1 > CAP) return;
+  it.i = order[e];
+  const int2 c = *reinterpret_cast<const int2 *>(pk_cnt + 2 * (int64_t)e);
+  it.c0 = c.x;
+  it.c1 = c.y;
+  if (c.x < 0 || c.y < 0) { it.c0 = it.c1 = CAP + 1; return; }
+  const int32_t *pn = pk_nbr + (int64_t)e * 2 * CAP;
+  const double *pw = pk_w + (int64_t)e * 2 * CAP;
 #pragma unroll
-  for (int t = 0; t < CAP; t++) {
-    it.nb[0][t] = t < it.c0 ? nbr[o0 + t] : 0;
-    it.wt[0][t] = t < it.c0 ? w[o0 + t] : 0.0;
-    it.nb[1][t] = t < it.c1 ? nbr[o1 + t] : 0;
-    it.wt[1][t] = t < it.c1 ? w[o1 + t] : 0.0;
+  for (int t = 0; t < CAP; t += 4) {
+    int4 a = *reinterpret_cast<const int4 *>(pn + t), b = *reinterpret_cast<const int4 *>(pn + CAP + t);
+    it.nb[0][t] = a.x; it.nb[0][t + 1] = a.y; it.nb[0][t + 2] = a.z; it.nb[0][t + 3] = a.w;
+    it.nb[1][t] = b.x; it.nb[1][t + 1] = b.y; it.nb[1][t + 2] = b.z; it.nb[1][t + 3] = b.w;
+  }
+#pragma unroll
+  for (int t = 0; t < CAP; t += 2) {
+    double2 a = *reinterpret_cast<const double2 *>(pw + t), b = *reinterpret_cast<const double2 *>(pw + CAP + t);
+    it.wt[0][t] = a.x; it.wt[0][t + 1] = a.y;
+    it.wt[1][t] = b.x; it.wt[1][t + 1] = b.y;
   }
 }
 
@@ -142,11 +162,15 @@ __global__ __launch_bounds__(PT) void k_phase(int64_t n, const double *__restric
                                               const double *__restrict__ w, int64_t min_nbr,
                                               int64_t iters, const int32_t *__restrict__ order,
                                               const int32_t *__restrict__ loff, int nlev,
+                                              const int32_t *__restrict__ pk_nbr, const double *__restrict__ pk_w,
+                                              const int32_t *__restrict__ pk_cnt,
                                               double *hap_g, double *__restrict__ imp,
                                               double *__restrict__ mean_out) {
   extern __shared__ __attribute__((aligned(16))) double s_hap[];
   __shared__ double s_mean;
   double *hap = USE_LDS ? s_hap : hap_g;
+  // per-sample "phased" flags (LDS variant: after hap; else reuse imp as scratch)
+  uint8_t *okf = USE_LDS ? reinterpret_cast<uint8_t *>(s_hap + 2 * n) : reinterpret_cast<uint8_t *>(imp);
   const int tid = threadIdx.x;
   const double qnan = __builtin_nan("");
   for (int64_t i = tid; i < n; i += PT) {
@@ -154,38 +178,40 @@ __global__ __launch_bounds__(PT) void k_phase(int64_t n, const double *__restric
     double v = ok ? irr[i] / 2 : qnan;
     hap[2 * i] = v;
     hap[2 * i + 1] = v;
+    okf[i] = ok;
   }
+  __syncthreads();
   if (tid == 0) {
+    // mean_IRRs: sequential sum in sample order (hi_inference.py:189-201);
+    // hap[2i] * 2 == IRRs[i] exactly (halving and doubling are exact)
     double m = 0.0;
     int64_t c = 0;
     for (int64_t i = 0; i < n; i++) {
-      bool ok = (off[2 * i + 1] - off[2 * i] >= min_nbr) && (off[2 * i + 2] - off[2 * i + 1] >= min_nbr);
-      if (ok) { m = m + irr[i]; c++; }
+      if (okf[i]) { m = m + hap[2 * i] * 2.0; c++; }
     }
     if (c > 0) m = m / (double)c;
     s_mean = m;
   }
   __syncthreads();
   if (iters > 0 && nlev > 0) {
-    // chunk cursor: (level l, base) ; advance = next PT samples of the level, else next level (wrapping)
+    // chunk cursor (level l, base); two register sets A/B alternate so the
+    // next chunk's lists load while the current chunk computes (no copies)
     int l = 0, base = loff[0];
     while (base >= loff[l + 1] && l + 1 < nlev) { l++; base = loff[l]; }
-    PhItem cur, nxt;
-    ph_fetch(base + tid, loff[l + 1], order, off, nbr, w, cur);
     int64_t it = 0;
-    while (it < iters) {
-      // next chunk position
-      int nl = l, nb = base + PT;
-      int64_t nit = it;
-      if (nb >= loff[nl + 1]) {
+    PhItem ia, ib;
+    ph_fetch(base + tid, loff[l + 1], order, pk_nbr, pk_w, pk_cnt, ia);
+    auto advance = [&](int &cl, int &cb, int64_t &cit) {
+      cb += PT;
+      if (cb >= loff[cl + 1]) {
         do {
-          nl++;
-          if (nl == nlev) { nl = 0; nit++; }
-          nb = loff[nl];
-        } while (nb >= loff[nl + 1]);
+          cl++;
+          if (cl == nlev) { cl = 0; cit++; }
+          cb = loff[cl];
+        } while (cb >= loff[cl + 1]);
       }
-      if (nit < iters) ph_fetch(nb + tid, loff[nl + 1], order, off, nbr, w, nxt);
-      // compute the current chunk
+    };
+    auto step = [&](PhItem &cur) {
       bool upd = false;
       double n0 = 0.0, n1 = 0.0;
       const int64_t i = cur.i;
@@ -203,7 +229,8 @@ __global__ __launch_bounds__(PT) void k_phase(int64_t n, const double *__restric
             double sw = 1e-9, sv = 0.0;
 #pragma unroll
             for (int t = 0; t < CAP; t++) {
-              if (t < c && x[t] == x[t]) {
+              if (t >= c) break;
+              if (x[t] == x[t]) {
                 sw = sw + cur.wt[h][t];
                 sv = sv + cur.wt[h][t] * x[t];
               }
@@ -221,16 +248,26 @@ __global__ __launch_bounds__(PT) void k_phase(int64_t n, const double *__restric
           upd = true;
         }
       }
-      __syncthreads();
+      wg_barrier<USE_LDS>();
       if (upd) {
         hap[2 * i] = n0;
         hap[2 * i + 1] = n1;
       }
-      __syncthreads();
-      l = nl;
-      base = nb;
-      it = nit;
-      cur = nxt;
+      wg_barrier<USE_LDS>();
+    };
+    while (true) {
+      int nl = l, nb = base;
+      int64_t nit = it;
+      advance(nl, nb, nit);
+      if (nit < iters) ph_fetch(nb + tid, loff[nl + 1], order, pk_nbr, pk_w, pk_cnt, ib);
+      step(ia);
+      l = nl; base = nb; it = nit;
+      if (it >= iters) break;
+      advance(nl, nb, nit);
+      if (nit < iters) ph_fetch(nb + tid, loff[nl + 1], order, pk_nbr, pk_w, pk_cnt, ia);
+      step(ib);
+      l = nl; base = nb; it = nit;
+      if (it >= iters) break;
     }
   }
   const double mean = s_mean;
@@ -279,12 +316,33 @@ int grid_dipcn(grid_ctx *ctx, int64_t n, const double *d_reads, const uint8_t *d
   return GRID_OK;
 }
 
+int grid_hi_pack(int64_t n, const int64_t *off, const int32_t *nbr, const double *w, const int32_t *order,
+                 int32_t cap, int32_t *pk_nbr, double *pk_w, int32_t *pk_cnt) {
+  REQUIRE(n >= 0 && off && order && pk_nbr && pk_w && pk_cnt, "bad args");
+  REQUIRE(cap == CAP, "pack capacity must be %d", CAP);
+  for (int64_t e = 0; e < n; e++) {
+    const int64_t i = order[e];
+    for (int h = 0; h < 2; h++) {
+      const int64_t o = off[2 * i + h], c = off[2 * i + h + 1] - o;
+      int32_t *pn = pk_nbr + (e * 2 + h) * CAP;
+      double *pw = pk_w + (e * 2 + h) * CAP;
+      for (int t = 0; t < CAP; t++) {
+        pn[t] = (t < c) ? nbr[o + t] : 0;
+        pw[t] = (t < c) ? w[o + t] : 0.0;
+      }
+      pk_cnt[e * 2 + h] = c <= CAP ? (int32_t)c : -1;
+    }
+  }
+  return GRID_OK;
+}
+
 int grid_hi_phase(grid_ctx *ctx, int64_t n, const double *d_irr, const int64_t *d_off, const int32_t *d_nbr,
                   const double *d_w, int64_t min_nbr, int64_t n_iters, const int32_t *d_order,
-                  const int32_t *d_loff, int32_t nlevels, double *d_hap, double *d_imp, double *d_mean) {
+                  const int32_t *d_loff, int32_t nlevels, const int32_t *d_pk_nbr, const double *d_pk_w,
+                  const int32_t *d_pk_cnt, double *d_hap, double *d_imp, double *d_mean) {
   REQUIRE(ctx && n >= 0 && n_iters >= 0 && nlevels >= 0, "bad args");
   if (n == 0) return GRID_OK;
-  const size_t lds = (size_t)2 * n * sizeof(double);
+  const size_t lds = (size_t)2 * n * sizeof(double) + (size_t)n;
   if (lds <= 120 * 1024) {
     static bool attr = false;
     if (!attr) {
@@ -293,10 +351,10 @@ int grid_hi_phase(grid_ctx *ctx, int64_t n, const double *d_irr, const int64_t *
       attr = true;
     }
     hipLaunchKernelGGL(k_phase<true>, dim3(1), dim3(PT), lds, ctx->stream, n, d_irr, d_off, d_nbr, d_w, min_nbr,
-                       n_iters, d_order, d_loff, nlevels, d_hap, d_imp, d_mean);
+                       n_iters, d_order, d_loff, nlevels, d_pk_nbr, d_pk_w, d_pk_cnt, d_hap, d_imp, d_mean);
   } else {
     hipLaunchKernelGGL(k_phase<false>, dim3(1), dim3(PT), 0, ctx->stream, n, d_irr, d_off, d_nbr, d_w, min_nbr,
-                       n_iters, d_order, d_loff, nlevels, d_hap, d_imp, d_mean);
+                       n_iters, d_order, d_loff, nlevels, d_pk_nbr, d_pk_w, d_pk_cnt, d_hap, d_imp, d_mean);
   }
   LAUNCHCHK();
   return GRID_OK;

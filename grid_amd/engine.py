@@ -195,11 +195,12 @@ def phase(dev: Device, irr: np.ndarray, off: np.ndarray, nbr: np.ndarray, w: np.
     n = len(irr)
     if n == 0:
         return np.zeros(0), np.zeros(0), 0.0
-    order, loff, nl = _abi.hi_levels(off, nbr)
+    order, loff, nl, pk_nbr, pk_w, pk_cnt = _abi.hi_schedule(off, nbr, w)
     bufs = [dev.upload(np.ascontiguousarray(a)) for a in
             (np.asarray(irr, F8), off.astype(I8), (nbr if nbr.size else np.zeros(1, I4)).astype(I4),
-             (w if w.size else np.zeros(1, F8)).astype(F8), order.astype(I4), loff.astype(I4))]
+             (w if w.size else np.zeros(1, F8)).astype(F8), order.astype(I4), loff.astype(I4), pk_nbr, pk_w,
+             pk_cnt)]
     hap, imp, mean = dev.alloc(2 * n, F8), dev.alloc(2 * n, F8), dev.alloc(1, F8)
     call("grid_hi_phase", dev.ctx, n, bufs[0].ptr, bufs[1].ptr, bufs[2].ptr, bufs[3].ptr, min_nbr, n_iters,
-         bufs[4].ptr, bufs[5].ptr, nl, hap.ptr, imp.ptr, mean.ptr)
+         bufs[4].ptr, bufs[5].ptr, nl, bufs[6].ptr, bufs[7].ptr, bufs[8].ptr, hap.ptr, imp.ptr, mean.ptr)
     return hap.numpy(), imp.numpy(), float(mean.numpy()[0])

@@ -147,12 +147,13 @@ class HipOps:
              n_nbr, ptr(out), ptr(valid), C.byref(self.zerodiv))
         return self.zerodiv.value
 
-    def phase(self, n, irr, off, nbr, w, min_nbr, iters, order, loff, nlev, hap, imp, mean):
+    def phase(self, n, irr, off, nbr, w, min_nbr, iters, sched, hap, imp, mean):
+        order, loff, nlev, pk_nbr, pk_w, pk_cnt = sched
         call("grid_hi_phase", self.ctx, n, ptr(irr), ptr(off), ptr(nbr), ptr(w), min_nbr, iters, ptr(order),
-             ptr(loff), nlev, ptr(hap), ptr(imp), ptr(mean))
+             ptr(loff), nlev, ptr(pk_nbr), ptr(pk_w), ptr(pk_cnt), ptr(hap), ptr(imp), ptr(mean))
 
-    def levels(self, off, nbr):
-        return _abi.hi_levels(off, nbr)
+    def schedule(self, off, nbr, w):
+        return _abi.hi_schedule(off, nbr, w)
 
 
 class Steps47:
@@ -215,12 +216,16 @@ class Steps47:
 
     # ------------------------------------------------------------------ inputs
     def set_phasing_graph(self, off, nbr, w):
-        order, loff, nl = self.ops.levels(off, nbr)
+        """IBS/IBD hap-neighbour CSR; the GS level schedule and the packed,
+        schedule-ordered lists are derived once here (input preparation, like
+        parsing the neighbour file)."""
+        order, loff, nl, pk_nbr, pk_w, pk_cnt = self.ops.schedule(off, nbr, w)
         up = self.A.upload
         self.off = up(np.asarray(off, I8))
         self.nbr = up(np.asarray(nbr if len(nbr) else np.zeros(1), I4))
         self.w = up(np.asarray(w if len(w) else np.zeros(1), F8))
-        self.order, self.loff, self.nlev = up(np.asarray(order, I4)), up(np.asarray(loff, I4)), nl
+        self.nlev = nl
+        self.sched = (up(np.asarray(order, I4)), up(np.asarray(loff, I4)), nl, up(pk_nbr), up(pk_w), up(pk_cnt))
 
     def set_reads(self, reads):
         self.reads = self.A.upload(np.asarray(reads, F8))
@@ -352,7 +357,7 @@ class Steps47:
             raise ZeroDivisionError("float division by zero")
         self._mark("dipcn")
         # ---- step 7: level-scheduled Gauss-Seidel phasing + imputation ----
-        o.phase(n, self.dip, self.off, self.nbr, self.w, self.min_nbr, self.n_iters, self.order, self.loff,
-                self.nlev, self.hap, self.imp, self.mean)
+        o.phase(n, self.dip, self.off, self.nbr, self.w, self.min_nbr, self.n_iters, self.sched, self.hap,
+                self.imp, self.mean)
         self._mark("phase")
         self.idx_out, self.cnt_out = idx, cnt

@@ -167,9 +167,16 @@ int grid_dipcn(grid_ctx *ctx, int64_t n, const double *d_reads, const uint8_t *d
  * sequential order.  Outputs hap[2n] (NaN = unphased), imp[2n], *h_mean. */
 int grid_hi_levels(int64_t n, const int64_t *h_off, const int32_t *h_nbr, int32_t *h_order,
                    int32_t *h_level_off, int32_t *h_nlevels);
+/* Host: schedule-ordered packed neighbour lists for the kernel (cap = 16 per
+ * haplotype; longer lists are flagged -1 in pk_cnt and read from the CSR).
+ * pk_nbr [n][2][cap], pk_w [n][2][cap], pk_cnt [n][2]. */
+int grid_hi_pack(int64_t n, const int64_t *h_off, const int32_t *h_nbr, const double *h_w,
+                 const int32_t *h_order, int32_t cap, int32_t *h_pk_nbr, double *h_pk_w,
+                 int32_t *h_pk_cnt);
 int grid_hi_phase(grid_ctx *ctx, int64_t n, const double *d_irr, const int64_t *d_off,
                   const int32_t *d_nbr, const double *d_w, int64_t min_nbr, int64_t n_iters,
                   const int32_t *d_order, const int32_t *d_level_off, int32_t nlevels,
+                  const int32_t *d_pk_nbr, const double *d_pk_w, const int32_t *d_pk_cnt,
                   double *d_hap, double *d_imp, double *d_mean);
 
 /* ---------------------------------------------------- synthetic input

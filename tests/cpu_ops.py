@@ -156,7 +156,7 @@ class NumpyOps:
                 _np(valid)[i] = 1
         return 0
 
-    def phase(self, n, irr, off, nbr, w, min_nbr, iters, order, loff, nlev, hap, imp, mean):
+    def phase(self, n, irr, off, nbr, w, min_nbr, iters, sched, hap, imp, mean):
         o, nb, ww = _np(off), _np(nbr), _np(w)
         hn = [[(int(nb[t]), float(ww[t])) for t in range(o[h], o[h + 1])] for h in range(2 * n)]
         hp, mn = steps.run_phasing([float(x) for x in _np(irr)[:n]], hn, min_nbr, iters)
@@ -165,6 +165,6 @@ class NumpyOps:
             _np(imp)[2 * i: 2 * i + 2] = steps.compute_imp(i, hp, hn, mn)
         _np(mean)[0] = mn
 
-    def levels(self, off, nbr):
+    def schedule(self, off, nbr, w):
         from grid_amd import _abi
-        return _abi.hi_levels(off, nbr)
+        return _abi.hi_schedule(off, nbr, w)
