@@ -128,11 +128,9 @@ __device__ __forceinline__ void ph_fetch(int e, int e1, const int32_t *__restric
                                          const int32_t *__restrict__ pk_cnt, PhItem &it) {
   it.i = -1;
   if (e >= e1) return;
+  // every load independent of the others: one memory round trip per chunk
   it.i = order[e];
   const int2 c = *reinterpret_cast<const int2 *>(pk_cnt + 2 * (int64_t)e);
-  it.c0 = c.x;
-  it.c1 = c.y;
-  if (c.x < 0 || c.y < 0) { it.c0 = it.c1 = CAP + 1; return; }
   const int32_t *pn = pk_nbr + (int64_t)e * 2 * CAP;
   const double *pw = pk_w + (int64_t)e * 2 * CAP;
 #pragma unroll
@@ -147,6 +145,8 @@ __device__ __forceinline__ void ph_fetch(int e, int e1, const int32_t *__restric
     it.wt[0][t] = a.x; it.wt[0][t + 1] = a.y;
     it.wt[1][t] = b.x; it.wt[1][t + 1] = b.y;
   }
+  it.c0 = c.x < 0 ? CAP + 1 : c.x;     // > CAP: read the CSR in the loop fallback
+  it.c1 = c.y < 0 ? CAP + 1 : c.y;
 }
 
 // One workgroup runs the whole phasing of one locus.  hap lives in LDS when
@@ -169,9 +169,16 @@ __global__ __launch_bounds__(PT) void k_phase(int64_t n, const double *__restric
   extern __shared__ __attribute__((aligned(16))) double s_hap[];
   __shared__ double s_mean;
   double *hap = USE_LDS ? s_hap : hap_g;
-  // per-sample "phased" flags (LDS variant: after hap; else reuse imp as scratch)
-  uint8_t *okf = USE_LDS ? reinterpret_cast<uint8_t *>(s_hap + 2 * n) : reinterpret_cast<uint8_t *>(imp);
+  // LDS layout (USE_LDS): hap[2n] | irr[n] | level offsets[nlev+1] | phased flags[n]
+  const double *irs = USE_LDS ? s_hap + 2 * n : irr;
+  int32_t *lof = USE_LDS ? reinterpret_cast<int32_t *>(s_hap + 3 * n) : nullptr;
+  uint8_t *okf = USE_LDS ? reinterpret_cast<uint8_t *>(lof + nlev + 1) : reinterpret_cast<uint8_t *>(imp);
   const int tid = threadIdx.x;
+  if (USE_LDS) {
+    for (int64_t i = tid; i < n; i += PT) s_hap[2 * n + i] = irr[i];
+    for (int l = tid; l <= nlev; l += PT) lof[l] = loff[l];
+  }
+  const int32_t *lo = USE_LDS ? lof : loff;
   const double qnan = __builtin_nan("");
   for (int64_t i = tid; i < n; i += PT) {
     bool ok = (off[2 * i + 1] - off[2 * i] >= min_nbr) && (off[2 * i + 2] - off[2 * i + 1] >= min_nbr);
@@ -196,19 +203,19 @@ __global__ __launch_bounds__(PT) void k_phase(int64_t n, const double *__restric
   if (iters > 0 && nlev > 0) {
     // chunk cursor (level l, base); two register sets A/B alternate so the
     // next chunk's lists load while the current chunk computes (no copies)
-    int l = 0, base = loff[0];
-    while (base >= loff[l + 1] && l + 1 < nlev) { l++; base = loff[l]; }
+    int l = 0, base = lo[0];
+    while (base >= lo[l + 1] && l + 1 < nlev) { l++; base = lo[l]; }
     int64_t it = 0;
     PhItem ia, ib;
-    ph_fetch(base + tid, loff[l + 1], order, pk_nbr, pk_w, pk_cnt, ia);
+    ph_fetch(base + tid, lo[l + 1], order, pk_nbr, pk_w, pk_cnt, ia);
     auto advance = [&](int &cl, int &cb, int64_t &cit) {
       cb += PT;
-      if (cb >= loff[cl + 1]) {
+      if (cb >= lo[cl + 1]) {
         do {
           cl++;
           if (cl == nlev) { cl = 0; cit++; }
-          cb = loff[cl];
-        } while (cb >= loff[cl + 1]);
+          cb = lo[cl];
+        } while (cb >= lo[cl + 1]);
       }
     };
     auto step = [&](PhItem &cur) {
@@ -243,8 +250,8 @@ __global__ __launch_bounds__(PT) void k_phase(int64_t n, const double *__restric
         double m1 = wv[1] / ws[1];
         double den = m0 + m1;
         if (den > 0.0) {
-          n0 = irr[i] * m0 / den;
-          n1 = irr[i] * m1 / den;
+          n0 = irs[i] * m0 / den;
+          n1 = irs[i] * m1 / den;
           upd = true;
         }
       }
@@ -259,12 +266,12 @@ __global__ __launch_bounds__(PT) void k_phase(int64_t n, const double *__restric
       int nl = l, nb = base;
       int64_t nit = it;
       advance(nl, nb, nit);
-      if (nit < iters) ph_fetch(nb + tid, loff[nl + 1], order, pk_nbr, pk_w, pk_cnt, ib);
+      if (nit < iters) ph_fetch(nb + tid, lo[nl + 1], order, pk_nbr, pk_w, pk_cnt, ib);
       step(ia);
       l = nl; base = nb; it = nit;
       if (it >= iters) break;
       advance(nl, nb, nit);
-      if (nit < iters) ph_fetch(nb + tid, loff[nl + 1], order, pk_nbr, pk_w, pk_cnt, ia);
+      if (nit < iters) ph_fetch(nb + tid, lo[nl + 1], order, pk_nbr, pk_w, pk_cnt, ia);
       step(ib);
       l = nl; base = nb; it = nit;
       if (it >= iters) break;
@@ -342,7 +349,7 @@ int grid_hi_phase(grid_ctx *ctx, int64_t n, const double *d_irr, const int64_t *
                   const int32_t *d_pk_cnt, double *d_hap, double *d_imp, double *d_mean) {
   REQUIRE(ctx && n >= 0 && n_iters >= 0 && nlevels >= 0, "bad args");
   if (n == 0) return GRID_OK;
-  const size_t lds = (size_t)2 * n * sizeof(double) + (size_t)n;
+  const size_t lds = (size_t)3 * n * sizeof(double) + (size_t)(nlevels + 1) * 4 + (size_t)n;
   if (lds <= 120 * 1024) {
     static bool attr = false;
     if (!attr) {
