@@ -178,8 +178,8 @@ def main():
 
     valid = int(st.valid[:n].sum().item())
     flops = 2.0 * n * n * st.ruse_loc                       # 2 N^2 R_use per launch
-    nt = st.np_ // 128
-    executed = 2.0 * (nt * (nt + 1) // 2) * 128 * 128 * (-(-st.ruse_loc // 64) * 64)
+    nt, ni = st.np_ // 128, st.np_ // 256            # k_gram6: 256x128 tiles (I, j >= 2I)
+    executed = 2.0 * sum(nt - 2 * i for i in range(ni)) * 256 * 128 * (-(-st.ruse_loc // 64) * 64)
     out = {
         "metric": METRIC,
         "value": n * args.steps / elapsed,
@@ -204,7 +204,7 @@ def main():
                      "frac": flops / (gram_ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS,
                      "traffic": None, "gram_ms": gram_ms,
                      "executed_mfma_tflops": executed / (gram_ms * 1e-3) / 1e12,
-                     "flops_def": "2*N^2*R_use per launch (SURVEY 8d); executed = upper-triangle tiles"},
+                     "flops_def": "2*N^2*R_use per launch (SURVEY 8d); executed = the 256x128 upper-triangle tiles k_gram6 computes"},
     }
     out["config"]["selected_regions"] = st.r_loc if world == 1 else None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

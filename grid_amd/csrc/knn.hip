@@ -4,11 +4,12 @@
 // grid/utils/find_neighbors.py:207-213.  Clipped z values are integers
 // |q| <= qmax <= 256 (hundredths), exactly representable in bf16, so the Gram
 // matrix G = Z Z^T is computed EXACTLY on the bf16 MFMA pipe:
-//   * fp32 MFMA accumulators hold partial sums of at most FS*64 products, kept
-//     below 2^24 so every fp32 partial is an exact integer;
-//   * every FS K-steps they are flushed into int32 accumulators (exact while a
-//     K-slice stays below 2^31 / qmax^2 products);
-//   * each workgroup owns one 128x128 tile of one K-slice and adds its int32
+//   * fp32 MFMA accumulators hold partial sums of a few K-steps of 64
+//     products, kept below 2^24 so every fp32 partial is an exact integer;
+//   * they are then flushed into int32 accumulators (exact while a K-slice
+//     stays below 2^31 / qmax^2 products);
+//   * each workgroup owns one output tile (256x128 in k_gram6, the default;
+//     128x128 in the k_gram_dma fallback) of one K-slice and adds its int32
 //     tile into the int64 Gram with integer atomics (order-free, exact).
 // d2(i,j) = G_ii + G_jj - 2 G_ij is then exact, and neighbours are ordered by
 // (d2, j).  That equals sklearn's order wherever exact distances differ.
@@ -36,131 +37,34 @@ __device__ __forceinline__ bf16x8 as_bf16x8(uint4 v) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
-__global__ __launch_bounds__(NT, 2) void k_gram(const uint16_t *__restrict__ z, int64_t ld, int nt,
-                                                int ntiles, int64_t nsteps, int sps, int fs,
-                                                int64_t np_, unsigned long long *__restrict__ gram) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_BYTES];
-  // XCD-aware bijective remap: workgroups that share an XCD get a contiguous
-  // range of (slice, tile) work items (same K-slice, neighbouring tiles).
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, loc = bid >> 3;
-  const int q8 = nwg >> 3, r8 = nwg & 7;
-  const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
-  const int slice = wid / ntiles;
-  int t = wid - slice * ntiles;
-  int ti = 0;
-  while (t >= nt - ti) { t -= nt - ti; ti++; }
-  const int tj = ti + t;
-
-  const int64_t s0 = (int64_t)slice * sps;
-  int64_t s1 = s0 + sps;
-  if (s1 > nsteps) s1 = nsteps;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
-
-  const uint16_t *za = z + (int64_t)ti * BM * ld;
-  const uint16_t *zb = z + (int64_t)tj * BM * ld;
-
-  f32x16 acc[2][2];
-  int32_t iacc[2][2][16];
-#pragma unroll
-  for (int a = 0; a < 2; a++)
-#pragma unroll
-    for (int b = 0; b < 2; b++) {
-#pragma unroll
-      for (int r = 0; r < 16; r++) { acc[a][b][r] = 0.0f; iacc[a][b][r] = 0; }
-    }
-
-  uint4 ra0, ra1, ra2, ra3, rb0, rb1, rb2, rb3;
-  // global -> registers for K-step `step` (16 B per thread per operand, x4)
-#define GRAM_GLOAD(step)                                                              \
-  do {                                                                                \
-    const int64_t kofs_ = (step) * BK;                                                \
-    ra0 = *reinterpret_cast<const uint4 *>(za + (int64_t)((tid + 0 * NT) >> 3) * ld + kofs_ + ((tid + 0 * NT) & 7) * 8); \
-    ra1 = *reinterpret_cast<const uint4 *>(za + (int64_t)((tid + 1 * NT) >> 3) * ld + kofs_ + ((tid + 1 * NT) & 7) * 8); \
-    ra2 = *reinterpret_cast<const uint4 *>(za + (int64_t)((tid + 2 * NT) >> 3) * ld + kofs_ + ((tid + 2 * NT) & 7) * 8); \
-    ra3 = *reinterpret_cast<const uint4 *>(za + (int64_t)((tid + 3 * NT) >> 3) * ld + kofs_ + ((tid + 3 * NT) & 7) * 8); \
-    rb0 = *reinterpret_cast<const uint4 *>(zb + (int64_t)((tid + 0 * NT) >> 3) * ld + kofs_ + ((tid + 0 * NT) & 7) * 8); \
-    rb1 = *reinterpret_cast<const uint4 *>(zb + (int64_t)((tid + 1 * NT) >> 3) * ld + kofs_ + ((tid + 1 * NT) & 7) * 8); \
-    rb2 = *reinterpret_cast<const uint4 *>(zb + (int64_t)((tid + 2 * NT) >> 3) * ld + kofs_ + ((tid + 2 * NT) & 7) * 8); \
-    rb3 = *reinterpret_cast<const uint4 *>(zb + (int64_t)((tid + 3 * NT) >> 3) * ld + kofs_ + ((tid + 3 * NT) & 7) * 8); \
-  } while (0)
-  // registers -> swizzled LDS image of buffer `b`
-#define GRAM_LSTORE(b)                                                                \
-  do {                                                                                \
-    char *A_ = smem + (b) * 2 * TILE_BYTES;                                           \
-    char *B_ = A_ + TILE_BYTES;                                                       \
-    *reinterpret_cast<uint4 *>(A_ + lds_off((tid + 0 * NT) >> 3, (tid + 0 * NT) & 7)) = ra0; \
-    *reinterpret_cast<uint4 *>(A_ + lds_off((tid + 1 * NT) >> 3, (tid + 1 * NT) & 7)) = ra1; \
-    *reinterpret_cast<uint4 *>(A_ + lds_off((tid + 2 * NT) >> 3, (tid + 2 * NT) & 7)) = ra2; \
-    *reinterpret_cast<uint4 *>(A_ + lds_off((tid + 3 * NT) >> 3, (tid + 3 * NT) & 7)) = ra3; \
-    *reinterpret_cast<uint4 *>(B_ + lds_off((tid + 0 * NT) >> 3, (tid + 0 * NT) & 7)) = rb0; \
-    *reinterpret_cast<uint4 *>(B_ + lds_off((tid + 1 * NT) >> 3, (tid + 1 * NT) & 7)) = rb1; \
-    *reinterpret_cast<uint4 *>(B_ + lds_off((tid + 2 * NT) >> 3, (tid + 2 * NT) & 7)) = rb2; \
-    *reinterpret_cast<uint4 *>(B_ + lds_off((tid + 3 * NT) >> 3, (tid + 3 * NT) & 7)) = rb3; \
-  } while (0)
-
-  if (s0 < s1) {
-    GRAM_GLOAD(s0);
-    GRAM_LSTORE(0);
-  }
-  __syncthreads();
-  int since = 0;
-  int buf = 0;
-  for (int64_t st = s0; st < s1; st++) {
-    const bool more = st + 1 < s1;
-    if (more) GRAM_GLOAD(st + 1);
-    const char *A = smem + buf * 2 * TILE_BYTES;
-    const char *B = A + TILE_BYTES;
-#pragma unroll
-    for (int s = 0; s < 4; s++) {
-      const int ch = 2 * s + (lane >> 5);
-      bf16x8 fa[2], fb[2];
-#pragma unroll
-      for (int m = 0; m < 2; m++) {
-        int rowa = wr * 64 + m * 32 + (lane & 31);
-        int rowb = wc * 64 + m * 32 + (lane & 31);
-        fa[m] = as_bf16x8(*reinterpret_cast<const uint4 *>(A + lds_off(rowa, ch)));
-        fb[m] = as_bf16x8(*reinterpret_cast<const uint4 *>(B + lds_off(rowb, ch)));
+// Upper-triangle tile t -> (ti, tj) in SUPER-BLOCK order: 8x8 groups of
+// 128-tiles are enumerated one after another (triangle of groups, then the
+// tiles of a group row-major), so the ~64 workgroups an XCD runs at once share
+// 8 A and 8 B row panels in its L2 instead of 1 A and 64 B panels.
+constexpr int SBK = 8;
+__device__ __forceinline__ void tile_blocked(int t, int nt, int &ti, int &tj) {
+  const int nb = (nt + SBK - 1) / SBK;
+  for (int bi = 0; bi < nb; bi++) {
+    const int hi = min(SBK, nt - bi * SBK);
+    for (int bj = bi; bj < nb; bj++) {
+      const int hj = min(SBK, nt - bj * SBK);
+      const int cnt = bi == bj ? hi * (hi + 1) / 2 : hi * hj;
+      if (t < cnt) {
+        if (bi != bj) {
+          ti = bi * SBK + t / hj;
+          tj = bj * SBK + t % hj;
+        } else {
+          int r = 0;
+          while (t >= hi - r) { t -= hi - r; r++; }
+          ti = bi * SBK + r;
+          tj = bi * SBK + r + t;
+        }
+        return;
       }
-#pragma unroll
-      for (int m = 0; m < 2; m++)
-#pragma unroll
-        for (int nn = 0; nn < 2; nn++)
-          acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[m], fb[nn], acc[m][nn], 0, 0, 0);
+      t -= cnt;
     }
-    if (++since == fs || st + 1 == s1) {
-      since = 0;
-#pragma unroll
-      for (int a = 0; a < 2; a++)
-#pragma unroll
-        for (int b = 0; b < 2; b++)
-#pragma unroll
-          for (int r = 0; r < 16; r++) {
-            iacc[a][b][r] += (int32_t)acc[a][b][r];
-            acc[a][b][r] = 0.0f;
-          }
-    }
-    if (more) GRAM_LSTORE(buf ^ 1);
-    __syncthreads();
-    buf ^= 1;
   }
-  // int64 atomics into the Gram tile (exact, order-free)
-#pragma unroll
-  for (int a = 0; a < 2; a++)
-#pragma unroll
-    for (int b = 0; b < 2; b++)
-#pragma unroll
-      for (int r = 0; r < 16; r++) {
-        int row = ti * BM + wr * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        int col = tj * BM + wc * 64 + b * 32 + (lane & 31);
-        int32_t v = iacc[a][b][r];
-        if (v != 0)
-          atomicAdd(gram + (int64_t)row * np_ + col, (unsigned long long)(long long)v);
-      }
+  ti = tj = 0;
 }
 
 // Variant 2: LDS-DMA staging (global_load_lds_dwordx4, 1 KiB per wave
@@ -172,7 +76,8 @@ typedef __attribute__((address_space(3))) void *lptr_t;
 
 __global__ __launch_bounds__(NT, 2) void k_gram_dma(const uint16_t *__restrict__ z, int64_t ld, int nt,
                                                     int ntiles, int64_t nsteps, int sps, int fs,
-                                                    int64_t np_, unsigned long long *__restrict__ gram) {
+                                                    int64_t np_, unsigned long long *__restrict__ gram,
+                                                    int blocked) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_BYTES];
   const int nwg = gridDim.x;
   const int bid = blockIdx.x;
@@ -181,9 +86,16 @@ __global__ __launch_bounds__(NT, 2) void k_gram_dma(const uint16_t *__restrict__
   const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
   const int slice = wid / ntiles;
   int t = wid - slice * ntiles;
-  int ti = 0;
-  while (t >= nt - ti) { t -= nt - ti; ti++; }
-  const int tj = ti + t;
+  int ti = 0, tj;
+  if (blocked == 2) {            // timing probe only (wrong results): every tile reads panel 0
+    tile_blocked(t, nt, ti, tj);
+    ti = tj = 0;
+  } else if (blocked) {
+    tile_blocked(t, nt, ti, tj);
+  } else {
+    while (t >= nt - ti) { t -= nt - ti; ti++; }
+    tj = ti + t;
+  }
   const int64_t s0 = (int64_t)slice * sps;
   int64_t s1 = s0 + sps;
   if (s1 > nsteps) s1 = nsteps;
@@ -286,16 +198,8 @@ __global__ __launch_bounds__(NT, 2) void k_gram_dma(const uint16_t *__restrict__
       }
 }
 
-// Variant 3: one 256-thread workgroup per CU (1 wave per SIMD, up to 512
-// VGPRs), 256x128 output tile (4 waves x 128x64 = 4x2 MFMA 32x32 blocks),
-// 3-slot LDS-DMA ring (48 KiB per slot) with two K-steps in flight: counted
-// `s_waitcnt vmcnt(12)` + raw s_barrier, so the DMA stream never drains in the
-// main loop.  Tiles (I, j): rows [256I, 256I+256) x cols [128j, 128j+128) with
-// j >= 2I (the upper triangle at 128-granularity; the strictly-lower half of
-// the diagonal tiles is computed and ignored).
 constexpr int BM3 = 256, BN3 = 128;
 constexpr int SLOT3 = (BM3 + BN3) * BK * 2;     // 48 KiB
-constexpr int DMA3 = (BM3 + BN3) / 8 / 4;       // 1-KiB DMA instructions per wave per K-step (12)
 
 __device__ __forceinline__ uint4 lds_read_b128(uint32_t addr) {
   uint4 v;
@@ -303,20 +207,79 @@ __device__ __forceinline__ uint4 lds_read_b128(uint32_t addr) {
   return v;
 }
 
-__global__ __launch_bounds__(NT, 1) void k_gram3(const uint16_t *__restrict__ z, int64_t ld, int nt, int ni,
-                                                 int ntiles, int64_t nsteps, int sps, int fs, int64_t np_,
-                                                 unsigned long long *__restrict__ gram) {
+// Variant 6 (default): 256x128 output tile per 512-thread workgroup (8
+// waves in a 4x2 grid, 64x64 = 2x2 MFMA blocks each, two waves per SIMD), a
+// 3-slot LDS-DMA ring (48 KiB per slot), pipelined so the MFMA pipe stays fed:
+//   * fragments are double-buffered in registers: the ds_reads of sub-step
+//     s+1 are in flight while the MFMAs of sub-step s issue;
+//   * the per-step barrier sits in the middle of the last sub-step, so the
+//     first fragments of the next step are read behind the last MFMAs, and
+//     the slot freed by that barrier immediately receives step st+3 (three
+//     steps of DMA lead);
+//   * the exact fp32 -> int32 flush is staggered: block b restarts its fp32
+//     chunk at sub-step 4b of every 4-step group (chunk = 16 sub-steps =
+//     4 K-steps, exact for qmax <= 256), so a sub-step carries at most one
+//     block's 32 VALU ops between its MFMAs.
+// Work map: 256x128 tiles (I, j >= 2I) in 4x8 super-blocks (one XCD's 32
+// concurrent workgroups share 4 A and 8 B panels in L2).
+constexpr int GI6 = 4, GJ6 = 8;
+// A wave-uniform pointer forced into SGPRs (keeps global_load_lds in its
+// saddr + 32-bit voffset form instead of 64-bit per-lane addresses).
+__device__ __forceinline__ const char *sgpr_ptr(const char *p) {
+  const uint64_t v = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<const char *>((uintptr_t)(((uint64_t)hi << 32) | lo));
+}
+__device__ void tile_blocked6(int t, int nt, int ni, int &I, int &tj) {
+  const int nbI = (ni + GI6 - 1) / GI6;
+  for (int bi = 0; bi < nbI; bi++) {
+    const int i0 = bi * GI6, i1 = min(ni, i0 + GI6);
+    int cnt = 0;
+    for (int i = i0; i < i1; i++) cnt += nt - 2 * i;
+    if (t >= cnt) { t -= cnt; continue; }
+    for (int bj = (2 * i0) / GJ6;; bj++) {
+      const int j0 = bj * GJ6, j1 = min(nt, j0 + GJ6);
+      int c = 0;
+      for (int i = i0; i < i1; i++) c += max(0, j1 - max(j0, 2 * i));
+      if (t >= c) { t -= c; continue; }
+      for (int i = i0; i < i1; i++) {
+        const int lo = max(j0, 2 * i), w = max(0, j1 - lo);
+        if (t < w) { I = i; tj = lo + t; return; }
+        t -= w;
+      }
+    }
+  }
+  I = 0; tj = 0;
+}
+
+// MODE 0: production.  Timing probes (wrong results, tools/bench_gram.py):
+// 1 every tile reads the same panels (all L2 hits); 2 = 1 without the flush;
+// 4 = 1 with half the fragment reads; 5 = 1 without any global loads;
+// 3 = production without the XCD remap.  MB = 32-row A blocks per wave:
+// 2 -> 8 waves (4x2 grid, 64x64 each, two waves per SIMD); 4 -> 4 waves
+// (128x64 each; needs more than the 512 registers hipcc will give it).
+template <int MODE, int SPLIT, int MB>
+__global__ __launch_bounds__(MB == 2 ? 512 : 256, 1) void k_gram6(const uint16_t *__restrict__ z, int64_t ld,
+                                                                  int nt, int ni, int ntiles, int64_t nsteps,
+                                                                  int sps, int64_t np_,
+                                                                  unsigned long long *__restrict__ gram) {
+  constexpr int NW = MB == 2 ? 8 : 4;           // waves
+  constexpr int RA = BM3 / NW, RB = BN3 / NW;   // DMA rows per wave (A, B)
+  constexpr int UA = RA / 8, UB = RB / 8;       // 1-KiB DMA pieces per wave (A, B)
+  constexpr int NDMA = UA + UB;                 // DMA instructions per wave per K-step
+  constexpr int NF = MB + 2;                    // fragments per sub-step
+  constexpr int FSP = 16 / (2 * MB);            // sub-steps between block flushes
   __shared__ __attribute__((aligned(16))) char smem[3 * SLOT3];
   const int nwg = gridDim.x;
   const int bid = blockIdx.x;
   const int xcd = bid & 7, loc = bid >> 3;
   const int q8 = nwg >> 3, r8 = nwg & 7;
-  const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const int wid = MODE == 3 ? bid : (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
   const int slice = wid / ntiles;
-  int t = wid - slice * ntiles;
-  int I = 0;
-  while (t >= nt - 2 * I) { t -= nt - 2 * I; I++; }
-  const int tj = 2 * I + t;
+  int I = 0, tj = 0;
+  tile_blocked6(wid - slice * ntiles, nt, ni, I, tj);
+  if (MODE == 1 || MODE == 2 || MODE == 4 || MODE == 5) { I = 0; tj = 0; }
   const int64_t s0 = (int64_t)slice * sps;
   int64_t s1 = s0 + sps;
   if (s1 > nsteps) s1 = nsteps;
@@ -324,97 +287,160 @@ __global__ __launch_bounds__(NT, 1) void k_gram3(const uint16_t *__restrict__ z,
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
-  const uint16_t *za = z + (int64_t)I * BM3 * ld;
-  const uint16_t *zb = z + (int64_t)tj * BN3 * ld;
-  const int rl = lane >> 3;
-  const int64_t abase = (int64_t)(wave * 64 + rl) * ld, bbase = (int64_t)(wave * 32 + rl) * ld;
-  const int64_t ld8 = 8 * ld;
-  const int cx = lane & 7;
-  // swizzle term (row>>1)&7 for rows wave*64 + u*8 + rl is ((u*4 + (wave*64+rl)/2) & 7) -> depends on u only via u*4&7
-  const int sa = ((wave * 64 + rl) >> 1) & 7, sb = ((wave * 32 + rl) >> 1) & 7;
-  // LDS byte addresses of this lane's fragment rows (chunk 0); chunk c adds ((c ^ swz) << 4) - swz already
-  // folded: lds_off(row, c) = row*128 + ((c ^ ((row>>1)&7)) << 4)
+  const int rl = lane >> 3, cx = lane & 7;
+  // Addresses: wave-uniform 64-bit row-piece bases (SGPRs, saddr form) plus a
+  // 32-bit per-lane byte offset (row rl of the piece, swizzled chunk).
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const int sa = ((wv * RA + rl) >> 1) & 7, sb = ((wv * RB + rl) >> 1) & 7;
+  const uint32_t voa0 = (uint32_t)((rl * ld + ((cx ^ sa) * 8)) * 2);
+  const uint32_t voa1 = (uint32_t)((rl * ld + ((cx ^ sa ^ 4) * 8)) * 2);
+  const uint32_t vob0 = (uint32_t)((rl * ld + ((cx ^ sb) * 8)) * 2);
+  const uint32_t vob1 = (uint32_t)((rl * ld + ((cx ^ sb ^ 4) * 8)) * 2);
+  const char *ga = reinterpret_cast<const char *>(z + ((int64_t)I * BM3 + wv * RA) * ld);
+  const char *gb = reinterpret_cast<const char *>(z + ((int64_t)tj * BN3 + wv * RB) * ld);
+  const int64_t ld8b = 16 * ld;       // bytes per 8 rows
   const uint32_t sbase = (uint32_t)(uintptr_t)smem;
-  int rowa[4], rowb[2];
+  // fragment byte offsets inside a slot at sub-step 0 (chunk lane/32); sub-step
+  // s reads chunk 2s + lane/32, i.e. the offset XOR (s << 5)
+  uint32_t offa[MB], offb[2];
 #pragma unroll
-  for (int m = 0; m < 4; m++) rowa[m] = wr * 128 + m * 32 + (lane & 31);
+  for (int m = 0; m < MB; m++) offa[m] = lds_off(wr * (32 * MB) + m * 32 + (lane & 31), lane >> 5);
 #pragma unroll
-  for (int nn = 0; nn < 2; nn++) rowb[nn] = wc * 64 + nn * 32 + (lane & 31);
+  for (int nn = 0; nn < 2; nn++) offb[nn] = BM3 * 128 + lds_off(wc * 64 + nn * 32 + (lane & 31), lane >> 5);
 
-  f32x16 acc[4][2];
-  int32_t iacc[4][2][16];
+  f32x16 acc[MB][2];
+  int32_t iacc[MB][2][16];
 #pragma unroll
-  for (int a = 0; a < 4; a++)
+  for (int a = 0; a < MB; a++)
 #pragma unroll
     for (int b = 0; b < 2; b++)
 #pragma unroll
       for (int r = 0; r < 16; r++) { acc[a][b][r] = 0.0f; iacc[a][b][r] = 0; }
+  const f32x16 zero16 = {};
+  uint4 fr0[NF], fr1[NF];
 
-  auto issue = [&](int64_t step, int slot) __attribute__((always_inline)) {
-    char *A_ = smem + slot * SLOT3;
-    const int64_t k_ = step * BK;
-#pragma unroll
-    for (int u = 0; u < 8; u++)
-      __builtin_amdgcn_global_load_lds((gptr_t)(za + abase + u * ld8 + k_ + ((cx ^ ((sa + 4 * u) & 7)) * 8)),
-                                       (lptr_t)(A_ + (wave * 64 + u * 8) * 128), 16, 0, 0);
-#pragma unroll
-    for (int u = 0; u < 4; u++)
-      __builtin_amdgcn_global_load_lds((gptr_t)(zb + bbase + u * ld8 + k_ + ((cx ^ ((sb + 4 * u) & 7)) * 8)),
-                                       (lptr_t)(A_ + BM3 * 128 + (wave * 32 + u * 8) * 128), 16, 0, 0);
-  };
+#define G6_WAIT_VM(n_) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n_) : "memory")
+#define G6_WAIT_LGKM(n_) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(n_) : "memory")
+#define G6_ISSUE(step_, slot_)                                                                 \
+  if (MODE != 5) do {                                                                           \
+    char *A_ = smem + (slot_) * SLOT3;                                                         \
+    const int64_t kb_ = (step_) * (BK * 2);                                                    \
+    _Pragma("unroll") for (int u = 0; u < UA; u++)                                             \
+      __builtin_amdgcn_global_load_lds((gptr_t)(sgpr_ptr(ga + (u * ld8b + kb_)) + ((u & 1) ? voa1 : voa0)), \
+                                       (lptr_t)(A_ + (wv * RA + u * 8) * 128), 16, 0, 0);      \
+    _Pragma("unroll") for (int u = 0; u < UB; u++)                                             \
+      __builtin_amdgcn_global_load_lds((gptr_t)(sgpr_ptr(gb + (u * ld8b + kb_)) + ((u & 1) ? vob1 : vob0)), \
+                                       (lptr_t)(A_ + BM3 * 128 + (wv * RB + u * 8) * 128), 16, 0, 0); \
+  } while (0)
+#define G6_READ(FR, base_, s_)                                                                 \
+  do {                                                                                         \
+    if (MODE != 4) _Pragma("unroll") for (int m = 0; m < MB; m++) FR[m] = lds_read_b128((base_) + (offa[m] ^ ((s_) << 5))); \
+    _Pragma("unroll") for (int nn = 0; nn < 2; nn++) FR[MB + nn] = lds_read_b128((base_) + (offb[nn] ^ ((s_) << 5))); \
+  } while (0)
+  // MFMAs of blocks m in [m0, m1) on fragments FR at in-group sub-step c_;
+  // block b = 2m + nn restarts its fp32 chunk at sub-step FSP*b
+#define G6_MFMA(FR, c_, m0, m1, STAG)                                                          \
+  do {                                                                                         \
+    _Pragma("unroll") for (int m = m0; m < m1; m++)                                            \
+      _Pragma("unroll") for (int nn = 0; nn < 2; nn++) {                                       \
+        if ((STAG) && (c_) == FSP * (m * 2 + nn)) {                                            \
+          _Pragma("unroll") for (int r = 0; r < 16; r++) iacc[m][nn][r] += (int32_t)acc[m][nn][r]; \
+          acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(FR[m]), as_bf16x8(FR[MB + nn]), \
+                                                               zero16, 0, 0, 0);               \
+        } else {                                                                               \
+          acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(FR[m]), as_bf16x8(FR[MB + nn]), \
+                                                               acc[m][nn], 0, 0, 0);           \
+        }                                                                                      \
+      }                                                                                        \
+  } while (0)
+  // one K-step `st_` (LDS slot `slot`), in-group index q_; fr0 holds sub-step 0 on entry
+#define G6_STEP(st_, q_, STAG, COND)                                                           \
+  do {                                                                                         \
+    const uint32_t base_ = sbase + slot * SLOT3;                                               \
+    G6_READ(fr1, base_, 1);                                                                    \
+    G6_WAIT_LGKM(MODE == 4 ? 2 : NF);                                                                          \
+    __builtin_amdgcn_sched_barrier(0);                                                         \
+    G6_MFMA(fr0, 4 * (q_) + 0, 0, MB, STAG);                                                   \
+    __builtin_amdgcn_sched_barrier(0);                                                         \
+    G6_READ(fr0, base_, 2);                                                                    \
+    G6_WAIT_LGKM(MODE == 4 ? 2 : NF);                                                                          \
+    __builtin_amdgcn_sched_barrier(0);                                                         \
+    G6_MFMA(fr1, 4 * (q_) + 1, 0, MB, STAG);                                                   \
+    __builtin_amdgcn_sched_barrier(0);                                                         \
+    G6_READ(fr1, base_, 3);                                                                    \
+    G6_WAIT_LGKM(MODE == 4 ? 2 : NF);                                                                          \
+    __builtin_amdgcn_sched_barrier(0);                                                         \
+    G6_MFMA(fr0, 4 * (q_) + 2, 0, MB, STAG);                                                   \
+    __builtin_amdgcn_sched_barrier(0);                                                         \
+    G6_WAIT_LGKM(0);                                                                           \
+    __builtin_amdgcn_sched_barrier(0);                                                         \
+    G6_MFMA(fr1, 4 * (q_) + 3, 0, SPLIT, STAG);                                                \
+    __builtin_amdgcn_sched_barrier(0);                                                         \
+    if (!(COND) || (st_) + 2 < s1) G6_WAIT_VM(NDMA);                                           \
+    else G6_WAIT_VM(0);                                                                        \
+    __builtin_amdgcn_s_barrier();                                                              \
+    __builtin_amdgcn_sched_barrier(0);                                                         \
+    if (!(COND) || (st_) + 3 < s1) G6_ISSUE((st_) + 3, slot);                                  \
+    slot = slot == 2 ? 0 : slot + 1;                                                           \
+    if (!(COND) || (st_) + 1 < s1) G6_READ(fr0, sbase + slot * SLOT3, 0);                      \
+    __builtin_amdgcn_sched_barrier(0);                                                         \
+    G6_MFMA(fr1, 4 * (q_) + 3, SPLIT, MB, STAG);                                               \
+    __builtin_amdgcn_sched_barrier(0);                                                         \
+  } while (0)
+#define G6_FLUSH()                                                                             \
+  do {                                                                                         \
+    _Pragma("unroll") for (int a = 0; a < MB; a++)                                             \
+      _Pragma("unroll") for (int b = 0; b < 2; b++)                                            \
+        _Pragma("unroll") for (int r = 0; r < 16; r++) {                                       \
+          iacc[a][b][r] += (int32_t)acc[a][b][r];                                              \
+          acc[a][b][r] = 0.0f;                                                                 \
+        }                                                                                      \
+  } while (0)
 
-  if (s0 < s1) issue(s0, 0);
-  if (s0 + 1 < s1) {
-    issue(s0 + 1, 1);
-    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __builtin_amdgcn_s_barrier();
-  int slot = 0, phase = 0;
-  for (int64_t st = s0; st < s1; st++) {
-    if (st + 2 < s1) issue(st + 2, slot == 0 ? 2 : slot - 1);
-    const uint32_t A = sbase + slot * SLOT3, B = A + BM3 * 128;
-#pragma unroll
-    for (int s = 0; s < 4; s++) {
-      const int ch = 2 * s + (lane >> 5);
-      uint4 fa[4], fb[2];
-#pragma unroll
-      for (int m = 0; m < 4; m++) fa[m] = lds_read_b128(A + lds_off(rowa[m], ch));
-#pragma unroll
-      for (int nn = 0; nn < 2; nn++) fb[nn] = lds_read_b128(B + lds_off(rowb[nn], ch));
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int m = 0; m < 4; m++)
-#pragma unroll
-        for (int nn = 0; nn < 2; nn++)
-          acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(fa[m]), as_bf16x8(fb[nn]), acc[m][nn], 0, 0, 0);
-    }
-    if (++phase == fs || st + 1 == s1) {
-      phase = 0;
-#pragma unroll
-      for (int a = 0; a < 4; a++)
-#pragma unroll
-        for (int b = 0; b < 2; b++)
-#pragma unroll
-          for (int r = 0; r < 16; r++) {
-            iacc[a][b][r] += (int32_t)acc[a][b][r];
-            acc[a][b][r] = 0.0f;
-          }
-    }
-    if (st + 2 < s1) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int slot = 0;
+  if (s0 < s1) {
+    G6_ISSUE(s0, 0);
+    if (s0 + 1 < s1) G6_ISSUE(s0 + 1, 1);
+    if (s0 + 2 < s1) G6_ISSUE(s0 + 2, 2);
+    if (s0 + 2 < s1) G6_WAIT_VM(2 * NDMA);
+    else if (s0 + 1 < s1) G6_WAIT_VM(NDMA);
+    else G6_WAIT_VM(0);
     __builtin_amdgcn_s_barrier();
-    slot = slot == 2 ? 0 : slot + 1;
+    __builtin_amdgcn_sched_barrier(0);
+    G6_READ(fr0, sbase, 0);
   }
+  int64_t st = s0;
+  const int64_t sfull = s0 + ((s1 - s0) & ~(int64_t)3);
+  // steady state: every step's DMA lead (st+3) exists
+  for (; st < sfull && st + 6 < s1; st += 4) {
+    G6_STEP(st, 0, MODE != 2, 0);
+    G6_STEP(st + 1, 1, MODE != 2, 0);
+    G6_STEP(st + 2, 2, MODE != 2, 0);
+    G6_STEP(st + 3, 3, MODE != 2, 0);
+  }
+  for (; st < sfull; st += 4) {
+    G6_STEP(st, 0, 1, 1);
+    G6_STEP(st + 1, 1, 1, 1);
+    G6_STEP(st + 2, 2, 1, 1);
+    G6_STEP(st + 3, 3, 1, 1);
+  }
+  G6_FLUSH();
+  for (; st < s1; st++) G6_STEP(st, 0, 0, 1);
+  G6_FLUSH();
+#undef G6_WAIT_VM
+#undef G6_WAIT_LGKM
+#undef G6_ISSUE
+#undef G6_READ
+#undef G6_MFMA
+#undef G6_STEP
+#undef G6_FLUSH
 #pragma unroll
-  for (int a = 0; a < 4; a++)
+  for (int a = 0; a < MB; a++)
 #pragma unroll
     for (int b = 0; b < 2; b++)
 #pragma unroll
       for (int r = 0; r < 16; r++) {
-        int row = I * BM3 + wr * 128 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        int row = I * BM3 + wr * (32 * MB) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         int col = tj * BN3 + wc * 64 + b * 32 + (lane & 31);
         int32_t v = iacc[a][b][r];
         if (v != 0) atomicAdd(gram + (int64_t)row * np_ + col, (unsigned long long)(long long)v);
@@ -551,21 +577,27 @@ int grid_knn_gram(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t kpad
   const int64_t nslices = ceil_div(nsteps, sps);
   const int64_t nwg = nslices * ntiles;
   REQUIRE(nwg < (1ll << 31), "too many work items");
-  const char *ve = getenv("GRID_GRAM_VARIANT");   // A/B switch for tools/bench_gram.py
-  const int variant = ve ? atoi(ve) : 2;
-  if (variant == 3 && np_ % BM3 == 0) {
+  // GRID_GRAM_VARIANT: A/B switch and timing probes for tools/bench_gram.py
+  const char *ve = getenv("GRID_GRAM_VARIANT");
+  const int variant = ve ? atoi(ve) : 6;
+  if (variant >= 6 && np_ % BM3 == 0) {
+    // 256x128 tiles; 4-step fp32 chunks stay exact: 4 * 64 * qmax^2 < 2^24 for qmax <= 256
     const int ni = (int)(np_ / BM3);
-    int nt3 = 0;
-    for (int i = 0; i < ni; i++) nt3 += nt - 2 * i;
-    const int64_t nwg3 = nslices * nt3;
-    hipLaunchKernelGGL(k_gram3, dim3((unsigned)nwg3), dim3(NT), 0, ctx->stream, d_zb, ld, nt, ni, nt3, nsteps,
-                       (int)sps, fs, np_, (unsigned long long *)d_gram);
-  } else if (variant == 1)
-    hipLaunchKernelGGL(k_gram, dim3((unsigned)nwg), dim3(NT), 0, ctx->stream, d_zb, ld, nt, ntiles, nsteps,
-                       (int)sps, fs, np_, (unsigned long long *)d_gram);
-  else
+    int nt6 = 0;
+    for (int i = 0; i < ni; i++) nt6 += nt - 2 * i;
+    int64_t sps6 = ceil_div(nsteps, ceil_div(256, nt6));
+    if (sps6 > sps_max) sps6 = sps_max;
+    const int64_t nsl6 = ceil_div(nsteps, sps6);
+    REQUIRE(nsl6 * nt6 < (1ll << 31), "too many work items");
+    // 6 production; 7, 8, 14, 15 timing probes (wrong results, see k_gram6); 11 without the XCD remap
+    auto kern = variant == 7 ? k_gram6<1, 1, 2> : variant == 8 ? k_gram6<2, 1, 2> : variant == 11 ? k_gram6<3, 1, 2>
+              : variant == 14 ? k_gram6<4, 1, 2> : variant == 15 ? k_gram6<5, 1, 2> : k_gram6<0, 1, 2>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)(nsl6 * nt6)), dim3(512), 0, ctx->stream, d_zb, ld, nt, ni, nt6,
+                       nsteps, (int)sps6, np_, (unsigned long long *)d_gram);
+  } else {
     hipLaunchKernelGGL(k_gram_dma, dim3((unsigned)nwg), dim3(NT), 0, ctx->stream, d_zb, ld, nt, ntiles, nsteps,
-                       (int)sps, fs, np_, (unsigned long long *)d_gram);
+                       (int)sps, fs, np_, (unsigned long long *)d_gram, variant == 4 ? 1 : 0);
+  }
   LAUNCHCHK();
   return GRID_OK;
 }

@@ -153,7 +153,7 @@ def knn_from_hundredths(dev: Device, zq: np.ndarray, k: int, qmax: int):
     n, r = zq.shape
     if n == 0:
         return np.zeros((0, max(k, 1)), I4), np.zeros((0, max(k, 1)), I8), np.zeros(0, I4)
-    np_ = pad_to(max(n, 1), 128)
+    np_ = pad_to(max(n, 1), 256)
     kpad = pad_to(max(r, 1), 64)
     zf = np.zeros((np_, kpad), dtype=np.float32)
     zf[:n, :r] = zq

@@ -145,6 +145,31 @@ def test_gram_exact_worst_case(dev):
                                       ref[ti*128:(ti+1)*128, tj*128:(tj+1)*128])
 
 
+@pytest.mark.parametrize("variant", ["2", "4", "6", "11"])
+def test_gram_variants_multi_slice(dev, variant, monkeypatch):
+    """Every Gram kernel variant on a shape with several int32 K-slices, a
+    partial last slice (remainder steps not a multiple of 4) and a partial
+    256-row block, against a float64 product (exact: |sums| < 2^53)."""
+    from grid_amd._abi import call
+    monkeypatch.setenv("GRID_GRAM_VARIANT", variant)
+    qmax, n, np_ = 200, 600, 768
+    r = 64 * (2 * 838 + 7)
+    rng = np.random.default_rng(int(variant))
+    q = np.zeros((np_, r), dtype=np.int64)
+    q[:n] = rng.integers(-qmax, qmax + 1, size=(n, r))
+    zf = (q.astype(np.float32).view(np.uint32) >> 16).astype(np.uint16)
+    zb = dev.upload(zf)
+    g = dev.zeros((np_, np_), np.int64)
+    call("grid_knn_gram", dev.ctx, zb.ptr, np_, r, r, qmax, g.ptr)
+    got = g.numpy()
+    qf = q.astype(np.float64)
+    ref = (qf @ qf.T).astype(np.int64)
+    for ti in range(np_ // 128):
+        for tj in range(ti, np_ // 128):
+            blk = (slice(ti * 128, (ti + 1) * 128), slice(tj * 128, (tj + 1) * 128))
+            assert np.array_equal(got[blk], ref[blk]), (ti, tj)
+
+
 def test_dipcn_random(dev):
     from grid_amd import engine
     rng = np.random.default_rng(7)
