@@ -325,8 +325,9 @@ __global__ __launch_bounds__(256) void k_col_vars(const int32_t *__restrict__ q,
 }
 
 // Per selected column s: j = sel[s], mu_j, sqrt(mu_j), 1/sqrt(mu_j).
-__global__ void k_zprep(const int32_t *__restrict__ sel, int64_t r, const double *__restrict__ mu,
-                        double *__restrict__ mus, double *__restrict__ sq, double *__restrict__ rsq) {
+__global__ void k_zprep(const int32_t *__restrict__ sel, int64_t r, const double *__restrict__ mu, double scale,
+                        double *__restrict__ mus, double *__restrict__ sq, double *__restrict__ rsq,
+                        float2 *__restrict__ mc32) {
   int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= r) return;
   double m = mu[sel[s]];
@@ -334,17 +335,30 @@ __global__ void k_zprep(const int32_t *__restrict__ sel, int64_t r, const double
   mus[s] = m;
   sq[s] = t;
   rsq[s] = 1.0 / t;
+  mc32[s] = make_float2((float)m, (float)(100.0 * scale / t));   // fast-path constants (k_zquant4)
 }
 
 constexpr int ZR = 8;    // rows per zquant block
 
 // 4 consecutive selected columns x ZR rows per thread.
+//
+// Fast path: the step-4 output only needs k = round_half_even(100 * z) (the
+// "%.2f" digits of z), so t = 100 z is first evaluated in fp32,
+//   t' = ((float)q * a_i - m_j) * c_j,  a_i = 0.01 / rm_i,  c_j = 100 scale / sqrt(m_j),
+// whose distance from the exact 100 z is at most
+//   delta = 2^-21 (|c_j| (|y'| + m_j) + |t'|)
+// (fp32 rounding of q, a_i, the product, m_j, the difference, c_j and the
+// final product: <= 5 units of 2^-24 relative per term, 1.6x margin; the fp64
+// chain's own error is ~2^-50 and is included in the margin).  When t' is
+// farther than delta from every half-integer, rint(t') IS k, and when it is
+// also farther than delta from 0 its sign is z's sign ("-0.00").  Otherwise
+// (probability ~1e-4 per cell) the exact fp64 chain below decides.
 __global__ __launch_bounds__(256) void k_zquant4(const int32_t *__restrict__ q, int64_t n, int64_t ld,
                                                  const int32_t *__restrict__ sel, int64_t r,
                                                  const double *__restrict__ rm, const double *__restrict__ rinv,
                                                  const double *__restrict__ mus, const double *__restrict__ sq,
-                                                 const double *__restrict__ rsq, double scale,
-                                                 int32_t *__restrict__ zq, int64_t ld_zq,
+                                                 const double *__restrict__ rsq, const float2 *__restrict__ mc32,
+                                                 double scale, int32_t *__restrict__ zq, int64_t ld_zq,
                                                  const int32_t *__restrict__ colmap, int32_t qmax,
                                                  uint16_t *__restrict__ zb, int64_t ld_zb,
                                                  int32_t *__restrict__ overflow) {
@@ -353,15 +367,15 @@ __global__ __launch_bounds__(256) void k_zquant4(const int32_t *__restrict__ q, 
   if (s0 >= r) return;
   const int w = (int)((r - s0) < 4 ? (r - s0) : 4);
   int32_t js[4], cm[4];
-  double m_[4], sq_[4], rs_[4];
+  float m32[4], c32[4];
 #pragma unroll
   for (int c = 0; c < 4; c++) {
     const bool ok = c < w;
     js[c] = ok ? sel[s0 + c] : 0;
     cm[c] = (ok && colmap) ? colmap[s0 + c] : (ok ? (int32_t)(s0 + c) : -1);
-    m_[c] = ok ? mus[s0 + c] : 1.0;
-    sq_[c] = ok ? sq[s0 + c] : 1.0;
-    rs_[c] = ok ? rsq[s0 + c] : 1.0;
+    const float2 mc = ok ? mc32[s0 + c] : make_float2(1.0f, 1.0f);
+    m32[c] = mc.x;
+    c32[c] = mc.y;
   }
   const bool vec_zq = zq && w == 4 && ((ld_zq & 3) == 0) && ((s0 & 3) == 0);
   const bool vec_zb = zb && w == 4 && cm[0] >= 0 && cm[1] == cm[0] + 1 && cm[2] == cm[0] + 2 &&
@@ -380,20 +394,39 @@ __global__ __launch_bounds__(256) void k_zquant4(const int32_t *__restrict__ q, 
     const int64_t i = i0 + u;
     if (i >= i1) break;
     const double rmi = rm[i], rii = rinv[i];
+    const bool rowok = rmi != 0.0 && rmi == rmi;
+    const float a32 = (float)(0.01 * rii);
     int32_t out[4];
+    bool slow[4];
 #pragma unroll
     for (int c = 0; c < 4; c++) {
       out[c] = GRID_ZQ_NAN;
-      if (c < w) {
+      slow[c] = false;
+      if (c < w && rowok && qv[u][c] != GRID_MISSING) {
+        const float y = (float)qv[u][c] * a32;
+        const float t = (y - m32[c]) * c32[c];
+        const float k = rintf(t);
+        const float f = fabsf(t - k);
+        const float dl = 0x1p-21f * fmaf(fabsf(c32[c]), fabsf(y) + m32[c], fabsf(t));
+        if ((0.5f - f) > dl && fabsf(t) < 0x1p21f && (k != 0.0f || fabsf(t) > dl)) {
+          out[c] = (int32_t)k;
+          if (out[c] == 0 && t < 0.0f) out[c] = GRID_ZQ_NEG0;
+        } else {
+          slow[c] = true;
+        }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      if (slow[c]) {      // exact fp64 chain (rare)
         double y;
-        if (yval(qv[u][c], rmi, rii, y)) {
-          double z = div_exact(y - m_[c], sq_[c], rs_[c]) * scale;
-          if (z == z) {
-            double k = round_dec_k(z, 100.0);
-            if (fabs(k) >= 2147483000.0) { of = 1; k = 0.0; }
-            out[c] = (int32_t)k;
-            if (out[c] == 0 && signbit(z)) out[c] = GRID_ZQ_NEG0;
-          }
+        yval(qv[u][c], rmi, rii, y);
+        double z = div_exact(y - mus[s0 + c], sq[s0 + c], rsq[s0 + c]) * scale;
+        if (z == z) {
+          double k = round_dec_k(z, 100.0);
+          if (fabs(k) >= 2147483000.0) { of = 1; k = 0.0; }
+          out[c] = (int32_t)k;
+          if (out[c] == 0 && signbit(z)) out[c] = GRID_ZQ_NEG0;
         }
       }
     }
@@ -558,17 +591,18 @@ int grid_norm_zquant(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t ld, c
   double *rinv;
   char *rest;
   size_t rb = (((size_t)r * 8 + 255) & ~size_t(255));
-  int rc = recip_rows(ctx, d_rm, n, 3 * rb, &rinv, &rest);
+  int rc = recip_rows(ctx, d_rm, n, 4 * rb, &rinv, &rest);
   if (rc) return rc;
   double *mus = (double *)rest, *sq = (double *)(rest + rb), *rsq = (double *)(rest + 2 * rb);
+  float2 *mc32 = (float2 *)(rest + 3 * rb);
   int32_t *d_of = (int32_t *)ctx->scratch;
   HIPCHK(hipMemsetAsync(d_of, 0, 4, ctx->stream));
-  hipLaunchKernelGGL(k_zprep, dim3((unsigned)ceil_div(r, 256)), dim3(256), 0, ctx->stream, d_sel, r, d_mu, mus, sq,
-                     rsq);
+  hipLaunchKernelGGL(k_zprep, dim3((unsigned)ceil_div(r, 256)), dim3(256), 0, ctx->stream, d_sel, r, d_mu, scale, mus,
+                     sq, rsq, mc32);
   LAUNCHCHK();
   hipLaunchKernelGGL(k_zquant4, dim3((unsigned)ceil_div(ceil_div(r, 4), 256), (unsigned)ceil_div(n, ZR)), dim3(256), 0,
-                     ctx->stream, d_q, n, ld, d_sel, r, d_rm, rinv, mus, sq, rsq, scale, d_zq, ld_zq, d_colmap, qmax,
-                     d_zb, ld_zb, d_of);
+                     ctx->stream, d_q, n, ld, d_sel, r, d_rm, rinv, mus, sq, rsq, mc32, scale, d_zq, ld_zq, d_colmap,
+                     qmax, d_zb, ld_zb, d_of);
   LAUNCHCHK();
   if (h_overflow) {
     HIPCHK(hipMemcpyAsync(ctx->pinned, d_of, 4, hipMemcpyDeviceToHost, ctx->stream));
