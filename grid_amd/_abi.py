@@ -61,6 +61,13 @@ _SIGS = {
     "grid_hi_phase": [_vp, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp],
     "grid_synth_depth": [_vp, C.c_uint64, _i64, _i64, _i64, _i64, _i32, _vp],
     "grid_format_hundredths": [_vp, _i64, _vp, _i64, C.POINTER(_i64)],
+    "grid_ingest_mosdepth": [_vp, _i64, C.c_char_p, C.c_int, _i64, _i64, _i64, _vp, _vp, _vp, _f64, _f64,
+                             C.c_int, _i64, C.POINTER(_vp)],
+    "grid_ingest_summary": [_vp, C.POINTER(_i64), _vp, _vp],
+    "grid_ingest_columns": [_vp, _vp, _vp],
+    "grid_ingest_population_means": [_vp, _vp, _vp, _vp, _i64, C.POINTER(_i64)],
+    "grid_ingest_fill": [_vp, _vp, _vp, _i64, _i64],
+    "grid_ingest_free": [_vp],
 }
 EXPORTS = tuple(_SIGS) + ("grid_last_error",)
 
@@ -265,3 +272,85 @@ def hi_schedule(off: np.ndarray, nbr: np.ndarray, w: np.ndarray):
     call("grid_hi_pack", n, off.ctypes.data, nbr.ctypes.data, w.ctypes.data, order.ctypes.data if n else None,
          PACK_CAP, pk_nbr.ctypes.data, pk_w.ctypes.data, pk_cnt.ctypes.data)
     return order, loff, nl, pk_nbr, pk_w, pk_cnt
+
+
+class IngestUnsupported(GridNativeError):
+    """A mosdepth file left the strict grammar the native parser covers."""
+
+
+class Ingest:
+    """Host C++ ingest of mosdepth regions files (grid_ingest_* in
+    include/grid_abi.h): one parse per file, ordered population means,
+    valid columns, then ``fill`` of the int32 hundredths matrix."""
+
+    def __init__(self, paths, chrom_prefix, window, mask, min_depth, max_depth, threads=1,
+                 cache_bytes=None):
+        lib = load()
+        self.n = len(paths)
+        enc = [(str(p).encode() if p is not None else b"") for p in paths]
+        arr = (C.c_char_p * max(self.n, 1))(*enc)
+        names = sorted(mask)
+        carr = (C.c_char_p * max(len(names), 1))(*[c.encode() for c in names])
+        moff = np.zeros(len(names) + 1, dtype=np.int64)
+        kb = []
+        for i, c in enumerate(names):
+            v = np.fromiter(mask[c], dtype=np.int64, count=len(mask[c]))
+            kb.append(v)
+            moff[i + 1] = moff[i] + len(v)
+        kbv = np.ascontiguousarray(np.concatenate(kb) if kb else np.zeros(1, np.int64))
+        if cache_bytes is None:
+            try:
+                cache_bytes = int(os.sysconf("SC_PAGE_SIZE") * os.sysconf("SC_PHYS_PAGES") * 0.5)
+            except (ValueError, OSError):
+                cache_bytes = 1 << 33
+        has_w = window is not None
+        s, e = window if has_w else (0, 0)
+        h = _vp()
+        rc = lib.grid_ingest_mosdepth(arr, self.n, chrom_prefix.encode() if chrom_prefix else None, int(has_w),
+                                      int(s), int(e), len(names), carr, moff.ctypes.data, kbv.ctypes.data,
+                                      float(min_depth), float(max_depth), int(max(1, threads)), int(cache_bytes),
+                                      C.byref(h))
+        if rc == GRID_EUNSUPPORTED:
+            raise IngestUnsupported(lib.grid_last_error().decode(errors="replace"))
+        check(rc, "grid_ingest_mosdepth")
+        self.h = h.value
+        m = _i64()
+        self.status = np.zeros(max(self.n, 1), dtype=np.int32)
+        self.nvalid = np.zeros(max(self.n, 1), dtype=np.int64)
+        call("grid_ingest_summary", self.h, C.byref(m), self.status.ctypes.data, self.nvalid.ctypes.data)
+        self.status, self.nvalid = self.status[: self.n], self.nvalid[: self.n]
+        self.m = m.value
+        st = np.zeros(max(self.m, 1), dtype=np.int64)
+        en = np.zeros(max(self.m, 1), dtype=np.int64)
+        call("grid_ingest_columns", self.h, st.ctypes.data, en.ctypes.data)
+        self.starts, self.ends = st[: self.m], en[: self.m]
+
+    def population_means(self):
+        nk = _i64()
+        call("grid_ingest_population_means", self.h, None, None, None, 0, C.byref(nk))
+        k = max(nk.value, 1)
+        st, en, mu = np.zeros(k, np.int64), np.zeros(k, np.int64), np.zeros(k)
+        call("grid_ingest_population_means", self.h, st.ctypes.data, en.ctypes.data, mu.ctypes.data, k,
+             C.byref(nk))
+        n = nk.value
+        return {(int(a), int(b)): float(v) for a, b, v in zip(st[:n], en[:n], mu[:n])}
+
+    def fill(self, row_of_file, out=None):
+        rof = np.ascontiguousarray(row_of_file, dtype=np.int32)
+        nrows = int(rof.max()) + 1 if rof.size and rof.max() >= 0 else 0
+        if out is None:
+            out = np.empty((nrows, self.m), dtype=np.int32)
+        call("grid_ingest_fill", self.h, rof.ctypes.data, out.ctypes.data if out.size else None, nrows,
+             out.shape[1] if out.ndim == 2 else self.m)
+        return out
+
+    def close(self):
+        if getattr(self, "h", None):
+            load().grid_ingest_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -16,7 +16,12 @@ struct grid_ctx {
   size_t scratch_bytes = 0;
   void *pinned = nullptr;      // small pinned host buffer for scalars
   hipEvent_t ev[8] = {};
+  int ncu = 0;                 // compute units (persistent-kernel grids)
+  void *aux = nullptr;         // small device workspace: Gram tile list + round counters
+  int32_t *aux_tiles_host = nullptr;   // host copy of the uploaded tile list (re-upload check)
+  int aux_tiles_n = 0;
 };
+constexpr size_t GRID_AUX_BYTES = 1 << 20;
 
 void grid_set_error(const char *fmt, ...);
 int grid_scratch(grid_ctx *ctx, size_t bytes, void **p);

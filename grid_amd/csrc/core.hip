@@ -58,6 +58,8 @@ int grid_ctx_create(int device, grid_ctx **out) {
   HIPCHK(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
   c->stream = c->own;
   HIPCHK(hipHostMalloc(&c->pinned, 4096, hipHostMallocDefault));
+  HIPCHK(hipMalloc(&c->aux, GRID_AUX_BYTES));
+  c->ncu = prop.multiProcessorCount;
   for (auto &e : c->ev) HIPCHK(hipEventCreate(&e));
   *out = c;
   return GRID_OK;
@@ -69,6 +71,8 @@ int grid_ctx_destroy(grid_ctx *ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+  if (ctx->aux) (void)hipFree(ctx->aux);
+  delete[] ctx->aux_tiles_host;
   for (auto &e : ctx->ev) (void)hipEventDestroy(e);
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
   delete ctx;

@@ -231,7 +231,7 @@ __device__ __forceinline__ const char *sgpr_ptr(const char *p) {
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
   return reinterpret_cast<const char *>((uintptr_t)(((uint64_t)hi << 32) | lo));
 }
-__device__ void tile_blocked6(int t, int nt, int ni, int &I, int &tj) {
+__host__ __device__ void tile_blocked6(int t, int nt, int ni, int &I, int &tj) {
   const int nbI = (ni + GI6 - 1) / GI6;
   for (int bi = 0; bi < nbI; bi++) {
     const int i0 = bi * GI6, i1 = min(ni, i0 + GI6);
@@ -253,37 +253,18 @@ __device__ void tile_blocked6(int t, int nt, int ni, int &I, int &tj) {
   I = 0; tj = 0;
 }
 
-// MODE 0: production.  Timing probes (wrong results, tools/bench_gram.py):
-// 1 every tile reads the same panels (all L2 hits); 2 = 1 without the flush;
-// 4 = 1 with half the fragment reads; 5 = 1 without any global loads;
-// 3 = production without the XCD remap.  MB = 32-row A blocks per wave:
-// 2 -> 8 waves (4x2 grid, 64x64 each, two waves per SIMD); 4 -> 4 waves
-// (128x64 each; needs more than the 512 registers hipcc will give it).
+// One workgroup's pass over K-steps [s0, s1) of output tile (I, tj): fp32
+// MFMA chunks flushed exactly into iacc (which the caller keeps or drains).
 template <int MODE, int SPLIT, int MB>
-__global__ __launch_bounds__(MB == 2 ? 512 : 256, 1) void k_gram6(const uint16_t *__restrict__ z, int64_t ld,
-                                                                  int nt, int ni, int ntiles, int64_t nsteps,
-                                                                  int sps, int64_t np_,
-                                                                  unsigned long long *__restrict__ gram) {
+__device__ __forceinline__ void g6_run(const uint16_t *__restrict__ z, int64_t ld, int I, int tj, int64_t s0,
+                                       int64_t s1, char *smem, f32x16 (&acc)[MB][2],
+                                       int32_t (&iacc)[MB][2][16]) {
   constexpr int NW = MB == 2 ? 8 : 4;           // waves
   constexpr int RA = BM3 / NW, RB = BN3 / NW;   // DMA rows per wave (A, B)
   constexpr int UA = RA / 8, UB = RB / 8;       // 1-KiB DMA pieces per wave (A, B)
   constexpr int NDMA = UA + UB;                 // DMA instructions per wave per K-step
   constexpr int NF = MB + 2;                    // fragments per sub-step
   constexpr int FSP = 16 / (2 * MB);            // sub-steps between block flushes
-  __shared__ __attribute__((aligned(16))) char smem[3 * SLOT3];
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, loc = bid >> 3;
-  const int q8 = nwg >> 3, r8 = nwg & 7;
-  const int wid = MODE == 3 ? bid : (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
-  const int slice = wid / ntiles;
-  int I = 0, tj = 0;
-  tile_blocked6(wid - slice * ntiles, nt, ni, I, tj);
-  if (MODE == 1 || MODE == 2 || MODE == 4 || MODE == 5) { I = 0; tj = 0; }
-  const int64_t s0 = (int64_t)slice * sps;
-  int64_t s1 = s0 + sps;
-  if (s1 > nsteps) s1 = nsteps;
-
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
@@ -308,14 +289,6 @@ __global__ __launch_bounds__(MB == 2 ? 512 : 256, 1) void k_gram6(const uint16_t
 #pragma unroll
   for (int nn = 0; nn < 2; nn++) offb[nn] = BM3 * 128 + lds_off(wc * 64 + nn * 32 + (lane & 31), lane >> 5);
 
-  f32x16 acc[MB][2];
-  int32_t iacc[MB][2][16];
-#pragma unroll
-  for (int a = 0; a < MB; a++)
-#pragma unroll
-    for (int b = 0; b < 2; b++)
-#pragma unroll
-      for (int r = 0; r < 16; r++) { acc[a][b][r] = 0.0f; iacc[a][b][r] = 0; }
   const f32x16 zero16 = {};
   uint4 fr0[NF], fr1[NF];
 
@@ -434,6 +407,14 @@ __global__ __launch_bounds__(MB == 2 ? 512 : 256, 1) void k_gram6(const uint16_t
 #undef G6_MFMA
 #undef G6_STEP
 #undef G6_FLUSH
+}
+
+// Drain iacc into the int64 Gram (order-free integer atomics) and clear it.
+template <int MB>
+__device__ __forceinline__ void g6_atomics(int32_t (&iacc)[MB][2][16], int I, int tj, int64_t np_,
+                                           unsigned long long *__restrict__ gram) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
 #pragma unroll
   for (int a = 0; a < MB; a++)
 #pragma unroll
@@ -444,7 +425,106 @@ __global__ __launch_bounds__(MB == 2 ? 512 : 256, 1) void k_gram6(const uint16_t
         int col = tj * BN3 + wc * 64 + b * 32 + (lane & 31);
         int32_t v = iacc[a][b][r];
         if (v != 0) atomicAdd(gram + (int64_t)row * np_ + col, (unsigned long long)(long long)v);
+        iacc[a][b][r] = 0;
       }
+}
+
+template <int MB>
+__device__ __forceinline__ void g6_zero(f32x16 (&acc)[MB][2], int32_t (&iacc)[MB][2][16]) {
+#pragma unroll
+  for (int a = 0; a < MB; a++)
+#pragma unroll
+    for (int b = 0; b < 2; b++)
+#pragma unroll
+      for (int r = 0; r < 16; r++) { acc[a][b][r] = 0.0f; iacc[a][b][r] = 0; }
+}
+
+// MODE 0: production.  Timing probes (wrong results, tools/bench_gram.py):
+// 1 every tile reads the same panels (all L2 hits); 2 = 1 without the flush;
+// 4 = 1 with half the fragment reads; 5 = 1 without any global loads;
+// 3 = production without the XCD remap.  MB = 32-row A blocks per wave:
+// 2 -> 8 waves (4x2 grid, 64x64 each, two waves per SIMD); 4 -> 4 waves
+// (128x64 each; needs more than the 512 registers hipcc will give it).
+template <int MODE, int SPLIT, int MB>
+__global__ __launch_bounds__(MB == 2 ? 512 : 256, 1) void k_gram6(const uint16_t *__restrict__ z, int64_t ld,
+                                                                  int nt, int ni, int ntiles, int64_t nsteps,
+                                                                  int sps, int64_t np_,
+                                                                  unsigned long long *__restrict__ gram) {
+  __shared__ __attribute__((aligned(16))) char smem[3 * SLOT3];
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, loc = bid >> 3;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int wid = MODE == 3 ? bid : (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const int slice = wid / ntiles;
+  int I = 0, tj = 0;
+  tile_blocked6(wid - slice * ntiles, nt, ni, I, tj);
+  if (MODE == 1 || MODE == 2 || MODE == 4 || MODE == 5) { I = 0; tj = 0; }
+  const int64_t s0 = (int64_t)slice * sps;
+  int64_t s1 = s0 + sps;
+  if (s1 > nsteps) s1 = nsteps;
+  f32x16 acc[MB][2];
+  int32_t iacc[MB][2][16];
+  g6_zero<MB>(acc, iacc);
+  g6_run<MODE, SPLIT, MB>(z, ld, I, tj, s0, s1, smem, acc, iacc);
+  g6_atomics<MB>(iacc, I, tj, np_, gram);
+}
+
+// Persistent variant: one workgroup per CU, XCD x = blockIdx % 8 (placement
+// is a performance assumption only; results never depend on it).  XCD x owns
+// K-steps [x*S/8, (x+1)*S/8) split into kc chunks; its 32 workgroups walk the
+// units (tile group g of 32 tiles, chunk c, tile) in ROUNDS of 32, so in any
+// round they all read the same K range of the same few A/B panels and the
+// XCD's L2 serves each panel byte to up to 8 workgroups.  A bounded spin on a
+// per-XCD round counter keeps the 32 in step (never a correctness barrier).
+// Every unit is at most sps_max K-steps (int32-exact) and drains its iacc.
+__global__ __launch_bounds__(512, 1) void k_gram7(const uint16_t *__restrict__ z, int64_t ld,
+                                                  const int32_t *__restrict__ tiles, int ntiles, int kc,
+                                                  int64_t nsteps, int lag, int spin_ticks,
+                                                  int64_t np_, unsigned long long *__restrict__ gram,
+                                                  unsigned *__restrict__ rounds) {
+  __shared__ __attribute__((aligned(16))) char smem[3 * SLOT3];
+  constexpr int MB = 2;
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, l = bid >> 3;
+  const int per = nwg >> 3;                       // workgroups per XCD (grid is a multiple of 8)
+  const int64_t xs0 = nsteps * xcd / 8, xs1 = nsteps * (xcd + 1) / 8;
+  const int64_t xlen = xs1 - xs0;
+  const int64_t units = (int64_t)ntiles * kc;
+  for (int64_t r = 0;; r++) {
+    const int64_t u = r * per + l;
+    if (u >= units) break;
+    // unit -> (group, chunk, tile)
+    const int64_t g = u / ((int64_t)per * kc);
+    const int64_t gbase = g * per;
+    const int gsz = (int)min((int64_t)per, (int64_t)ntiles - gbase);
+    const int64_t v = u - g * (int64_t)per * kc;
+    const int c = (int)(v / gsz);
+    const int t = (int)(gbase + v % gsz);
+    const int32_t tv = tiles[t];
+    const int I = tv >> 16, tj = tv & 0xFFFF;
+    const int64_t s0 = xs0 + xlen * c / kc, s1 = xs0 + xlen * (c + 1) / kc;
+    // pace: wait (bounded) until the XCD's round r - lag is complete
+    if (r >= lag && threadIdx.x == 0) {
+      const unsigned need = (unsigned)((r - lag + 1) * per);
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(rounds + xcd * 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+        __builtin_amdgcn_s_sleep(2);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)spin_ticks) break;
+      }
+    }
+    __syncthreads();
+    if (s1 > s0) {
+      f32x16 acc[MB][2];
+      int32_t iacc[MB][2][16];
+      g6_zero<MB>(acc, iacc);
+      g6_run<0, 1, MB>(z, ld, I, tj, s0, s1, smem, acc, iacc);
+      g6_atomics<MB>(iacc, I, tj, np_, gram);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(rounds + xcd * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 constexpr int SELCAP = 4096;
@@ -578,9 +658,10 @@ int grid_knn_gram(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t kpad
   const int64_t nwg = nslices * ntiles;
   REQUIRE(nwg < (1ll << 31), "too many work items");
   // GRID_GRAM_VARIANT: A/B switch and timing probes for tools/bench_gram.py
+  // (7 = persistent XCD-paced k_gram7, the default; 6 = k_gram6 grid)
   const char *ve = getenv("GRID_GRAM_VARIANT");
-  const int variant = ve ? atoi(ve) : 6;
-  if (variant >= 6 && np_ % BM3 == 0) {
+  const int variant = ve ? atoi(ve) : 7;
+  if (variant >= 6 && variant != 7 && np_ % BM3 == 0) {
     // 256x128 tiles; 4-step fp32 chunks stay exact: 4 * 64 * qmax^2 < 2^24 for qmax <= 256
     const int ni = (int)(np_ / BM3);
     int nt6 = 0;
@@ -589,11 +670,49 @@ int grid_knn_gram(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t kpad
     if (sps6 > sps_max) sps6 = sps_max;
     const int64_t nsl6 = ceil_div(nsteps, sps6);
     REQUIRE(nsl6 * nt6 < (1ll << 31), "too many work items");
-    // 6 production; 7, 8, 14, 15 timing probes (wrong results, see k_gram6); 11 without the XCD remap
-    auto kern = variant == 7 ? k_gram6<1, 1, 2> : variant == 8 ? k_gram6<2, 1, 2> : variant == 11 ? k_gram6<3, 1, 2>
+    // 6 production; 8, 14, 15 timing probes (wrong results, see k_gram6); 11 without the XCD remap
+    auto kern = variant == 8 ? k_gram6<2, 1, 2> : variant == 11 ? k_gram6<3, 1, 2>
               : variant == 14 ? k_gram6<4, 1, 2> : variant == 15 ? k_gram6<5, 1, 2> : k_gram6<0, 1, 2>;
     hipLaunchKernelGGL(kern, dim3((unsigned)(nsl6 * nt6)), dim3(512), 0, ctx->stream, d_zb, ld, nt, ni, nt6,
                        nsteps, (int)sps6, np_, (unsigned long long *)d_gram);
+  } else if (variant == 7 && np_ % BM3 == 0) {
+    // persistent, XCD-paced (k_gram7): one 512-thread workgroup per CU
+    const int ni = (int)(np_ / BM3);
+    int nt6 = 0;
+    for (int i = 0; i < ni; i++) nt6 += nt - 2 * i;
+    REQUIRE((size_t)nt6 * 4 <= GRID_AUX_BYTES / 2, "too many Gram tiles");
+    if (ctx->aux_tiles_n != nt6 || !ctx->aux_tiles_host) {
+      delete[] ctx->aux_tiles_host;
+      ctx->aux_tiles_host = new int32_t[nt6];
+      for (int t = 0; t < nt6; t++) {
+        int I = 0, tj = 0;
+        tile_blocked6(t, nt, ni, I, tj);
+        ctx->aux_tiles_host[t] = (I << 16) | tj;
+      }
+      HIPCHK(hipMemcpyAsync(ctx->aux, ctx->aux_tiles_host, (size_t)nt6 * 4, hipMemcpyHostToDevice, ctx->stream));
+      HIPCHK(hipStreamSynchronize(ctx->stream));
+      ctx->aux_tiles_n = nt6;
+    }
+    unsigned *rounds = (unsigned *)((char *)ctx->aux + GRID_AUX_BYTES / 2);
+    HIPCHK(hipMemsetAsync(rounds, 0, 8 * 16 * 4, ctx->stream));
+    const int per = ctx->ncu >= 8 ? ctx->ncu / 8 : 1;
+    const int64_t xlen = ceil_div(nsteps, 8);   // longest XCD range
+    // chunks per XCD: each chunk <= sps_max steps; pick the count that wastes
+    // the fewest workgroup-rounds
+    const int64_t kcmin = ceil_div(xlen, sps_max);
+    int64_t kc = kcmin, best = -1;
+    for (int64_t c = kcmin; c < kcmin + 32; c++) {
+      const int64_t units = (int64_t)nt6 * c;
+      const int64_t waste = ceil_div(units, per) * per - units;
+      // waste fraction compared as waste/units (cross-multiplied)
+      if (best < 0 || waste * (nt6 * kc) < best * units) { best = waste; kc = c; }
+    }
+    const char *le = getenv("GRID_GRAM_LAG"), *se = getenv("GRID_GRAM_SPIN"), *ke = getenv("GRID_GRAM_KC");
+    const int lag = le ? atoi(le) : 1, spin = se ? atoi(se) : 20000;
+    if (ke) kc = atoi(ke) > kc ? atoi(ke) : kc;
+    hipLaunchKernelGGL(k_gram7, dim3((unsigned)(8 * per)), dim3(512), 0, ctx->stream, d_zb, ld,
+                       (const int32_t *)ctx->aux, nt6, (int)kc, nsteps, lag, spin, np_,
+                       (unsigned long long *)d_gram, rounds);
   } else {
     hipLaunchKernelGGL(k_gram_dma, dim3((unsigned)nwg), dim3(NT), 0, ctx->stream, d_zb, ld, nt, ntiles, nsteps,
                        (int)sps, fs, np_, (unsigned long long *)d_gram, variant == 4 ? 1 : 0);

@@ -252,6 +252,55 @@ def _read_all(individuals, mosdepth_dir, chromosome, start, end, excluded, threa
 
 def ingest(individuals, mosdepth_dir, chromosome, start, end, excluded, min_depth, max_depth, threads,
            console=None):
+    """R1-R4 (:218-416): mosdepth files -> (ids, regions, int32 hundredths).
+    The host C++ parser (``grid_ingest_*``, grid_amd/csrc/ingest.cpp) does
+    it with one multithreaded parse per file; a cohort whose text leaves the
+    strict mosdepth grammar (or a non-integer window) goes through the
+    line-by-line restatement ``ingest_py`` instead."""
+    ints = all(v is None or (isinstance(v, int) and not isinstance(v, bool)) for v in (start, end))
+    if ints:
+        try:
+            return ingest_native(individuals, mosdepth_dir, chromosome, start, end, excluded, min_depth,
+                                 max_depth, threads, console)
+        except _abi.IngestUnsupported as e:
+            msg = f"native mosdepth parser: {e}; using the line-by-line parser"
+            log(console, msg, style="warning") if console else print(msg)
+    return ingest_py(individuals, mosdepth_dir, chromosome, start, end, excluded, min_depth, max_depth,
+                     threads, console)
+
+
+def ingest_native(individuals, mosdepth_dir, chromosome, start, end, excluded, min_depth, max_depth, threads,
+                  console=None):
+    """R1-R4 on the host C++ parser (see ``ingest``)."""
+    inds = list(individuals)
+    paths = []
+    for ind in inds:
+        p = find_bed_gz_for_individual(ind, mosdepth_dir)
+        paths.append(str(p) if p.exists() else None)
+    window = (start, end) if start is not None and end is not None else None
+    ing = _abi.Ingest(paths, norm_chrom(chromosome) if chromosome else None, window, excluded or {},
+                      min_depth, max_depth, threads=max(1, int(threads or 1)))
+    try:
+        keep = {ind: i for i, ind in enumerate(inds) if ing.status[i] == 0 and ing.nvalid[i] > 0}
+        removed = len(inds) - len(keep)
+        if removed > 0:                       # filter_empty_samples (:576-600)
+            msg = f"Removed {removed} samples with 0 regions"
+            log(console, msg, style="warning") if console else print(msg)
+        ids = sorted(keep)
+        rof = np.full(len(inds), -1, dtype=np.int32)
+        for r, ind in enumerate(ids):
+            rof[keep[ind]] = r
+        q = ing.fill(rof) if ids else np.zeros((0, ing.m), dtype=np.int32)
+        regions = list(zip(ing.starts.tolist(), ing.ends.tolist())) if ids else []
+        if not ids:
+            q = np.zeros((0, 0), dtype=np.int32)
+        return ids, regions, q
+    finally:
+        ing.close()
+
+
+def ingest_py(individuals, mosdepth_dir, chromosome, start, end, excluded, min_depth, max_depth, threads,
+              console=None):
     """R1-R4 in one parse per file: population means (:218-301) -> valid
     regions (:81-83) -> per-sample extraction (:304-357) -> empty-sample
     filter (:576) -> sorted rows x sorted (start, end) columns (:379-416).

@@ -191,6 +191,41 @@ int grid_synth_depth(grid_ctx *ctx, uint64_t seed, int64_t n, int64_t m, int64_t
 int grid_format_hundredths(const int32_t *h_v, int64_t n, char *h_out, int64_t cap,
                            int64_t *h_len);
 
+/* ---------------------------------------------------- host ingest (R1-R4)
+ * mosdepth *.regions.bed.gz files -> int32-hundredths matrix, replacing the
+ * reference's two Python passes: compute_population_mean_depths
+ * (normalize_mosdepth.py:218-301), process_one_individual (:304-357) and
+ * build_matrix_from_regions (:379-416).  One multithreaded inflate+parse per
+ * file (a second and third only when the parsed records exceed cache_bytes);
+ * population means accumulated in h_paths order (the reference's threads=1
+ * order), valid = min_depth <= mean <= max_depth.
+ *  h_paths[i]    file of sample i (NULL or "" = missing, contributes nothing)
+ *  chrom_prefix  raw-line startswith filter (norm_chrom'd), NULL = none
+ *  has_window    1 = keep end >= start && start <= end (start_bp, end_bp)
+ *  mask          n_mask chromosomes (norm_chrom'd names), kb values of chrom c
+ *                in mask_kb[mask_off[c] .. mask_off[c+1])
+ * Returns GRID_EUNSUPPORTED if a file leaves the strict mosdepth grammar
+ * (the caller then uses its line-by-line restatement).  Per-file status:
+ * 0 ok, 1 failed (the reference drops the sample), 3 missing. */
+typedef struct grid_ingest grid_ingest;
+int grid_ingest_mosdepth(const char *const *h_paths, int64_t n_files, const char *chrom_prefix,
+                         int has_window, int64_t start, int64_t end, int64_t n_mask,
+                         const char *const *mask_chroms, const int64_t *mask_off,
+                         const int64_t *mask_kb, double min_depth, double max_depth, int threads,
+                         int64_t cache_bytes, grid_ingest **out);
+/* columns (valid regions), per-file status and valid-record counts */
+int grid_ingest_summary(const grid_ingest *h, int64_t *n_cols, int32_t *h_file_status,
+                        int64_t *h_nvalid);
+/* sorted (start, end) of the n_cols columns */
+int grid_ingest_columns(const grid_ingest *h, int64_t *h_starts, int64_t *h_ends);
+/* every (start, end) seen and its population mean (size query if cap < n) */
+int grid_ingest_population_means(const grid_ingest *h, int64_t *h_starts, int64_t *h_ends,
+                                 double *h_means, int64_t cap, int64_t *n_keys);
+/* fill rows: h_q[row_of_file[i]*ld + col] (GRID_MISSING elsewhere); -1 = skip */
+int grid_ingest_fill(grid_ingest *h, const int32_t *h_row_of_file, int32_t *h_q, int64_t n_rows,
+                     int64_t ld);
+int grid_ingest_free(grid_ingest *h);
+
 #ifdef __cplusplus
 }
 #endif

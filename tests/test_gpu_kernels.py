@@ -145,7 +145,7 @@ def test_gram_exact_worst_case(dev):
                                       ref[ti*128:(ti+1)*128, tj*128:(tj+1)*128])
 
 
-@pytest.mark.parametrize("variant", ["2", "4", "6", "11"])
+@pytest.mark.parametrize("variant", ["2", "4", "6", "7", "11"])
 def test_gram_variants_multi_slice(dev, variant, monkeypatch):
     """Every Gram kernel variant on a shape with several int32 K-slices, a
     partial last slice (remainder steps not a multiple of 4) and a partial

@@ -1,0 +1,208 @@
+"""Host C++ mosdepth ingest (grid_ingest_*, grid_amd/csrc/ingest.cpp) against
+the line-by-line restatement of normalize_mosdepth.py:218-416 (ingest_py,
+itself pinned to the oracle and the reference's golden cohorts in
+test_host_cpu.py).  CPU only: the ingest is host code."""
+import gzip
+import os
+
+import numpy as np
+import pytest
+
+from grid_amd import _abi
+from grid_amd.utils import normalize_mosdepth as nm
+
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _write(path, lines, gz=True, members=1):
+    data = "".join(lines).encode()
+    if not gz:
+        path.write_bytes(data)
+        return
+    # several gzip members back to back (BGZF-like)
+    cut = [len(data) * i // members for i in range(members + 1)]
+    with open(path, "wb") as f:
+        for a, b in zip(cut, cut[1:]):
+            f.write(gzip.compress(data[a:b]))
+
+
+def _cohort(tmp_path, files, gz=True, members=1):
+    d = tmp_path / "md"
+    d.mkdir()
+    for name, lines in files.items():
+        _write(d / f"{name}.regions.bed.gz", lines, gz=gz, members=members)
+    return d
+
+
+def _both(d, samples, chrom=None, start=None, end=None, excluded=None, lo=20, hi=100, threads=3, **kw):
+    inds = nm.map_mosdepth_files_to_samples(d, samples)
+    ex = excluded or {}
+    a = nm.ingest_native(inds, d, chrom, start, end, ex, lo, hi, threads, **kw)
+    b = nm.ingest_py(inds, d, chrom, start, end, ex, lo, hi, threads)
+    return a, b
+
+
+def _same(a, b):
+    assert a[0] == b[0]
+    assert a[1] == b[1]
+    assert a[2].shape == b[2].shape and np.array_equal(a[2], b[2])
+
+
+def _rand_lines(rng, n, chrom="chr1", step=1000, lo=5.0, hi=120.0):
+    out = []
+    for i in range(n):
+        d = rng.uniform(lo, hi)
+        out.append(f"{chrom}\t{i * step}\t{(i + 1) * step}\t{d:.2f}\n")
+    return out
+
+
+def test_random_cohort_matches(tmp_path):
+    rng = np.random.default_rng(1)
+    files = {f"S{i:03d}": _rand_lines(rng, 3000) for i in range(12)}
+    d = _cohort(tmp_path, files, members=3)
+    a, b = _both(d, sorted(files))
+    _same(a, b)
+    assert a[2].shape[0] == 12 and a[2].shape[1] > 100
+
+
+def test_streaming_mode_matches(tmp_path, monkeypatch):
+    rng = np.random.default_rng(2)
+    files = {f"S{i:03d}": _rand_lines(rng, 2000) for i in range(6)}
+    d = _cohort(tmp_path, files)
+    inds = nm.map_mosdepth_files_to_samples(d, sorted(files))
+    paths = [str(nm.find_bed_gz_for_individual(i, d)) for i in inds]
+    full = _abi.Ingest(paths, None, None, {}, 20, 100, threads=2)
+    stream = _abi.Ingest(paths, None, None, {}, 20, 100, threads=2, cache_bytes=0)
+    rof = np.arange(len(paths), dtype=np.int32)
+    assert np.array_equal(full.fill(rof), stream.fill(rof))
+    assert full.population_means() == stream.population_means()
+
+
+def test_population_means_are_the_reference_chain(tmp_path):
+    """Sums in sample order, fp64, float(text) each (normalize_mosdepth.py:218-301)."""
+    rng = np.random.default_rng(3)
+    files = {f"S{i:03d}": _rand_lines(rng, 500, lo=0.01, hi=3.0) for i in range(25)}
+    d = _cohort(tmp_path, files)
+    inds = nm.map_mosdepth_files_to_samples(d, sorted(files))
+    paths = [str(nm.find_bed_gz_for_individual(i, d)) for i in inds]
+    ing = _abi.Ingest(paths, None, None, {}, 0, 1e9, threads=4)
+    got = ing.population_means()
+    exp = nm.compute_population_mean_depths(inds, d, None, None, None, {}, threads=1)
+    assert got.keys() == exp.keys()
+    assert all(got[k] == exp[k] for k in exp)     # bit-exact
+
+
+def test_quirks_chrom_prefix_window_mask_duplicates(tmp_path):
+    lines_a = [
+        "chr1\t0\t1000\t30.00\n",
+        "chr10\t0\t1000\t55.50\n",          # startswith("chr1") quirk: same (s, e) key, last wins
+        "chr1\t1000\t2000\t40.1\n",
+        "chr1\t2000\t3000\t0.00\n",          # depth 0 dropped
+        "chr1\t3000\t4000\t-5\n",            # negative depth dropped
+        "chr2\t4000\t5000\t44.00\n",         # other chromosome
+        "chr1\t6000\t7000\t35\n",
+        "chr1\t5000\t6000\t33.33\n",         # unsorted
+        "chr1\t7000\t9000\t36.00\n",         # masked (kb 7..9)
+        "chr1\t9500\t9600\t37.00\t\textra\n",
+        "chr1\t12000\t13000\t38.00\t\n",     # trailing tab stripped
+        "short\tline\n",
+        "\n",
+    ]
+    lines_b = [l.replace("30.00", "31.00") for l in lines_a]
+    d = _cohort(tmp_path, {"A": lines_a, "B": lines_b})
+    for chrom in (None, "1", "chr1"):
+        for win in ((None, None), (1500, 9550), (0, 100000)):
+            a, b = _both(d, ["A", "B"], chrom=chrom, start=win[0], end=win[1], excluded={"chr1": {8}})
+            _same(a, b)
+    # with no chromosome filter the "short\tline" text is still < 4 fields -> skipped
+
+
+def test_invalid_number_drops_sample(tmp_path):
+    good = ["chr1\t0\t1000\t30.00\n", "chr1\t1000\t2000\t40.00\n"]
+    bad = ["chr1\t0\t1000\t30.00\n", "chr1\tx\t2000\t40.00\n"]
+    bad2 = ["chr1\t0\t1000\t30.00\n", "chr1\t1000\t2000\t4o.00\n"]
+    d = _cohort(tmp_path, {"A": good, "B": bad, "C": bad2, "D": good})
+    a, b = _both(d, ["A", "B", "C", "D", "E"])       # E: no file
+    _same(a, b)
+    assert a[0] == ["A", "D"]
+
+
+def test_exotic_text_falls_back_identically(tmp_path, capsys):
+    rng = np.random.default_rng(4)
+    base = _rand_lines(rng, 50, lo=20.0, hi=90.0)
+    variants = {
+        "exp": base + ["chr1\t50000\t51000\t3e1\n"],
+        "ws": base + ["chr1\t50000\t51000\t 30.00\n"],
+        "crlf": [l.replace("\n", "\r\n") for l in base],
+        "under": base + ["chr1\t50_000\t51000\t30.00\n"],
+        "decimals": base + ["chr1\t50000\t51000\t30.125\n"],
+        "nan": base + ["chr1\t50000\t51000\tnan\n"],
+    }
+    for k, extra in variants.items():
+        sub = tmp_path / k
+        sub.mkdir()
+        d = _cohort(sub, {"A": base, "B": extra})
+        inds = nm.map_mosdepth_files_to_samples(d, ["A", "B"])
+        with pytest.raises(_abi.IngestUnsupported):
+            nm.ingest_native(inds, d, None, None, None, {}, 20, 100, 2)
+        if k == "decimals":
+            # the reference keeps 30.125 in the matrix -> the int32 path refuses it
+            with pytest.raises(nm.UnsupportedDepth):
+                nm.ingest(inds, d, None, None, None, {}, 20, 100, 2)
+            continue
+        got = nm.ingest(inds, d, None, None, None, {}, 20, 100, 2)
+        _same(got, nm.ingest_py(inds, d, None, None, None, {}, 20, 100, 2))
+
+
+def test_plain_text_and_empty_files(tmp_path):
+    rng = np.random.default_rng(5)
+    d = tmp_path / "md"
+    d.mkdir()
+    _write(d / "A.regions.bed.gz", _rand_lines(rng, 300), gz=False)   # not gzip: Python drops the sample
+    _write(d / "B.regions.bed.gz", _rand_lines(rng, 300))
+    _write(d / "C.regions.bed.gz", [])
+    a, b = _both(d, ["A", "B", "C"])
+    _same(a, b)
+
+
+def test_depth_boundaries_of_the_valid_filter(tmp_path):
+    """Population means landing exactly on min/max depth (inclusive)."""
+    lines = lambda v: [f"chr1\t{i * 1000}\t{(i + 1) * 1000}\t{v[i]}\n" for i in range(len(v))]  # noqa: E731
+    d = _cohort(tmp_path, {"A": lines(["20.00", "100.00", "19.99", "100.01", "20.10"]),
+                           "B": lines(["20.00", "100.00", "20.01", "99.99", "19.90"])})
+    a, b = _both(d, ["A", "B"])
+    _same(a, b)
+    assert len(a[1]) == 5      # every mean lands on 20.0 or 100.0 (inclusive bounds)
+
+
+@pytest.mark.parametrize("name", ["g1", "g1b", "g1c"])
+def test_golden_cohorts_streaming(name, monkeypatch):
+    import yaml
+    with open(os.path.join(G, name, "config.yaml")) as f:
+        c = yaml.safe_load(f)
+    p = lambda r: os.path.join(G, name, r)  # noqa: E731
+    ncfg = c["mosdepth"]["normalize"]
+    samples = [s.strip() for s in open(p(c["samples_file"])) if s.strip()]
+    wd = p(c["mosdepth"]["work_dir"])
+    inds = nm.map_mosdepth_files_to_samples(wd, samples)
+    ex = nm.load_repeat_mask(p(ncfg["repeat_mask_file"]))
+    args = (inds, wd, c.get("chrom"), c.get("start_bp"), c.get("end_bp"), ex, ncfg["min_depth"],
+            ncfg["max_depth"], 4)
+    real = _abi.Ingest.__init__
+    monkeypatch.setattr(_abi.Ingest, "__init__",
+                        lambda self, *a, **k: real(self, *a, **{**k, "cache_bytes": 0}))
+    _same(nm.ingest_native(*args), nm.ingest_py(*args))
+
+
+def test_truncated_and_garbage_gzip_drop_sample(tmp_path):
+    rng = np.random.default_rng(6)
+    d = tmp_path / "md"
+    d.mkdir()
+    _write(d / "A.regions.bed.gz", _rand_lines(rng, 400))
+    _write(d / "B.regions.bed.gz", _rand_lines(rng, 400))
+    blob = (d / "B.regions.bed.gz").read_bytes()
+    (d / "B.regions.bed.gz").write_bytes(blob[: len(blob) // 2])          # truncated
+    _write(d / "C.regions.bed.gz", _rand_lines(rng, 400))
+    a, b = _both(d, ["A", "B", "C"])
+    _same(a, b)
+    assert a[0] == ["A", "C"]
