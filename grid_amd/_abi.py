@@ -58,7 +58,8 @@ _SIGS = {
     "grid_dipcn": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, C.POINTER(_i32)],
     "grid_hi_levels": [_i64, _vp, _vp, _vp, _vp, C.POINTER(_i32)],
     "grid_hi_pack": [_i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp],
-    "grid_hi_phase": [_vp, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp],
+    "grid_hi_phase": [_vp, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
+                      _i32, _i32],
     "grid_synth_depth": [_vp, C.c_uint64, _i64, _i64, _i64, _i64, _i32, _vp],
     "grid_format_hundredths": [_vp, _i64, _vp, _i64, C.POINTER(_i64)],
     "grid_ingest_mosdepth": [_vp, _i64, C.c_char_p, C.c_int, _i64, _i64, _i64, _vp, _vp, _vp, _f64, _f64,
@@ -257,6 +258,7 @@ def hi_levels(off: np.ndarray, nbr: np.ndarray):
 
 
 PACK_CAP = 16
+HI_UNIT_WEIGHTS, HI_LEGACY = 1, 2     # grid_hi_phase flags
 
 
 def hi_schedule(off: np.ndarray, nbr: np.ndarray, w: np.ndarray):
@@ -271,7 +273,9 @@ def hi_schedule(off: np.ndarray, nbr: np.ndarray, w: np.ndarray):
     pk_cnt = np.zeros((max(n, 1), 2), dtype=np.int32)
     call("grid_hi_pack", n, off.ctypes.data, nbr.ctypes.data, w.ctypes.data, order.ctypes.data if n else None,
          PACK_CAP, pk_nbr.ctypes.data, pk_w.ctypes.data, pk_cnt.ctypes.data)
-    return order, loff, nl, pk_nbr, pk_w, pk_cnt
+    lens = np.diff(off) if len(off) > 1 else np.zeros(1, np.int64)
+    flags = HI_UNIT_WEIGHTS if (len(w) == 0 or bool(np.all(np.asarray(w) == 1.0))) else 0
+    return order, loff, nl, pk_nbr, pk_w, pk_cnt, flags, int(lens.max()) if lens.size else 0
 
 
 class IngestUnsupported(GridNativeError):

@@ -3,6 +3,8 @@
 //   step 7: grid/utils/hi_inference.py:175-250 (_run_phasing + _compute_imp)
 #include "common.hpp"
 
+#include <cstdlib>
+
 namespace {
 
 __global__ void k_dipcn(int64_t n, const double *__restrict__ reads, const uint8_t *__restrict__ has,
@@ -295,6 +297,261 @@ __global__ __launch_bounds__(PT) void k_phase(int64_t n, const double *__restric
   if (tid == 0) *mean_out = mean;
 }
 
+
+// Level-schedule phasing, register-pipelined (default when hap fits in LDS).
+// Per chunk of PT schedule entries, thread t owns entry base + t:
+//   1. the NEXT chunk's packed lists are loaded from global memory into a
+//      second register set (no wait: they land while this chunk computes);
+//   2. all 2*CAPT neighbour values are gathered from LDS with unconditional
+//      reads (padding indices are valid), so the gather costs one LDS round
+//      trip instead of one per neighbour;
+//   3. the reference's sequential weighted sums (hi_inference.py:207-217) run
+//      branch-free on registers (selects keep the order and the NaN skips);
+//   4. read barrier, write, write barrier; then `cur = nxt` (the one vmcnt
+//      wait of the chunk, by which time the loads have landed).
+// UNITW: every weight is 1.0 (IBS lists): s + 1.0 and v + 1.0 * x == v + x
+// exactly, so weights are neither loaded nor multiplied.  Lists longer than
+// CAPT take the CSR loop (nbr_means).
+template <bool UNITW, int CAPT>
+struct PhReg {
+  // raw loaded words (decoded only after the load has been waited for, so
+  // issuing the prefetch never stalls on it)
+  int32_t i;        // order[e] (valid only if ok)
+  int32_t c0, c1;   // pk_cnt (< 0: list longer than CAP)
+  int32_t ok;
+  int32_t nb[2][CAPT];
+  double wt[UNITW ? 1 : 2][UNITW ? 1 : CAPT];
+};
+
+template <bool UNITW, int CAPT>
+__device__ __forceinline__ void ph2_fetch(int e, int e1, const int32_t *__restrict__ order,
+                                          const int32_t *__restrict__ pk_nbr, const double *__restrict__ pk_w,
+                                          const int32_t *__restrict__ pk_cnt, PhReg<UNITW, CAPT> &it) {
+  const bool ok = e < e1;
+  const int ee = ok ? e : 0;                       // loads stay unconditional (entry 0 exists)
+  const int32_t oi = order[ee];
+  const int2 c = *reinterpret_cast<const int2 *>(pk_cnt + 2 * (int64_t)ee);
+  const int32_t *pn = pk_nbr + (int64_t)ee * 2 * CAP;
+#pragma unroll
+  for (int h = 0; h < 2; h++)
+#pragma unroll
+    for (int t = 0; t < CAPT; t += 4) {
+      const int4 a = *reinterpret_cast<const int4 *>(pn + h * CAP + t);
+      it.nb[h][t] = a.x; it.nb[h][t + 1] = a.y; it.nb[h][t + 2] = a.z; it.nb[h][t + 3] = a.w;
+    }
+  if (!UNITW) {
+    const double *pw = pk_w + (int64_t)ee * 2 * CAP;
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+#pragma unroll
+      for (int t = 0; t < CAPT; t += 2) {
+        const double2 a = *reinterpret_cast<const double2 *>(pw + h * CAP + t);
+        it.wt[UNITW ? 0 : h][UNITW ? 0 : t] = a.x;
+        it.wt[UNITW ? 0 : h][UNITW ? 0 : t + 1] = a.y;
+      }
+  }
+  it.i = oi;
+  it.c0 = c.x;
+  it.c1 = c.y;
+  it.ok = ok;
+}
+
+// Decode after the wait: entry index (-1 = no entry) and list lengths, with
+// pk_cnt < 0 (longer than CAP) or > CAPT mapped to CAPT + 1 (CSR loop).
+template <bool UNITW, int CAPT>
+__device__ __forceinline__ void ph2_decode(PhReg<UNITW, CAPT> &it) {
+  it.i = it.ok ? it.i : -1;
+  it.c0 = (it.c0 < 0 || it.c0 > CAPT) ? CAPT + 1 : it.c0;
+  it.c1 = (it.c1 < 0 || it.c1 > CAPT) ? CAPT + 1 : it.c1;
+}
+
+template <bool UNITW, int CAPT, int PROBE = 0>
+__global__ __launch_bounds__(PT) void k_phase2(int64_t n, const double *__restrict__ irr,
+                                               const int64_t *__restrict__ off, const int32_t *__restrict__ nbr,
+                                               const double *__restrict__ w, int64_t min_nbr, int64_t iters,
+                                               const int32_t *__restrict__ order, const int32_t *__restrict__ loff,
+                                               int nlev, const int32_t *__restrict__ pk_nbr,
+                                               const double *__restrict__ pk_w, const int32_t *__restrict__ pk_cnt,
+                                               double *hap_g, double *__restrict__ imp,
+                                               double *__restrict__ mean_out) {
+  extern __shared__ __attribute__((aligned(16))) double s_hap[];
+  __shared__ double s_mean;
+  __shared__ double s_unit[CAPT + 1];
+  double *hap = s_hap;
+  if (threadIdx.x == 0) {
+    double u = 1e-9;
+    for (int k = 0; k <= CAPT; k++) {
+      s_unit[k] = u;
+      u = u + 1.0;
+    }
+  }
+  // LDS: hap[2n] | irr[n] | level offsets[nlev+1] | phased flags[n]
+  double *irs = s_hap + 2 * n;
+  int32_t *lof = reinterpret_cast<int32_t *>(s_hap + 3 * n);
+  uint8_t *okf = reinterpret_cast<uint8_t *>(lof + nlev + 1);
+  const int tid = threadIdx.x;
+  for (int64_t i = tid; i < n; i += PT) irs[i] = irr[i];
+  for (int l = tid; l <= nlev; l += PT) lof[l] = loff[l];
+  const double qnan = __builtin_nan("");
+  for (int64_t i = tid; i < n; i += PT) {
+    bool ok = (off[2 * i + 1] - off[2 * i] >= min_nbr) && (off[2 * i + 2] - off[2 * i + 1] >= min_nbr);
+    double v = ok ? irr[i] / 2 : qnan;
+    hap[2 * i] = v;
+    hap[2 * i + 1] = v;
+    okf[i] = ok;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    // mean_IRRs: sequential sum in sample order (hi_inference.py:189-201)
+    double m = 0.0;
+    int64_t c = 0;
+    for (int64_t i = 0; i < n; i++) {
+      if (okf[i]) { m = m + hap[2 * i] * 2.0; c++; }
+    }
+    if (c > 0) m = m / (double)c;
+    s_mean = m;
+  }
+  __syncthreads();
+  // chunk table: one sweep = nch chunks of <= PT entries, none crossing a level
+  // (pointer arithmetic from s_hap, not via an integer, keeps it an LDS pointer)
+  int2 *chk = reinterpret_cast<int2 *>(okf + ((n + 15) & ~15ll) + ((16 - (3 * n * 8 + (nlev + 1) * 4) % 16) % 16));
+  __shared__ int s_nch;
+  if (tid == 0) {
+    int c = 0;
+    for (int l = 0; l < nlev; l++)
+      for (int b = lof[l]; b < lof[l + 1]; b += PT) chk[c++] = make_int2(b, min(b + PT, lof[l + 1]));
+    s_nch = c;
+  }
+  __syncthreads();
+  const int nch = s_nch;
+  if (iters > 0 && nch > 0) {
+    // two register sets: the chunk in work and the next one (in flight)
+    PhReg<UNITW, CAPT> cur, nxt;
+    auto pin = [&](PhReg<UNITW, CAPT> &it) {
+#pragma unroll
+      for (int h = 0; h < 2; h++)
+#pragma unroll
+        for (int t = 0; t < CAPT; t++) asm volatile("" : "+v"(it.nb[h][t]));
+      if (!UNITW) {
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+#pragma unroll
+          for (int t = 0; t < CAPT; t++) asm volatile("" : "+v"(it.wt[UNITW ? 0 : h][UNITW ? 0 : t]));
+      }
+      asm volatile("" : "+v"(it.i), "+v"(it.c0), "+v"(it.c1), "+v"(it.ok));
+      ph2_decode<UNITW, CAPT>(it);
+    };
+    auto fetch = [&](int chunk, PhReg<UNITW, CAPT> &it) {
+      const int2 cb = chk[chunk];
+      ph2_fetch<UNITW, CAPT>(cb.x + tid, cb.y, order, pk_nbr, pk_w, pk_cnt, it);
+    };
+    auto work = [&](PhReg<UNITW, CAPT> &cur) {
+        // wave-uniform count of 4-wide neighbour segments any lane needs
+        const int cmx = cur.i >= 0 ? max(min(cur.c0, CAPT), min(cur.c1, CAPT)) : 0;
+        int nseg = 0;
+#pragma unroll
+        for (int sg = 0; sg < CAPT / 4; sg++) nseg += __ballot(cmx > 4 * sg) != 0;
+        // gather: every needed value in flight at once (one LDS round trip)
+        const int me = cur.i >= 0 ? cur.i : 0;
+        const double hv = hap[2 * me];
+        double x[2][CAPT];
+#pragma unroll
+        for (int sg = 0; sg < CAPT / 4; sg++)
+          if (sg < nseg) {
+#pragma unroll
+            for (int h = 0; h < 2; h++)
+#pragma unroll
+              for (int j = 0; j < 4; j++) x[h][4 * sg + j] = hap[cur.nb[h][4 * sg + j]];
+          }
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+#pragma unroll
+          for (int t = 0; t < CAPT; t++) asm volatile("" : "+v"(x[h][t]));
+        bool upd = false;
+        double n0 = 0.0, n1 = 0.0;
+        if (PROBE != 2 && PROBE != 3 && cur.i >= 0 && hv == hv) {
+          double ws[2], wv[2];
+          if (cur.c0 > CAPT || cur.c1 > CAPT) {
+            nbr_means(cur.i, hap, off, nbr, w, ws, wv);
+          } else {
+            // the reference's sequential sums (hi_inference.py:212-217) as pure
+            // add chains: a skipped term adds +0.0, which is exact here (sw >=
+            // 1e-9 and sv start positive/+0 and never become -0.0)
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+              const int cc = h ? cur.c1 : cur.c0;
+              double sw = 1e-9, sv = 0.0;
+              int k = 0;
+#pragma unroll
+              for (int sg = 0; sg < CAPT / 4; sg++)
+                if (sg < nseg) {
+#pragma unroll
+                  for (int j = 0; j < 4; j++) {
+                    const int t = 4 * sg + j;
+                    const bool take = (t < cc) && (x[h][t] == x[h][t]);
+                    if (UNITW) {
+                      sv = sv + (take ? x[h][t] : 0.0);
+                      k += take;
+                    } else {
+                      const double wt = cur.wt[UNITW ? 0 : h][UNITW ? 0 : t];
+                      const double p = wt * x[h][t];
+                      sw = sw + (take ? wt : 0.0);
+                      sv = sv + (take ? p : 0.0);
+                    }
+                  }
+                }
+              ws[h] = UNITW ? s_unit[k] : sw;   // unit weights: 1e-9 + 1 + ... + 1 (k terms)
+              wv[h] = sv;
+            }
+          }
+          const double m0 = wv[0] / ws[0];
+          const double m1 = wv[1] / ws[1];
+          const double den = m0 + m1;
+          if (den > 0.0) {
+            n0 = irs[cur.i] * m0 / den;
+            n1 = irs[cur.i] * m1 / den;
+            upd = true;
+          }
+        }
+        wg_barrier<true>();
+        if (upd) {
+          hap[2 * cur.i] = n0;
+          hap[2 * cur.i + 1] = n1;
+        }
+        wg_barrier<true>();
+    };
+    const int64_t total = iters * (int64_t)nch;
+    fetch(0, cur);
+    pin(cur);                      // the loop header sees no load pending on cur
+    int c = 0;                     // chunk index within the sweep of chunk g
+    for (int64_t g = 0; g < total; g++) {
+      const int cn = c + 1 == nch ? 0 : c + 1;
+      if (g + 1 < total && PROBE != 1 && PROBE != 3) fetch(cn, nxt);
+      asm volatile("" ::: "memory");   // the prefetch stays issued here (no sinking)
+      work(cur);
+      c = cn;
+      if (PROBE != 1 && PROBE != 3) {
+        pin(nxt);                      // the chunk's one vmcnt wait, after its work
+        cur = nxt;
+      }
+    }
+  }
+  const double mean = s_mean;
+  for (int64_t i = tid; i < n; i += PT) {
+    double ws[2], wv[2];
+    nbr_means(i, hap, off, nbr, w, ws, wv);
+    double i0 = wv[0] / ws[0];
+    double i1 = wv[1] / ws[1];
+    if (ws[0] <= 1e-9) i0 = mean / 2;
+    if (ws[1] <= 1e-9) i1 = mean / 2;
+    imp[2 * i] = i0;
+    imp[2 * i + 1] = i1;
+  }
+  __syncthreads();
+  for (int64_t e = tid; e < 2 * n; e += PT) hap_g[e] = hap[e];
+  if (tid == 0) *mean_out = mean;
+}
+
 }  // namespace
 
 extern "C" {
@@ -346,11 +603,33 @@ int grid_hi_pack(int64_t n, const int64_t *off, const int32_t *nbr, const double
 int grid_hi_phase(grid_ctx *ctx, int64_t n, const double *d_irr, const int64_t *d_off, const int32_t *d_nbr,
                   const double *d_w, int64_t min_nbr, int64_t n_iters, const int32_t *d_order,
                   const int32_t *d_loff, int32_t nlevels, const int32_t *d_pk_nbr, const double *d_pk_w,
-                  const int32_t *d_pk_cnt, double *d_hap, double *d_imp, double *d_mean) {
-  REQUIRE(ctx && n >= 0 && n_iters >= 0 && nlevels >= 0, "bad args");
+                  const int32_t *d_pk_cnt, double *d_hap, double *d_imp, double *d_mean, int32_t flags,
+                  int32_t max_list) {
+  REQUIRE(ctx && n >= 0 && n_iters >= 0 && nlevels >= 0 && max_list >= 0, "bad args");
   if (n == 0) return GRID_OK;
   const size_t lds = (size_t)3 * n * sizeof(double) + (size_t)(nlevels + 1) * 4 + (size_t)n;
-  if (lds <= 120 * 1024) {
+  // k_phase2 adds its chunk table (<= nlevels + n/PT + 1 entries, 16-B aligned)
+  const size_t lds2 = lds + 32 + (size_t)(nlevels + n / PT + 2) * 8;
+  const bool unitw = flags & GRID_HI_UNIT_WEIGHTS;
+  if (lds2 <= 120 * 1024 && !(flags & GRID_HI_LEGACY)) {
+    // register-pipelined kernel; CAPT covers the longest list when it can
+    // GRID_PHASE_PROBE (timing probes, wrong results): 1 = no list prefetch, 2 = no arithmetic
+    const char *pe = getenv("GRID_PHASE_PROBE");
+    const int probe = pe ? atoi(pe) : 0;
+    auto kern = unitw ? (max_list <= 8 ? k_phase2<true, 8> : k_phase2<true, 16>)
+                      : (max_list <= 8 ? k_phase2<false, 8> : k_phase2<false, 16>);
+    if (probe == 1) kern = k_phase2<true, 16, 1>;
+    if (probe == 2) kern = k_phase2<true, 16, 2>;
+    if (probe == 3) kern = k_phase2<true, 16, 3>;
+    static bool attr2[7] = {false, false, false, false, false, false, false};
+    const int slot = probe ? 3 + probe : (unitw ? 2 : 0) + (max_list <= 8 ? 0 : 1);
+    if (!attr2[slot]) {
+      HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024));
+      attr2[slot] = true;
+    }
+    hipLaunchKernelGGL(kern, dim3(1), dim3(PT), lds2, ctx->stream, n, d_irr, d_off, d_nbr, d_w, min_nbr, n_iters,
+                       d_order, d_loff, nlevels, d_pk_nbr, d_pk_w, d_pk_cnt, d_hap, d_imp, d_mean);
+  } else if (lds <= 120 * 1024) {
     static bool attr = false;
     if (!attr) {
       HIPCHK(hipFuncSetAttribute((const void *)k_phase<true>, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -190,17 +190,24 @@ def csr_from_lists(hap_nbrs):
     return off, nbr, w
 
 
+def _legacy_flag() -> int:
+    """GRID_PHASE_LEGACY=1 selects the previous phasing kernel (A/B tests)."""
+    import os
+    return _abi.HI_LEGACY if os.environ.get("GRID_PHASE_LEGACY") == "1" else 0
+
+
 def phase(dev: Device, irr: np.ndarray, off: np.ndarray, nbr: np.ndarray, w: np.ndarray, min_nbr: int,
           n_iters: int):
     n = len(irr)
     if n == 0:
         return np.zeros(0), np.zeros(0), 0.0
-    order, loff, nl, pk_nbr, pk_w, pk_cnt = _abi.hi_schedule(off, nbr, w)
+    order, loff, nl, pk_nbr, pk_w, pk_cnt, flags, max_list = _abi.hi_schedule(off, nbr, w)
     bufs = [dev.upload(np.ascontiguousarray(a)) for a in
             (np.asarray(irr, F8), off.astype(I8), (nbr if nbr.size else np.zeros(1, I4)).astype(I4),
              (w if w.size else np.zeros(1, F8)).astype(F8), order.astype(I4), loff.astype(I4), pk_nbr, pk_w,
              pk_cnt)]
     hap, imp, mean = dev.alloc(2 * n, F8), dev.alloc(2 * n, F8), dev.alloc(1, F8)
     call("grid_hi_phase", dev.ctx, n, bufs[0].ptr, bufs[1].ptr, bufs[2].ptr, bufs[3].ptr, min_nbr, n_iters,
-         bufs[4].ptr, bufs[5].ptr, nl, bufs[6].ptr, bufs[7].ptr, bufs[8].ptr, hap.ptr, imp.ptr, mean.ptr)
+         bufs[4].ptr, bufs[5].ptr, nl, bufs[6].ptr, bufs[7].ptr, bufs[8].ptr, hap.ptr, imp.ptr, mean.ptr,
+         flags | _legacy_flag(), max_list)
     return hap.numpy(), imp.numpy(), float(mean.numpy()[0])

@@ -148,9 +148,9 @@ class HipOps:
         return self.zerodiv.value
 
     def phase(self, n, irr, off, nbr, w, min_nbr, iters, sched, hap, imp, mean):
-        order, loff, nlev, pk_nbr, pk_w, pk_cnt = sched
+        order, loff, nlev, pk_nbr, pk_w, pk_cnt, flags, max_list = sched
         call("grid_hi_phase", self.ctx, n, ptr(irr), ptr(off), ptr(nbr), ptr(w), min_nbr, iters, ptr(order),
-             ptr(loff), nlev, ptr(pk_nbr), ptr(pk_w), ptr(pk_cnt), ptr(hap), ptr(imp), ptr(mean))
+             ptr(loff), nlev, ptr(pk_nbr), ptr(pk_w), ptr(pk_cnt), ptr(hap), ptr(imp), ptr(mean), flags, max_list)
 
     def schedule(self, off, nbr, w):
         return _abi.hi_schedule(off, nbr, w)
@@ -219,13 +219,14 @@ class Steps47:
         """IBS/IBD hap-neighbour CSR; the GS level schedule and the packed,
         schedule-ordered lists are derived once here (input preparation, like
         parsing the neighbour file)."""
-        order, loff, nl, pk_nbr, pk_w, pk_cnt = self.ops.schedule(off, nbr, w)
+        order, loff, nl, pk_nbr, pk_w, pk_cnt, flags, max_list = self.ops.schedule(off, nbr, w)
         up = self.A.upload
         self.off = up(np.asarray(off, I8))
         self.nbr = up(np.asarray(nbr if len(nbr) else np.zeros(1), I4))
         self.w = up(np.asarray(w if len(w) else np.zeros(1), F8))
         self.nlev = nl
-        self.sched = (up(np.asarray(order, I4)), up(np.asarray(loff, I4)), nl, up(pk_nbr), up(pk_w), up(pk_cnt))
+        self.sched = (up(np.asarray(order, I4)), up(np.asarray(loff, I4)), nl, up(pk_nbr), up(pk_w), up(pk_cnt),
+                      flags, max_list)
 
     def set_reads(self, reads):
         self.reads = self.A.upload(np.asarray(reads, F8))

@@ -164,7 +164,9 @@ int grid_dipcn(grid_ctx *ctx, int64_t n, const double *d_reads, const uint8_t *d
  * :229-250.  Hap-neighbour lists in CSR over 2n haplotypes (d_off[2n+1],
  * d_nbr hap indices, d_w weights).  The in-place Gauss-Seidel sweep is run
  * as a level schedule (grid_hi_levels) that is bit-identical to the
- * sequential order.  Outputs hap[2n] (NaN = unphased), imp[2n], *h_mean. */
+ * sequential order.  Outputs hap[2n] (NaN = unphased), imp[2n], *h_mean.
+ * grid_hi_phase flags: GRID_HI_UNIT_WEIGHTS when every weight is 1.0;
+ * max_list = longest list (selects the register capacity of the kernel). */
 int grid_hi_levels(int64_t n, const int64_t *h_off, const int32_t *h_nbr, int32_t *h_order,
                    int32_t *h_level_off, int32_t *h_nlevels);
 /* Host: schedule-ordered packed neighbour lists for the kernel (cap = 16 per
@@ -177,7 +179,9 @@ int grid_hi_phase(grid_ctx *ctx, int64_t n, const double *d_irr, const int64_t *
                   const int32_t *d_nbr, const double *d_w, int64_t min_nbr, int64_t n_iters,
                   const int32_t *d_order, const int32_t *d_level_off, int32_t nlevels,
                   const int32_t *d_pk_nbr, const double *d_pk_w, const int32_t *d_pk_cnt,
-                  double *d_hap, double *d_imp, double *d_mean);
+                  double *d_hap, double *d_imp, double *d_mean, int32_t flags, int32_t max_list);
+#define GRID_HI_UNIT_WEIGHTS 1   /* every weight is 1.0 (IBS lists): weights are not read */
+#define GRID_HI_LEGACY 2         /* A/B: the previous (per-neighbour LDS round trip) kernel */
 
 /* ---------------------------------------------------- synthetic input
  * Counter-based synthetic cohort (bench/smoke input, not a product path):

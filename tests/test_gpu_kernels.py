@@ -224,3 +224,33 @@ def test_phasing_random(dev, n, seed):
     assert mean == em
     ei = [steps.compute_imp(i, eh, hn, em) for i in range(n)]
     assert np.array_equal(imp, np.array(ei).reshape(-1))
+
+
+@pytest.mark.parametrize("weighted,maxlen,legacy", [(False, 6, False), (True, 6, False), (True, 14, False),
+                                                    (False, 40, False), (True, 40, False), (True, 14, True)])
+def test_phasing_kernel_variants(dev, weighted, maxlen, legacy, monkeypatch):
+    """Register capacities 8/16, unit and general weights, lists longer than
+    the packed capacity (CSR loop), and the legacy kernel, vs the oracle."""
+    from grid_amd import engine
+    if legacy:
+        monkeypatch.setenv("GRID_PHASE_LEGACY", "1")
+    rng = np.random.default_rng(maxlen * 2 + weighted)
+    n = 700
+    irr = rng.uniform(0.1, 4.0, n)
+    irr[3] = np.nan
+    hn = []
+    for h in range(2 * n):
+        c = (h // 2) % 13
+        lst = []
+        for _ in range(int(rng.integers(0, maxlen + 1))):
+            j = int(rng.integers(0, n // 13)) * 13 + c
+            wt = float(rng.uniform(0.05, 3.0)) if weighted else 1.0
+            lst.append((min(2 * j + int(rng.integers(0, 2)), 2 * n - 1), wt))
+        hn.append(lst)
+    off, nbr, w = engine.csr_from_lists(hn)
+    hap, imp, mean = engine.phase(dev, irr, off, nbr, w, 1, 15)
+    eh, em = steps.run_phasing(list(irr), hn, 1, 15)
+    assert np.array_equal(hap, np.array(eh), equal_nan=True)
+    assert mean == em or (np.isnan(mean) and np.isnan(em))
+    ei = [steps.compute_imp(i, eh, hn, em) for i in range(n)]
+    assert np.array_equal(imp, np.array(ei).reshape(-1), equal_nan=True)

@@ -1,4 +1,5 @@
-"""Phasing kernel cost vs neighbour-list length (same level structure)."""
+"""Phasing kernel cost vs neighbour-list length (same level structure), the
+register-pipelined kernel against the previous one (GRID_HI_LEGACY)."""
 import os
 import sys
 
@@ -17,7 +18,7 @@ A = TorchAlloc(0)
 reads, off0, nbr0, w0 = bench.synth_reads_and_ibs(n)
 order, loff, nl = _abi.hi_levels(off0, nbr0)        # keep the real schedule
 irr = A.upload(np.random.default_rng(0).uniform(0.5, 3, n))
-for keep in (10, 4, 1, 0):
+for keep in (10, 0):
     # truncate every list to `keep` entries, same schedule
     off = np.zeros_like(off0)
     nb, ww = [], []
@@ -37,14 +38,17 @@ for keep in (10, 4, 1, 0):
     d = [A.upload(x) for x in (off, nb if nb.size else np.zeros(1, np.int32), ww if ww.size else np.zeros(1),
                                order, loff, pk_nbr, pk_w, pk_cnt)]
     hap, imp, mean = A.empty(2 * n, np.float64), A.empty(2 * n, np.float64), A.empty(1, np.float64)
-    ts = []
-    for rep in range(3):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        _abi.call("grid_hi_phase", dev.ctx, n, irr.data_ptr(), d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(),
-                  0, 100, d[3].data_ptr(), d[4].data_ptr(), nl, d[5].data_ptr(), d[6].data_ptr(), d[7].data_ptr(),
-                  hap.data_ptr(), imp.data_ptr(), mean.data_ptr())
-        e1.record()
-        torch.cuda.synchronize()
-        ts.append(e0.elapsed_time(e1))
-    print(f"list len {keep}: {min(ts):.3f} ms -> {min(ts) / (100 * nl) * 1000:.2f} us/level", flush=True)
+    for flags, name, probe in ((1, "k_phase2", "0"), (1 | 2, "legacy", "0"), (1, "probe-noprefetch", "1"),
+                               (1, "probe-noarith", "2"), (1, "probe-barriers-only", "3")):
+        os.environ["GRID_PHASE_PROBE"] = probe
+        ts = []
+        for rep in range(3):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            _abi.call("grid_hi_phase", dev.ctx, n, irr.data_ptr(), d[0].data_ptr(), d[1].data_ptr(),
+                      d[2].data_ptr(), 0, 100, d[3].data_ptr(), d[4].data_ptr(), nl, d[5].data_ptr(),
+                      d[6].data_ptr(), d[7].data_ptr(), hap.data_ptr(), imp.data_ptr(), mean.data_ptr(), flags, keep)
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        print(f"{name} list len {keep}: {min(ts):.3f} ms -> {min(ts) / (100 * nl) * 1000:.2f} us/level", flush=True)
