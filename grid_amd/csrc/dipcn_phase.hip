@@ -477,31 +477,34 @@ __global__ __launch_bounds__(PT) void k_phase2(int64_t n, const double *__restri
             // the reference's sequential sums (hi_inference.py:212-217) as pure
             // add chains: a skipped term adds +0.0, which is exact here (sw >=
             // 1e-9 and sv start positive/+0 and never become -0.0)
+            // both haplotype chains advance together (independent, so their
+            // add latencies overlap)
+            double sw[2] = {1e-9, 1e-9}, sv[2] = {0.0, 0.0};
+            int k[2] = {0, 0};
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-              const int cc = h ? cur.c1 : cur.c0;
-              double sw = 1e-9, sv = 0.0;
-              int k = 0;
+            for (int sg = 0; sg < CAPT / 4; sg++)
+              if (sg < nseg) {
 #pragma unroll
-              for (int sg = 0; sg < CAPT / 4; sg++)
-                if (sg < nseg) {
+                for (int j = 0; j < 4; j++)
 #pragma unroll
-                  for (int j = 0; j < 4; j++) {
+                  for (int h = 0; h < 2; h++) {
                     const int t = 4 * sg + j;
-                    const bool take = (t < cc) && (x[h][t] == x[h][t]);
+                    const bool take = (t < (h ? cur.c1 : cur.c0)) && (x[h][t] == x[h][t]);
                     if (UNITW) {
-                      sv = sv + (take ? x[h][t] : 0.0);
-                      k += take;
+                      sv[h] = sv[h] + (take ? x[h][t] : 0.0);
+                      k[h] += take;
                     } else {
                       const double wt = cur.wt[UNITW ? 0 : h][UNITW ? 0 : t];
                       const double p = wt * x[h][t];
-                      sw = sw + (take ? wt : 0.0);
-                      sv = sv + (take ? p : 0.0);
+                      sw[h] = sw[h] + (take ? wt : 0.0);
+                      sv[h] = sv[h] + (take ? p : 0.0);
                     }
                   }
-                }
-              ws[h] = UNITW ? s_unit[k] : sw;   // unit weights: 1e-9 + 1 + ... + 1 (k terms)
-              wv[h] = sv;
+              }
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+              ws[h] = UNITW ? s_unit[k[h]] : sw[h];   // unit weights: 1e-9 + 1 + ... + 1 (k terms)
+              wv[h] = sv[h];
             }
           }
           const double m0 = wv[0] / ws[0];
