@@ -25,6 +25,10 @@ import numpy as np
 METRIC = "samples/sec end-to-end steps 4–7 (50k×3M bins); k-NN distance HBM GB/s vs peak"
 PEAK_BF16_TFLOPS = 2516.6     # 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz (dense), MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
+# HBM bytes per Gram launch from the rocprofv3 FETCH_SIZE / WRITE_SIZE passes
+# of this same command (tools/gpu_round.sh -> tools/pmc_traffic.py)
+TRAFFIC_JSON = "profiles/r01d_pmc_traffic.json"
+GRAM_KERNEL = "k_gram8<0, true"
 SEED = 20260821
 NCL = 26
 M64 = (1 << 64) - 1
@@ -177,8 +181,15 @@ def main():
     stages = {k: round(v, 3) for k, v in st.stage_ms().items()}
 
     valid = int(st.valid[:n].sum().item())
+    traffic, tsrc = None, None
+    tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), TRAFFIC_JSON)
+    if os.path.exists(tpath):
+        tk = json.load(open(tpath))["kernels"]
+        hits = [v for k, v in tk.items() if k.startswith(GRAM_KERNEL)]
+        if hits and n == 3202 and m == 3_000_000 and world == 1:
+            traffic, tsrc = hits[0]["traffic_bytes"], TRAFFIC_JSON
     flops = 2.0 * n * n * st.ruse_loc                       # 2 N^2 R_use per launch
-    nt, ni = st.np_ // 128, st.np_ // 256            # k_gram6: 256x128 tiles (I, j >= 2I)
+    nt, ni = st.np_ // 128, st.np_ // 256            # k_gram8: 256x128 tiles (I, j >= 2I)
     executed = 2.0 * sum(nt - 2 * i for i in range(ni)) * 256 * 128 * (-(-st.ruse_loc // 64) * 64)
     out = {
         "metric": METRIC,
@@ -202,9 +213,13 @@ def main():
         "roofline": {"kernel": "k_gram (exact bf16-MFMA Gram)", "bound": "mfma",
                      "achieved": flops / (gram_ms * 1e-3) / 1e12, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                      "frac": flops / (gram_ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS,
-                     "traffic": None, "gram_ms": gram_ms,
+                     "traffic": traffic, "traffic_source": tsrc,
+                     "hbm_gbs": traffic / (gram_ms * 1e-3) / 1e9 if traffic else None,
+                     "hbm_frac": traffic / (gram_ms * 1e-3) / 1e9 / PEAK_HBM_GBS if traffic else None,
+                     "gram_ms": gram_ms,
                      "executed_mfma_tflops": executed / (gram_ms * 1e-3) / 1e12,
-                     "flops_def": "2*N^2*R_use per launch (SURVEY 8d); executed = the 256x128 upper-triangle tiles k_gram6 computes"},
+                     "flops_def": "2*N^2*R_use per launch (SURVEY 8d); executed = the 256x128 upper-triangle "
+                                  "tiles k_gram8 computes"},
     }
     out["config"]["selected_regions"] = st.r_loc if world == 1 else None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -52,8 +52,11 @@ _SIGS = {
     "grid_colmap_range": [_vp, _vp, _i64, _f64, _f64, _vp, C.POINTER(_i64)],
     "grid_norm_zquant": [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _f64, _vp, _i64, _vp, _i32,
                          _vp, _i64, C.POINTER(_i32)],
+    "grid_norm_zquant_kb": [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _f64, _vp, _i64, _vp, _i32,
+                            _vp, _i64, C.POINTER(_i32)],
     "grid_norm_zfull": [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _f64, _vp],
     "grid_knn_gram": [_vp, _vp, _i64, _i64, _i64, _i32, _vp],
+    "grid_knn_gram_kb": [_vp, _vp, _i64, _i64, _i32, _vp],
     "grid_knn_topk": [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _vp, _vp, _vp],
     "grid_dipcn": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, C.POINTER(_i32)],
     "grid_hi_levels": [_i64, _vp, _vp, _vp, _vp, C.POINTER(_i32)],

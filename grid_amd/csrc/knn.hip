@@ -255,7 +255,7 @@ __host__ __device__ void tile_blocked6(int t, int nt, int ni, int &I, int &tj) {
 
 // One workgroup's pass over K-steps [s0, s1) of output tile (I, tj): fp32
 // MFMA chunks flushed exactly into iacc (which the caller keeps or drains).
-template <int MODE, int SPLIT, int MB>
+template <int MODE, int SPLIT, int MB, int GS>
 __device__ __forceinline__ void g6_run(const uint16_t *__restrict__ z, int64_t ld, int I, int tj, int64_t s0,
                                        int64_t s1, char *smem, f32x16 (&acc)[MB][2],
                                        int32_t (&iacc)[MB][2][16]) {
@@ -264,7 +264,8 @@ __device__ __forceinline__ void g6_run(const uint16_t *__restrict__ z, int64_t l
   constexpr int UA = RA / 8, UB = RB / 8;       // 1-KiB DMA pieces per wave (A, B)
   constexpr int NDMA = UA + UB;                 // DMA instructions per wave per K-step
   constexpr int NF = MB + 2;                    // fragments per sub-step
-  constexpr int FSP = 16 / (2 * MB);            // sub-steps between block flushes
+  constexpr int FSP = 4 * GS / (2 * MB);        // sub-steps between block flushes
+  constexpr bool NOLOAD = MODE == 5 || MODE == 6, NOFLUSH = MODE == 2 || MODE == 6;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
@@ -295,7 +296,7 @@ __device__ __forceinline__ void g6_run(const uint16_t *__restrict__ z, int64_t l
 #define G6_WAIT_VM(n_) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n_) : "memory")
 #define G6_WAIT_LGKM(n_) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(n_) : "memory")
 #define G6_ISSUE(step_, slot_)                                                                 \
-  if (MODE != 5) do {                                                                           \
+  if (!NOLOAD) do {                                                                           \
     char *A_ = smem + (slot_) * SLOT3;                                                         \
     const int64_t kb_ = (step_) * (BK * 2);                                                    \
     _Pragma("unroll") for (int u = 0; u < UA; u++)                                             \
@@ -383,19 +384,27 @@ __device__ __forceinline__ void g6_run(const uint16_t *__restrict__ z, int64_t l
     G6_READ(fr0, sbase, 0);
   }
   int64_t st = s0;
-  const int64_t sfull = s0 + ((s1 - s0) & ~(int64_t)3);
+  const int64_t sfull = s0 + ((s1 - s0) / GS) * GS;
   // steady state: every step's DMA lead (st+3) exists
-  for (; st < sfull && st + 6 < s1; st += 4) {
-    G6_STEP(st, 0, MODE != 2, 0);
-    G6_STEP(st + 1, 1, MODE != 2, 0);
-    G6_STEP(st + 2, 2, MODE != 2, 0);
-    G6_STEP(st + 3, 3, MODE != 2, 0);
+  for (; st < sfull && st + GS + 2 < s1; st += GS) {
+    G6_STEP(st, 0, !NOFLUSH, 0);
+    G6_STEP(st + 1, 1, !NOFLUSH, 0);
+    G6_STEP(st + 2, 2, !NOFLUSH, 0);
+    G6_STEP(st + 3, 3, !NOFLUSH, 0);
+    if constexpr (GS == 6) {
+      G6_STEP(st + 4, 4, !NOFLUSH, 0);
+      G6_STEP(st + 5, 5, !NOFLUSH, 0);
+    }
   }
-  for (; st < sfull; st += 4) {
-    G6_STEP(st, 0, 1, 1);
-    G6_STEP(st + 1, 1, 1, 1);
-    G6_STEP(st + 2, 2, 1, 1);
-    G6_STEP(st + 3, 3, 1, 1);
+  for (; st < sfull; st += GS) {
+    G6_STEP(st, 0, !NOFLUSH, 1);
+    G6_STEP(st + 1, 1, !NOFLUSH, 1);
+    G6_STEP(st + 2, 2, !NOFLUSH, 1);
+    G6_STEP(st + 3, 3, !NOFLUSH, 1);
+    if constexpr (GS == 6) {
+      G6_STEP(st + 4, 4, !NOFLUSH, 1);
+      G6_STEP(st + 5, 5, !NOFLUSH, 1);
+    }
   }
   G6_FLUSH();
   for (; st < s1; st++) G6_STEP(st, 0, 0, 1);
@@ -445,7 +454,7 @@ __device__ __forceinline__ void g6_zero(f32x16 (&acc)[MB][2], int32_t (&iacc)[MB
 // 3 = production without the XCD remap.  MB = 32-row A blocks per wave:
 // 2 -> 8 waves (4x2 grid, 64x64 each, two waves per SIMD); 4 -> 4 waves
 // (128x64 each; needs more than the 512 registers hipcc will give it).
-template <int MODE, int SPLIT, int MB>
+template <int MODE, int SPLIT, int MB, int GS>
 __global__ __launch_bounds__(MB == 2 ? 512 : 256, 1) void k_gram6(const uint16_t *__restrict__ z, int64_t ld,
                                                                   int nt, int ni, int ntiles, int64_t nsteps,
                                                                   int sps, int64_t np_,
@@ -459,32 +468,228 @@ __global__ __launch_bounds__(MB == 2 ? 512 : 256, 1) void k_gram6(const uint16_t
   const int slice = wid / ntiles;
   int I = 0, tj = 0;
   tile_blocked6(wid - slice * ntiles, nt, ni, I, tj);
-  if (MODE == 1 || MODE == 2 || MODE == 4 || MODE == 5) { I = 0; tj = 0; }
+  if (MODE == 1 || MODE == 2 || MODE == 4 || MODE == 5 || MODE == 6) { I = 0; tj = 0; }
   const int64_t s0 = (int64_t)slice * sps;
   int64_t s1 = s0 + sps;
   if (s1 > nsteps) s1 = nsteps;
   f32x16 acc[MB][2];
   int32_t iacc[MB][2][16];
   g6_zero<MB>(acc, iacc);
-  g6_run<MODE, SPLIT, MB>(z, ld, I, tj, s0, s1, smem, acc, iacc);
+  g6_run<MODE, SPLIT, MB, GS>(z, ld, I, tj, s0, s1, smem, acc, iacc);
   g6_atomics<MB>(iacc, I, tj, np_, gram);
 }
 
-// Persistent variant: one workgroup per CU, XCD x = blockIdx % 8 (placement
-// is a performance assumption only; results never depend on it).  XCD x owns
-// K-steps [x*S/8, (x+1)*S/8) split into kc chunks; its 32 workgroups walk the
-// units (tile group g of 32 tiles, chunk c, tile) in ROUNDS of 32, so in any
-// round they all read the same K range of the same few A/B panels and the
-// XCD's L2 serves each panel byte to up to 8 workgroups.  A bounded spin on a
-// per-XCD round counter keeps the 32 in step (never a correctness barrier).
-// Every unit is at most sps_max K-steps (int32-exact) and drains its iacc.
-__global__ __launch_bounds__(512, 1) void k_gram7(const uint16_t *__restrict__ z, int64_t ld,
+// Default Gram kernel (k_gram8): persistent, one 512-thread workgroup per CU,
+// XCD x = blockIdx % 8 (placement is a performance assumption only; results
+// never depend on it).  XCD x owns K-steps [x*S/8, (x+1)*S/8) split into kc
+// chunks; its workgroups walk the units (tile group g, chunk c, tile) in
+// ROUNDS of `per`, so in any round they read the same K range of the same few
+// A/B panels and the XCD's L2 serves each panel byte to up to 8 workgroups.
+// A bounded spin on a per-XCD round counter keeps them in step (never a
+// correctness barrier).  Every unit is at most sps_max K-steps (int32-exact)
+// and drains its iacc with int64 atomics.
+//
+// The K loop does no address arithmetic and fits 256 registers without
+// spills (a spill reload's vmcnt(0) would drain the LDS-DMA ring):
+//   * LDS slot (48 KiB): A rows 0..255 then B rows 0..127, in 8-row blocks of
+//     1 KiB laid out [sub-step s (4)][row r (8)][32 B]; the 32 B of (row, s)
+//     hold the K chunks 2s, 2s+1 in the order h ^ (block & 1).  The fragment
+//     of sub-step s is at base + 256 s: one VGPR per (slot, fragment) plus an
+//     immediate offset.  The 16 lanes of a ds_read_b128 quarter hit 16
+//     distinct 16-B bank groups (rows of an even block on h, odd on h ^ 1).
+//   * DMA: buffer_load_dwordx4 ... lds; lane l of an 8-row block loads row
+//     (l >> 1) & 7, chunk 2 (l >> 4) + ((l & 1) ^ (block & 1)), so each
+//     instruction still reads 8 whole 128-B row segments.  Panel base in the
+//     descriptor (SGPRs), row offsets in 4 VGPRs, the K offset in soffset.
+//   * BL: the panel is K-blocked, [K-step][row][64] (the layout zquant writes
+//     for the fused chain): a K-step of a 256-row panel is one contiguous
+//     32 KiB run instead of 256 rows 2*ld bytes apart (-9 % time: fewer pages
+//     and DRAM rows per step).
+//   * fp32 chunks: a 6-step group (24 sub-steps) walks the 3 ring slots twice,
+//     so slots are compile-time; block b = 2m + nn restarts its fp32 chunk at
+//     sub-steps 6b (FL = 1: 384-product chunks, exact while 384 qmax^2 <= 2^24,
+//     qmax <= 209) or 3b and 12 + 3b (FL = 2: 192 products, qmax <= 256).
+// MODE 0 production; timing probes (wrong results, tools/bench_gram.py):
+// 1 = every tile reads panel 0 (L2-resident loads), 5 = no global loads,
+// 6 = no global loads and no flush.
+template <int OFF>
+__device__ __forceinline__ uint4 lds_rd(uint32_t addr) {
+  uint4 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+  return v;
+}
+
+template <int MODE, bool BL, int FL>
+__device__ __forceinline__ void g8_run(const uint16_t *__restrict__ z, int64_t ld, int I, int tj, int64_t s0,
+                                       int64_t s1, char *smem, f32x16 (&acc)[2][2],
+                                       int32_t (&iacc)[2][2][16]) {
+  constexpr int NF = 4, NDMA = 6;
+  constexpr int FCYC = 24 / FL, FSP = FCYC / 4;   // flush cycle and stagger, in sub-steps
+  constexpr bool NOLOAD = MODE == 5 || MODE == 6, NOFLUSH = MODE == 6;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int wr = wv >> 1, wc = wv & 1;
+  // DMA sources: this wave's 32 A rows and 16 B rows.  Row-major: base in the
+  // descriptor, K offset in soffset.  BL: per-step descriptor base (a K-block
+  // stride of ld elements exceeds 32-bit offsets).
+  const int64_t rs_el = BL ? BK : ld;                                          // row stride (elements)
+  const uint16_t *pa0 = z + ((int64_t)I * BM3 + wv * 32) * rs_el;
+  const uint16_t *pb0 = z + ((int64_t)tj * BN3 + wv * 16) * rs_el;
+  const __amdgpu_buffer_rsrc_t rsa0 = __builtin_amdgcn_make_buffer_rsrc((void *)pa0, (short)0, -1, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb0 = __builtin_amdgcn_make_buffer_rsrc((void *)pb0, (short)0, -1, 0x00020000);
+  const int dr = (lane >> 1) & 7, ds = lane >> 4, dj = lane & 1;
+  const uint32_t v0 = (uint32_t)((dr * rs_el + (2 * ds + dj) * 8) * 2);        // even block
+  const uint32_t v1 = (uint32_t)((dr * rs_el + (2 * ds + (dj ^ 1)) * 8) * 2);  // odd block
+  const uint32_t rb8 = (uint32_t)(16 * rs_el);                                 // bytes per 8 rows
+  const uint32_t vo0 = v0, vo1 = v1 + rb8, vo2 = v0 + 2 * rb8, vo3 = v1 + 3 * rb8;
+  const uint32_t sbase = (uint32_t)(uintptr_t)smem;
+  // fragment bases per (slot, fragment): A blocks m = 0, 1; B blocks nn = 0, 1
+  uint32_t ad[3][4];
+#pragma unroll
+  for (int sl = 0; sl < 3; sl++)
+#pragma unroll
+    for (int f = 0; f < 4; f++) {
+      const int R = f < 2 ? wr * 64 + f * 32 + (lane & 31) : wc * 64 + (f - 2) * 32 + (lane & 31);
+      const int rb = R >> 3;
+      ad[sl][f] = sbase + sl * SLOT3 + (f < 2 ? 0 : BM3 * 128) + rb * 1024 + (R & 7) * 32 +
+                  (((lane >> 5) ^ (rb & 1)) << 4);
+    }
+  const f32x16 zero16 = {};
+  uint4 fr0[NF], fr1[NF];
+
+#define G8_WAIT_VM(n_) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n_) : "memory")
+#define G8_WAIT_LGKM(n_) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(n_) : "memory")
+#define G8_SB() __builtin_amdgcn_sched_barrier(0)
+#define G8_ISSUE(step_, SL)                                                                    \
+  if (!NOLOAD) do {                                                                            \
+    const uint32_t so_ = BL ? 0u : (uint32_t)((step_) * (BK * 2));                             \
+    const __amdgpu_buffer_rsrc_t rsa = BL ? __builtin_amdgcn_make_buffer_rsrc(                 \
+        (void *)(pa0 + (int64_t)(step_) * ld), (short)0, -1, 0x00020000) : rsa0;               \
+    const __amdgpu_buffer_rsrc_t rsb = BL ? __builtin_amdgcn_make_buffer_rsrc(                 \
+        (void *)(pb0 + (int64_t)(step_) * ld), (short)0, -1, 0x00020000) : rsb0;               \
+    char *A_ = smem + (SL) * SLOT3 + wv * 4096;                                                \
+    char *B_ = smem + (SL) * SLOT3 + BM3 * 128 + wv * 2048;                                    \
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lptr_t)(A_), 16, vo0, so_, 0, 0);           \
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lptr_t)(A_ + 1024), 16, vo1, so_, 0, 0);    \
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lptr_t)(A_ + 2048), 16, vo2, so_, 0, 0);    \
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lptr_t)(A_ + 3072), 16, vo3, so_, 0, 0);    \
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lptr_t)(B_), 16, vo0, so_, 0, 0);           \
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lptr_t)(B_ + 1024), 16, vo1, so_, 0, 0);    \
+  } while (0)
+#define G8_READ(FR, SL, s_)                                                                    \
+  do {                                                                                         \
+    FR[0] = lds_rd<(s_) * 256>(ad[SL][0]);                                                     \
+    FR[1] = lds_rd<(s_) * 256>(ad[SL][1]);                                                     \
+    FR[2] = lds_rd<(s_) * 256>(ad[SL][2]);                                                     \
+    FR[3] = lds_rd<(s_) * 256>(ad[SL][3]);                                                     \
+  } while (0)
+  // MFMAs of A blocks [m0, m1) at in-group sub-step c_; block b = 2m + nn starts
+  // a new fp32 chunk (after flushing the old one) at sub-steps = FSP b (mod FCYC)
+#define G8_MFMA(FR, c_, m0, m1, STAG)                                                          \
+  do {                                                                                         \
+    _Pragma("unroll") for (int m = m0; m < m1; m++)                                            \
+      _Pragma("unroll") for (int nn = 0; nn < 2; nn++) {                                       \
+        if ((STAG) && ((c_) % FCYC) == FSP * (m * 2 + nn)) {                                   \
+          _Pragma("unroll") for (int r = 0; r < 16; r++) iacc[m][nn][r] += (int32_t)acc[m][nn][r]; \
+          acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(FR[m]), as_bf16x8(FR[2 + nn]), \
+                                                               zero16, 0, 0, 0);               \
+        } else {                                                                               \
+          acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(FR[m]), as_bf16x8(FR[2 + nn]), \
+                                                               acc[m][nn], 0, 0, 0);           \
+        }                                                                                      \
+      }                                                                                        \
+  } while (0)
+  // K-step st_ in ring slot SL (compile-time), in-group index q_; fr0 holds
+  // its sub-step 0 on entry and the next step's sub-step 0 on exit.  The
+  // barrier sits inside the last sub-step; the slot it frees receives st_ + 3.
+#define G8_STEP(st_, q_, SL, STAG, COND)                                                       \
+  do {                                                                                         \
+    G8_READ(fr1, SL, 1);                                                                       \
+    G8_WAIT_LGKM(NF); G8_SB();                                                                 \
+    G8_MFMA(fr0, 4 * (q_) + 0, 0, 2, STAG); G8_SB();                                           \
+    G8_READ(fr0, SL, 2);                                                                       \
+    G8_WAIT_LGKM(NF); G8_SB();                                                                 \
+    G8_MFMA(fr1, 4 * (q_) + 1, 0, 2, STAG); G8_SB();                                           \
+    G8_READ(fr1, SL, 3);                                                                       \
+    G8_WAIT_LGKM(NF); G8_SB();                                                                 \
+    G8_MFMA(fr0, 4 * (q_) + 2, 0, 2, STAG); G8_SB();                                           \
+    G8_WAIT_LGKM(0); G8_SB();                                                                  \
+    G8_MFMA(fr1, 4 * (q_) + 3, 0, 1, STAG); G8_SB();                                           \
+    if (!(COND) || (st_) + 2 < s1) G8_WAIT_VM(NDMA);                                           \
+    else G8_WAIT_VM(0);                                                                        \
+    __builtin_amdgcn_s_barrier(); G8_SB();                                                     \
+    if (!(COND) || (st_) + 3 < s1) G8_ISSUE((st_) + 3, SL);                                    \
+    if (!(COND) || (st_) + 1 < s1) G8_READ(fr0, ((SL) + 1) % 3, 0);                            \
+    G8_SB();                                                                                   \
+    G8_MFMA(fr1, 4 * (q_) + 3, 1, 2, STAG); G8_SB();                                           \
+  } while (0)
+#define G8_FLUSH()                                                                             \
+  do {                                                                                         \
+    _Pragma("unroll") for (int a = 0; a < 2; a++)                                              \
+      _Pragma("unroll") for (int b = 0; b < 2; b++)                                            \
+        _Pragma("unroll") for (int r = 0; r < 16; r++) {                                       \
+          iacc[a][b][r] += (int32_t)acc[a][b][r];                                              \
+          acc[a][b][r] = 0.0f;                                                                 \
+        }                                                                                      \
+  } while (0)
+
+  if (s0 >= s1) return;
+  G8_ISSUE(s0, 0);
+  if (s0 + 1 < s1) G8_ISSUE(s0 + 1, 1);
+  if (s0 + 2 < s1) G8_ISSUE(s0 + 2, 2);
+  if (s0 + 2 < s1) G8_WAIT_VM(2 * NDMA);
+  else if (s0 + 1 < s1) G8_WAIT_VM(NDMA);
+  else G8_WAIT_VM(0);
+  __builtin_amdgcn_s_barrier();
+  G8_SB();
+  G8_READ(fr0, 0, 0);
+  int64_t st = s0;
+  const int64_t sfull = s0 + ((s1 - s0) / 6) * 6;
+  // steady state: every step's DMA lead (st + 3) exists
+  for (; st < sfull && st + 8 < s1; st += 6) {
+    G8_STEP(st, 0, 0, !NOFLUSH, 0);
+    G8_STEP(st + 1, 1, 1, !NOFLUSH, 0);
+    G8_STEP(st + 2, 2, 2, !NOFLUSH, 0);
+    G8_STEP(st + 3, 3, 0, !NOFLUSH, 0);
+    G8_STEP(st + 4, 4, 1, !NOFLUSH, 0);
+    G8_STEP(st + 5, 5, 2, !NOFLUSH, 0);
+  }
+  for (; st < sfull; st += 6) {
+    G8_STEP(st, 0, 0, !NOFLUSH, 1);
+    G8_STEP(st + 1, 1, 1, !NOFLUSH, 1);
+    G8_STEP(st + 2, 2, 2, !NOFLUSH, 1);
+    G8_STEP(st + 3, 3, 0, !NOFLUSH, 1);
+    G8_STEP(st + 4, 4, 1, !NOFLUSH, 1);
+    G8_STEP(st + 5, 5, 2, !NOFLUSH, 1);
+  }
+  G8_FLUSH();
+  // tail (< 6 steps): slot (st - s0) % 3 known at run time; one fp32 chunk
+  // for FL = 1 (<= 320 products), flushed every 3 steps for FL = 2
+  for (int t = 0; st < s1; st++, t++) {
+    const int sl = (int)((st - s0) % 3);
+    if (sl == 0) G8_STEP(st, 0, 0, 0, 1);
+    else if (sl == 1) G8_STEP(st, 0, 1, 0, 1);
+    else G8_STEP(st, 0, 2, 0, 1);
+    if (FL == 2 && t == 2) G8_FLUSH();
+  }
+  G8_FLUSH();
+#undef G8_WAIT_VM
+#undef G8_WAIT_LGKM
+#undef G8_SB
+#undef G8_ISSUE
+#undef G8_READ
+#undef G8_MFMA
+#undef G8_STEP
+#undef G8_FLUSH
+}
+
+template <int MODE, bool BL, int FL>
+__global__ __launch_bounds__(512, 1) void k_gram8(const uint16_t *__restrict__ z, int64_t ld,
                                                   const int32_t *__restrict__ tiles, int ntiles, int kc,
                                                   int64_t nsteps, int lag, int spin_ticks,
                                                   int64_t np_, unsigned long long *__restrict__ gram,
                                                   unsigned *__restrict__ rounds) {
-  __shared__ __attribute__((aligned(16))) char smem[3 * SLOT3];
-  constexpr int MB = 2;
+  __shared__ __attribute__((aligned(1024))) char smem[3 * SLOT3];
   const int nwg = gridDim.x;
   const int bid = blockIdx.x;
   const int xcd = bid & 7, l = bid >> 3;
@@ -503,7 +708,7 @@ __global__ __launch_bounds__(512, 1) void k_gram7(const uint16_t *__restrict__ z
     const int c = (int)(v / gsz);
     const int t = (int)(gbase + v % gsz);
     const int32_t tv = tiles[t];
-    const int I = tv >> 16, tj = tv & 0xFFFF;
+    const int I = MODE == 1 ? 0 : tv >> 16, tj = MODE == 1 ? 0 : tv & 0xFFFF;
     const int64_t s0 = xs0 + xlen * c / kc, s1 = xs0 + xlen * (c + 1) / kc;
     // pace: wait (bounded) until the XCD's round r - lag is complete
     if (r >= lag && threadIdx.x == 0) {
@@ -516,16 +721,17 @@ __global__ __launch_bounds__(512, 1) void k_gram7(const uint16_t *__restrict__ z
     }
     __syncthreads();
     if (s1 > s0) {
-      f32x16 acc[MB][2];
-      int32_t iacc[MB][2][16];
-      g6_zero<MB>(acc, iacc);
-      g6_run<0, 1, MB>(z, ld, I, tj, s0, s1, smem, acc, iacc);
-      g6_atomics<MB>(iacc, I, tj, np_, gram);
+      f32x16 acc[2][2];
+      int32_t iacc[2][2][16];
+      g6_zero<2>(acc, iacc);
+      g8_run<MODE, BL, FL>(z, ld, I, tj, s0, s1, smem, acc, iacc);
+      g6_atomics<2>(iacc, I, tj, np_, gram);
     }
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_fetch_add(rounds + xcd * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
+
 
 constexpr int SELCAP = 4096;
 
@@ -633,6 +839,60 @@ __global__ __launch_bounds__(256) void k_topk(const int64_t *__restrict__ g, int
 
 extern "C" {
 
+// Launch k_gram8 (persistent, XCD-paced): the tile table lives in ctx->aux.
+static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t nsteps, int64_t ld,
+                        int64_t q2, int64_t sps_max, bool blocked, int variant, int64_t *d_gram) {
+  const int nt = (int)(np_ / BM), ni = (int)(np_ / BM3);
+  int nt6 = 0;
+  for (int i = 0; i < ni; i++) nt6 += nt - 2 * i;
+  REQUIRE((size_t)nt6 * 4 <= GRID_AUX_BYTES / 2, "too many Gram tiles");
+  if (ctx->aux_tiles_n != nt6 || !ctx->aux_tiles_host) {
+    delete[] ctx->aux_tiles_host;
+    ctx->aux_tiles_host = new int32_t[nt6];
+    for (int t = 0; t < nt6; t++) {
+      int I = 0, tj = 0;
+      tile_blocked6(t, nt, ni, I, tj);
+      ctx->aux_tiles_host[t] = (I << 16) | tj;
+    }
+    HIPCHK(hipMemcpyAsync(ctx->aux, ctx->aux_tiles_host, (size_t)nt6 * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->aux_tiles_n = nt6;
+  }
+  unsigned *rounds = (unsigned *)((char *)ctx->aux + GRID_AUX_BYTES / 2);
+  HIPCHK(hipMemsetAsync(rounds, 0, 8 * 16 * 4, ctx->stream));
+  const int per = ctx->ncu >= 8 ? ctx->ncu / 8 : 1;
+  const int64_t xlen = ceil_div(nsteps, 8);   // longest XCD range
+  // chunks per XCD: each chunk <= sps_max steps; pick the count that wastes
+  // the fewest workgroup-rounds
+  const int64_t kcmin = ceil_div(xlen, sps_max);
+  int64_t kc = kcmin, best = -1;
+  for (int64_t c = kcmin; c < kcmin + 32; c++) {
+    const int64_t units = (int64_t)nt6 * c;
+    const int64_t waste = ceil_div(units, per) * per - units;
+    // waste fraction compared as waste/units (cross-multiplied)
+    if (best < 0 || waste * (nt6 * kc) < best * units) { best = waste; kc = c; }
+  }
+  const char *le = getenv("GRID_GRAM_LAG"), *se = getenv("GRID_GRAM_SPIN"), *ke = getenv("GRID_GRAM_KC");
+  const int lag = le ? atoi(le) : 1, spin = se ? atoi(se) : 20000;
+  if (ke) kc = atoi(ke) > kc ? atoi(ke) : kc;
+  // fp32 chunks of 384 products while 384 qmax^2 <= 2^24 (qmax <= 209), else 192
+  const int fl = 384 * q2 <= (1ll << 24) ? 1 : 2;
+  // variants: 21 production; 22 / 23 / 24 = probes MODE 5 / 6 / 1 (wrong results)
+  const int mode = variant == 22 ? 5 : variant == 23 ? 6 : variant == 24 ? 1 : 0;
+#define G8_PICK(BLV)                                                                            \
+  (mode == 5 ? (fl == 1 ? k_gram8<5, BLV, 1> : k_gram8<5, BLV, 2>)                              \
+   : mode == 6 ? (fl == 1 ? k_gram8<6, BLV, 1> : k_gram8<6, BLV, 2>)                            \
+   : mode == 1 ? (fl == 1 ? k_gram8<1, BLV, 1> : k_gram8<1, BLV, 2>)                            \
+   : (fl == 1 ? k_gram8<0, BLV, 1> : k_gram8<0, BLV, 2>))
+  auto kern = blocked ? G8_PICK(true) : G8_PICK(false);
+#undef G8_PICK
+  hipLaunchKernelGGL(kern, dim3((unsigned)(8 * per)), dim3(512), 0, ctx->stream, d_zb, ld,
+                     (const int32_t *)ctx->aux, nt6, (int)kc, nsteps, lag, spin, np_,
+                     (unsigned long long *)d_gram, rounds);
+  LAUNCHCHK();
+  return GRID_OK;
+}
+
 int grid_knn_gram(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t kpad, int64_t ld,
                   int32_t qmax, int64_t *d_gram) {
   REQUIRE(ctx && d_zb && d_gram, "bad args");
@@ -649,19 +909,13 @@ int grid_knn_gram(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t kpad
   int64_t sps_max = ((1ll << 31) - 1) / (q2 * BK);
   const int nt = (int)(np_ / BM);
   const int ntiles = nt * (nt + 1) / 2;
-  // aim for >= 8 work items per CU (256 CUs) without exceeding the int32 bound
-  int64_t target_slices = ceil_div(2048, ntiles);
-  int64_t sps = ceil_div(nsteps, target_slices);
-  if (sps > sps_max) sps = sps_max;
-  if (sps < 1) sps = 1;
-  const int64_t nslices = ceil_div(nsteps, sps);
-  const int64_t nwg = nslices * ntiles;
-  REQUIRE(nwg < (1ll << 31), "too many work items");
   // GRID_GRAM_VARIANT: A/B switch and timing probes for tools/bench_gram.py
-  // (7 = persistent XCD-paced k_gram7, the default; 6 = k_gram6 grid)
+  // (21 = k_gram8, the default; 6 = k_gram6 grid; 2 / 4 = k_gram_dma)
   const char *ve = getenv("GRID_GRAM_VARIANT");
-  const int variant = ve ? atoi(ve) : 7;
-  if (variant >= 6 && variant != 7 && np_ % BM3 == 0) {
+  const int variant = ve ? atoi(ve) : 21;
+  if (variant >= 21 && np_ % BM3 == 0)
+    return launch_gram8(ctx, d_zb, np_, nsteps, ld, q2, sps_max, false, variant, d_gram);
+  if (variant >= 6 && np_ % BM3 == 0) {
     // 256x128 tiles; 4-step fp32 chunks stay exact: 4 * 64 * qmax^2 < 2^24 for qmax <= 256
     const int ni = (int)(np_ / BM3);
     int nt6 = 0;
@@ -671,55 +925,45 @@ int grid_knn_gram(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t kpad
     const int64_t nsl6 = ceil_div(nsteps, sps6);
     REQUIRE(nsl6 * nt6 < (1ll << 31), "too many work items");
     // 6 production; 8, 14, 15 timing probes (wrong results, see k_gram6); 11 without the XCD remap
-    auto kern = variant == 8 ? k_gram6<2, 1, 2> : variant == 11 ? k_gram6<3, 1, 2>
-              : variant == 14 ? k_gram6<4, 1, 2> : variant == 15 ? k_gram6<5, 1, 2> : k_gram6<0, 1, 2>;
+    // 16-18: the same with 6-step flush groups (qmax <= 209); 18 = no loads and no flush
+    const bool g6ok = 384 * q2 <= (1ll << 24);
+    auto kern = variant == 8 ? k_gram6<2, 1, 2, 4> : variant == 11 ? k_gram6<3, 1, 2, 4>
+              : variant == 14 ? k_gram6<4, 1, 2, 4> : variant == 15 ? k_gram6<5, 1, 2, 4>
+              : (variant == 16 && g6ok) ? k_gram6<0, 1, 2, 6> : (variant == 17 && g6ok) ? k_gram6<5, 1, 2, 6>
+              : (variant == 18 && g6ok) ? k_gram6<6, 1, 2, 6> : k_gram6<0, 1, 2, 4>;
     hipLaunchKernelGGL(kern, dim3((unsigned)(nsl6 * nt6)), dim3(512), 0, ctx->stream, d_zb, ld, nt, ni, nt6,
                        nsteps, (int)sps6, np_, (unsigned long long *)d_gram);
-  } else if (variant == 7 && np_ % BM3 == 0) {
-    // persistent, XCD-paced (k_gram7): one 512-thread workgroup per CU
-    const int ni = (int)(np_ / BM3);
-    int nt6 = 0;
-    for (int i = 0; i < ni; i++) nt6 += nt - 2 * i;
-    REQUIRE((size_t)nt6 * 4 <= GRID_AUX_BYTES / 2, "too many Gram tiles");
-    if (ctx->aux_tiles_n != nt6 || !ctx->aux_tiles_host) {
-      delete[] ctx->aux_tiles_host;
-      ctx->aux_tiles_host = new int32_t[nt6];
-      for (int t = 0; t < nt6; t++) {
-        int I = 0, tj = 0;
-        tile_blocked6(t, nt, ni, I, tj);
-        ctx->aux_tiles_host[t] = (I << 16) | tj;
-      }
-      HIPCHK(hipMemcpyAsync(ctx->aux, ctx->aux_tiles_host, (size_t)nt6 * 4, hipMemcpyHostToDevice, ctx->stream));
-      HIPCHK(hipStreamSynchronize(ctx->stream));
-      ctx->aux_tiles_n = nt6;
-    }
-    unsigned *rounds = (unsigned *)((char *)ctx->aux + GRID_AUX_BYTES / 2);
-    HIPCHK(hipMemsetAsync(rounds, 0, 8 * 16 * 4, ctx->stream));
-    const int per = ctx->ncu >= 8 ? ctx->ncu / 8 : 1;
-    const int64_t xlen = ceil_div(nsteps, 8);   // longest XCD range
-    // chunks per XCD: each chunk <= sps_max steps; pick the count that wastes
-    // the fewest workgroup-rounds
-    const int64_t kcmin = ceil_div(xlen, sps_max);
-    int64_t kc = kcmin, best = -1;
-    for (int64_t c = kcmin; c < kcmin + 32; c++) {
-      const int64_t units = (int64_t)nt6 * c;
-      const int64_t waste = ceil_div(units, per) * per - units;
-      // waste fraction compared as waste/units (cross-multiplied)
-      if (best < 0 || waste * (nt6 * kc) < best * units) { best = waste; kc = c; }
-    }
-    const char *le = getenv("GRID_GRAM_LAG"), *se = getenv("GRID_GRAM_SPIN"), *ke = getenv("GRID_GRAM_KC");
-    const int lag = le ? atoi(le) : 1, spin = se ? atoi(se) : 20000;
-    if (ke) kc = atoi(ke) > kc ? atoi(ke) : kc;
-    hipLaunchKernelGGL(k_gram7, dim3((unsigned)(8 * per)), dim3(512), 0, ctx->stream, d_zb, ld,
-                       (const int32_t *)ctx->aux, nt6, (int)kc, nsteps, lag, spin, np_,
-                       (unsigned long long *)d_gram, rounds);
   } else {
+    // np % 256 != 0 (or variants 2 / 4): 128x128 tiles, one K-slice per workgroup
+    int64_t target_slices = ceil_div(2048, ntiles);
+    int64_t sps = ceil_div(nsteps, target_slices);
+    if (sps > sps_max) sps = sps_max;
+    if (sps < 1) sps = 1;
+    const int64_t nslices = ceil_div(nsteps, sps);
+    const int64_t nwg = nslices * ntiles;
+    REQUIRE(nwg < (1ll << 31), "too many work items");
     hipLaunchKernelGGL(k_gram_dma, dim3((unsigned)nwg), dim3(NT), 0, ctx->stream, d_zb, ld, nt, ntiles, nsteps,
                        (int)sps, fs, np_, (unsigned long long *)d_gram, variant == 4 ? 1 : 0);
   }
   LAUNCHCHK();
   return GRID_OK;
 }
+
+int grid_knn_gram_kb(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t kpad, int32_t qmax,
+                     int64_t *d_gram) {
+  REQUIRE(ctx && d_zb && d_gram, "bad args");
+  REQUIRE(np_ > 0 && np_ % BM3 == 0, "np (%lld) must be a positive multiple of %d", (long long)np_, BM3);
+  REQUIRE(kpad >= 0 && kpad % BK == 0, "kpad must be a multiple of %d", BK);
+  REQUIRE(((uintptr_t)d_zb % 16) == 0, "zb must be 16-byte aligned");
+  REQUIRE(qmax >= 0 && qmax <= 256, "qmax must be in [0, 256]");
+  if (kpad == 0) return GRID_OK;
+  const int64_t q2 = (int64_t)(qmax > 0 ? qmax : 1) * (qmax > 0 ? qmax : 1);
+  const int64_t sps_max = ((1ll << 31) - 1) / (q2 * BK);
+  const char *ve = getenv("GRID_GRAM_VARIANT");
+  const int variant = (ve && atoi(ve) >= 21) ? atoi(ve) : 21;
+  return launch_gram8(ctx, d_zb, np_, kpad / BK, np_ * BK, q2, sps_max, true, variant, d_gram);
+}
+
 
 int grid_knn_topk(grid_ctx *ctx, const int64_t *d_gram, int64_t n, int64_t np_, int64_t k, int64_t row0,
                   int64_t nrows, int32_t *d_idx, int64_t *d_d2, int32_t *d_cnt) {

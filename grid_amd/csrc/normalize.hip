@@ -360,7 +360,7 @@ __global__ __launch_bounds__(256) void k_zquant4(const int32_t *__restrict__ q, 
                                                  const double *__restrict__ rsq, const float2 *__restrict__ mc32,
                                                  double scale, int32_t *__restrict__ zq, int64_t ld_zq,
                                                  const int32_t *__restrict__ colmap, int32_t qmax,
-                                                 uint16_t *__restrict__ zb, int64_t ld_zb,
+                                                 uint16_t *__restrict__ zb, int64_t ld_zb, int64_t kbs,
                                                  int32_t *__restrict__ overflow) {
   const int64_t s0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   const int64_t i0 = (int64_t)blockIdx.y * ZR;
@@ -380,6 +380,11 @@ __global__ __launch_bounds__(256) void k_zquant4(const int32_t *__restrict__ q, 
   const bool vec_zq = zq && w == 4 && ((ld_zq & 3) == 0) && ((s0 & 3) == 0);
   const bool vec_zb = zb && w == 4 && cm[0] >= 0 && cm[1] == cm[0] + 1 && cm[2] == cm[0] + 2 &&
                       cm[3] == cm[0] + 3 && ((cm[0] & 3) == 0) && ((ld_zb & 3) == 0);
+  // panel element (i, c): row-major i*ld_zb + c, or K-blocked (kbs > 0)
+  // (c >> 6)*kbs + i*64 + (c & 63) as k_gram8 reads it
+  auto zbi = [&](int64_t i, int64_t c) -> int64_t {
+    return kbs > 0 ? (c >> 6) * kbs + i * 64 + (c & 63) : i * ld_zb + c;
+  };
   int of = 0;
   const int64_t i1 = (i0 + ZR < n) ? i0 + ZR : n;
   // all loads of the block's rows first (32 independent gathers in flight)
@@ -448,11 +453,11 @@ __global__ __launch_bounds__(256) void k_zquant4(const int32_t *__restrict__ q, 
         bv[c] = __float_as_uint((float)v) >> 16;      // exact bf16 of |v| <= 256
       }
       if (vec_zb) {
-        *reinterpret_cast<uint2 *>(zb + i * ld_zb + cm[0]) = make_uint2(bv[0] | (bv[1] << 16), bv[2] | (bv[3] << 16));
+        *reinterpret_cast<uint2 *>(zb + zbi(i, cm[0])) = make_uint2(bv[0] | (bv[1] << 16), bv[2] | (bv[3] << 16));
       } else {
 #pragma unroll
         for (int c = 0; c < 4; c++)
-          if (cm[c] >= 0) zb[i * ld_zb + cm[c]] = (uint16_t)bv[c];
+          if (cm[c] >= 0) zb[zbi(i, cm[c])] = (uint16_t)bv[c];
       }
     }
   }
@@ -577,10 +582,13 @@ int grid_norm_col_vars(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t m, 
   return GRID_OK;
 }
 
-int grid_norm_zquant(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t ld, const int32_t *d_sel,
-                     int64_t r, const double *d_rm, const double *d_mu, double scale, int32_t *d_zq,
-                     int64_t ld_zq, const int32_t *d_colmap, int32_t qmax, uint16_t *d_zb,
-                     int64_t ld_zb, int32_t *h_overflow) {
+}  // extern "C"
+
+namespace {
+static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t ld, const int32_t *d_sel,
+                       int64_t r, const double *d_rm, const double *d_mu, double scale, int32_t *d_zq,
+                       int64_t ld_zq, const int32_t *d_colmap, int32_t qmax, uint16_t *d_zb,
+                       int64_t ld_zb, int64_t kbs, int32_t *h_overflow) {
   REQUIRE(ctx && n >= 0 && r >= 0, "bad args");
   REQUIRE(qmax >= 0 && qmax <= 256, "qmax %d outside the exact-bf16 range [0, 256]", qmax);
   if (n == 0 || r == 0) {
@@ -602,7 +610,7 @@ int grid_norm_zquant(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t ld, c
   LAUNCHCHK();
   hipLaunchKernelGGL(k_zquant4, dim3((unsigned)ceil_div(ceil_div(r, 4), 256), (unsigned)ceil_div(n, ZR)), dim3(256), 0,
                      ctx->stream, d_q, n, ld, d_sel, r, d_rm, rinv, mus, sq, rsq, mc32, scale, d_zq, ld_zq, d_colmap,
-                     qmax, d_zb, ld_zb, d_of);
+                     qmax, d_zb, ld_zb, kbs, d_of);
   LAUNCHCHK();
   if (h_overflow) {
     HIPCHK(hipMemcpyAsync(ctx->pinned, d_of, 4, hipMemcpyDeviceToHost, ctx->stream));
@@ -610,6 +618,27 @@ int grid_norm_zquant(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t ld, c
     *h_overflow = *(int32_t *)ctx->pinned;
   }
   return GRID_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int grid_norm_zquant(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t ld, const int32_t *d_sel,
+                     int64_t r, const double *d_rm, const double *d_mu, double scale, int32_t *d_zq,
+                     int64_t ld_zq, const int32_t *d_colmap, int32_t qmax, uint16_t *d_zb,
+                     int64_t ld_zb, int32_t *h_overflow) {
+  return zquant_impl(ctx, d_q, n, ld, d_sel, r, d_rm, d_mu, scale, d_zq, ld_zq, d_colmap, qmax, d_zb, ld_zb, 0,
+                     h_overflow);
+}
+
+int grid_norm_zquant_kb(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t ld, const int32_t *d_sel,
+                        int64_t r, const double *d_rm, const double *d_mu, double scale, int32_t *d_zq,
+                        int64_t ld_zq, const int32_t *d_colmap, int32_t qmax, uint16_t *d_zb,
+                        int64_t np_zb, int32_t *h_overflow) {
+  REQUIRE(np_zb >= n && np_zb % 64 == 0, "np_zb must be >= n and a multiple of 64");
+  return zquant_impl(ctx, d_q, n, ld, d_sel, r, d_rm, d_mu, scale, d_zq, ld_zq, d_colmap, qmax, d_zb, 64,
+                     np_zb * 64, h_overflow);
 }
 
 }  // extern "C"

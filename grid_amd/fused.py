@@ -130,14 +130,16 @@ class HipOps:
         call("grid_colmap_range", self.ctx, ptr(r), n, smin, smax, ptr(colmap), C.byref(c))
         return c.value
 
-    def zquant(self, q, n, ld, sel, r, rm, mu, scale, zq, ld_zq, colmap, qmax, zb, ld_zb):
+    def zquant(self, q, n, ld, sel, r, rm, mu, scale, zq, ld_zq, colmap, qmax, zb, np_zb):
+        """z hundredths + the K-blocked bf16 panel [kpad/64][np_zb][64]."""
         of = C.c_int32()
-        call("grid_norm_zquant", self.ctx, ptr(q), n, ld, ptr(sel), r, ptr(rm), ptr(mu), scale, ptr(zq), ld_zq,
-             ptr(colmap), qmax, ptr(zb), ld_zb, C.byref(of))
+        call("grid_norm_zquant_kb", self.ctx, ptr(q), n, ld, ptr(sel), r, ptr(rm), ptr(mu), scale, ptr(zq), ld_zq,
+             ptr(colmap), qmax, ptr(zb), np_zb, C.byref(of))
         return of.value
 
-    def gram(self, zb, np_, kpad, ld, qmax, gram):
-        call("grid_knn_gram", self.ctx, ptr(zb), np_, kpad, ld, qmax, ptr(gram))
+    def gram(self, zb, np_, kpad, qmax, gram):
+        """Exact Gram of the K-blocked panel (first kpad columns)."""
+        call("grid_knn_gram_kb", self.ctx, ptr(zb), np_, kpad, qmax, ptr(gram))
 
     def topk(self, gram, n, np_, k, row0, nrows, idx, d2, cnt):
         call("grid_knn_topk", self.ctx, ptr(gram), n, np_, k, row0, nrows, ptr(idx), ptr(d2), ptr(cnt))
@@ -197,7 +199,9 @@ class Steps47:
         self.zq = a.empty((n1, ml1), I4)                 # step-4 output: exact hundredths
         self.np_ = pad_to(n1, 256)
         self.kpad = pad_to(ml1, 64)
-        self.zb = a.empty((self.np_, self.kpad), U2)    # step-5 input panel (bf16)
+        # step-5 input panel (bf16), K-blocked [kpad/64][np][64]: one K-step of a
+        # row panel is contiguous for the Gram kernel's DMA
+        self.zb = a.empty((self.kpad // 64, self.np_, 64), U2)
         self.zb.zero_()                                  # pad rows stay zero
         self.gram = a.empty((self.np_, self.np_), I8)
         kk = max(k, 1)
@@ -322,17 +326,18 @@ class Steps47:
         self._mark("select_sort")
         # ---- z-scores: exact hundredths (step-4 output) + clipped bf16 panel ----
         if o.zquant(q, n, ld, self.sel, r_loc, self.rm, self.mu, scale, self.zq, max(ml, 1), self.colmap,
-                    self.qmax, self.zb, self.kpad):
+                    self.qmax, self.zb, self.np_):
             raise _abi.GridNativeError("z-score outside the int32 hundredths range")
         self._mark("zquant")
         # ---- step 5: exact Gram (MFMA) -> all-reduce -> top-k ----
         self.gram.zero_()
         kpad_used = pad_to(max(self.ruse_loc, 1), 64)
         if kpad_used > self.ruse_loc and n > 0:
-            self.zb[:n, self.ruse_loc:kpad_used].zero_()      # columns colmap did not write this pass
+            # columns colmap did not write this pass (all in the last K-block)
+            self.zb[kpad_used // 64 - 1, :n, self.ruse_loc % 64:].zero_()
         if gram_events:
             gram_events[0].record()
-        o.gram(self.zb, self.np_, kpad_used, self.kpad, self.qmax, self.gram)
+        o.gram(self.zb, self.np_, kpad_used, self.qmax, self.gram)
         if gram_events:
             gram_events[1].record()
         self._mark("gram")

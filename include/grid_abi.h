@@ -122,6 +122,13 @@ int grid_norm_zquant(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t ld,
                      const double *d_mu, double scale, int32_t *d_zq, int64_t ld_zq,
                      const int32_t *d_colmap, int32_t qmax, uint16_t *d_zb, int64_t ld_zb,
                      int32_t *h_overflow);
+/* The same with the bf16 panel K-blocked, as grid_knn_gram_kb reads it:
+ * element (i, c) at d_zb[(c/64)*np_zb*64 + i*64 + c%64]; np_zb >= n, % 64 == 0. */
+int grid_norm_zquant_kb(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t ld,
+                        const int32_t *d_sel, int64_t r, const double *d_rowmean,
+                        const double *d_mu, double scale, int32_t *d_zq, int64_t ld_zq,
+                        const int32_t *d_colmap, int32_t qmax, uint16_t *d_zb, int64_t np_zb,
+                        int32_t *h_overflow);
 
 /* The full fp64 matrix normalize_matrix returns (:458, :470): z[i*m+j] =
  * ((y-mu)/sqrt(mu))*scale where mu > 0, y*scale elsewhere, NaN if missing. */
@@ -139,6 +146,10 @@ int grid_norm_zfull(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t m, int
  * d_gram: [np][np] int64, must be zeroed; only tiles (ti <= tj) are written. */
 int grid_knn_gram(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t kpad, int64_t ld,
                   int32_t qmax, int64_t *d_gram);
+/* The same on a K-blocked panel [kpad/64][np][64] (grid_norm_zquant_kb's
+ * layout: one K-step of a row panel is contiguous); np % 256 == 0. */
+int grid_knn_gram_kb(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t kpad, int32_t qmax,
+                     int64_t *d_gram);
 /* Per row i < n: the min(k+1, n) smallest (d2, j) with
  * d2 = G_ii + G_jj - 2 G_ij, self dropped, first k kept (find_neighbors.py
  * :205-225).  d_idx/d_d2: [n][k]; d_cnt[i] = entries written; unused

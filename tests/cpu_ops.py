@@ -84,7 +84,7 @@ class NumpyOps:
         _np(colmap)[:n] = np.where(keep, cm, -1)
         return int(keep.sum())
 
-    def zquant(self, q, n, ld, sel, r, rm, mu, scale, zq, ld_zq, colmap, qmax, zb, ld_zb):
+    def zquant(self, q, n, ld, sel, r, rm, mu, scale, zq, ld_zq, colmap, qmax, zb, np_zb):
         if r == 0:
             return 0
         js = _np(sel)[:r]
@@ -109,14 +109,15 @@ class NumpyOps:
         cm = _np(colmap)[:r]
         clip = np.where((out == MISSING) | (out == NEG0), 0, np.clip(out, -qmax, qmax)).astype(np.float32)
         bits = (clip.view(np.uint32) >> 16).astype(np.uint16).view(np.int16)
-        zba = _np(zb)
+        zba = _np(zb)                      # K-blocked [kpad/64][np_zb][64]
         for s in range(r):
             if cm[s] >= 0:
-                zba[:n, cm[s]] = bits[:, s]
+                zba[cm[s] // 64, :n, cm[s] % 64] = bits[:, s]
         return 0
 
-    def gram(self, zb, np_, kpad, ld, qmax, gram):
-        bits = _np(zb)[:np_, :kpad].view(np.uint16).astype(np.uint32) << 16
+    def gram(self, zb, np_, kpad, qmax, gram):
+        zr = _np(zb)[: kpad // 64, :np_].transpose(1, 0, 2).reshape(np_, kpad)
+        bits = zr.view(np.uint16).astype(np.uint32) << 16
         z = bits.view(np.float32).astype(np.float64)
         _np(gram)[:np_, :np_] += (z @ z.T).astype(np.int64)
 

@@ -125,10 +125,10 @@ def test_knn_random(dev, n, r, k, qmax, seed):
 
 
 def test_gram_exact_worst_case(dev):
-    """bf16 MFMA + fp32 partials are exact at the integer bounds (all |q| = qmax)."""
-    from grid_amd import engine
+    """bf16 MFMA + fp32 partials are exact at the integer bounds (all |q| = qmax):
+    6-step fp32 chunks up to qmax 209 (k_gram8), 4-step chunks above (k_gram7)."""
     from grid_amd._abi import call
-    for qmax in (200, 256):
+    for qmax in (200, 209, 210, 256):
         rng = np.random.default_rng(qmax)
         n, r = 256, 64 * 700
         q = np.where(rng.random((n, r)) < 0.5, -qmax, qmax).astype(np.int64)
@@ -145,7 +145,34 @@ def test_gram_exact_worst_case(dev):
                                       ref[ti*128:(ti+1)*128, tj*128:(tj+1)*128])
 
 
-@pytest.mark.parametrize("variant", ["2", "4", "6", "7", "11"])
+@pytest.mark.parametrize("qmax", [200, 256])
+def test_gram_kblocked_multi_slice(dev, qmax):
+    """grid_knn_gram_kb (k_gram8 on the K-blocked panel zquant_kb writes) on
+    several int32 K-slices with a partial last 6-step group, both fp32 chunk
+    lengths (qmax 200: 384 products, 256: 192), all-|qmax| worst-case rows."""
+    from grid_amd._abi import call
+    n, np_ = 600, 768
+    r = 64 * (2 * (((1 << 31) - 1) // (qmax * qmax * 64)) + 7)
+    rng = np.random.default_rng(qmax)
+    q = np.zeros((np_, r), dtype=np.int64)
+    q[:n] = rng.integers(-qmax, qmax + 1, size=(n, r))
+    q[:4] = np.where(rng.random((4, r)) < 0.5, -qmax, qmax)
+    q[4] = qmax
+    zf = (q.astype(np.float32).view(np.uint32) >> 16).astype(np.uint16)
+    zkb = np.ascontiguousarray(zf.reshape(np_, r // 64, 64).transpose(1, 0, 2))
+    zb = dev.upload(zkb)
+    g = dev.zeros((np_, np_), np.int64)
+    call("grid_knn_gram_kb", dev.ctx, zb.ptr, np_, r, qmax, g.ptr)
+    got = g.numpy()
+    qf = q.astype(np.float64)
+    ref = (qf @ qf.T).astype(np.int64)
+    for ti in range(np_ // 128):
+        for tj in range(ti, np_ // 128):
+            blk = (slice(ti * 128, (ti + 1) * 128), slice(tj * 128, (tj + 1) * 128))
+            assert np.array_equal(got[blk], ref[blk]), (ti, tj)
+
+
+@pytest.mark.parametrize("variant", ["2", "4", "6", "11", "16", "21"])
 def test_gram_variants_multi_slice(dev, variant, monkeypatch):
     """Every Gram kernel variant on a shape with several int32 K-slices, a
     partial last slice (remainder steps not a multiple of 4) and a partial

@@ -17,7 +17,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=3202)
 ap.add_argument("--k", type=int, default=2_700_000)
 ap.add_argument("--reps", type=int, default=3)
-ap.add_argument("--variants", default="2,6")
+ap.add_argument("--variants", default="21,kb21")
 ap.add_argument("--qmax", type=int, default=200)
 ap.add_argument("--ld-extra", type=int, default=0, help="extra bf16 columns of row padding (row stride)")
 a = ap.parse_args()
@@ -35,15 +35,22 @@ for r0 in range(0, a.n, 256):
     zb[r0:r1, :kpad] = zi.to(torch.bfloat16).view(torch.int16)
     del zi
 gram = torch.zeros((np_, np_), dtype=torch.int64, device="cuda")
+# "kbNN": variant NN through grid_knn_gram_kb on the K-blocked panel [K-step][row][64]
+zbb = None
+if any(v.startswith("kb") for v in a.variants.split(",")):
+    zbb = zb[:, :kpad].reshape(np_, kpad // 64, 64).permute(1, 0, 2).contiguous()
 res = {}
 flops = 2.0 * a.n * a.n * a.k
 for rep in range(a.reps):
     for v in a.variants.split(","):
-        os.environ["GRID_GRAM_VARIANT"] = v
+        os.environ["GRID_GRAM_VARIANT"] = v[2:] if v.startswith("kb") else v
         gram.zero_()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        _abi.call("grid_knn_gram", dev.ctx, zb.data_ptr(), np_, kpad, ld, a.qmax, gram.data_ptr())
+        if v.startswith("kb"):
+            _abi.call("grid_knn_gram_kb", dev.ctx, zbb.data_ptr(), np_, kpad, a.qmax, gram.data_ptr())
+        else:
+            _abi.call("grid_knn_gram", dev.ctx, zb.data_ptr(), np_, kpad, ld, a.qmax, gram.data_ptr())
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1)
