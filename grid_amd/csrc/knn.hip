@@ -878,6 +878,8 @@ static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_
   // fp32 chunks of 384 products while 384 qmax^2 <= 2^24 (qmax <= 209), else 192
   const int fl = 384 * q2 <= (1ll << 24) ? 1 : 2;
   // variants: 21 production; 22 / 23 / 24 = probes MODE 5 / 6 / 1 (wrong results)
+  // (measured alternatives that lost: register-staged loads + ds_write_b128,
+  // 37.4 vs 31.1 ms; DMA issue spread over the sub-steps, no change)
   const int mode = variant == 22 ? 5 : variant == 23 ? 6 : variant == 24 ? 1 : 0;
 #define G8_PICK(BLV)                                                                            \
   (mode == 5 ? (fl == 1 ? k_gram8<5, BLV, 1> : k_gram8<5, BLV, 2>)                              \

@@ -167,8 +167,15 @@ class Steps47:
     """
 
     def __init__(self, ops, alloc, n, m_total, col0, m_local, *, k=10, n_nbr=300, top_frac=0.1, zmax=2.0,
-                 sigma2_max=1000.0, frac_r=1.0, min_nbr=1, n_iters=100, comm=None):
+                 sigma2_max=1000.0, frac_r=1.0, min_nbr=1, n_iters=100, comm=None, phase_lane=None):
+        """``phase_lane``: optional (ops, torch.cuda.Stream) pair on which step
+        7 runs, ordered after this pass's dipCN by an event; the next pass's
+        dipCN waits for it.  Phasing is one workgroup for ~6 ms, so on its own
+        stream it overlaps the next pass's steps 4-5 instead of idling the
+        other 255 CUs (and, multi-GPU, it no longer adds to every rank's step)."""
         self.ops, self.A, self.comm = ops, alloc, comm
+        self.phase_lane = phase_lane
+        self.ev_phase = None
         self.rank = comm.rank if comm else 0
         self.world = comm.world if comm else 1
         self.n, self.m, self.col0, self.ml = n, m_total, col0, m_local
@@ -356,6 +363,10 @@ class Steps47:
             idx, self.d2, cnt = self.idx_l, self.d2_l, self.cnt_l
         self._mark("topk")
         # ---- step 6: dipCN (scales as printed "%.2f", neighbour gather) ----
+        lane = None if profile else self.phase_lane
+        if lane is not None and self.ev_phase is not None:
+            import torch
+            torch.cuda.current_stream().wait_event(self.ev_phase)   # previous pass's phasing read dip
         o.round_decimals(self.rm, n, 2, self.scale2)
         o.gather(self.scale2, idx, n * max(self.k, 1), self.nscale)
         if o.dipcn(n, self.reads, self.has, self.scale2, idx, self.nscale, cnt, max(self.k, 1), self.n_nbr,
@@ -363,7 +374,18 @@ class Steps47:
             raise ZeroDivisionError("float division by zero")
         self._mark("dipcn")
         # ---- step 7: level-scheduled Gauss-Seidel phasing + imputation ----
-        o.phase(n, self.dip, self.off, self.nbr, self.w, self.min_nbr, self.n_iters, self.sched, self.hap,
-                self.imp, self.mean)
+        if lane is not None:
+            import torch
+            pops, pstream = lane
+            ev = torch.cuda.Event()
+            ev.record()
+            pstream.wait_event(ev)
+            pops.phase(n, self.dip, self.off, self.nbr, self.w, self.min_nbr, self.n_iters, self.sched, self.hap,
+                       self.imp, self.mean)
+            self.ev_phase = torch.cuda.Event()
+            self.ev_phase.record(pstream)
+        else:
+            o.phase(n, self.dip, self.off, self.nbr, self.w, self.min_nbr, self.n_iters, self.sched, self.hap,
+                    self.imp, self.mean)
         self._mark("phase")
         self.idx_out, self.cnt_out = idx, cnt
