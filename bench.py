@@ -131,12 +131,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # GRID_BENCH_SHARE_GPU=1 (rehearsal only): ranks share the visible GPUs
+    # round-robin, with GRID_DIST_BACKEND=gloo since RCCL needs one GPU per rank
+    if os.environ.get("GRID_BENCH_SHARE_GPU") == "1":
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     dist = None
     comm = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("GRID_DIST_BACKEND", "nccl")     # "nccl" = RCCL on ROCm
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
         from grid_amd.fused import TorchComm
         comm = TorchComm(dist)
 

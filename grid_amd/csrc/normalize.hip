@@ -338,7 +338,8 @@ __global__ void k_zprep(const int32_t *__restrict__ sel, int64_t r, const double
   mc32[s] = make_float2((float)m, (float)(100.0 * scale / t));   // fast-path constants (k_zquant4)
 }
 
-constexpr int ZR = 8;    // rows per zquant block
+constexpr int ZR = 8;    // rows per zquant batch
+constexpr int ZRB = 1;   // row batches per thread (4 measured slower: 22.6 vs 20.5 ms)
 
 // 4 consecutive selected columns x ZR rows per thread.
 //
@@ -353,6 +354,27 @@ constexpr int ZR = 8;    // rows per zquant block
 // farther than delta from every half-integer, rint(t') IS k, and when it is
 // also farther than delta from 0 its sign is z's sign ("-0.00").  Otherwise
 // (probability ~1e-4 per cell) the exact fp64 chain below decides.
+// Select element d (0..7) of the 8 consecutive ints (a, b).
+__device__ __forceinline__ int32_t pick8(const int4 &a, const int4 &b, int d) {
+  const int4 h = (d & 4) ? b : a;
+  return (d & 2) ? ((d & 1) ? h.w : h.z) : ((d & 1) ? h.y : h.x);
+}
+
+__device__ __forceinline__ void zquant_rows(const int32_t (&qv)[ZR][4], int64_t s0, int64_t i0, int64_t i1, int w,
+                                            const int32_t (&cm)[4], const float (&m32)[4], const float (&c32)[4],
+                                            const double *__restrict__ rm, const double *__restrict__ rinv,
+                                            const double *__restrict__ mus, const double *__restrict__ sq,
+                                            const double *__restrict__ rsq, double scale,
+                                            int32_t *__restrict__ zq, int64_t ld_zq, int32_t qmax,
+                                            uint16_t *__restrict__ zb, int64_t ld_zb, int64_t kbs,
+                                            int32_t *__restrict__ overflow);
+
+// q reads: a thread's 4 selected columns usually lie within 8 consecutive
+// source columns (the selection keeps ~90 % of them), so each row is read
+// as two aligned int4 loads and the 4 values picked in registers; 4 dword
+// gathers per row (16 B used per 64-B line each) took 2x the HBM time.
+// Threads whose columns spread wider gather them one by one.
+template <bool VEC>
 __global__ __launch_bounds__(256) void k_zquant4(const int32_t *__restrict__ q, int64_t n, int64_t ld,
                                                  const int32_t *__restrict__ sel, int64_t r,
                                                  const double *__restrict__ rm, const double *__restrict__ rinv,
@@ -363,20 +385,65 @@ __global__ __launch_bounds__(256) void k_zquant4(const int32_t *__restrict__ q, 
                                                  uint16_t *__restrict__ zb, int64_t ld_zb, int64_t kbs,
                                                  int32_t *__restrict__ overflow) {
   const int64_t s0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  const int64_t i0 = (int64_t)blockIdx.y * ZR;
   if (s0 >= r) return;
   const int w = (int)((r - s0) < 4 ? (r - s0) : 4);
+  // per-column constants, loaded once for ZRB row batches
   int32_t js[4], cm[4];
   float m32[4], c32[4];
 #pragma unroll
   for (int c = 0; c < 4; c++) {
     const bool ok = c < w;
-    js[c] = ok ? sel[s0 + c] : 0;
+    js[c] = sel[ok ? s0 + c : s0];
     cm[c] = (ok && colmap) ? colmap[s0 + c] : (ok ? (int32_t)(s0 + c) : -1);
     const float2 mc = ok ? mc32[s0 + c] : make_float2(1.0f, 1.0f);
     m32[c] = mc.x;
     c32[c] = mc.y;
   }
+  const int64_t base = js[0] & ~3ll;
+  const bool fast = VEC && js[w - 1] - base < 8 && base + 8 <= ld;
+  int d[4];
+#pragma unroll
+  for (int c = 0; c < 4; c++) d[c] = (int)(js[c] - base);
+  for (int b = 0; b < ZRB; b++) {
+    const int64_t i0 = ((int64_t)blockIdx.y * ZRB + b) * ZR;
+    if (i0 >= n) break;
+    const int64_t i1 = (i0 + ZR < n) ? i0 + ZR : n;
+    int32_t qv[ZR][4];
+    if (fast) {
+      int4 va[ZR], vb[ZR];
+#pragma unroll
+      for (int u = 0; u < ZR; u++) {
+        const int64_t i = (i0 + u < i1) ? i0 + u : i0;
+        const int4 *p = reinterpret_cast<const int4 *>(q + i * ld + base);
+        va[u] = p[0];
+        vb[u] = p[1];
+      }
+#pragma unroll
+      for (int u = 0; u < ZR; u++)
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+          qv[u][c] = (i0 + u < i1 && c < w) ? pick8(va[u], vb[u], d[c]) : GRID_MISSING;
+    } else {
+#pragma unroll
+      for (int u = 0; u < ZR; u++)
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+          qv[u][c] = (i0 + u < i1 && c < w) ? q[(i0 + u) * ld + js[c]] : GRID_MISSING;
+    }
+    zquant_rows(qv, s0, i0, i1, w, cm, m32, c32, rm, rinv, mus, sq, rsq, scale, zq, ld_zq, qmax, zb, ld_zb,
+                kbs, overflow);
+  }
+}
+
+// Quantise ZR rows x 4 selected columns of one thread (qv: the depths).
+__device__ __forceinline__ void zquant_rows(const int32_t (&qv)[ZR][4], int64_t s0, int64_t i0, int64_t i1, int w,
+                                            const int32_t (&cm)[4], const float (&m32)[4], const float (&c32)[4],
+                                            const double *__restrict__ rm, const double *__restrict__ rinv,
+                                            const double *__restrict__ mus, const double *__restrict__ sq,
+                                            const double *__restrict__ rsq, double scale,
+                                            int32_t *__restrict__ zq, int64_t ld_zq, int32_t qmax,
+                                            uint16_t *__restrict__ zb, int64_t ld_zb, int64_t kbs,
+                                            int32_t *__restrict__ overflow) {
   const bool vec_zq = zq && w == 4 && ((ld_zq & 3) == 0) && ((s0 & 3) == 0);
   const bool vec_zb = zb && w == 4 && cm[0] >= 0 && cm[1] == cm[0] + 1 && cm[2] == cm[0] + 2 &&
                       cm[3] == cm[0] + 3 && ((cm[0] & 3) == 0) && ((ld_zb & 3) == 0);
@@ -386,14 +453,6 @@ __global__ __launch_bounds__(256) void k_zquant4(const int32_t *__restrict__ q, 
     return kbs > 0 ? (c >> 6) * kbs + i * 64 + (c & 63) : i * ld_zb + c;
   };
   int of = 0;
-  const int64_t i1 = (i0 + ZR < n) ? i0 + ZR : n;
-  // all loads of the block's rows first (32 independent gathers in flight)
-  int32_t qv[ZR][4];
-#pragma unroll
-  for (int u = 0; u < ZR; u++)
-#pragma unroll
-    for (int c = 0; c < 4; c++)
-      qv[u][c] = (i0 + u < i1 && c < w) ? q[(i0 + u) * ld + js[c]] : GRID_MISSING;
 #pragma unroll
   for (int u = 0; u < ZR; u++) {
     const int64_t i = i0 + u;
@@ -595,7 +654,7 @@ static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t ld,
     if (h_overflow) *h_overflow = 0;
     return GRID_OK;
   }
-  REQUIRE(ceil_div(n, ZR) <= 65535, "n too large for one launch");
+  REQUIRE(ceil_div(n, ZR * ZRB) <= 65535, "n too large for one launch");
   double *rinv;
   char *rest;
   size_t rb = (((size_t)r * 8 + 255) & ~size_t(255));
@@ -608,7 +667,8 @@ static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t ld,
   hipLaunchKernelGGL(k_zprep, dim3((unsigned)ceil_div(r, 256)), dim3(256), 0, ctx->stream, d_sel, r, d_mu, scale, mus,
                      sq, rsq, mc32);
   LAUNCHCHK();
-  hipLaunchKernelGGL(k_zquant4, dim3((unsigned)ceil_div(ceil_div(r, 4), 256), (unsigned)ceil_div(n, ZR)), dim3(256), 0,
+  auto kz = vec4_ok(d_q, ld) ? k_zquant4<true> : k_zquant4<false>;
+  hipLaunchKernelGGL(kz, dim3((unsigned)ceil_div(ceil_div(r, 4), 256), (unsigned)ceil_div(n, ZR * ZRB)), dim3(256), 0,
                      ctx->stream, d_q, n, ld, d_sel, r, d_rm, rinv, mus, sq, rsq, mc32, scale, d_zq, ld_zq, d_colmap,
                      qmax, d_zb, ld_zb, kbs, d_of);
   LAUNCHCHK();

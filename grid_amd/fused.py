@@ -76,15 +76,23 @@ class TorchComm:
         self.dist = dist
         self.rank = dist.get_rank()
         self.world = dist.get_world_size()
+        # gloo with device tensors (multi-rank rehearsal on one GPU): stage on host
+        self.host = dist.get_backend() == "gloo"
 
     def all_gather(self, t):
         import torch
         t = t.contiguous()
-        parts = [torch.empty_like(t) for _ in range(self.world)]
-        self.dist.all_gather(parts, t)
-        return torch.stack(parts)
+        src = t.cpu() if self.host and t.is_cuda else t
+        parts = [torch.empty_like(src) for _ in range(self.world)]
+        self.dist.all_gather(parts, src)
+        return torch.stack(parts).to(t.device)
 
     def all_reduce_sum(self, t):
+        if self.host and t.is_cuda:
+            h = t.cpu()
+            self.dist.all_reduce(h)
+            t.copy_(h)
+            return t
         self.dist.all_reduce(t)
         return t
 

@@ -1,0 +1,52 @@
+"""Microbenchmark of the step-4 quantisation kernel at the bench shape:
+full output vs without the int32 z matrix (zq) vs without the bf16 panel (zb),
+to split its time between the q reads and the two writes.
+
+    python tools/bench_zquant.py [--reps 3]
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from grid_amd import _abi  # noqa: E402
+from grid_amd._abi import call, ptr  # noqa: E402
+from grid_amd.fused import HipOps, Steps47, TorchAlloc  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--n", type=int, default=3202)
+ap.add_argument("--m", type=int, default=3_000_000)
+ap.add_argument("--reps", type=int, default=3)
+a = ap.parse_args()
+
+dev = _abi.Device(0)
+dev.set_stream(torch.cuda.current_stream())
+q = torch.empty((a.n, a.m), dtype=torch.int32, device="cuda")
+call("grid_synth_depth", dev.ctx, bench.SEED, a.n, a.m, a.m, 0, bench.NCL, q.data_ptr())
+reads, off, nbr, w = bench.synth_reads_and_ibs(a.n)
+st = Steps47(HipOps(dev), TorchAlloc(0), a.n, a.m, 0, a.m, k=10, n_nbr=300, n_iters=1)
+st.set_reads(reads)
+st.set_phasing_graph(off, nbr, w)
+st.run(q, a.m)
+torch.cuda.synchronize()
+of = C.c_int32()
+cases = {"full": (st.zq, st.zb), "no_zq": (None, st.zb), "no_zb": (st.zq, None), "read_only": (None, None)}
+res = {}
+for rep in range(a.reps):
+    for name, (zq, zb) in cases.items():
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        call("grid_norm_zquant_kb", dev.ctx, q.data_ptr(), a.n, a.m, ptr(st.sel), st.r_loc, ptr(st.rm), ptr(st.mu),
+             st.scale, ptr(zq), a.m, ptr(st.colmap), st.qmax, ptr(zb), st.np_, C.byref(of))
+        e1.record()
+        torch.cuda.synchronize()
+        res.setdefault(name, []).append(e0.elapsed_time(e1))
+R = st.r_loc
+for name, t in res.items():
+    print(f"{name}: min {min(t):.2f} ms  median {np.median(t):.2f} ms", flush=True)
+print(f"bytes: q {a.n * a.m * 4 / 1e9:.1f} GB, zq {a.n * R * 4 / 1e9:.1f} GB, zb {st.np_ * st.kpad * 2 / 1e9:.1f} GB")
