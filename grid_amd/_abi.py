@@ -63,6 +63,7 @@ _SIGS = {
     "grid_hi_pack": [_i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp],
     "grid_hi_phase": [_vp, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
                       _i32, _i32],
+    "grid_hi_phase_batch": [_vp, _i64, _vp, _i64, _i32, _i64, _i64, _i32, _i32],
     "grid_synth_depth": [_vp, C.c_uint64, _i64, _i64, _i64, _i64, _i32, _vp],
     "grid_format_hundredths": [_vp, _i64, _vp, _i64, C.POINTER(_i64)],
     "grid_ingest_mosdepth": [_vp, _i64, C.c_char_p, C.c_int, _i64, _i64, _i64, _vp, _vp, _vp, _f64, _f64,
@@ -279,6 +280,14 @@ def hi_schedule(off: np.ndarray, nbr: np.ndarray, w: np.ndarray):
     lens = np.diff(off) if len(off) > 1 else np.zeros(1, np.int64)
     flags = HI_UNIT_WEIGHTS if (len(w) == 0 or bool(np.all(np.asarray(w) == 1.0))) else 0
     return order, loff, nl, pk_nbr, pk_w, pk_cnt, flags, int(lens.max()) if lens.size else 0
+
+
+class HiLocus(C.Structure):
+    """include/grid_abi.h grid_hi_locus (device pointers of one locus)."""
+    _fields_ = [("n", C.c_int64), ("irr", C.c_void_p), ("off", C.c_void_p), ("nbr", C.c_void_p),
+                ("w", C.c_void_p), ("order", C.c_void_p), ("loff", C.c_void_p), ("nlev", C.c_int32),
+                ("reserved", C.c_int32), ("pk_nbr", C.c_void_p), ("pk_w", C.c_void_p), ("pk_cnt", C.c_void_p),
+                ("hap", C.c_void_p), ("imp", C.c_void_p), ("mean", C.c_void_p)]
 
 
 class IngestUnsupported(GridNativeError):

@@ -158,17 +158,16 @@ __device__ __forceinline__ void ph_fetch(int e, int e1, const int32_t *__restric
 // all write.  The next chunk's neighbour lists are prefetched into registers
 // while the current chunk computes, so a chunk costs ~LDS latency + barriers.
 template <bool USE_LDS>
-__global__ __launch_bounds__(PT) void k_phase(int64_t n, const double *__restrict__ irr,
-                                              const int64_t *__restrict__ off,
-                                              const int32_t *__restrict__ nbr,
-                                              const double *__restrict__ w, int64_t min_nbr,
-                                              int64_t iters, const int32_t *__restrict__ order,
-                                              const int32_t *__restrict__ loff, int nlev,
-                                              const int32_t *__restrict__ pk_nbr, const double *__restrict__ pk_w,
-                                              const int32_t *__restrict__ pk_cnt,
-                                              double *hap_g, double *__restrict__ imp,
-                                              double *__restrict__ mean_out) {
-  extern __shared__ __attribute__((aligned(16))) double s_hap[];
+__device__ __forceinline__ void ph_run(int64_t n, const double *__restrict__ irr,
+                                       const int64_t *__restrict__ off,
+                                       const int32_t *__restrict__ nbr,
+                                       const double *__restrict__ w, int64_t min_nbr,
+                                       int64_t iters, const int32_t *__restrict__ order,
+                                       const int32_t *__restrict__ loff, int nlev,
+                                       const int32_t *__restrict__ pk_nbr, const double *__restrict__ pk_w,
+                                       const int32_t *__restrict__ pk_cnt,
+                                       double *hap_g, double *__restrict__ imp,
+                                       double *__restrict__ mean_out, double *s_hap) {
   __shared__ double s_mean;
   double *hap = USE_LDS ? s_hap : hap_g;
   // LDS layout (USE_LDS): hap[2n] | irr[n] | level offsets[nlev+1] | phased flags[n]
@@ -297,6 +296,32 @@ __global__ __launch_bounds__(PT) void k_phase(int64_t n, const double *__restric
   if (tid == 0) *mean_out = mean;
 }
 
+template <bool USE_LDS>
+__global__ __launch_bounds__(PT) void k_phase(int64_t n, const double *__restrict__ irr,
+                                              const int64_t *__restrict__ off,
+                                              const int32_t *__restrict__ nbr,
+                                              const double *__restrict__ w, int64_t min_nbr,
+                                              int64_t iters, const int32_t *__restrict__ order,
+                                              const int32_t *__restrict__ loff, int nlev,
+                                              const int32_t *__restrict__ pk_nbr, const double *__restrict__ pk_w,
+                                              const int32_t *__restrict__ pk_cnt,
+                                              double *hap_g, double *__restrict__ imp,
+                                              double *__restrict__ mean_out) {
+  extern __shared__ __attribute__((aligned(16))) double s_hap[];
+  ph_run<USE_LDS>(n, irr, off, nbr, w, min_nbr, iters, order, loff, nlev, pk_nbr, pk_w, pk_cnt, hap_g, imp,
+                  mean_out, s_hap);
+}
+
+// Batched loci (config 5): workgroup b runs locus b's whole phasing.
+template <bool USE_LDS>
+__global__ __launch_bounds__(PT) void k_phase_batch(const grid_hi_locus *__restrict__ loci, int64_t min_nbr,
+                                                    int64_t iters) {
+  extern __shared__ __attribute__((aligned(16))) double s_hap[];
+  const grid_hi_locus &L = loci[blockIdx.x];
+  ph_run<USE_LDS>(L.n, L.irr, L.off, L.nbr, L.w, min_nbr, iters, L.order, L.loff, L.nlev, L.pk_nbr, L.pk_w,
+                  L.pk_cnt, L.hap, L.imp, L.mean, s_hap);
+}
+
 
 // Level-schedule phasing, register-pipelined (default when hap fits in LDS).
 // Per chunk of PT schedule entries, thread t owns entry base + t:
@@ -366,15 +391,14 @@ __device__ __forceinline__ void ph2_decode(PhReg<UNITW, CAPT> &it) {
 }
 
 template <bool UNITW, int CAPT, int PROBE = 0>
-__global__ __launch_bounds__(PT) void k_phase2(int64_t n, const double *__restrict__ irr,
-                                               const int64_t *__restrict__ off, const int32_t *__restrict__ nbr,
-                                               const double *__restrict__ w, int64_t min_nbr, int64_t iters,
-                                               const int32_t *__restrict__ order, const int32_t *__restrict__ loff,
-                                               int nlev, const int32_t *__restrict__ pk_nbr,
-                                               const double *__restrict__ pk_w, const int32_t *__restrict__ pk_cnt,
-                                               double *hap_g, double *__restrict__ imp,
-                                               double *__restrict__ mean_out) {
-  extern __shared__ __attribute__((aligned(16))) double s_hap[];
+__device__ __forceinline__ void ph2_run(int64_t n, const double *__restrict__ irr,
+                                        const int64_t *__restrict__ off, const int32_t *__restrict__ nbr,
+                                        const double *__restrict__ w, int64_t min_nbr, int64_t iters,
+                                        const int32_t *__restrict__ order, const int32_t *__restrict__ loff,
+                                        int nlev, const int32_t *__restrict__ pk_nbr,
+                                        const double *__restrict__ pk_w, const int32_t *__restrict__ pk_cnt,
+                                        double *hap_g, double *__restrict__ imp,
+                                        double *__restrict__ mean_out, double *s_hap) {
   __shared__ double s_mean;
   __shared__ double s_unit[CAPT + 1];
   double *hap = s_hap;
@@ -555,6 +579,29 @@ __global__ __launch_bounds__(PT) void k_phase2(int64_t n, const double *__restri
   if (tid == 0) *mean_out = mean;
 }
 
+template <bool UNITW, int CAPT, int PROBE = 0>
+__global__ __launch_bounds__(PT) void k_phase2(int64_t n, const double *__restrict__ irr,
+                                               const int64_t *__restrict__ off, const int32_t *__restrict__ nbr,
+                                               const double *__restrict__ w, int64_t min_nbr, int64_t iters,
+                                               const int32_t *__restrict__ order, const int32_t *__restrict__ loff,
+                                               int nlev, const int32_t *__restrict__ pk_nbr,
+                                               const double *__restrict__ pk_w, const int32_t *__restrict__ pk_cnt,
+                                               double *hap_g, double *__restrict__ imp,
+                                               double *__restrict__ mean_out) {
+  extern __shared__ __attribute__((aligned(16))) double s_hap[];
+  ph2_run<UNITW, CAPT, PROBE>(n, irr, off, nbr, w, min_nbr, iters, order, loff, nlev, pk_nbr, pk_w, pk_cnt, hap_g,
+                              imp, mean_out, s_hap);
+}
+
+template <bool UNITW, int CAPT>
+__global__ __launch_bounds__(PT) void k_phase2_batch(const grid_hi_locus *__restrict__ loci, int64_t min_nbr,
+                                                     int64_t iters) {
+  extern __shared__ __attribute__((aligned(16))) double s_hap[];
+  const grid_hi_locus &L = loci[blockIdx.x];
+  ph2_run<UNITW, CAPT, 0>(L.n, L.irr, L.off, L.nbr, L.w, min_nbr, iters, L.order, L.loff, L.nlev, L.pk_nbr,
+                          L.pk_w, L.pk_cnt, L.hap, L.imp, L.mean, s_hap);
+}
+
 }  // namespace
 
 extern "C" {
@@ -644,6 +691,43 @@ int grid_hi_phase(grid_ctx *ctx, int64_t n, const double *d_irr, const int64_t *
   } else {
     hipLaunchKernelGGL(k_phase<false>, dim3(1), dim3(PT), 0, ctx->stream, n, d_irr, d_off, d_nbr, d_w, min_nbr,
                        n_iters, d_order, d_loff, nlevels, d_pk_nbr, d_pk_w, d_pk_cnt, d_hap, d_imp, d_mean);
+  }
+  LAUNCHCHK();
+  return GRID_OK;
+}
+
+int grid_hi_phase_batch(grid_ctx *ctx, int64_t n_loci, const grid_hi_locus *d_loci, int64_t max_n,
+                        int32_t max_nlev, int64_t min_nbr, int64_t n_iters, int32_t flags, int32_t max_list) {
+  REQUIRE(ctx && n_loci >= 0 && max_n >= 0 && max_nlev >= 0 && n_iters >= 0 && max_list >= 0, "bad args");
+  REQUIRE(n_loci <= 0x7fffffff, "too many loci");
+  if (n_loci == 0 || max_n == 0) return GRID_OK;
+  REQUIRE(d_loci, "d_loci is NULL");
+  const size_t lds = (size_t)3 * max_n * sizeof(double) + (size_t)(max_nlev + 1) * 4 + (size_t)max_n;
+  const size_t lds2 = lds + 32 + (size_t)(max_nlev + max_n / PT + 2) * 8;
+  const bool unitw = flags & GRID_HI_UNIT_WEIGHTS;
+  if (lds2 <= 120 * 1024 && !(flags & GRID_HI_LEGACY)) {
+    auto kern = unitw ? (max_list <= 8 ? k_phase2_batch<true, 8> : k_phase2_batch<true, 16>)
+                      : (max_list <= 8 ? k_phase2_batch<false, 8> : k_phase2_batch<false, 16>);
+    static bool attr[4] = {false, false, false, false};
+    const int slot = (unitw ? 2 : 0) + (max_list <= 8 ? 0 : 1);
+    if (!attr[slot]) {
+      HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024));
+      attr[slot] = true;
+    }
+    hipLaunchKernelGGL(kern, dim3((unsigned)n_loci), dim3(PT), lds2, ctx->stream, d_loci, min_nbr, n_iters);
+  } else if (lds <= 120 * 1024) {
+    static bool attr = false;
+    if (!attr) {
+      HIPCHK(hipFuncSetAttribute((const void *)k_phase_batch<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 120 * 1024));
+      attr = true;
+    }
+    hipLaunchKernelGGL(k_phase_batch<true>, dim3((unsigned)n_loci), dim3(PT), lds, ctx->stream, d_loci, min_nbr,
+                       n_iters);
+  } else {
+    // hap in each locus's global output buffer (L2-resident per workgroup)
+    hipLaunchKernelGGL(k_phase_batch<false>, dim3((unsigned)n_loci), dim3(PT), 0, ctx->stream, d_loci, min_nbr,
+                       n_iters);
   }
   LAUNCHCHK();
   return GRID_OK;

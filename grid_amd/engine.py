@@ -211,3 +211,40 @@ def phase(dev: Device, irr: np.ndarray, off: np.ndarray, nbr: np.ndarray, w: np.
          bufs[4].ptr, bufs[5].ptr, nl, bufs[6].ptr, bufs[7].ptr, bufs[8].ptr, hap.ptr, imp.ptr, mean.ptr,
          flags | _legacy_flag(), max_list)
     return hap.numpy(), imp.numpy(), float(mean.numpy()[0])
+
+
+def phase_batch(dev: Device, loci, min_nbr: int, n_iters: int):
+    """Batched phasing + imputation of L independent loci in one launch (one
+    workgroup per locus; BASELINE config 5).  ``loci``: sequence of
+    (irr [n], off [2n+1], nbr, w) per locus (CSR as csr_from_lists).  Returns
+    a list of (hap [2n], imp [2n], mean) equal to phase() per locus."""
+    import ctypes as C
+    sched, descs, keep, outs = [], [], [], []
+    flags_all, max_list, max_n, max_nlev = _abi.HI_UNIT_WEIGHTS, 0, 0, 0
+    for irr, off, nbr, w in loci:
+        order, loff, nl, pk_nbr, pk_w, pk_cnt, flags, ml = _abi.hi_schedule(off, nbr, w)
+        flags_all &= flags
+        max_list, max_n, max_nlev = max(max_list, ml), max(max_n, len(irr)), max(max_nlev, nl)
+        sched.append((order, loff, nl, pk_nbr, pk_w, pk_cnt))
+    for (irr, off, nbr, w), (order, loff, nl, pk_nbr, pk_w, pk_cnt) in zip(loci, sched):
+        n = len(irr)
+        b = [dev.upload(np.ascontiguousarray(a)) for a in
+             (np.asarray(irr if n else np.zeros(1), F8), np.asarray(off, I8),
+              np.asarray(nbr if len(nbr) else np.zeros(1), I4), np.asarray(w if len(w) else np.zeros(1), F8),
+              np.asarray(order if n else np.zeros(1), I4), np.asarray(loff, I4), pk_nbr, pk_w, pk_cnt)]
+        hap, imp, mean = dev.alloc(max(2 * n, 1), F8), dev.alloc(max(2 * n, 1), F8), dev.alloc(1, F8)
+        keep += b
+        outs.append((n, hap, imp, mean))
+        descs.append(_abi.HiLocus(n, b[0].ptr, b[1].ptr, b[2].ptr, b[3].ptr, b[4].ptr, b[5].ptr, nl, 0, b[6].ptr,
+                                  b[7].ptr, b[8].ptr, hap.ptr, imp.ptr, mean.ptr))
+    if not descs:
+        return []
+    arr = (_abi.HiLocus * len(descs))(*descs)
+    d_arr = dev.alloc(C.sizeof(arr), np.uint8)
+    call("grid_h2d", dev.ctx, d_arr.ptr, C.addressof(arr), C.sizeof(arr))
+    call("grid_hi_phase_batch", dev.ctx, len(descs), d_arr.ptr, max_n, max_nlev, min_nbr, n_iters,
+         flags_all | _legacy_flag(), max_list)
+    res = []
+    for n, hap, imp, mean in outs:
+        res.append((hap.numpy()[: 2 * n], imp.numpy()[: 2 * n], float(mean.numpy()[0]) if n else 0.0))
+    return res

@@ -141,6 +141,18 @@ def _phase_device(IRRs, hap_nbrs, MIN_NBR, N_ITERS, console=None, dev=None):
     return engine.phase(dev or get_device(), np.asarray(IRRs, dtype=np.float64), off, nbr, w, MIN_NBR, N_ITERS)
 
 
+def run_phasing_batch(IRRs_per_locus, hap_nbrs_per_locus, MIN_NBR, N_ITERS, dev=None):
+    """_run_phasing + _compute_imp (:175-250) for many loci (VNTR regions) in
+    one GPU launch, one workgroup per locus (BASELINE config 5).  Equal, locus
+    by locus, to calling the reference per region.  Returns a list of
+    (hap_IRRs [2n], imp [2n], mean_IRRs)."""
+    loci = []
+    for irrs, hap_nbrs in zip(IRRs_per_locus, hap_nbrs_per_locus):
+        off, nbr, w = engine.csr_from_lists(hap_nbrs)
+        loci.append((np.asarray(irrs, dtype=np.float64), off, nbr, w))
+    return engine.phase_batch(dev or get_device(), loci, MIN_NBR, N_ITERS)
+
+
 def _compute_imp(i, hap_IRRs, hap_nbrs, mean_IRRs):
     """:229-250 (single-sample API; the step computes all samples on the GPU)."""
     import math

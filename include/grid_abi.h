@@ -194,6 +194,33 @@ int grid_hi_phase(grid_ctx *ctx, int64_t n, const double *d_irr, const int64_t *
 #define GRID_HI_UNIT_WEIGHTS 1   /* every weight is 1.0 (IBS lists): weights are not read */
 #define GRID_HI_LEGACY 2         /* A/B: the previous (per-neighbour LDS round trip) kernel */
 
+/* Batched loci (BASELINE config 5: one _run_phasing + _compute_imp per VNTR
+ * region, hi_inference.py:175-250, all in one launch, one workgroup per
+ * locus).  Every pointer is a device pointer with grid_hi_phase's meaning for
+ * that locus; the array of descriptors itself is in device memory. */
+typedef struct grid_hi_locus {
+  int64_t n;                       /* samples of this locus */
+  const double *irr;               /* [n] */
+  const int64_t *off;              /* [2n+1] CSR offsets into nbr / w */
+  const int32_t *nbr;
+  const double *w;
+  const int32_t *order;            /* [n] level schedule (grid_hi_levels) */
+  const int32_t *loff;             /* [nlev+1] */
+  int32_t nlev;
+  int32_t reserved;
+  const int32_t *pk_nbr;           /* grid_hi_pack output, schedule order */
+  const double *pk_w;
+  const int32_t *pk_cnt;
+  double *hap;                     /* [2n] out */
+  double *imp;                     /* [2n] out */
+  double *mean;                    /* [1] out */
+} grid_hi_locus;
+/* max_n / max_nlev: the largest n / nlev in the batch (LDS sizing); flags and
+ * max_list as grid_hi_phase, over the whole batch. */
+int grid_hi_phase_batch(grid_ctx *ctx, int64_t n_loci, const grid_hi_locus *d_loci, int64_t max_n,
+                        int32_t max_nlev, int64_t min_nbr, int64_t n_iters, int32_t flags,
+                        int32_t max_list);
+
 /* ---------------------------------------------------- synthetic input
  * Counter-based synthetic cohort (bench/smoke input, not a product path):
  * d_q[i*ld + j] = hundredths depth of sample i at GLOBAL bin col0 + j. */

@@ -281,3 +281,37 @@ def test_phasing_kernel_variants(dev, weighted, maxlen, legacy, monkeypatch):
     assert mean == em or (np.isnan(mean) and np.isnan(em))
     ei = [steps.compute_imp(i, eh, hn, em) for i in range(n)]
     assert np.array_equal(imp, np.array(ei).reshape(-1), equal_nan=True)
+
+
+def _random_locus(rng, n, weighted, maxlen):
+    irr = rng.uniform(0.1, 4.0, n)
+    irr[rng.random(n) < 0.02] = 0.0
+    hn = []
+    for h in range(2 * n):
+        lst = []
+        for _ in range(int(rng.integers(0, maxlen + 1))):
+            j = int(rng.integers(0, 2 * n))
+            lst.append((j, float(rng.uniform(0.05, 3.0)) if weighted else 1.0))
+        hn.append(lst)
+    return list(irr), hn
+
+
+@pytest.mark.parametrize("big,weighted,min_nbr", [(False, False, 1), (False, True, 2), (True, False, 1),
+                                                  (True, True, 0)])
+def test_phasing_batch_equals_per_locus_oracle(dev, big, weighted, min_nbr):
+    """grid_hi_phase_batch (one workgroup per locus, config 5) on loci of
+    different sizes against the reference arithmetic run per locus; big=True
+    puts a 5,000-sample locus in the batch, which moves every locus to the
+    global-memory kernel (LDS too small)."""
+    from grid_amd.utils.hi_inference import run_phasing_batch
+    rng = np.random.default_rng(7 + big * 2 + weighted)
+    sizes = [1, 37, 256, 300, 1201] + ([5000] if big else [])
+    loci = [_random_locus(rng, n, weighted and i % 2 == 0, 12 if i != 2 else 20) for i, n in enumerate(sizes)]
+    iters = 9
+    got = run_phasing_batch([a for a, _ in loci], [b for _, b in loci], min_nbr, iters, dev=dev)
+    for (irr, hn), (hap, imp, mean) in zip(loci, got):
+        eh, em = steps.run_phasing(irr, hn, min_nbr, iters)
+        assert np.array_equal(hap, np.array(eh), equal_nan=True)
+        assert mean == em
+        ei = [steps.compute_imp(i, eh, hn, em) for i in range(len(irr))]
+        assert np.array_equal(imp, np.array(ei).reshape(-1), equal_nan=True)
