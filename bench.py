@@ -125,6 +125,9 @@ def main():
     ap.add_argument("--cpu-bins", type=int, default=16384)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-overlap", action="store_true", help="run step 7 inline on the main stream")
+    ap.add_argument("--depth-format", choices=["int32", "q16"], default="int32",
+                    help="depth matrix in HBM: int32 hundredths (default) or the compact uint16 + escapes form "
+                         "(half the bytes; measured slower: the step-4 passes are not byte-bound)")
     args = ap.parse_args()
 
     import torch
@@ -149,15 +152,23 @@ def main():
         comm = TorchComm(dist)
 
     from grid_amd import _abi
-    from grid_amd.fused import HipOps, Steps47, TorchAlloc, shard_range
+    from grid_amd.fused import Depth16, HipOps, Steps47, TorchAlloc, shard_range
 
     dev = _abi.Device(local)
     dev.set_stream(torch.cuda.current_stream())
     n, m = args.samples, args.bins
     c0, c1 = shard_range(m, rank, world)
     ml = c1 - c0
-    q = torch.empty((n, max(ml, 1)), dtype=torch.int32, device="cuda")
-    _abi.call("grid_synth_depth", dev.ctx, SEED, n, ml, ml, c0, NCL, q.data_ptr())
+    talloc = TorchAlloc(local)
+    if args.depth_format == "q16":
+        # compact depth matrix: uint16 hundredths + escape table (half the HBM
+        # bytes of the four step-4 passes; same int32 values after decoding)
+        q = Depth16.synth(talloc, dev.ctx, SEED, n, ml, c0, NCL)
+        ldq = q.ld
+    else:
+        q = torch.empty((n, max(ml, 1)), dtype=torch.int32, device="cuda")
+        _abi.call("grid_synth_depth", dev.ctx, SEED, n, ml, ml, c0, NCL, q.data_ptr())
+        ldq = ml
     reads, off, nbr, w = synth_reads_and_ibs(n)
     # step 7 on its own stream: it overlaps the next pass's steps 4-5 (every
     # pass is still complete inside the timed region: the final synchronize
@@ -168,13 +179,13 @@ def main():
         pstream = torch.cuda.Stream()
         pdev.set_stream(pstream)
         lane = (HipOps(pdev), pstream)
-    st = Steps47(HipOps(dev), TorchAlloc(local), n, m, c0, ml, k=args.k, n_nbr=300, top_frac=0.1, zmax=2.0,
+    st = Steps47(HipOps(dev), talloc, n, m, c0, ml, k=args.k, n_nbr=300, top_frac=0.1, zmax=2.0,
                  sigma2_max=1000.0, frac_r=1.0, min_nbr=1, n_iters=args.n_iters, comm=comm, phase_lane=lane)
     st.set_reads(reads)
     st.set_phasing_graph(off, nbr, w)
 
     for _ in range(args.warmup):
-        st.run(q, ml)
+        st.run(q, ldq)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -184,7 +195,7 @@ def main():
         dist.barrier()
     t0 = time.perf_counter()
     for s in range(args.steps):
-        st.run(q, ml, gram_events=ev[s])
+        st.run(q, ldq, gram_events=ev[s])
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -194,7 +205,7 @@ def main():
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
     gram_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    st.run(q, ml, profile=True)              # untimed pass: per-stage device times
+    st.run(q, ldq, profile=True)              # untimed pass: per-stage device times
     torch.cuda.synchronize()
     stages = {k: round(v, 3) for k, v in st.stage_ms().items()}
 
@@ -225,6 +236,7 @@ def main():
         "config": {"workload": f"BASELINE config 2: {n} samples x {m} bins (hg38 @ 1 kb), k={args.k}, "
                                f"n_iters={args.n_iters}", "samples": n, "bins": m, "k": args.k,
                    "n_iters": args.n_iters, "parallelism": f"bin-sharded x{world}",
+                   "depth_format": args.depth_format,
                    "selected_regions": None, "R_use_rank0": st.ruse_loc, "dipcn_valid": valid,
                    "phasing_levels": st.nlev},
         "stages_ms": stages,
@@ -242,7 +254,10 @@ def main():
     out["config"]["selected_regions"] = st.r_loc if world == 1 else None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         ms = min(args.cpu_bins, ml)
-        qh = q[:, :ms].cpu().numpy()
+        qs = torch.empty((n, ms), dtype=torch.int32, device="cuda")   # same cells, int32 form
+        _abi.call("grid_synth_depth", dev.ctx, SEED, n, ms, ms, c0, NCL, qs.data_ptr())
+        qh = qs.cpu().numpy()
+        del qs
         out["cpu_baseline"] = cpu_baseline(qh, n, m, reads, off, nbr, w, args.k, args.n_iters)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -64,6 +64,14 @@ _SIGS = {
     "grid_hi_phase": [_vp, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
                       _i32, _i32],
     "grid_hi_phase_batch": [_vp, _i64, _vp, _i64, _i32, _i64, _i64, _i32, _i32],
+    "grid_q16_encode": [_vp, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _vp, _i64, C.POINTER(_i64)],
+    "grid_synth_depth_q16": [_vp, C.c_uint64, _i64, _i64, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _i64,
+                             C.POINTER(_i64)],
+    "grid_norm_row_blocks_q16": [_vp, _vp, _i64, _i64, _i64, _vp, _vp],
+    "grid_norm_col_means_q16": [_vp, _vp, _i64, _i64, _i64, _vp, _vp],
+    "grid_norm_col_vars_q16": [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
+    "grid_norm_zquant_kb_q16": [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _f64, _vp, _i64, _vp, _i32,
+                                _vp, _i64, C.POINTER(_i32)],
     "grid_synth_depth": [_vp, C.c_uint64, _i64, _i64, _i64, _i64, _i32, _vp],
     "grid_format_hundredths": [_vp, _i64, _vp, _i64, C.POINTER(_i64)],
     "grid_ingest_mosdepth": [_vp, _i64, C.c_char_p, C.c_int, _i64, _i64, _i64, _vp, _vp, _vp, _f64, _f64,
@@ -280,6 +288,11 @@ def hi_schedule(off: np.ndarray, nbr: np.ndarray, w: np.ndarray):
     lens = np.diff(off) if len(off) > 1 else np.zeros(1, np.int64)
     flags = HI_UNIT_WEIGHTS if (len(w) == 0 or bool(np.all(np.asarray(w) == 1.0))) else 0
     return order, loff, nl, pk_nbr, pk_w, pk_cnt, flags, int(lens.max()) if lens.size else 0
+
+
+class Depth16Desc(C.Structure):
+    """include/grid_abi.h grid_depth16 (device pointers)."""
+    _fields_ = [("q", C.c_void_p), ("eoff", C.c_void_p), ("ecol", C.c_void_p), ("eval", C.c_void_p)]
 
 
 class HiLocus(C.Structure):

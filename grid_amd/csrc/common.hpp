@@ -91,3 +91,31 @@ __host__ __device__ inline double div_exact(double x, double b, double r) {
   e = fma(-y, b, x);
   return fma(e, r, y);
 }
+
+// ---- compact depth matrix (uint16 hundredths + escapes) --------------------
+// q16[i*ld + j]: v <= GRID_Q16_MAXV is the depth in hundredths, GRID_Q16_MISS
+// a missing cell, GRID_Q16_ESC a value > GRID_Q16_MAXV stored exactly in the
+// row-sorted escape table (eoff[n+1] CSR offsets, ecol column, eval value).
+// Half the bytes of the int32 matrix for the four HBM passes of step 4.
+struct Q16 {
+  const uint16_t *q;
+  const int64_t *eoff;
+  const int32_t *ecol;
+  const int32_t *eval;
+};
+// Out of line: escapes are rare, and an inlined binary search at every
+// decode site bloats the unrolled kernels (registers, code size).
+__device__ __attribute__((noinline)) int32_t q16_slow(uint32_t v, int64_t i, int64_t j, Q16 s) {
+  if (v == GRID_Q16_MISS) return GRID_MISSING;
+  int64_t lo = s.eoff[i], hi = s.eoff[i + 1];
+  const int64_t end = hi;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (s.ecol[mid] < j) lo = mid + 1;
+    else hi = mid;
+  }
+  return (lo < end && s.ecol[lo] == j) ? s.eval[lo] : GRID_MISSING;
+}
+__device__ __forceinline__ int32_t q16_val(uint32_t v, int64_t i, int64_t j, const Q16 &s) {
+  return v <= GRID_Q16_MAXV ? (int32_t)v : q16_slow(v, i, j, s);
+}

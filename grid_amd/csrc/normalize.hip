@@ -23,8 +23,9 @@ __device__ __forceinline__ double qval(int32_t q) {
 // ---- full 8192-element blocks: one 256-thread workgroup per (row, block) ----
 // 64 leaves x 8 chains = 512 chains, 2 per thread; leaf results combined in
 // the fixed binary tree of pairwise(8192).
-template <bool VEC>
-__global__ __launch_bounds__(256) void k_row_blocks_full(const int32_t *__restrict__ q, int64_t ld,
+// SRC: 0 = int32 (int4 loads), 1 = int32 (scalar loads), 2 = compact uint16 (s16)
+template <int SRC>
+__global__ __launch_bounds__(256) void k_row_blocks_full(const int32_t *__restrict__ q, Q16 s16, int64_t ld,
                                                          int64_t nblk_full, int64_t nblk,
                                                          double *__restrict__ bsum,
                                                          int32_t *__restrict__ bcnt) {
@@ -34,22 +35,43 @@ __global__ __launch_bounds__(256) void k_row_blocks_full(const int32_t *__restri
   const int64_t b = blockIdx.x;
   const int64_t row = blockIdx.y;
   const int tid = threadIdx.x;
-  const int32_t *srcp = q + row * ld + b * BLK;
-  const int4 *src = reinterpret_cast<const int4 *>(srcp);
   int cnt = 0;
+  if constexpr (SRC == 2) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(s16.q + row * ld + b * BLK);
 #pragma unroll
-  for (int it = 0; it < 8; it++) {
-    int e4 = it * 256 + tid;                 // int4 index within block
-    int4 v;
-    if (VEC) {
-      v = src[e4];
-    } else {
-      v.x = srcp[4 * e4]; v.y = srcp[4 * e4 + 1]; v.z = srcp[4 * e4 + 2]; v.w = srcp[4 * e4 + 3];
+    for (int it = 0; it < 4; it++) {
+      const int e8 = it * 256 + tid;         // 8-value group within the block
+      const uint4 u = src[e8];
+      const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
+      int32_t v[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint32_t c = (wd[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+        v[k] = q16_val(c, row, b * BLK + e8 * 8 + k, s16);
+        cnt += v[k] != GRID_MISSING;
+      }
+      const int e = e8 * 8;
+      const int leaf = e >> 7, w = e & 127;
+      *reinterpret_cast<int4 *>(&s_q[leaf * LEAF_PAD + w]) = make_int4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<int4 *>(&s_q[leaf * LEAF_PAD + w + 4]) = make_int4(v[4], v[5], v[6], v[7]);
     }
-    int e = e4 * 4;
-    int leaf = e >> 7, w = e & 127;
-    *reinterpret_cast<int4 *>(&s_q[leaf * LEAF_PAD + w]) = v;
-    cnt += (v.x != GRID_MISSING) + (v.y != GRID_MISSING) + (v.z != GRID_MISSING) + (v.w != GRID_MISSING);
+  } else {
+    const int32_t *srcp = q + row * ld + b * BLK;
+    const int4 *src = reinterpret_cast<const int4 *>(srcp);
+#pragma unroll
+    for (int it = 0; it < 8; it++) {
+      int e4 = it * 256 + tid;                 // int4 index within block
+      int4 v;
+      if (SRC == 0) {
+        v = src[e4];
+      } else {
+        v.x = srcp[4 * e4]; v.y = srcp[4 * e4 + 1]; v.z = srcp[4 * e4 + 2]; v.w = srcp[4 * e4 + 3];
+      }
+      int e = e4 * 4;
+      int leaf = e >> 7, w = e & 127;
+      *reinterpret_cast<int4 *>(&s_q[leaf * LEAF_PAD + w]) = v;
+      cnt += (v.x != GRID_MISSING) + (v.y != GRID_MISSING) + (v.z != GRID_MISSING) + (v.w != GRID_MISSING);
+    }
   }
   // wave-level count reduction
   for (int o = 32; o > 0; o >>= 1) cnt += __shfl_down(cnt, o, 64);
@@ -97,29 +119,33 @@ __global__ __launch_bounds__(256) void k_row_blocks_full(const int32_t *__restri
 }
 
 // ---- generic pairwise_sum (numpy) for a partial block, one thread ----
-__device__ double pairwise_leaf(const int32_t *a, int n) {
+// G: element accessor, get(k) -> int32 hundredths of element k.
+template <class G>
+__device__ double pairwise_leaf(const G &get, int lo, int n) {
+  auto a = [&](int i) { return qval(get(lo + i)); };
   if (n < 8) {
     double res = 0.0;
-    for (int i = 0; i < n; i++) res = res + qval(a[i]);
+    for (int i = 0; i < n; i++) res = res + a(i);
     return res;
   }
-  double r0 = qval(a[0]), r1 = qval(a[1]), r2 = qval(a[2]), r3 = qval(a[3]);
-  double r4 = qval(a[4]), r5 = qval(a[5]), r6 = qval(a[6]), r7 = qval(a[7]);
+  double r0 = a(0), r1 = a(1), r2 = a(2), r3 = a(3);
+  double r4 = a(4), r5 = a(5), r6 = a(6), r7 = a(7);
   int i = 8;
   int stop = n - (n % 8);
   for (; i < stop; i += 8) {
-    r0 = r0 + qval(a[i + 0]); r1 = r1 + qval(a[i + 1]);
-    r2 = r2 + qval(a[i + 2]); r3 = r3 + qval(a[i + 3]);
-    r4 = r4 + qval(a[i + 4]); r5 = r5 + qval(a[i + 5]);
-    r6 = r6 + qval(a[i + 6]); r7 = r7 + qval(a[i + 7]);
+    r0 = r0 + a(i + 0); r1 = r1 + a(i + 1);
+    r2 = r2 + a(i + 2); r3 = r3 + a(i + 3);
+    r4 = r4 + a(i + 4); r5 = r5 + a(i + 5);
+    r6 = r6 + a(i + 6); r7 = r7 + a(i + 7);
   }
   double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-  for (; i < n; i++) res = res + qval(a[i]);
+  for (; i < n; i++) res = res + a(i);
   return res;
 }
 
 // Iterative post-order evaluation of numpy's recursion (depth <= 7 for n < 8192).
-__device__ double pairwise_any(const int32_t *a, int n) {
+template <class G>
+__device__ double pairwise_any(const G &get, int n) {
   struct Fr { int lo, n, state; double left; };
   Fr st[16];
   int sp = 0;
@@ -128,7 +154,7 @@ __device__ double pairwise_any(const int32_t *a, int n) {
   while (sp >= 0) {
     Fr &f = st[sp];
     if (f.n <= LEAF) {
-      ret = pairwise_leaf(a + f.lo, f.n);
+      ret = pairwise_leaf(get, f.lo, f.n);
       sp--;
       continue;
     }
@@ -151,17 +177,22 @@ __device__ double pairwise_any(const int32_t *a, int n) {
   return ret;
 }
 
-__global__ void k_row_block_tail(const int32_t *__restrict__ q, int64_t n, int64_t ld, int64_t m,
+template <bool S16>
+__global__ void k_row_block_tail(const int32_t *__restrict__ q, Q16 s16, int64_t n, int64_t ld, int64_t m,
                                  int64_t nblk, double *__restrict__ bsum,
                                  int32_t *__restrict__ bcnt) {
   int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (row >= n) return;
   int64_t b = nblk - 1;
   int len = (int)(m - b * BLK);
-  const int32_t *a = q + row * ld + b * BLK;
+  const int64_t c0 = b * BLK;
+  auto get = [&](int k) -> int32_t {
+    if constexpr (S16) return q16_val(s16.q[row * ld + c0 + k], row, c0 + k, s16);
+    else return q[row * ld + c0 + k];
+  };
   int c = 0;
-  for (int i = 0; i < len; i++) c += a[i] != GRID_MISSING;
-  bsum[row * nblk + b] = pairwise_any(a, len);
+  for (int i = 0; i < len; i++) c += get(i) != GRID_MISSING;
+  bsum[row * nblk + b] = pairwise_any(get, len);
   bcnt[row * nblk + b] = c;
 }
 
@@ -193,20 +224,39 @@ __global__ void k_recip(const double *__restrict__ v, int64_t n, double *__restr
 
 constexpr int CU = 8;   // rows unrolled per iteration in the column kernels
 
-// VW adjacent columns per thread (int4 loads when VW == 4), sequential over rows.
-template <int VW>
-__device__ __forceinline__ void load_cols(const int32_t *p, int32_t (&v)[VW]) {
-  if constexpr (VW == 4) {
-    int4 t = *reinterpret_cast<const int4 *>(p);
+// VW adjacent columns per thread, sequential over rows: int4 loads of int32
+// (VW == 4), or one 8-B load of 4 compact uint16 values (S16).
+template <int VW, bool S16>
+__device__ __forceinline__ void load_row(const int32_t *__restrict__ q, const Q16 &s16, int64_t i, int64_t ld,
+                                         int64_t j0, int32_t (&v)[VW]) {
+  if constexpr (S16) {
+    static_assert(VW == 4, "compact rows load 4 columns (8 bytes)");
+    const uint2 u = *reinterpret_cast<const uint2 *>(s16.q + i * ld + j0);
+    v[0] = (int32_t)(u.x & 0xFFFFu); v[1] = (int32_t)(u.x >> 16);
+    v[2] = (int32_t)(u.y & 0xFFFFu); v[3] = (int32_t)(u.y >> 16);
+    // rare: missing cells and escapes (one out-of-line loop, not per element)
+    if (__builtin_expect(max(max(v[0], v[1]), max(v[2], v[3])) > GRID_Q16_MAXV, 0)) {
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (v[k] > GRID_Q16_MAXV) v[k] = q16_slow((uint32_t)v[k], i, j0 + k, s16);
+    }
+  } else if constexpr (VW == 4) {
+    int4 t = *reinterpret_cast<const int4 *>(q + i * ld + j0);
     v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
   } else {
 #pragma unroll
-    for (int c = 0; c < VW; c++) v[c] = p[c];
+    for (int c = 0; c < VW; c++) v[c] = q[i * ld + j0 + c];
   }
 }
+template <bool S16>
+__device__ __forceinline__ int32_t q_at(const int32_t *__restrict__ q, const Q16 &s16, int64_t i, int64_t ld,
+                                        int64_t j) {
+  if constexpr (S16) return q16_val(s16.q[i * ld + j], i, j, s16);
+  else return q[i * ld + j];
+}
 
-template <int VW>
-__global__ __launch_bounds__(256) void k_col_means(const int32_t *__restrict__ q, int64_t n, int64_t m,
+template <int VW, bool S16>
+__global__ __launch_bounds__(256) void k_col_means(const int32_t *__restrict__ q, Q16 s16, int64_t n, int64_t m,
                                                    int64_t ld, const double *__restrict__ rm,
                                                    const double *__restrict__ rinv, double *__restrict__ mu) {
   const int64_t j0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * VW;
@@ -217,7 +267,7 @@ __global__ __launch_bounds__(256) void k_col_means(const int32_t *__restrict__ q
       int64_t c = 0;
       for (int64_t i = 0; i < n; i++) {
         double y;
-        if (yval(q[i * ld + j], rm[i], rinv[i], y)) { acc = acc + y; c++; }
+        if (yval(q_at<S16>(q, s16, i, ld, j), rm[i], rinv[i], y)) { acc = acc + y; c++; }
       }
       mu[j] = acc / (double)c;
     }
@@ -227,12 +277,11 @@ __global__ __launch_bounds__(256) void k_col_means(const int32_t *__restrict__ q
   int64_t cnt[VW];
 #pragma unroll
   for (int c = 0; c < VW; c++) { acc[c] = 0.0; cnt[c] = 0; }
-  const int32_t *col = q + j0;
   int64_t i = 0;
   for (; i + CU <= n; i += CU) {
     int32_t v[CU][VW];
 #pragma unroll
-    for (int u = 0; u < CU; u++) load_cols<VW>(col + (i + u) * ld, v[u]);
+    for (int u = 0; u < CU; u++) load_row<VW, S16>(q, s16, i + u, ld, j0, v[u]);
 #pragma unroll
     for (int u = 0; u < CU; u++) {
       const double r = rm[i + u], ri = rinv[i + u];
@@ -245,7 +294,7 @@ __global__ __launch_bounds__(256) void k_col_means(const int32_t *__restrict__ q
   }
   for (; i < n; i++) {
     int32_t v[VW];
-    load_cols<VW>(col + i * ld, v);
+    load_row<VW, S16>(q, s16, i, ld, j0, v);
 #pragma unroll
     for (int c = 0; c < VW; c++) {
       double y;
@@ -256,8 +305,8 @@ __global__ __launch_bounds__(256) void k_col_means(const int32_t *__restrict__ q
   for (int c = 0; c < VW; c++) mu[j0 + c] = acc[c] / (double)cnt[c];   // 0/0 -> NaN (numpy)
 }
 
-template <int VW>
-__global__ __launch_bounds__(256) void k_col_vars(const int32_t *__restrict__ q, int64_t n, int64_t m,
+template <int VW, bool S16>
+__global__ __launch_bounds__(256) void k_col_vars(const int32_t *__restrict__ q, Q16 s16, int64_t n, int64_t m,
                                                   int64_t ld, const double *__restrict__ rm,
                                                   const double *__restrict__ rinv,
                                                   const double *__restrict__ mu, double *__restrict__ var,
@@ -271,7 +320,7 @@ __global__ __launch_bounds__(256) void k_col_vars(const int32_t *__restrict__ q,
       double acc = 0.0;
       for (int64_t i = 0; i < n; i++) {
         double y;
-        if (yval(q[i * ld + j], rm[i], rinv[i], y)) {
+        if (yval(q_at<S16>(q, s16, i, ld, j), rm[i], rinv[i], y)) {
           double d = y - mj, dd = d * d;
           if (dd == dd) acc = acc + dd;
         }
@@ -285,12 +334,11 @@ __global__ __launch_bounds__(256) void k_col_vars(const int32_t *__restrict__ q,
   double acc[VW], mj[VW];
 #pragma unroll
   for (int c = 0; c < VW; c++) { acc[c] = 0.0; mj[c] = mu[j0 + c]; }
-  const int32_t *col = q + j0;
   int64_t i = 0;
   for (; i + CU <= n; i += CU) {
     int32_t v[CU][VW];
 #pragma unroll
-    for (int u = 0; u < CU; u++) load_cols<VW>(col + (i + u) * ld, v[u]);
+    for (int u = 0; u < CU; u++) load_row<VW, S16>(q, s16, i + u, ld, j0, v[u]);
 #pragma unroll
     for (int u = 0; u < CU; u++) {
       const double r = rm[i + u], ri = rinv[i + u];
@@ -306,7 +354,7 @@ __global__ __launch_bounds__(256) void k_col_vars(const int32_t *__restrict__ q,
   }
   for (; i < n; i++) {
     int32_t v[VW];
-    load_cols<VW>(col + i * ld, v);
+    load_row<VW, S16>(q, s16, i, ld, j0, v);
 #pragma unroll
     for (int c = 0; c < VW; c++) {
       double y;
@@ -354,6 +402,13 @@ constexpr int ZRB = 1;   // row batches per thread (4 measured slower: 22.6 vs 2
 // farther than delta from every half-integer, rint(t') IS k, and when it is
 // also farther than delta from 0 its sign is z's sign ("-0.00").  Otherwise
 // (probability ~1e-4 per cell) the exact fp64 chain below decides.
+// Select code d (0..7) of the 8 consecutive uint16 in (a, b).
+__device__ __forceinline__ uint32_t pick8u16(const uint2 &a, const uint2 &b, int d) {
+  const uint2 h = (d & 4) ? b : a;
+  const uint32_t w = (d & 2) ? h.y : h.x;
+  return (d & 1) ? (w >> 16) : (w & 0xFFFFu);
+}
+
 // Select element d (0..7) of the 8 consecutive ints (a, b).
 __device__ __forceinline__ int32_t pick8(const int4 &a, const int4 &b, int d) {
   const int4 h = (d & 4) ? b : a;
@@ -374,8 +429,8 @@ __device__ __forceinline__ void zquant_rows(const int32_t (&qv)[ZR][4], int64_t 
 // as two aligned int4 loads and the 4 values picked in registers; 4 dword
 // gathers per row (16 B used per 64-B line each) took 2x the HBM time.
 // Threads whose columns spread wider gather them one by one.
-template <bool VEC>
-__global__ __launch_bounds__(256) void k_zquant4(const int32_t *__restrict__ q, int64_t n, int64_t ld,
+template <bool VEC, bool S16>
+__global__ __launch_bounds__(256) void k_zquant4(const int32_t *__restrict__ q, Q16 s16, int64_t n, int64_t ld,
                                                  const int32_t *__restrict__ sel, int64_t r,
                                                  const double *__restrict__ rm, const double *__restrict__ rinv,
                                                  const double *__restrict__ mus, const double *__restrict__ sq,
@@ -399,8 +454,9 @@ __global__ __launch_bounds__(256) void k_zquant4(const int32_t *__restrict__ q, 
     m32[c] = mc.x;
     c32[c] = mc.y;
   }
+  // two aligned loads cover 8 columns: int4 pairs (int32) or uint2 pairs (compact)
   const int64_t base = js[0] & ~3ll;
-  const bool fast = VEC && js[w - 1] - base < 8 && base + 8 <= ld;
+  const bool fast = (S16 || VEC) && js[w - 1] - base < 8 && base + 8 <= ld;
   int d[4];
 #pragma unroll
   for (int c = 0; c < 4; c++) d[c] = (int)(js[c] - base);
@@ -409,7 +465,45 @@ __global__ __launch_bounds__(256) void k_zquant4(const int32_t *__restrict__ q, 
     if (i0 >= n) break;
     const int64_t i1 = (i0 + ZR < n) ? i0 + ZR : n;
     int32_t qv[ZR][4];
-    if (fast) {
+    if (S16 && fast) {
+      uint2 va[ZR], vb[ZR];
+#pragma unroll
+      for (int u = 0; u < ZR; u++) {
+        const int64_t i = (i0 + u < i1) ? i0 + u : i0;
+        const uint2 *p = reinterpret_cast<const uint2 *>(s16.q + i * ld + base);
+        va[u] = p[0];
+        vb[u] = p[1];
+      }
+      uint32_t mx = 0;
+#pragma unroll
+      for (int u = 0; u < ZR; u++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+          const uint32_t code = pick8u16(va[u], vb[u], d[c]);
+          qv[u][c] = (int32_t)code;
+          mx = max(mx, (i0 + u < i1 && c < w) ? code : 0u);
+        }
+      if (__builtin_expect(mx > GRID_Q16_MAXV, 0)) {       // rare: missing / escapes
+#pragma unroll
+        for (int u = 0; u < ZR; u++)
+#pragma unroll
+          for (int c = 0; c < 4; c++)
+            if (i0 + u < i1 && c < w && (uint32_t)qv[u][c] > GRID_Q16_MAXV)
+              qv[u][c] = q16_slow((uint32_t)qv[u][c], i0 + u, js[c], s16);
+      }
+#pragma unroll
+      for (int u = 0; u < ZR; u++)
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+          if (!(i0 + u < i1 && c < w)) qv[u][c] = GRID_MISSING;
+    } else if (S16) {
+#pragma unroll
+      for (int u = 0; u < ZR; u++)
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+          qv[u][c] = (i0 + u < i1 && c < w) ? q16_val(s16.q[(i0 + u) * ld + js[c]], i0 + u, js[c], s16)
+                                             : GRID_MISSING;
+    } else if (fast) {
       int4 va[ZR], vb[ZR];
 #pragma unroll
       for (int u = 0; u < ZR; u++) {
@@ -556,27 +650,45 @@ int grid_norm_zfull(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t m, int
 }
 
 
-int grid_norm_row_blocks(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t m, int64_t ld,
-                         double *d_bsum, int32_t *d_bcnt) {
+static bool vec4_ok(const void *p, int64_t ld) { return ((uintptr_t)p % 16) == 0 && ld % 4 == 0; }
+static const Q16 kNoQ16 = {nullptr, nullptr, nullptr, nullptr};
+static bool q16_ok(const grid_depth16 *q, int64_t ld) {
+  return q && q->q && q->eoff && ((uintptr_t)q->q % 16) == 0 && ld % 8 == 0;
+}
+static Q16 to_q16(const grid_depth16 *q) { return Q16{q->q, q->eoff, q->ecol, q->eval}; }
+
+// Row blocks from an int32 (d_q) or compact (s16.q) matrix.
+static int row_blocks_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, int64_t n, int64_t m, int64_t ld,
+                           double *d_bsum, int32_t *d_bcnt) {
   REQUIRE(ctx && n >= 0 && m >= 0 && ld >= m, "bad args");
   if (n == 0 || m == 0) return GRID_OK;
+  const bool c16 = s16.q != nullptr;
   int64_t nblk = ceil_div(m, BLK), nfull = m / BLK;
   if (nfull > 0) {
     REQUIRE(n <= 65535, "n > 65535 rows per launch");
-    if (((uintptr_t)d_q % 16) == 0 && ld % 4 == 0)
-      hipLaunchKernelGGL(k_row_blocks_full<true>, dim3((unsigned)nfull, (unsigned)n), dim3(256), 0, ctx->stream,
-                         d_q, ld, nfull, nblk, d_bsum, d_bcnt);
-    else
-      hipLaunchKernelGGL(k_row_blocks_full<false>, dim3((unsigned)nfull, (unsigned)n), dim3(256), 0, ctx->stream,
-                         d_q, ld, nfull, nblk, d_bsum, d_bcnt);
+    auto kern = c16 ? k_row_blocks_full<2> : vec4_ok(d_q, ld) ? k_row_blocks_full<0> : k_row_blocks_full<1>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)nfull, (unsigned)n), dim3(256), 0, ctx->stream, d_q, s16, ld, nfull, nblk,
+                       d_bsum, d_bcnt);
     LAUNCHCHK();
   }
   if (nblk > nfull) {
-    hipLaunchKernelGGL(k_row_block_tail, dim3((unsigned)ceil_div(n, 64)), dim3(64), 0, ctx->stream, d_q, n,
-                       ld, m, nblk, d_bsum, d_bcnt);
+    auto kern = c16 ? k_row_block_tail<true> : k_row_block_tail<false>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)ceil_div(n, 64)), dim3(64), 0, ctx->stream, d_q, s16, n, ld, m, nblk,
+                       d_bsum, d_bcnt);
     LAUNCHCHK();
   }
   return GRID_OK;
+}
+
+int grid_norm_row_blocks(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t m, int64_t ld,
+                         double *d_bsum, int32_t *d_bcnt) {
+  return row_blocks_impl(ctx, d_q, kNoQ16, n, m, ld, d_bsum, d_bcnt);
+}
+
+int grid_norm_row_blocks_q16(grid_ctx *ctx, const grid_depth16 *q, int64_t n, int64_t m, int64_t ld,
+                             double *d_bsum, int32_t *d_bcnt) {
+  REQUIRE(q16_ok(q, ld), "compact matrix: 16-byte aligned q, ld %% 8 == 0 and escape offsets required");
+  return row_blocks_impl(ctx, nullptr, to_q16(q), n, m, ld, d_bsum, d_bcnt);
 }
 
 int grid_norm_row_means(grid_ctx *ctx, const double *d_bsum, const int32_t *d_bcnt, int64_t n,
@@ -603,48 +715,55 @@ static int recip_rows(grid_ctx *ctx, const double *d_rm, int64_t n, size_t extra
   return GRID_OK;
 }
 
-static bool vec4_ok(const void *p, int64_t ld) { return ((uintptr_t)p % 16) == 0 && ld % 4 == 0; }
-
-int grid_norm_col_means(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t m, int64_t ld,
-                        const double *d_rm, double *d_mu) {
+static int col_stats_impl(grid_ctx *ctx, bool vars, const int32_t *d_q, const Q16 &s16, int64_t n, int64_t m,
+                          int64_t ld, const double *d_rm, const double *d_mu, double *d_out, double *d_ratio) {
   REQUIRE(ctx && n >= 0 && m >= 0 && ld >= m, "bad args");
   if (m == 0) return GRID_OK;
   double *rinv;
   char *rest;
   int rc = recip_rows(ctx, d_rm, n, 0, &rinv, &rest);
   if (rc) return rc;
-  if (vec4_ok(d_q, ld))
-    hipLaunchKernelGGL(k_col_means<4>, dim3((unsigned)ceil_div(ceil_div(m, 4), 256)), dim3(256), 0, ctx->stream,
-                       d_q, n, m, ld, d_rm, rinv, d_mu);
-  else
-    hipLaunchKernelGGL(k_col_means<1>, dim3((unsigned)ceil_div(m, 256)), dim3(256), 0, ctx->stream, d_q, n, m,
-                       ld, d_rm, rinv, d_mu);
+  const int vw = (s16.q || vec4_ok(d_q, ld)) ? 4 : 1;
+  const dim3 grid((unsigned)ceil_div(ceil_div(m, vw), 256));
+  if (!vars) {
+    auto kern = s16.q ? k_col_means<4, true> : vw == 4 ? k_col_means<4, false> : k_col_means<1, false>;
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, ctx->stream, d_q, s16, n, m, ld, d_rm, rinv, d_out);
+  } else {
+    auto kern = s16.q ? k_col_vars<4, true> : vw == 4 ? k_col_vars<4, false> : k_col_vars<1, false>;
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, ctx->stream, d_q, s16, n, m, ld, d_rm, rinv, d_mu, d_out,
+                       d_ratio);
+  }
   LAUNCHCHK();
   return GRID_OK;
 }
 
+int grid_norm_col_means(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t m, int64_t ld,
+                        const double *d_rm, double *d_mu) {
+  return col_stats_impl(ctx, false, d_q, kNoQ16, n, m, ld, d_rm, nullptr, d_mu, nullptr);
+}
+
 int grid_norm_col_vars(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t m, int64_t ld,
                        const double *d_rm, const double *d_mu, double *d_var, double *d_ratio) {
-  REQUIRE(ctx && n >= 0 && m >= 0 && ld >= m, "bad args");
-  if (m == 0) return GRID_OK;
-  double *rinv;
-  char *rest;
-  int rc = recip_rows(ctx, d_rm, n, 0, &rinv, &rest);
-  if (rc) return rc;
-  if (vec4_ok(d_q, ld))
-    hipLaunchKernelGGL(k_col_vars<4>, dim3((unsigned)ceil_div(ceil_div(m, 4), 256)), dim3(256), 0, ctx->stream,
-                       d_q, n, m, ld, d_rm, rinv, d_mu, d_var, d_ratio);
-  else
-    hipLaunchKernelGGL(k_col_vars<1>, dim3((unsigned)ceil_div(m, 256)), dim3(256), 0, ctx->stream, d_q, n, m,
-                       ld, d_rm, rinv, d_mu, d_var, d_ratio);
-  LAUNCHCHK();
-  return GRID_OK;
+  return col_stats_impl(ctx, true, d_q, kNoQ16, n, m, ld, d_rm, d_mu, d_var, d_ratio);
+}
+
+int grid_norm_col_means_q16(grid_ctx *ctx, const grid_depth16 *q, int64_t n, int64_t m, int64_t ld,
+                            const double *d_rm, double *d_mu) {
+  REQUIRE(q16_ok(q, ld), "compact matrix: 16-byte aligned q, ld %% 8 == 0 and escape offsets required");
+  return col_stats_impl(ctx, false, nullptr, to_q16(q), n, m, ld, d_rm, nullptr, d_mu, nullptr);
+}
+
+int grid_norm_col_vars_q16(grid_ctx *ctx, const grid_depth16 *q, int64_t n, int64_t m, int64_t ld,
+                           const double *d_rm, const double *d_mu, double *d_var, double *d_ratio) {
+  REQUIRE(q16_ok(q, ld), "compact matrix: 16-byte aligned q, ld %% 8 == 0 and escape offsets required");
+  return col_stats_impl(ctx, true, nullptr, to_q16(q), n, m, ld, d_rm, d_mu, d_var, d_ratio);
 }
 
 }  // extern "C"
 
 namespace {
-static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t ld, const int32_t *d_sel,
+static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, int64_t n, int64_t ld,
+                       const int32_t *d_sel,
                        int64_t r, const double *d_rm, const double *d_mu, double scale, int32_t *d_zq,
                        int64_t ld_zq, const int32_t *d_colmap, int32_t qmax, uint16_t *d_zb,
                        int64_t ld_zb, int64_t kbs, int32_t *h_overflow) {
@@ -667,9 +786,9 @@ static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t ld,
   hipLaunchKernelGGL(k_zprep, dim3((unsigned)ceil_div(r, 256)), dim3(256), 0, ctx->stream, d_sel, r, d_mu, scale, mus,
                      sq, rsq, mc32);
   LAUNCHCHK();
-  auto kz = vec4_ok(d_q, ld) ? k_zquant4<true> : k_zquant4<false>;
+  auto kz = s16.q ? k_zquant4<false, true> : vec4_ok(d_q, ld) ? k_zquant4<true, false> : k_zquant4<false, false>;
   hipLaunchKernelGGL(kz, dim3((unsigned)ceil_div(ceil_div(r, 4), 256), (unsigned)ceil_div(n, ZR * ZRB)), dim3(256), 0,
-                     ctx->stream, d_q, n, ld, d_sel, r, d_rm, rinv, mus, sq, rsq, mc32, scale, d_zq, ld_zq, d_colmap,
+                     ctx->stream, d_q, s16, n, ld, d_sel, r, d_rm, rinv, mus, sq, rsq, mc32, scale, d_zq, ld_zq, d_colmap,
                      qmax, d_zb, ld_zb, kbs, d_of);
   LAUNCHCHK();
   if (h_overflow) {
@@ -688,8 +807,8 @@ int grid_norm_zquant(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t ld, c
                      int64_t r, const double *d_rm, const double *d_mu, double scale, int32_t *d_zq,
                      int64_t ld_zq, const int32_t *d_colmap, int32_t qmax, uint16_t *d_zb,
                      int64_t ld_zb, int32_t *h_overflow) {
-  return zquant_impl(ctx, d_q, n, ld, d_sel, r, d_rm, d_mu, scale, d_zq, ld_zq, d_colmap, qmax, d_zb, ld_zb, 0,
-                     h_overflow);
+  return zquant_impl(ctx, d_q, kNoQ16, n, ld, d_sel, r, d_rm, d_mu, scale, d_zq, ld_zq, d_colmap, qmax, d_zb,
+                     ld_zb, 0, h_overflow);
 }
 
 int grid_norm_zquant_kb(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t ld, const int32_t *d_sel,
@@ -697,8 +816,18 @@ int grid_norm_zquant_kb(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t ld
                         int64_t ld_zq, const int32_t *d_colmap, int32_t qmax, uint16_t *d_zb,
                         int64_t np_zb, int32_t *h_overflow) {
   REQUIRE(np_zb >= n && np_zb % 64 == 0, "np_zb must be >= n and a multiple of 64");
-  return zquant_impl(ctx, d_q, n, ld, d_sel, r, d_rm, d_mu, scale, d_zq, ld_zq, d_colmap, qmax, d_zb, 64,
+  return zquant_impl(ctx, d_q, kNoQ16, n, ld, d_sel, r, d_rm, d_mu, scale, d_zq, ld_zq, d_colmap, qmax, d_zb, 64,
                      np_zb * 64, h_overflow);
+}
+
+int grid_norm_zquant_kb_q16(grid_ctx *ctx, const grid_depth16 *q, int64_t n, int64_t ld, const int32_t *d_sel,
+                            int64_t r, const double *d_rm, const double *d_mu, double scale, int32_t *d_zq,
+                            int64_t ld_zq, const int32_t *d_colmap, int32_t qmax, uint16_t *d_zb,
+                            int64_t np_zb, int32_t *h_overflow) {
+  REQUIRE(q16_ok(q, ld), "compact matrix: 16-byte aligned q, ld %% 8 == 0 and escape offsets required");
+  REQUIRE(np_zb >= n && np_zb % 64 == 0, "np_zb must be >= n and a multiple of 64");
+  return zquant_impl(ctx, nullptr, to_q16(q), n, ld, d_sel, r, d_rm, d_mu, scale, d_zq, ld_zq, d_colmap, qmax, d_zb,
+                     64, np_zb * 64, h_overflow);
 }
 
 }  // extern "C"

@@ -1,0 +1,50 @@
+// The synthetic mosdepth cohort model shared by grid_synth_depth (int32) and
+// grid_synth_depth_q16 (compact form).  Every cell is a pure function of
+// (seed, sample, GLOBAL bin), so bin shards generated on different GPUs
+// concatenate to the same matrix.
+//   depth = base_b * (1 + off_{c(i),b}) * scale_i * cnv_{i,b} * noise_{i,b} * spike_{i,b}
+//   base_b in [25,55), |off| < 8 % for 26 ancestry clusters, scale_i in
+//   [0.6,1.4), 2 % CNV cells at x0.5 / x1.5, +-20 % triangular noise, and
+//   1 in 65536 cells a x40 collapsed-repeat spike (depths of 500-3000: the
+//   values the compact form stores in its escape table); int32 hundredths
+//   (mosdepth prints %.2f).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace synth {
+
+__device__ __forceinline__ uint64_t mix(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ float unif(uint64_t h) { return (float)(h >> 40) * (1.0f / 16777216.0f); }
+
+// Per-sample part (cluster, depth scale): hoisted out of the column loop.
+struct Sample {
+  int c;
+  float scale;
+};
+__device__ __forceinline__ Sample sample(uint64_t seed, int64_t i, int ncl) {
+  const uint64_t hs = mix(seed ^ (0xA5A5ull << 48) ^ (uint64_t)i);
+  return Sample{(int)(mix(hs) % (uint64_t)ncl), 0.6f + 0.8f * unif(hs)};
+}
+
+__device__ __forceinline__ int32_t depth_q(uint64_t seed, int64_t i, const Sample &sm, uint64_t b) {
+  const float base = 25.0f + 30.0f * unif(mix(seed ^ (b * 0x9E37ull) ^ 0x1234ull));
+  const float off = 0.16f * (unif(mix(seed ^ (b << 8) ^ (uint64_t)sm.c ^ 0x77ull)) - 0.5f);
+  const uint64_t hc = mix(seed ^ ((uint64_t)i << 40) ^ b);
+  const float u1 = unif(hc), u2 = unif(mix(hc)), u3 = unif(mix(hc ^ 0x55ull));
+  float cnv = 1.0f;
+  if (u3 < 0.02f) cnv = (u3 < 0.01f) ? 0.5f : 1.5f;
+  const float spike = ((hc & 0xFFFFull) == 0x2A2Aull) ? 40.0f : 1.0f;
+  const float noise = 1.0f + 0.2f * (u1 + u2 - 1.0f);
+  const float d = base * (1.0f + off) * sm.scale * cnv * noise * spike;
+  return (int32_t)rintf(d * 100.0f);
+}
+
+}  // namespace synth

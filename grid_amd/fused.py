@@ -45,6 +45,35 @@ def shard_range(m: int, rank: int, world: int):
     return min(b0 * BLOCK, m), min(b1 * BLOCK, m)
 
 
+class Depth16:
+    """Compact depth matrix on the device (include/grid_abi.h grid_depth16):
+    uint16 hundredths [n][ld] (ld % 8 == 0) plus the row-sorted escape table
+    for depths above 655.33.  Half the HBM bytes of the int32 matrix in each
+    of step 4's four passes; the kernels decode it to the same int32 values."""
+
+    def __init__(self, q16, eoff, ecol, evals, ld):
+        self.q16, self.eoff, self.ecol, self.evals, self.ld = q16, eoff, ecol, evals, ld
+        self.desc = _abi.Depth16Desc(ptr(q16), ptr(eoff), ptr(ecol), ptr(evals))
+
+    @classmethod
+    def synth(cls, alloc, ctx, seed, n, m, col0, ncl, exc_cap=None):
+        """The bench cohort (csrc/synth_model.hpp) generated in compact form."""
+        ld = -(-max(m, 1) // 8) * 8
+        q16 = alloc.empty((max(n, 1), ld), U2)
+        eoff = alloc.empty(max(n, 1) + 1, I8)
+        cap = exc_cap if exc_cap is not None else n * m // 32768 + 4096
+        while True:
+            ecol, evals = alloc.empty(max(cap, 1), I4), alloc.empty(max(cap, 1), I4)
+            need = C.c_int64()
+            rc = _abi.load().grid_synth_depth_q16(ctx, seed, n, m, ld, col0, ncl, ptr(q16), ptr(eoff),
+                                                  ptr(ecol), ptr(evals), cap, C.byref(need))
+            if rc == 0:
+                return cls(q16, eoff, ecol, evals, ld)
+            if rc != 5 or need.value <= cap:            # GRID_ERANGE: grow and retry
+                _abi.check(rc, "grid_synth_depth_q16")
+            cap = need.value
+
+
 class TorchAlloc:
     """Buffers as torch tensors (device "cuda:i", or "cpu" in tests)."""
 
@@ -105,17 +134,28 @@ class HipOps:
         self.ctx = dev.ctx
         self.zerodiv = C.c_int32()
 
+    # q: an int32 hundredths buffer, or a Depth16 (compact form, *_q16 entry points)
     def row_blocks(self, q, n, m, ld, bsum, bcnt):
-        call("grid_norm_row_blocks", self.ctx, ptr(q), n, m, ld, ptr(bsum), ptr(bcnt))
+        if isinstance(q, Depth16):
+            call("grid_norm_row_blocks_q16", self.ctx, C.byref(q.desc), n, m, q.ld, ptr(bsum), ptr(bcnt))
+        else:
+            call("grid_norm_row_blocks", self.ctx, ptr(q), n, m, ld, ptr(bsum), ptr(bcnt))
 
     def row_means(self, bsum, bcnt, n, nblk, rm):
         call("grid_norm_row_means", self.ctx, ptr(bsum), ptr(bcnt), n, nblk, ptr(rm))
 
     def col_means(self, q, n, m, ld, rm, mu):
-        call("grid_norm_col_means", self.ctx, ptr(q), n, m, ld, ptr(rm), ptr(mu))
+        if isinstance(q, Depth16):
+            call("grid_norm_col_means_q16", self.ctx, C.byref(q.desc), n, m, q.ld, ptr(rm), ptr(mu))
+        else:
+            call("grid_norm_col_means", self.ctx, ptr(q), n, m, ld, ptr(rm), ptr(mu))
 
     def col_vars(self, q, n, m, ld, rm, mu, var, ratio):
-        call("grid_norm_col_vars", self.ctx, ptr(q), n, m, ld, ptr(rm), ptr(mu), ptr(var), ptr(ratio))
+        if isinstance(q, Depth16):
+            call("grid_norm_col_vars_q16", self.ctx, C.byref(q.desc), n, m, q.ld, ptr(rm), ptr(mu), ptr(var),
+                 ptr(ratio))
+        else:
+            call("grid_norm_col_vars", self.ctx, ptr(q), n, m, ld, ptr(rm), ptr(mu), ptr(var), ptr(ratio))
 
     def sort_valid(self, v, n, out):
         nv = C.c_int64()
@@ -141,8 +181,12 @@ class HipOps:
     def zquant(self, q, n, ld, sel, r, rm, mu, scale, zq, ld_zq, colmap, qmax, zb, np_zb):
         """z hundredths + the K-blocked bf16 panel [kpad/64][np_zb][64]."""
         of = C.c_int32()
-        call("grid_norm_zquant_kb", self.ctx, ptr(q), n, ld, ptr(sel), r, ptr(rm), ptr(mu), scale, ptr(zq), ld_zq,
-             ptr(colmap), qmax, ptr(zb), np_zb, C.byref(of))
+        if isinstance(q, Depth16):
+            call("grid_norm_zquant_kb_q16", self.ctx, C.byref(q.desc), n, q.ld, ptr(sel), r, ptr(rm), ptr(mu), scale,
+                 ptr(zq), ld_zq, ptr(colmap), qmax, ptr(zb), np_zb, C.byref(of))
+        else:
+            call("grid_norm_zquant_kb", self.ctx, ptr(q), n, ld, ptr(sel), r, ptr(rm), ptr(mu), scale, ptr(zq),
+                 ld_zq, ptr(colmap), qmax, ptr(zb), np_zb, C.byref(of))
         return of.value
 
     def gram(self, zb, np_, kpad, qmax, gram):

@@ -45,6 +45,10 @@ extern "C" {
 #define GRID_ZQ_NAN ((int32_t)0x80000000)    /* z printed as "NA"         */
 #define GRID_ZQ_NEG0 ((int32_t)0x80000001)   /* z printed as "-0.00"      */
 #define GRID_BLOCK 8192                      /* NumPy reduction buffer    */
+/* Compact depth matrix codes (uint16 hundredths; see grid_depth16). */
+#define GRID_Q16_MAXV 0xFFFD                 /* largest value stored inline */
+#define GRID_Q16_ESC 0xFFFE                  /* value in the escape table   */
+#define GRID_Q16_MISS 0xFFFF                 /* NaN depth cell              */
 
 typedef struct grid_ctx grid_ctx;
 
@@ -78,6 +82,30 @@ int grid_event_elapsed(grid_ctx *ctx, int slot_a, int slot_b, float *ms);
  *
  * d_q: [n][ld] int32 hundredths, columns [0, m) are this shard, whose first
  * column sits at a GLOBAL offset that is a multiple of GRID_BLOCK. */
+
+/* Compact depth matrix: the same hundredths as uint16 q[i*ld + j] (half the
+ * HBM bytes of every pass), values > GRID_Q16_MAXV exactly in a row-sorted
+ * escape table (eoff: [n+1] offsets, ecol / eval: column and value).  All
+ * pointers are device pointers; the struct itself is passed from the host. */
+typedef struct grid_depth16 {
+  const uint16_t *q;
+  const int64_t *eoff;
+  const int32_t *ecol;
+  const int32_t *eval;
+} grid_depth16;
+/* int32 hundredths -> compact form.  Escape table capacity exc_cap entries;
+ * *h_nexc receives the number needed (GRID_ERANGE if > exc_cap). */
+int grid_q16_encode(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t m, int64_t ld,
+                    uint16_t *d_q16, int64_t ld16, int64_t *d_eoff, int32_t *d_ecol,
+                    int32_t *d_eval, int64_t exc_cap, int64_t *h_nexc);
+/* The q16 forms of the four step-4 passes below (same outputs bit for bit). */
+int grid_norm_row_blocks_q16(grid_ctx *ctx, const grid_depth16 *q, int64_t n, int64_t m,
+                             int64_t ld, double *d_blocksum, int32_t *d_blockcnt);
+int grid_norm_col_means_q16(grid_ctx *ctx, const grid_depth16 *q, int64_t n, int64_t m,
+                            int64_t ld, const double *d_rowmean, double *d_mu);
+int grid_norm_col_vars_q16(grid_ctx *ctx, const grid_depth16 *q, int64_t n, int64_t m,
+                           int64_t ld, const double *d_rowmean, const double *d_mu,
+                           double *d_var, double *d_ratio);
 
 /* Per-row, per-8192-block pairwise sums of q/100 (NaN->0) and counts.
  * d_blocksum/d_blockcnt: [n][ceil(m/8192)]. */
@@ -129,6 +157,12 @@ int grid_norm_zquant_kb(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t ld
                         const double *d_mu, double scale, int32_t *d_zq, int64_t ld_zq,
                         const int32_t *d_colmap, int32_t qmax, uint16_t *d_zb, int64_t np_zb,
                         int32_t *h_overflow);
+
+int grid_norm_zquant_kb_q16(grid_ctx *ctx, const grid_depth16 *q, int64_t n, int64_t ld,
+                            const int32_t *d_sel, int64_t r, const double *d_rowmean,
+                            const double *d_mu, double scale, int32_t *d_zq, int64_t ld_zq,
+                            const int32_t *d_colmap, int32_t qmax, uint16_t *d_zb, int64_t np_zb,
+                            int32_t *h_overflow);
 
 /* The full fp64 matrix normalize_matrix returns (:458, :470): z[i*m+j] =
  * ((y-mu)/sqrt(mu))*scale where mu > 0, y*scale elsewhere, NaN if missing. */
@@ -226,6 +260,10 @@ int grid_hi_phase_batch(grid_ctx *ctx, int64_t n_loci, const grid_hi_locus *d_lo
  * d_q[i*ld + j] = hundredths depth of sample i at GLOBAL bin col0 + j. */
 int grid_synth_depth(grid_ctx *ctx, uint64_t seed, int64_t n, int64_t m, int64_t ld, int64_t col0,
                      int32_t nclusters, int32_t *d_q);
+/* The same cohort in the compact form (grid_depth16), escapes included. */
+int grid_synth_depth_q16(grid_ctx *ctx, uint64_t seed, int64_t n, int64_t m, int64_t ld16, int64_t col0,
+                         int32_t nclusters, uint16_t *d_q16, int64_t *d_eoff, int32_t *d_ecol,
+                         int32_t *d_eval, int64_t exc_cap, int64_t *h_nexc);
 
 /* ---------------------------------------------------- host formatting
  * Exact "%.2f" text for integer hundredths (GRID_ZQ_* sentinels -> "NA",

@@ -1,0 +1,138 @@
+"""Compact depth matrix (grid_depth16: uint16 hundredths + row-sorted escape
+table): the encoder round-trips exactly, the synthetic generator's compact
+form equals the encoded int32 cohort, and every step-4 kernel gives the same
+bits from either form (so the whole chain does)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+MISSING = -(2 ** 31)
+MAXV, ESC, MISS = 0xFFFD, 0xFFFE, 0xFFFF
+
+
+@pytest.fixture(scope="module")
+def dev():
+    from grid_amd import _abi
+    d = _abi.Device(0)
+    d.set_stream(torch.cuda.current_stream())
+    return d
+
+
+def encode(dev, q):
+    """int32 device tensor [n][m] -> (q16, eoff, ecol, eval) torch tensors."""
+    from grid_amd import _abi
+    n, m = q.shape
+    ld16 = -(-m // 8) * 8
+    q16 = torch.zeros((n, ld16), dtype=torch.int16, device="cuda")
+    eoff = torch.zeros(n + 1, dtype=torch.int64, device="cuda")
+    cap = int((q.cpu() > MAXV).sum() + 1)
+    ecol = torch.zeros(cap, dtype=torch.int32, device="cuda")
+    ev = torch.zeros(cap, dtype=torch.int32, device="cuda")
+    need = C.c_int64()
+    _abi.call("grid_q16_encode", dev.ctx, q.data_ptr(), n, m, m, q16.data_ptr(), ld16, eoff.data_ptr(),
+              ecol.data_ptr(), ev.data_ptr(), cap, C.byref(need))
+    return q16, eoff, ecol[: need.value], ev[: need.value], ld16
+
+
+def decode_host(q16, eoff, ecol, ev, m):
+    c = q16.cpu().numpy().view(np.uint16)[:, :m].astype(np.int64)
+    out = np.where(c == MISS, MISSING, c)
+    eo, ec, evv = eoff.cpu().numpy(), ecol.cpu().numpy(), ev.cpu().numpy()
+    for i in range(c.shape[0]):
+        cols = ec[eo[i]: eo[i + 1]]
+        assert np.all(np.diff(cols) > 0)
+        assert np.all(c[i, cols] == ESC)
+        out[i, cols] = evv[eo[i]: eo[i + 1]]
+    assert int((c == ESC).sum()) == len(ec)
+    return out.astype(np.int64)
+
+
+def random_depths(n, m, seed):
+    rng = np.random.default_rng(seed)
+    q = rng.integers(0, 9000, (n, m)).astype(np.int64)
+    q[rng.random((n, m)) < 0.01] = MISSING
+    big = rng.random((n, m)) < 0.002
+    q[big] = rng.integers(MAXV - 2, 400000, int(big.sum()))
+    q[0, :5] = [MAXV, MAXV + 1, 0, MISSING, 2 ** 31 - 1]
+    return q.astype(np.int32)
+
+
+def test_encode_roundtrip(dev):
+    q = random_depths(37, 20003, 1)
+    qd = torch.from_numpy(q).cuda()
+    q16, eoff, ecol, ev, _ = encode(dev, qd)
+    assert np.array_equal(decode_host(q16, eoff, ecol, ev, q.shape[1]), q.astype(np.int64))
+
+
+def test_synth_q16_equals_encoded_synth(dev):
+    from grid_amd import _abi
+    from grid_amd.fused import Depth16, TorchAlloc
+    n, m, col0 = 50, 70001, 8192 * 3
+    q = torch.empty((n, m), dtype=torch.int32, device="cuda")
+    _abi.call("grid_synth_depth", dev.ctx, 77, n, m, m, col0, 26, q.data_ptr())
+    q16, eoff, ecol, ev, _ = encode(dev, q)
+    assert len(ecol) > 10                      # the model's x40 spikes reach the escape table
+    d = Depth16.synth(TorchAlloc(0), dev.ctx, 77, n, m, col0, 26, exc_cap=4)   # exercises the regrow
+    assert torch.equal(d.q16[:, :m], q16[:, :m])
+    assert torch.equal(d.eoff, eoff)
+    k = int(eoff[-1])
+    assert torch.equal(d.ecol[:k], ecol) and torch.equal(d.evals[:k], ev)
+
+
+def test_step4_kernels_q16_equal_int32(dev):
+    from grid_amd import _abi
+    from grid_amd.fused import Depth16, HipOps
+    n, m = 300, 2 * 8192 + 517
+    q = random_depths(n, m, 2)
+    q[:, 100] = MISSING
+    qd = torch.from_numpy(q).cuda()
+    q16, eoff, ecol, ev, ld16 = encode(dev, qd)
+    d16 = Depth16(q16, eoff, ecol, ev, ld16)
+    ops = HipOps(dev)
+    nblk = -(-m // 8192)
+    out = {}
+    for name, src, ld in (("i32", qd, m), ("q16", d16, ld16)):
+        bsum = torch.zeros((n, nblk), dtype=torch.float64, device="cuda")
+        bcnt = torch.zeros((n, nblk), dtype=torch.int32, device="cuda")
+        ops.row_blocks(src, n, m, ld, bsum, bcnt)
+        rm = torch.zeros(n, dtype=torch.float64, device="cuda")
+        ops.row_means(bsum, bcnt, n, nblk, rm)
+        mu, var, ratio = (torch.zeros(m, dtype=torch.float64, device="cuda") for _ in range(3))
+        ops.col_means(src, n, m, ld, rm, mu)
+        ops.col_vars(src, n, m, ld, rm, mu, var, ratio)
+        sel = torch.arange(0, m, 3, dtype=torch.int32, device="cuda")
+        r = len(sel)
+        colmap = torch.arange(r, dtype=torch.int32, device="cuda")
+        zq = torch.zeros((n, r), dtype=torch.int32, device="cuda")
+        kp = -(-r // 64) * 64
+        zb = torch.zeros((kp // 64, 512, 64), dtype=torch.int16, device="cuda")
+        ops.zquant(src, n, ld, sel, r, rm, mu, 1.7, zq, r, colmap, 200, zb, 512)
+        out[name] = [t.cpu().numpy() for t in (bsum, bcnt, rm, mu, var, ratio, zq, zb)]
+    for a, b in zip(out["i32"], out["q16"]):
+        assert np.array_equal(a, b, equal_nan=True)
+
+
+def test_chain_q16_equals_int32(dev):
+    from grid_amd import _abi
+    from grid_amd.fused import Depth16, HipOps, Steps47, TorchAlloc
+    import bench
+    n, m, k, iters = 260, 3 * 8192 + 100, 6, 10
+    reads, off, nbr, w = bench.synth_reads_and_ibs(n, seed=3, per_hap=4)
+    q = torch.empty((n, m), dtype=torch.int32, device="cuda")
+    _abi.call("grid_synth_depth", dev.ctx, 3, n, m, m, 0, 26, q.data_ptr())
+    d16 = Depth16.synth(TorchAlloc(0), dev.ctx, 3, n, m, 0, 26)
+    res = {}
+    for name, src, ld in (("i32", q, m), ("q16", d16, d16.ld)):
+        st = Steps47(HipOps(dev), TorchAlloc(0), n, m, 0, m, k=k, n_nbr=3, n_iters=iters)
+        st.set_reads(reads)
+        st.set_phasing_graph(off, nbr, w)
+        st.run(src, ld)
+        torch.cuda.synchronize()
+        res[name] = [t.cpu().numpy() for t in (st.rm[:n], st.mu[:m], st.var[:m], st.zq[:n, : st.r_loc],
+                                               st.idx_out[:n], st.d2[:n], st.dip[:n], st.hap[: 2 * n])]
+    for a, b in zip(res["i32"], res["q16"]):
+        assert np.array_equal(a, b, equal_nan=True)
