@@ -64,6 +64,11 @@ _SIGS = {
     "grid_hi_phase": [_vp, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
                       _i32, _i32],
     "grid_hi_phase_batch": [_vp, _i64, _vp, _i64, _i32, _i64, _i64, _i32, _i32],
+    "grid_write_normalized_gz": [C.c_char_p, _i64, _i64, C.c_char_p, _vp, _vp, _vp, _vp, _i64, _i32, _i32],
+    "grid_read_normalized_gz": [C.c_char_p, _i32, C.POINTER(_vp), C.POINTER(_i64), C.POINTER(_i64)],
+    "grid_ntext_ids_len": [_vp, C.POINTER(_i64)],
+    "grid_ntext_fetch": [_vp, _vp, _i64, _vp, _vp, _vp, _vp],
+    "grid_ntext_free": [_vp],
     "grid_q16_encode": [_vp, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _vp, _i64, C.POINTER(_i64)],
     "grid_synth_depth_q16": [_vp, C.c_uint64, _i64, _i64, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _i64,
                              C.POINTER(_i64)],
@@ -86,7 +91,12 @@ EXPORTS = tuple(_SIGS) + ("grid_last_error",)
 
 
 class GridNativeError(RuntimeError):
-    """The HIP native path failed or is unavailable (no silent fallback)."""
+    """The HIP native path failed or is unavailable (no silent fallback).
+    ``code``: the GRID_E* return code (None when not from a library call)."""
+
+    def __init__(self, msg, code=None):
+        super().__init__(msg)
+        self.code = code
 
 
 _lib = None
@@ -119,7 +129,7 @@ def check(rc: int, what: str = ""):
     msg = load().grid_last_error().decode(errors="replace")
     if rc == GRID_EZERODIV:
         raise ZeroDivisionError(msg or "float division by zero")
-    raise GridNativeError(f"{what}: {msg} (code {rc})")
+    raise GridNativeError(f"{what}: {msg} (code {rc})", rc)
 
 
 def call(name: str, *args):
@@ -254,6 +264,44 @@ def format_hundredths(v: np.ndarray) -> str:
     n = _i64()
     call("grid_format_hundredths", v.ctypes.data if v.size else None, v.size, buf, cap, C.byref(n))
     return buf.raw[: n.value].decode("ascii")
+
+
+def write_normalized_gz(path, ids, raw, sel_means, sel_ratios, zq, level=6, threads=None):
+    """Step-4 output file (normalize_mosdepth.py:502-554 text), threaded host
+    C++ formatting + multi-member gzip.  zq: [n][r] int32 hundredths."""
+    zq = np.ascontiguousarray(zq, dtype=np.int32)
+    n, r = (zq.shape if zq.ndim == 2 else (len(ids), 0))
+    raw = np.ascontiguousarray(raw, dtype=np.float64)
+    mu = np.ascontiguousarray(sel_means, dtype=np.float64)
+    rt = np.ascontiguousarray(sel_ratios, dtype=np.float64)
+    ids_b = "\n".join(ids).encode()
+    thr = threads or min(16, os.cpu_count() or 1)
+    call("grid_write_normalized_gz", str(path).encode(), n, r, ids_b, raw.ctypes.data, mu.ctypes.data,
+         rt.ctypes.data, zq.ctypes.data if zq.size else None, max(r, 0), level, thr)
+
+
+def read_normalized_gz(path, threads=None):
+    """Parse the step-4 file: (ids, scales [n], means [r], ratios [r], zq [n][r]
+    int32 hundredths).  Raises GridNativeError(code GRID_EUNSUPPORTED) when
+    the text leaves the "%.2f" grammar."""
+    lib = load()
+    h, n, r = _vp(), _i64(), _i64()
+    thr = threads or min(16, os.cpu_count() or 1)
+    check(lib.grid_read_normalized_gz(str(path).encode(), thr, C.byref(h), C.byref(n), C.byref(r)),
+          "grid_read_normalized_gz")
+    try:
+        n, r = n.value, r.value
+        ln = _i64()
+        call("grid_ntext_ids_len", h, C.byref(ln))
+        ids_buf = C.create_string_buffer(max(ln.value, 1))
+        scales, means, ratios = np.empty(n), np.empty(r), np.empty(r)
+        zq = np.empty((n, r), dtype=np.int32)
+        call("grid_ntext_fetch", h, ids_buf, ln.value, scales.ctypes.data, means.ctypes.data, ratios.ctypes.data,
+             zq.ctypes.data)
+        ids = ids_buf.raw[: ln.value].decode().split("\n")[:n]
+        return ids, scales, means, ratios, zq
+    finally:
+        lib.grid_ntext_free(h)
 
 
 def hi_levels(off: np.ndarray, nbr: np.ndarray):

@@ -44,6 +44,19 @@ def read_normalized_data(input_file):
 
 
 def _read_normalized_q(input_file):
+    """-> (ids, {id: scale}, zq [n][r] int hundredths, ratios).  Threaded host
+    C++ parser (grid_read_normalized_gz); text outside its strict "%.2f"
+    grammar goes through the general line parser below."""
+    try:
+        ids, sc, _means, ratios, zq = _abi.read_normalized_gz(input_file)
+        return ids, {i: float(v) for i, v in zip(ids, sc)}, zq.astype(np.int64), ratios
+    except _abi.GridNativeError as e:
+        if e.code != _abi.GRID_EUNSUPPORTED:
+            raise
+    return _read_normalized_q_py(input_file)
+
+
+def _read_normalized_q_py(input_file):
     ids, scales, rows = [], {}, []
     with gzip.open(input_file, "rt") as f:
         f.readline()

@@ -268,6 +268,27 @@ int grid_synth_depth_q16(grid_ctx *ctx, uint64_t seed, int64_t n, int64_t m, int
 /* ---------------------------------------------------- host formatting
  * Exact "%.2f" text for integer hundredths (GRID_ZQ_* sentinels -> "NA",
  * "-0.00"), tab-joined.  Returns bytes written in *h_len (no terminator). */
+/* ---------------------------------------------------- normalised-matrix text
+ * The step 4 -> 5 file (normalize_mosdepth.py:502-554 writes it,
+ * find_neighbors.py:81-124 reads it), host C++, threaded.
+ * Writer: rows formatted exactly ("%.2f" from integer hundredths, "%.3f"
+ * header values, "NA") and deflated as independent gzip members in parallel,
+ * written in order (multi-member gzip: the decompressed text is the
+ * reference's byte for byte).  ids_nl: IDs joined by '\n'. */
+int grid_write_normalized_gz(const char *path, int64_t n, int64_t r, const char *ids_nl,
+                             const double *raw, const double *sel_means, const double *sel_ratios,
+                             const int32_t *zq, int64_t ld_zq, int32_t level, int32_t threads);
+/* Reader: parse into a handle (*n_out rows, *r_out columns); z values as
+ * integer hundredths (GRID_MISSING for "NA").  GRID_EUNSUPPORTED if the text
+ * leaves the grammar (e.g. more than 2 decimals): callers fall back to the
+ * general parser.  Fetch with grid_ntext_fetch, release with grid_ntext_free. */
+int grid_read_normalized_gz(const char *path, int32_t threads, void **h_out, int64_t *n_out,
+                            int64_t *r_out);
+int grid_ntext_ids_len(const void *h, int64_t *len);
+int grid_ntext_fetch(const void *h, char *ids_nl, int64_t ids_cap, double *scales, double *means,
+                     double *ratios, int32_t *zq);
+int grid_ntext_free(void *h);
+
 int grid_format_hundredths(const int32_t *h_v, int64_t n, char *h_out, int64_t cap,
                            int64_t *h_len);
 
