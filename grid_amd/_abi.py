@@ -69,6 +69,11 @@ _SIGS = {
     "grid_ntext_ids_len": [_vp, C.POINTER(_i64)],
     "grid_ntext_fetch": [_vp, _vp, _i64, _vp, _vp, _vp, _vp],
     "grid_ntext_free": [_vp],
+    "grid_load_ibs": [C.c_char_p, C.c_char_p, _i64, _i64, C.POINTER(_vp), C.POINTER(_i64)],
+    "grid_load_ibd": [C.c_char_p, C.c_char_p, _i64, _i64, _i32, _i64, _i64, _f64, _f64, _f64, C.POINTER(_vp),
+                      C.POINTER(_i64)],
+    "grid_hapnbr_fetch": [_vp, _vp, _vp, _vp],
+    "grid_hapnbr_free": [_vp],
     "grid_q16_encode": [_vp, _vp, _i64, _i64, _i64, _vp, _i64, _vp, _vp, _vp, _i64, C.POINTER(_i64)],
     "grid_synth_depth_q16": [_vp, C.c_uint64, _i64, _i64, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _i64,
                              C.POINTER(_i64)],
@@ -302,6 +307,35 @@ def read_normalized_gz(path, threads=None):
         return ids, scales, means, ratios, zq
     finally:
         lib.grid_ntext_free(h)
+
+
+def _hapnbr_result(rc, h, nnz, n, what):
+    check(rc, what)
+    try:
+        off = np.empty(2 * n + 1, dtype=np.int64)
+        nbr = np.empty(max(nnz.value, 1), dtype=np.int32)
+        w = np.empty(max(nnz.value, 1), dtype=np.float64)
+        call("grid_hapnbr_fetch", h, off.ctypes.data, nbr.ctypes.data, w.ctypes.data)
+        return off, nbr[: nnz.value], w[: nnz.value]
+    finally:
+        load().grid_hapnbr_free(h)
+
+
+def load_ibs(path, ids, max_nbr):
+    """computeIBSpbwt file -> CSR (off [2n+1], nbr, w); hi_inference.py:34-74."""
+    h, nnz = _vp(), _i64()
+    rc = load().grid_load_ibs(str(path).encode(), "\n".join(ids).encode(), len(ids), int(max_nbr), C.byref(h),
+                              C.byref(nnz))
+    return _hapnbr_result(rc, h, nnz, len(ids), "grid_load_ibs")
+
+
+def load_ibd(path, ids, max_nbr, region_start, region_end, min_length, min_match, weighted, weight_scale):
+    """iLASH file -> CSR (off [2n+1], nbr, w); hi_inference.py:86-172."""
+    h, nnz = _vp(), _i64()
+    rc = load().grid_load_ibd(str(path).encode(), "\n".join(ids).encode(), len(ids), int(max_nbr),
+                              1 if weighted else 0, int(region_start or 0), int(region_end or 0),
+                              float(min_length), float(min_match), float(weight_scale), C.byref(h), C.byref(nnz))
+    return _hapnbr_result(rc, h, nnz, len(ids), "grid_load_ibd")
 
 
 def hi_levels(off: np.ndarray, nbr: np.ndarray):

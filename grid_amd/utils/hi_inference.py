@@ -15,7 +15,7 @@ from pathlib import Path
 
 import numpy as np
 
-from .. import engine
+from .. import _abi, engine
 from ..device import get_device
 from .utils import log, open_maybe_gz
 
@@ -41,7 +41,74 @@ def _read_dip_cn_file(dip_cn_file):
     return ids, irrs, idx
 
 
+def _ids_in_order(IDtoInd):
+    """The sample IDs by index, or None when the mapping is not 0..N-1 (the
+    native loaders need it to be; duplicates in the dipCN file break it)."""
+    ids = [None] * len(IDtoInd)
+    for k, v in IDtoInd.items():
+        if not (isinstance(v, int) and 0 <= v < len(ids)) or ids[v] is not None:
+            return None
+        ids[v] = k
+    return ids
+
+
+def _native_csr(loader, *args):
+    """Run a native loader; None when it declines (GRID_EUNSUPPORTED)."""
+    try:
+        return loader(*args)
+    except _abi.GridNativeError as e:
+        if e.code != _abi.GRID_EUNSUPPORTED:
+            raise
+        return None
+
+
+def _csr_to_lists(off, nbr, w):
+    return [[(int(nbr[t]), float(w[t])) for t in range(off[h], off[h + 1])] for h in range(len(off) - 1)]
+
+
+def _load_ibs_csr(neighbors_file, IDtoInd, MAX_NBR):
+    """(off, nbr, w) of _load_ibs_neighbors: host C++ parser, Python restatement
+    for inputs it declines."""
+    ids = _ids_in_order(IDtoInd)
+    if ids is not None and isinstance(MAX_NBR, int) and -(1 << 62) < MAX_NBR < (1 << 62):
+        r = _native_csr(_abi.load_ibs, neighbors_file, ids, MAX_NBR)
+        if r is not None:
+            return r
+    return engine.csr_from_lists(_load_ibs_neighbors_py(neighbors_file, IDtoInd, MAX_NBR))
+
+
+def _load_ibd_csr(ilash_file, IDtoInd, MAX_NBR, region_start, region_end, min_length=0.5, min_match=0.70,
+                  weighted=False, weight_scale=1_000_000):
+    """(off, nbr, w) of _load_ibd_neighbors (see _load_ibs_csr)."""
+    ids = _ids_in_order(IDtoInd)
+    num = (int, float)
+    lim = 1 << 62   # region bounds the native int64 arithmetic takes exactly
+    ok = (ids is not None and isinstance(MAX_NBR, int) and MAX_NBR >= 0 and isinstance(min_length, num)
+          and isinstance(min_match, num) and isinstance(weight_scale, num)
+          and (not weighted or (isinstance(region_start, int) and isinstance(region_end, int)
+                                and abs(region_start) < lim and abs(region_end) < lim)))
+    if ok:
+        r = _native_csr(_abi.load_ibd, ilash_file, ids, MAX_NBR, region_start, region_end, min_length, min_match,
+                        weighted, weight_scale)
+        if r is not None:
+            return r
+    return engine.csr_from_lists(_load_ibd_neighbors_py(ilash_file, IDtoInd, MAX_NBR, region_start, region_end,
+                                                        min_length, min_match, weighted, weight_scale))
+
+
 def _load_ibs_neighbors(neighbors_file, IDtoInd, MAX_NBR):
+    """:34-74 -> hap_nbrs lists (reference API; the step itself uses the CSR)."""
+    return _csr_to_lists(*_load_ibs_csr(neighbors_file, IDtoInd, MAX_NBR))
+
+
+def _load_ibd_neighbors(ilash_file, IDtoInd, MAX_NBR, region_start, region_end, min_length=0.5,
+                        min_match=0.70, weighted=False, weight_scale=1_000_000):
+    """:86-172 -> hap_nbrs lists (reference API; the step itself uses the CSR)."""
+    return _csr_to_lists(*_load_ibd_csr(ilash_file, IDtoInd, MAX_NBR, region_start, region_end, min_length,
+                                        min_match, weighted, weight_scale))
+
+
+def _load_ibs_neighbors_py(neighbors_file, IDtoInd, MAX_NBR):
     """:34-74 (computeIBSpbwt: header + ID hap nbrInd cMlen cMedge IDnbr hapNbr)."""
     hap_nbrs = [[] for _ in range(2 * len(IDtoInd))]
     with open_maybe_gz(neighbors_file) as f:
@@ -76,8 +143,8 @@ def _segment_distance(bp1, bp2, region_start, region_end):
     return 0.0
 
 
-def _load_ibd_neighbors(ilash_file, IDtoInd, MAX_NBR, region_start, region_end, min_length=0.5,
-                        min_match=0.70, weighted=False, weight_scale=1_000_000):
+def _load_ibd_neighbors_py(ilash_file, IDtoInd, MAX_NBR, region_start, region_end, min_length=0.5,
+                           min_match=0.70, weighted=False, weight_scale=1_000_000):
     """:86-172 (iLASH, 11 columns; symmetric; sorted by cM desc; optional
     Lorentzian distance x match weight)."""
     raw = defaultdict(list)
@@ -129,8 +196,11 @@ def _run_phasing(IRRs, hap_nbrs, MIN_NBR, N_ITERS, console=None):
 
 
 def _phase_device(IRRs, hap_nbrs, MIN_NBR, N_ITERS, console=None, dev=None):
+    return _phase_device_csr(IRRs, *engine.csr_from_lists(hap_nbrs), MIN_NBR, N_ITERS, console, dev)
+
+
+def _phase_device_csr(IRRs, off, nbr, w, MIN_NBR, N_ITERS, console=None, dev=None):
     n = len(IRRs)
-    off, nbr, w = engine.csr_from_lists(hap_nbrs)
     n_ph = sum(1 for i in range(n) if off[2 * i + 1] - off[2 * i] >= MIN_NBR
                and off[2 * i + 2] - off[2 * i + 1] >= MIN_NBR)
     log(console, f"Phasing {n_ph} samples with >={MIN_NBR} neighbors for both haps")
@@ -198,7 +268,7 @@ def hi_inference(config, console):
             log(console, "Config error: ibs_output required for method='ibs'", style="danger")
             return
         log(console, f"Loading IBS neighbors from {ibs}")
-        hap_nbrs = _load_ibs_neighbors(ibs, IDtoInd, MAX_NBR)
+        csr = _load_ibs_csr(ibs, IDtoInd, MAX_NBR)
     elif method == "ibd":
         ibd = hc.get("ibd_output")
         if not ibd:
@@ -206,14 +276,14 @@ def hi_inference(config, console):
             return
         weighted = hc.get("weighted", False)
         log(console, f"Loading IBD neighbors from {ibd} (weighted={weighted})")
-        hap_nbrs = _load_ibd_neighbors(ibd, IDtoInd, MAX_NBR, config.get("start_bp"), config.get("end_bp"),
-                                       min_length=hc.get("min_length", 0.5), min_match=hc.get("min_match", 0.70),
-                                       weighted=weighted, weight_scale=hc.get("weight_scale", 1_000_000))
+        csr = _load_ibd_csr(ibd, IDtoInd, MAX_NBR, config.get("start_bp"), config.get("end_bp"),
+                            min_length=hc.get("min_length", 0.5), min_match=hc.get("min_match", 0.70),
+                            weighted=weighted, weight_scale=hc.get("weight_scale", 1_000_000))
     else:
         log(console, f"Config error: unknown method '{method}', must be 'ibs' or 'ibd'", style="danger")
         return
 
-    hap, imp, _ = _phase_device(IRRs, hap_nbrs, MIN_NBR, N_ITERS, console, get_device(config))
+    hap, imp, _ = _phase_device_csr(IRRs, *csr, MIN_NBR, N_ITERS, console, get_device(config))
     with open_maybe_gz(output_file, "wt") as fout:
         fout.write("ID\tIRRs\thap1phased\thap2phased\thap1imp\thap2imp\n")
         for i in range(N):

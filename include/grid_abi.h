@@ -228,6 +228,19 @@ int grid_hi_phase(grid_ctx *ctx, int64_t n, const double *d_irr, const int64_t *
 #define GRID_HI_UNIT_WEIGHTS 1   /* every weight is 1.0 (IBS lists): weights are not read */
 #define GRID_HI_LEGACY 2         /* A/B: the previous (per-neighbour LDS round trip) kernel */
 
+/* Haplotype-neighbour files -> CSR (host C++; Python text semantics for ASCII
+ * input).  ids_nl: the dipCN file's sample IDs joined by '\n' (index = line
+ * order).  GRID_EUNSUPPORTED for inputs whose Python behaviour the parser does
+ * not restate (non-ASCII text, NaN segment lengths, duplicate IDs); callers
+ * then run the Python loaders.  Fetch: off [2n+1], nbr / w [nnz]. */
+int grid_load_ibs(const char *path, const char *ids_nl, int64_t n_ids, int64_t max_nbr,
+                  void **h_out, int64_t *nnz);                          /* hi_inference.py:34-74 */
+int grid_load_ibd(const char *path, const char *ids_nl, int64_t n_ids, int64_t max_nbr,
+                  int32_t weighted, int64_t region_start, int64_t region_end, double min_length,
+                  double min_match, double weight_scale, void **h_out, int64_t *nnz); /* :86-172 */
+int grid_hapnbr_fetch(const void *h, int64_t *off, int32_t *nbr, double *w);
+int grid_hapnbr_free(void *h);
+
 /* Batched loci (BASELINE config 5: one _run_phasing + _compute_imp per VNTR
  * region, hi_inference.py:175-250, all in one launch, one workgroup per
  * locus).  Every pointer is a device pointer with grid_hi_phase's meaning for
