@@ -415,14 +415,129 @@ __device__ __forceinline__ int32_t pick8(const int4 &a, const int4 &b, int d) {
   return (d & 2) ? ((d & 1) ? h.w : h.z) : ((d & 1) ? h.y : h.x);
 }
 
-__device__ __forceinline__ void zquant_rows(const int32_t (&qv)[ZR][4], int64_t s0, int64_t i0, int64_t i1, int w,
-                                            const int32_t (&cm)[4], const float (&m32)[4], const float (&c32)[4],
-                                            const double *__restrict__ rm, const double *__restrict__ rinv,
-                                            const double *__restrict__ mus, const double *__restrict__ sq,
-                                            const double *__restrict__ rsq, double scale,
-                                            int32_t *__restrict__ zq, int64_t ld_zq, int32_t qmax,
+// zquant_rows: below the kernel body helpers (defined before use).
+
+
+// Pick element c (0..3) of a 4-vector held in registers (selects, no scratch).
+// (Masks, not a ternary chain: the compiler turns the chain back into an
+// indexed array in scratch memory.)
+__device__ __forceinline__ int32_t sel4(const int32_t (&v)[4], int c) {
+  int32_t r = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    int32_t x = v[k];
+    asm volatile("" : "+v"(x));
+    r |= x & -(int32_t)(c == k);
+  }
+  return r;
+}
+
+// Quantise ZR rows x 4 selected columns of one thread (qv: the depths).
+// Straight-line fast path on every cell; a cell it cannot decide is marked in
+// a bit mask and redone after the stores by the exact fp64 chain, in a loop
+// that is not unrolled (getq(u, c) re-reads its depth), so the rare path adds
+// neither code to the unrolled body nor live registers.
+// Fast-path acceptance: good = min(0.5 - f, |t|) > dl.  It equals the
+// original test (0.5 - f > dl) && |t| < 2^21 && (k != 0 || |t| > dl):
+// 0.5 - f > dl gives dl < 0.5, so |t| <= fl(|c|(|y|+m) + |t|) < 2^20, and
+// k != 0 gives |t| > |k| - f > 0.5 > dl; NaN/inf t fail both forms.  With
+// |t| > dl > 0 the sign of t is certain, and rint(t) == -0.0 exactly when the
+// output is "-0.00".
+template <class GETQ>
+__device__ __forceinline__ void zquant_rows(const int32_t (&qv)[ZR][4], GETQ getq, int64_t s0, int64_t i0,
+                                            int64_t i1, int w, const int32_t (&cm)[4], const float (&m32)[4],
+                                            const float (&c32)[4], const double *__restrict__ rm,
+                                            const double *__restrict__ rinv, const double *__restrict__ mus,
+                                            const double *__restrict__ sq, const double *__restrict__ rsq,
+                                            double scale, int32_t *__restrict__ zq, int64_t ld_zq, int32_t qmax,
                                             uint16_t *__restrict__ zb, int64_t ld_zb, int64_t kbs,
-                                            int32_t *__restrict__ overflow);
+                                            int32_t *__restrict__ overflow) {
+  const bool vec_zq = zq && w == 4 && ((ld_zq & 3) == 0) && ((s0 & 3) == 0);
+  const bool vec_zb = zb && w == 4 && cm[0] >= 0 && cm[1] == cm[0] + 1 && cm[2] == cm[0] + 2 &&
+                      cm[3] == cm[0] + 3 && ((cm[0] & 3) == 0) && ((ld_zb & 3) == 0);
+  // panel element (i, c): row-major i*ld_zb + c, or K-blocked (kbs > 0)
+  // (c >> 6)*kbs + i*64 + (c & 63) as k_gram8 reads it
+  auto zbi = [&](int64_t i, int64_t c) -> int64_t {
+    return kbs > 0 ? (c >> 6) * kbs + i * 64 + (c & 63) : i * ld_zb + c;
+  };
+  const float qf = (float)qmax;
+  float ac[4];
+#pragma unroll
+  for (int c = 0; c < 4; c++) ac[c] = 0x1p-21f * fabsf(c32[c]);
+  uint32_t slowm = 0;
+#pragma unroll
+  for (int u = 0; u < ZR; u++) {
+    const int64_t i = i0 + u;
+    if (i >= i1) break;
+    const double rmi = rm[i], rii = rinv[i];
+    const bool rowok = rmi != 0.0 && rmi == rmi;
+    const float a32 = (float)(0.01 * rii);
+    int32_t out[4];
+    uint32_t bv[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const bool valid = c < w && rowok && qv[u][c] != GRID_MISSING;
+      const float y = (float)qv[u][c] * a32;
+      const float t = (y - m32[c]) * c32[c];
+      const float k = rintf(t);
+      const float f = fabsf(t - k);
+      const float dl = fmaf(ac[c], fabsf(y) + m32[c], 0x1p-21f * fabsf(t));
+      const bool good = fminf(0.5f - f, fabsf(t)) > dl;
+      const int32_t o = (__float_as_uint(k) == 0x80000000u) ? GRID_ZQ_NEG0 : (int32_t)k;
+      out[c] = valid ? o : GRID_ZQ_NAN;
+      const float zf = (valid && good) ? fminf(fmaxf(k, -qf), qf) + 0.0f : 0.0f;
+      bv[c] = __float_as_uint(zf) >> 16;             // exact bf16 of |v| <= 256
+      slowm |= (valid && !good) ? (1u << (u * 4 + c)) : 0u;
+    }
+    if (zq) {
+      if (vec_zq) {
+        *reinterpret_cast<int4 *>(zq + i * ld_zq + s0) = make_int4(out[0], out[1], out[2], out[3]);
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+          if (c < w) zq[i * ld_zq + s0 + c] = out[c];
+      }
+    }
+    if (zb) {
+      if (vec_zb) {
+        *reinterpret_cast<uint2 *>(zb + zbi(i, cm[0])) = make_uint2(bv[0] | (bv[1] << 16), bv[2] | (bv[3] << 16));
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+          if (cm[c] >= 0) zb[zbi(i, cm[c])] = (uint16_t)bv[c];
+      }
+    }
+  }
+  if (__builtin_expect(slowm != 0, 0)) {       // exact fp64 chain (rare), after the fast stores
+    int of = 0;
+#pragma unroll 1
+    while (slowm) {
+      const int e = __builtin_ctz(slowm);
+      slowm &= slowm - 1;
+      const int u = e >> 2, c = e & 3;
+      const int64_t i = i0 + u, sc = s0 + c;
+      double y;
+      yval(getq(u, c), rm[i], rinv[i], y);
+      const double z = div_exact(y - mus[sc], sq[sc], rsq[sc]) * scale;
+      int32_t o = GRID_ZQ_NAN;
+      int32_t v = 0;
+      if (z == z) {
+        double kk = round_dec_k(z, 100.0);
+        if (fabs(kk) >= 2147483000.0) { of = 1; kk = 0.0; }
+        o = (int32_t)kk;
+        v = o;
+        if (o == 0 && signbit(z)) o = GRID_ZQ_NEG0;
+      }
+      if (zq) zq[i * ld_zq + sc] = o;
+      const int32_t cmc = sel4(cm, c);
+      if (zb && cmc >= 0) {
+        v = v > qmax ? qmax : (v < -qmax ? -qmax : v);
+        zb[zbi(i, cmc)] = (uint16_t)(__float_as_uint((float)v) >> 16);
+      }
+    }
+    if (of) atomicOr(overflow, 1);
+  }
+}
 
 // q reads: a thread's 4 selected columns usually lie within 8 consecutive
 // source columns (the selection keeps ~90 % of them), so each row is read
@@ -524,95 +639,190 @@ __global__ __launch_bounds__(256) void k_zquant4(const int32_t *__restrict__ q, 
         for (int c = 0; c < 4; c++)
           qv[u][c] = (i0 + u < i1 && c < w) ? q[(i0 + u) * ld + js[c]] : GRID_MISSING;
     }
-    zquant_rows(qv, s0, i0, i1, w, cm, m32, c32, rm, rinv, mus, sq, rsq, scale, zq, ld_zq, qmax, zb, ld_zb,
+    auto getq = [&](int u, int c) -> int32_t {
+      const int64_t j = sel4(js, c);
+      if constexpr (S16) return q16_val(s16.q[(i0 + u) * ld + j], i0 + u, j, s16);
+      else return q[(i0 + u) * ld + j];
+    };
+    zquant_rows(qv, getq, s0, i0, i1, w, cm, m32, c32, rm, rinv, mus, sq, rsq, scale, zq, ld_zq, qmax, zb, ld_zb,
                 kbs, overflow);
   }
 }
 
-// Quantise ZR rows x 4 selected columns of one thread (qv: the depths).
-__device__ __forceinline__ void zquant_rows(const int32_t (&qv)[ZR][4], int64_t s0, int64_t i0, int64_t i1, int w,
-                                            const int32_t (&cm)[4], const float (&m32)[4], const float (&c32)[4],
-                                            const double *__restrict__ rm, const double *__restrict__ rinv,
-                                            const double *__restrict__ mus, const double *__restrict__ sq,
-                                            const double *__restrict__ rsq, double scale,
-                                            int32_t *__restrict__ zq, int64_t ld_zq, int32_t qmax,
-                                            uint16_t *__restrict__ zb, int64_t ld_zb, int64_t kbs,
-                                            int32_t *__restrict__ overflow) {
-  const bool vec_zq = zq && w == 4 && ((ld_zq & 3) == 0) && ((s0 & 3) == 0);
-  const bool vec_zb = zb && w == 4 && cm[0] >= 0 && cm[1] == cm[0] + 1 && cm[2] == cm[0] + 2 &&
-                      cm[3] == cm[0] + 3 && ((cm[0] & 3) == 0) && ((ld_zb & 3) == 0);
-  // panel element (i, c): row-major i*ld_zb + c, or K-blocked (kbs > 0)
-  // (c >> 6)*kbs + i*64 + (c & 63) as k_gram8 reads it
+// ---- zquant over SOURCE columns (int32 depths, ld % 4 == 0) ----------------
+// Thread = 4 consecutive source columns x ZR rows: every row is ONE aligned
+// int4 load, a wave reads 1 KiB contiguous (no overlapping windows, no
+// register picks).  Unselected columns are computed and dropped.  Outputs are
+// compacted through a per-wave LDS row buffer: a wave's 256 source columns own
+// a contiguous range of selected indices s (and of used columns c' =
+// colmap[s], monotone), so each row leaves as contiguous dword (zq) and
+// 2-byte (zb) stores, 256 B / 128 B per wave instruction.  sidx[j] = s or -1.
+__global__ void k_sidx(const int32_t *__restrict__ sel, int64_t r, int32_t *__restrict__ sidx) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < r) sidx[sel[s]] = (int32_t)s;
+}
+
+__device__ __forceinline__ int wave_min_i32(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_max_i32(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+constexpr int Z6G = 1;   // default row groups of ZR rows per workgroup (per-column setup amortised)
+
+template <bool LOOP>
+__global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, int64_t n, int64_t ld,
+                                                 const int32_t *__restrict__ sidx,
+                                                 const double *__restrict__ rm, const double *__restrict__ rinv,
+                                                 const double *__restrict__ mus, const double *__restrict__ sq,
+                                                 const double *__restrict__ rsq, const float2 *__restrict__ mc32,
+                                                 double scale, int32_t *__restrict__ zq, int64_t ld_zq,
+                                                 const int32_t *__restrict__ colmap, int32_t qmax,
+                                                 uint16_t *__restrict__ zb, int64_t ld_zb, int64_t kbs,
+                                                 int32_t *__restrict__ overflow, int rpw) {
+  __shared__ int32_t s_zq[4][256 + 64];
+  __shared__ uint16_t s_zb[4][256 + 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t j0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  const int64_t r0 = (int64_t)blockIdx.y * rpw;
+  const int64_t r1 = (r0 + rpw < n) ? r0 + rpw : n;
+  const bool full4 = j0 + 4 <= ld;
+  // rows i0 .. i0+ZR-1 of this thread's 4 columns (rows past r1 re-read row r0)
+  auto load_group = [&](int64_t i0, int4 (&v)[ZR]) {
+#pragma unroll
+    for (int u = 0; u < ZR; u++) {
+      const int64_t i = (i0 + u < r1) ? i0 + u : r0;
+      if (full4) {
+        v[u] = *reinterpret_cast<const int4 *>(q + i * ld + j0);
+      } else {
+        v[u].x = (j0 + 0 < ld) ? q[i * ld + j0 + 0] : GRID_MISSING;
+        v[u].y = (j0 + 1 < ld) ? q[i * ld + j0 + 1] : GRID_MISSING;
+        v[u].z = (j0 + 2 < ld) ? q[i * ld + j0 + 2] : GRID_MISSING;
+        v[u].w = (j0 + 3 < ld) ? q[i * ld + j0 + 3] : GRID_MISSING;
+      }
+    }
+  };
+  int4 v[ZR];
+  load_group(r0, v);                        // in flight while the column setup runs
+  int32_t sk[4], ck[4];
+  float m32[4], c32[4], ac[4];
+  if (full4) {
+    const int4 t = *reinterpret_cast<const int4 *>(sidx + j0);
+    sk[0] = t.x; sk[1] = t.y; sk[2] = t.z; sk[3] = t.w;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; k++) sk[k] = (j0 + k < ld) ? sidx[j0 + k] : -1;
+  }
+  int smin = INT_MAX, smax = -1, cmin = INT_MAX, cmax = -1;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int32_t sv = sk[k];
+    ck[k] = sv >= 0 ? (colmap ? colmap[sv] : sv) : -1;
+    const float2 mc = sv >= 0 ? mc32[sv] : make_float2(1.0f, 1.0f);
+    m32[k] = mc.x;
+    c32[k] = mc.y;
+    ac[k] = 0x1p-21f * fabsf(mc.y);
+    if (sv >= 0) { smin = min(smin, sv); smax = max(smax, sv); }
+    if (ck[k] >= 0) { cmin = min(cmin, ck[k]); cmax = max(cmax, ck[k]); }
+  }
+  const int Slo = wave_min_i32(smin), Shi = wave_max_i32(smax);
+  const int Clo = wave_min_i32(cmin), Chi = wave_max_i32(cmax);
+  const int nS = Shi >= Slo ? Shi - Slo + 1 : 0, nC = Chi >= Clo ? Chi - Clo + 1 : 0;
+  if (nS == 0) return;                      // no selected column in this wave (wave-uniform)
   auto zbi = [&](int64_t i, int64_t c) -> int64_t {
     return kbs > 0 ? (c >> 6) * kbs + i * 64 + (c & 63) : i * ld_zb + c;
   };
+  // row-invariant panel offsets of this lane's used columns Clo + lane + 64 m
+  int64_t zoff[4];
+#pragma unroll
+  for (int m = 0; m < 4; m++) zoff[m] = zbi(0, Clo + lane + 64 * m);
+  const float qf = (float)qmax;
   int of = 0;
+  for (int64_t i0 = r0; i0 < r1; i0 += ZR) {
+    if (LOOP && i0 != r0) load_group(i0, v);
+    uint32_t slowm = 0;
 #pragma unroll
-  for (int u = 0; u < ZR; u++) {
-    const int64_t i = i0 + u;
-    if (i >= i1) break;
-    const double rmi = rm[i], rii = rinv[i];
-    const bool rowok = rmi != 0.0 && rmi == rmi;
-    const float a32 = (float)(0.01 * rii);
-    int32_t out[4];
-    bool slow[4];
+    for (int u = 0; u < ZR; u++) {
+      const int64_t i = i0 + u;
+      if (i >= r1) break;
+      const double rmi = rm[i], rii = rinv[i];
+      const bool rowok = rmi != 0.0 && rmi == rmi;
+      const float a32 = (float)(0.01 * rii);
+      const int32_t qv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
-    for (int c = 0; c < 4; c++) {
-      out[c] = GRID_ZQ_NAN;
-      slow[c] = false;
-      if (c < w && rowok && qv[u][c] != GRID_MISSING) {
-        const float y = (float)qv[u][c] * a32;
-        const float t = (y - m32[c]) * c32[c];
-        const float k = rintf(t);
-        const float f = fabsf(t - k);
-        const float dl = 0x1p-21f * fmaf(fabsf(c32[c]), fabsf(y) + m32[c], fabsf(t));
-        if ((0.5f - f) > dl && fabsf(t) < 0x1p21f && (k != 0.0f || fabsf(t) > dl)) {
-          out[c] = (int32_t)k;
-          if (out[c] == 0 && t < 0.0f) out[c] = GRID_ZQ_NEG0;
-        } else {
-          slow[c] = true;
+      for (int k = 0; k < 4; k++) {
+        // fast path and acceptance test: see zquant_rows
+        const bool valid = rowok && qv[k] != GRID_MISSING;
+        const float y = (float)qv[k] * a32;
+        const float t = (y - m32[k]) * c32[k];
+        const float kk = rintf(t);
+        const float f = fabsf(t - kk);
+        const float dl = fmaf(ac[k], fabsf(y) + m32[k], 0x1p-21f * fabsf(t));
+        const bool good = fminf(0.5f - f, fabsf(t)) > dl;
+        const int32_t o = (__float_as_uint(kk) == 0x80000000u) ? GRID_ZQ_NEG0 : (int32_t)kk;
+        const float zf = (valid && good) ? fminf(fmaxf(kk, -qf), qf) + 0.0f : 0.0f;
+        // unselected / unused columns write a per-lane spill slot (no branch)
+        s_zq[wv][sk[k] >= 0 ? sk[k] - Slo : 256 + lane] = valid ? o : GRID_ZQ_NAN;
+        s_zb[wv][ck[k] >= 0 ? ck[k] - Clo : 256 + lane] = (uint16_t)(__float_as_uint(zf) >> 16);
+        slowm |= (sk[k] >= 0 && valid && !good) ? (1u << (u * 4 + k)) : 0u;
+      }
+      // the wave's LDS row is complete (LDS ops of one wave retire in order;
+      // the clobber keeps the compiler from moving the reads above the writes)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (zq) {
+        int32_t *zrow = zq + i * ld_zq + Slo;
+#pragma unroll
+        for (int m = 0; m < 4; m++) {
+          const int32_t val = s_zq[wv][lane + 64 * m];
+          if (64 * m + 64 <= nS) zrow[lane + 64 * m] = val;              // whole chunk (wave-uniform)
+          else if (lane + 64 * m < nS) zrow[lane + 64 * m] = val;
         }
       }
-    }
+      if (zb) {
+        uint16_t *brow = zb + (kbs > 0 ? i * 64 : i * ld_zb);
 #pragma unroll
-    for (int c = 0; c < 4; c++) {
-      if (slow[c]) {      // exact fp64 chain (rare)
+        for (int m = 0; m < 4; m++) {
+          const uint16_t val = s_zb[wv][lane + 64 * m];
+          if (64 * m + 64 <= nC) brow[zoff[m]] = val;
+          else if (lane + 64 * m < nC) brow[zoff[m]] = val;
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the next row's writes
+    }
+    if (__builtin_expect(slowm != 0, 0)) {     // exact fp64 chain (rare), after the row stores
+      // another lane stored this cell's fast value: let those stores complete
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll 1
+      while (slowm) {
+        const int e = __builtin_ctz(slowm);
+        slowm &= slowm - 1;
+        const int u = e >> 2, k = e & 3;
+        const int64_t i = i0 + u;
+        const int32_t sc = sel4(sk, k), cc = sel4(ck, k);
         double y;
-        yval(qv[u][c], rmi, rii, y);
-        double z = div_exact(y - mus[s0 + c], sq[s0 + c], rsq[s0 + c]) * scale;
+        yval(q[i * ld + j0 + k], rm[i], rinv[i], y);
+        const double z = div_exact(y - mus[sc], sq[sc], rsq[sc]) * scale;
+        int32_t o = GRID_ZQ_NAN, w = 0;
         if (z == z) {
-          double k = round_dec_k(z, 100.0);
-          if (fabs(k) >= 2147483000.0) { of = 1; k = 0.0; }
-          out[c] = (int32_t)k;
-          if (out[c] == 0 && signbit(z)) out[c] = GRID_ZQ_NEG0;
+          double kd = round_dec_k(z, 100.0);
+          if (fabs(kd) >= 2147483000.0) { of = 1; kd = 0.0; }
+          o = (int32_t)kd;
+          w = o;
+          if (o == 0 && signbit(z)) o = GRID_ZQ_NEG0;
+        }
+        if (zq) zq[i * ld_zq + sc] = o;
+        if (zb && cc >= 0) {
+          w = w > qmax ? qmax : (w < -qmax ? -qmax : w);
+          zb[zbi(i, cc)] = (uint16_t)(__float_as_uint((float)w) >> 16);
         }
       }
     }
-    if (zq) {
-      if (vec_zq) {
-        *reinterpret_cast<int4 *>(zq + i * ld_zq + s0) = make_int4(out[0], out[1], out[2], out[3]);
-      } else {
-#pragma unroll
-        for (int c = 0; c < 4; c++)
-          if (c < w) zq[i * ld_zq + s0 + c] = out[c];
-      }
-    }
-    if (zb) {
-      uint32_t bv[4];
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        int32_t v = (out[c] == GRID_ZQ_NAN || out[c] == GRID_ZQ_NEG0) ? 0 : out[c];
-        v = v > qmax ? qmax : (v < -qmax ? -qmax : v);
-        bv[c] = __float_as_uint((float)v) >> 16;      // exact bf16 of |v| <= 256
-      }
-      if (vec_zb) {
-        *reinterpret_cast<uint2 *>(zb + zbi(i, cm[0])) = make_uint2(bv[0] | (bv[1] << 16), bv[2] | (bv[3] << 16));
-      } else {
-#pragma unroll
-        for (int c = 0; c < 4; c++)
-          if (cm[c] >= 0) zb[zbi(i, cm[c])] = (uint16_t)bv[c];
-      }
-    }
+    if (!LOOP) break;
   }
   if (of) atomicOr(overflow, 1);
 }
@@ -777,7 +987,7 @@ static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, int64_
   double *rinv;
   char *rest;
   size_t rb = (((size_t)r * 8 + 255) & ~size_t(255));
-  int rc = recip_rows(ctx, d_rm, n, 4 * rb, &rinv, &rest);
+  int rc = recip_rows(ctx, d_rm, n, 4 * rb + (size_t)ld * 4, &rinv, &rest);
   if (rc) return rc;
   double *mus = (double *)rest, *sq = (double *)(rest + rb), *rsq = (double *)(rest + 2 * rb);
   float2 *mc32 = (float2 *)(rest + 3 * rb);
@@ -786,11 +996,26 @@ static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, int64_
   hipLaunchKernelGGL(k_zprep, dim3((unsigned)ceil_div(r, 256)), dim3(256), 0, ctx->stream, d_sel, r, d_mu, scale, mus,
                      sq, rsq, mc32);
   LAUNCHCHK();
+  const char *zv = getenv("GRID_ZQUANT_VARIANT");   // 4 = the selected-column kernel (A/B)
+  if (!s16.q && vec4_ok(d_q, ld) && !(zv && atoi(zv) == 4)) {
+    int32_t *sidx = (int32_t *)(rest + 4 * rb);
+    HIPCHK(hipMemsetAsync(sidx, 0xFF, (size_t)ld * 4, ctx->stream));
+    hipLaunchKernelGGL(k_sidx, dim3((unsigned)ceil_div(r, 256)), dim3(256), 0, ctx->stream, d_sel, r, sidx);
+    LAUNCHCHK();
+    const char *ge = getenv("GRID_ZQUANT_GROUPS");
+    const int rpw = ZR * ((ge && atoi(ge) > 0) ? atoi(ge) : Z6G);
+    REQUIRE(ceil_div(n, rpw) <= 65535, "n too large for one launch");
+    hipLaunchKernelGGL(rpw > ZR ? k_zquant6<true> : k_zquant6<false>, dim3((unsigned)ceil_div(ceil_div(ld, 4), 256), (unsigned)ceil_div(n, rpw)),
+                       dim3(256), 0, ctx->stream, d_q, n, ld, sidx, d_rm, rinv, mus, sq, rsq, mc32, scale, d_zq, ld_zq,
+                       d_colmap, qmax, d_zb, ld_zb, kbs, d_of, rpw);
+    LAUNCHCHK();
+  } else {
   auto kz = s16.q ? k_zquant4<false, true> : vec4_ok(d_q, ld) ? k_zquant4<true, false> : k_zquant4<false, false>;
   hipLaunchKernelGGL(kz, dim3((unsigned)ceil_div(ceil_div(r, 4), 256), (unsigned)ceil_div(n, ZR * ZRB)), dim3(256), 0,
                      ctx->stream, d_q, s16, n, ld, d_sel, r, d_rm, rinv, mus, sq, rsq, mc32, scale, d_zq, ld_zq, d_colmap,
                      qmax, d_zb, ld_zb, kbs, d_of);
   LAUNCHCHK();
+  }
   if (h_overflow) {
     HIPCHK(hipMemcpyAsync(ctx->pinned, d_of, 4, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
