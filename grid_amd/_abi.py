@@ -20,6 +20,7 @@ GRID_OK, GRID_EINVAL, GRID_EHIP, GRID_EZERODIV, GRID_EUNSUPPORTED, GRID_ERANGE =
 MISSING = -(2 ** 31)          # GRID_MISSING / GRID_ZQ_NAN
 ZQ_NAN = -(2 ** 31)
 ZQ_NEG0 = -(2 ** 31) + 1
+ZQ16_NAN, ZQ16_NEG0, ZQ16_ESC = -32768, -32767, -32766   # GRID_ZQ16_* (grid_norm_zquant_kb16)
 BLOCK = 8192
 
 _i64, _i32, _f64, _vp = C.c_int64, C.c_int32, C.c_double, C.c_void_p
@@ -54,6 +55,8 @@ _SIGS = {
                          _vp, _i64, C.POINTER(_i32)],
     "grid_norm_zquant_kb": [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _f64, _vp, _i64, _vp, _i32,
                             _vp, _i64, C.POINTER(_i32)],
+    "grid_norm_zquant_kb16": [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _f64, _vp, _i64, _vp, _i32,
+                              _vp, _i64, _vp, _vp, _i64, C.POINTER(_i64), C.POINTER(_i32)],
     "grid_norm_zfull": [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _f64, _vp],
     "grid_knn_gram": [_vp, _vp, _i64, _i64, _i64, _i32, _vp],
     "grid_knn_gram_kb": [_vp, _vp, _i64, _i64, _i32, _vp],

@@ -675,17 +675,49 @@ __device__ __forceinline__ int wave_max_i32(int v) {
 
 constexpr int Z6G = 1;   // default row groups of ZR rows per workgroup (per-column setup amortised)
 
-template <bool LOOP>
+// ZT = int16_t: the compact step-4 output (GRID_ZQ16_* codes).  A value
+// outside [GRID_ZQ16_MIN, GRID_ZQ16_MAX] is written as GRID_ZQ16_ESC and
+// recorded exactly in the escape list (flat index i*ld_zq + s, value); a full
+// list sets overflow bit 1 and the caller reruns with int32 output.
+struct ZEsc {
+  int64_t *idx;
+  int32_t *val;
+  unsigned long long *cnt;
+  int64_t cap;
+};
+__device__ __forceinline__ int16_t zq16_escape(int32_t o, int64_t flat, const ZEsc &e, int *of) {
+  const unsigned long long slot = atomicAdd(e.cnt, 1ull);
+  if ((int64_t)slot < e.cap) {
+    e.idx[slot] = flat;
+    e.val[slot] = o;
+  } else {
+    *of |= 2;
+  }
+  return (int16_t)GRID_ZQ16_ESC;
+}
+template <class ZT>
+__device__ __forceinline__ ZT zq_code(int32_t o, int64_t flat, const ZEsc &e, int &of) {
+  if constexpr (sizeof(ZT) == 2) {
+    if (o == GRID_ZQ_NAN) return (int16_t)GRID_ZQ16_NAN;
+    if (o == GRID_ZQ_NEG0) return (int16_t)GRID_ZQ16_NEG0;
+    if (__builtin_expect(o < GRID_ZQ16_MIN || o > GRID_ZQ16_MAX, 0)) return zq16_escape(o, flat, e, &of);
+    return (int16_t)o;
+  } else {
+    return o;
+  }
+}
+
+template <bool LOOP, class ZT>
 __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, int64_t n, int64_t ld,
                                                  const int32_t *__restrict__ sidx,
                                                  const double *__restrict__ rm, const double *__restrict__ rinv,
                                                  const double *__restrict__ mus, const double *__restrict__ sq,
                                                  const double *__restrict__ rsq, const float2 *__restrict__ mc32,
-                                                 double scale, int32_t *__restrict__ zq, int64_t ld_zq,
+                                                 double scale, ZT *__restrict__ zq, int64_t ld_zq,
                                                  const int32_t *__restrict__ colmap, int32_t qmax,
                                                  uint16_t *__restrict__ zb, int64_t ld_zb, int64_t kbs,
-                                                 int32_t *__restrict__ overflow, int rpw) {
-  __shared__ int32_t s_zq[4][256 + 64];
+                                                 int32_t *__restrict__ overflow, int rpw, ZEsc esc) {
+  __shared__ ZT s_zq[4][256 + 64];
   __shared__ uint16_t s_zb[4][256 + 64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t j0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
@@ -754,6 +786,10 @@ __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, 
       const bool rowok = rmi != 0.0 && rmi == rmi;
       const float a32 = (float)(0.01 * rii);
       const int32_t qv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+      // used columns need not be contiguous (any colmap): slots no lane fills
+      // keep the marker 0xFFFF (a NaN bf16 the conversion never produces) and
+      // are not stored
+      if (zb) *reinterpret_cast<uint2 *>(&s_zb[wv][4 * lane]) = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         // fast path and acceptance test: see zquant_rows
@@ -767,18 +803,27 @@ __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, 
         const int32_t o = (__float_as_uint(kk) == 0x80000000u) ? GRID_ZQ_NEG0 : (int32_t)kk;
         const float zf = (valid && good) ? fminf(fmaxf(kk, -qf), qf) + 0.0f : 0.0f;
         // unselected / unused columns write a per-lane spill slot (no branch)
-        s_zq[wv][sk[k] >= 0 ? sk[k] - Slo : 256 + lane] = valid ? o : GRID_ZQ_NAN;
+        // int16 output: a value outside the codes goes to the deferred loop
+        // too (it records the escape); those cells store a placeholder here
+        const bool esc16 = sizeof(ZT) == 2 && o != GRID_ZQ_NEG0 && (o < GRID_ZQ16_MIN || o > GRID_ZQ16_MAX);
+        const bool defer = sk[k] >= 0 && valid && (!good || esc16);
+        int32_t code;
+        if constexpr (sizeof(ZT) == 2)
+          code = !valid ? GRID_ZQ16_NAN : defer ? 0 : o == GRID_ZQ_NEG0 ? GRID_ZQ16_NEG0 : o;
+        else
+          code = !valid ? GRID_ZQ_NAN : o;
+        s_zq[wv][sk[k] >= 0 ? sk[k] - Slo : 256 + lane] = (ZT)code;
         s_zb[wv][ck[k] >= 0 ? ck[k] - Clo : 256 + lane] = (uint16_t)(__float_as_uint(zf) >> 16);
-        slowm |= (sk[k] >= 0 && valid && !good) ? (1u << (u * 4 + k)) : 0u;
+        slowm |= defer ? (1u << (u * 4 + k)) : 0u;
       }
       // the wave's LDS row is complete (LDS ops of one wave retire in order;
       // the clobber keeps the compiler from moving the reads above the writes)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (zq) {
-        int32_t *zrow = zq + i * ld_zq + Slo;
+        ZT *zrow = zq + i * ld_zq + Slo;
 #pragma unroll
         for (int m = 0; m < 4; m++) {
-          const int32_t val = s_zq[wv][lane + 64 * m];
+          const ZT val = s_zq[wv][lane + 64 * m];
           if (64 * m + 64 <= nS) zrow[lane + 64 * m] = val;              // whole chunk (wave-uniform)
           else if (lane + 64 * m < nS) zrow[lane + 64 * m] = val;
         }
@@ -788,8 +833,7 @@ __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, 
 #pragma unroll
         for (int m = 0; m < 4; m++) {
           const uint16_t val = s_zb[wv][lane + 64 * m];
-          if (64 * m + 64 <= nC) brow[zoff[m]] = val;
-          else if (lane + 64 * m < nC) brow[zoff[m]] = val;
+          if (lane + 64 * m < nC && val != 0xFFFFu) brow[zoff[m]] = val;
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the next row's writes
@@ -810,12 +854,12 @@ __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, 
         int32_t o = GRID_ZQ_NAN, w = 0;
         if (z == z) {
           double kd = round_dec_k(z, 100.0);
-          if (fabs(kd) >= 2147483000.0) { of = 1; kd = 0.0; }
+          if (fabs(kd) >= 2147483000.0) { of |= 1; kd = 0.0; }
           o = (int32_t)kd;
           w = o;
           if (o == 0 && signbit(z)) o = GRID_ZQ_NEG0;
         }
-        if (zq) zq[i * ld_zq + sc] = o;
+        if (zq) zq[i * ld_zq + sc] = zq_code<ZT>(o, i * ld_zq + sc, esc, of);
         if (zb && cc >= 0) {
           w = w > qmax ? qmax : (w < -qmax ? -qmax : w);
           zb[zbi(i, cc)] = (uint16_t)(__float_as_uint((float)w) >> 16);
@@ -824,7 +868,7 @@ __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, 
     }
     if (!LOOP) break;
   }
-  if (of) atomicOr(overflow, 1);
+  if (of) atomicOr(overflow, of);
 }
 
 // Full fp64 z matrix (normalize_matrix's returned array, :458 and :470):
@@ -976,7 +1020,9 @@ static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, int64_
                        const int32_t *d_sel,
                        int64_t r, const double *d_rm, const double *d_mu, double scale, int32_t *d_zq,
                        int64_t ld_zq, const int32_t *d_colmap, int32_t qmax, uint16_t *d_zb,
-                       int64_t ld_zb, int64_t kbs, int32_t *h_overflow) {
+                       int64_t ld_zb, int64_t kbs, int32_t *h_overflow, int16_t *d_zq16 = nullptr,
+                       int64_t *d_esc_idx = nullptr, int32_t *d_esc_val = nullptr, int64_t esc_cap = 0,
+                       int64_t *h_nesc = nullptr) {
   REQUIRE(ctx && n >= 0 && r >= 0, "bad args");
   REQUIRE(qmax >= 0 && qmax <= 256, "qmax %d outside the exact-bf16 range [0, 256]", qmax);
   if (n == 0 || r == 0) {
@@ -991,13 +1037,15 @@ static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, int64_
   if (rc) return rc;
   double *mus = (double *)rest, *sq = (double *)(rest + rb), *rsq = (double *)(rest + 2 * rb);
   float2 *mc32 = (float2 *)(rest + 3 * rb);
-  int32_t *d_of = (int32_t *)ctx->scratch;
-  HIPCHK(hipMemsetAsync(d_of, 0, 4, ctx->stream));
+  int32_t *d_of = (int32_t *)ctx->scratch;          // [0, 4): overflow flags; [8, 16): escape count
+  HIPCHK(hipMemsetAsync(d_of, 0, 16, ctx->stream));
+  const ZEsc esc{d_esc_idx, d_esc_val, (unsigned long long *)((char *)ctx->scratch + 8), esc_cap};
   hipLaunchKernelGGL(k_zprep, dim3((unsigned)ceil_div(r, 256)), dim3(256), 0, ctx->stream, d_sel, r, d_mu, scale, mus,
                      sq, rsq, mc32);
   LAUNCHCHK();
   const char *zv = getenv("GRID_ZQUANT_VARIANT");   // 4 = the selected-column kernel (A/B)
-  if (!s16.q && vec4_ok(d_q, ld) && !(zv && atoi(zv) == 4)) {
+  REQUIRE(!d_zq16 || (!s16.q && vec4_ok(d_q, ld)), "int16 z output needs the int32 depth layout (ld % 4 == 0)");
+  if (d_zq16 || (!s16.q && vec4_ok(d_q, ld) && !(zv && atoi(zv) == 4))) {
     int32_t *sidx = (int32_t *)(rest + 4 * rb);
     HIPCHK(hipMemsetAsync(sidx, 0xFF, (size_t)ld * 4, ctx->stream));
     hipLaunchKernelGGL(k_sidx, dim3((unsigned)ceil_div(r, 256)), dim3(256), 0, ctx->stream, d_sel, r, sidx);
@@ -1005,9 +1053,16 @@ static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, int64_
     const char *ge = getenv("GRID_ZQUANT_GROUPS");
     const int rpw = ZR * ((ge && atoi(ge) > 0) ? atoi(ge) : Z6G);
     REQUIRE(ceil_div(n, rpw) <= 65535, "n too large for one launch");
-    hipLaunchKernelGGL(rpw > ZR ? k_zquant6<true> : k_zquant6<false>, dim3((unsigned)ceil_div(ceil_div(ld, 4), 256), (unsigned)ceil_div(n, rpw)),
-                       dim3(256), 0, ctx->stream, d_q, n, ld, sidx, d_rm, rinv, mus, sq, rsq, mc32, scale, d_zq, ld_zq,
-                       d_colmap, qmax, d_zb, ld_zb, kbs, d_of, rpw);
+    const dim3 g6((unsigned)ceil_div(ceil_div(ld, 4), 256), (unsigned)ceil_div(n, rpw));
+    if (d_zq16) {
+      auto k16 = rpw > ZR ? k_zquant6<true, int16_t> : k_zquant6<false, int16_t>;
+      hipLaunchKernelGGL(k16, g6, dim3(256), 0, ctx->stream, d_q, n, ld, sidx, d_rm, rinv, mus, sq, rsq, mc32, scale,
+                         d_zq16, ld_zq, d_colmap, qmax, d_zb, ld_zb, kbs, d_of, rpw, esc);
+    } else {
+      auto k32 = rpw > ZR ? k_zquant6<true, int32_t> : k_zquant6<false, int32_t>;
+      hipLaunchKernelGGL(k32, g6, dim3(256), 0, ctx->stream, d_q, n, ld, sidx, d_rm, rinv, mus, sq, rsq, mc32, scale,
+                         d_zq, ld_zq, d_colmap, qmax, d_zb, ld_zb, kbs, d_of, rpw, esc);
+    }
     LAUNCHCHK();
   } else {
   auto kz = s16.q ? k_zquant4<false, true> : vec4_ok(d_q, ld) ? k_zquant4<true, false> : k_zquant4<false, false>;
@@ -1017,9 +1072,10 @@ static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, int64_
   LAUNCHCHK();
   }
   if (h_overflow) {
-    HIPCHK(hipMemcpyAsync(ctx->pinned, d_of, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(ctx->pinned, d_of, 16, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     *h_overflow = *(int32_t *)ctx->pinned;
+    if (h_nesc) *h_nesc = (int64_t) * (unsigned long long *)((char *)ctx->pinned + 8);
   }
   return GRID_OK;
 }
@@ -1043,6 +1099,18 @@ int grid_norm_zquant_kb(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t ld
   REQUIRE(np_zb >= n && np_zb % 64 == 0, "np_zb must be >= n and a multiple of 64");
   return zquant_impl(ctx, d_q, kNoQ16, n, ld, d_sel, r, d_rm, d_mu, scale, d_zq, ld_zq, d_colmap, qmax, d_zb, 64,
                      np_zb * 64, h_overflow);
+}
+
+int grid_norm_zquant_kb16(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t ld, const int32_t *d_sel,
+                          int64_t r, const double *d_rm, const double *d_mu, double scale, int16_t *d_zq16,
+                          int64_t ld_zq, const int32_t *d_colmap, int32_t qmax, uint16_t *d_zb,
+                          int64_t np_zb, int64_t *d_esc_idx, int32_t *d_esc_val, int64_t esc_cap,
+                          int64_t *h_nesc, int32_t *h_overflow) {
+  REQUIRE(np_zb >= n && np_zb % 64 == 0, "np_zb must be >= n and a multiple of 64");
+  REQUIRE(d_zq16 && h_overflow && h_nesc && esc_cap >= 0 && (esc_cap == 0 || (d_esc_idx && d_esc_val)),
+          "grid_norm_zquant_kb16: bad escape list / outputs");
+  return zquant_impl(ctx, d_q, kNoQ16, n, ld, d_sel, r, d_rm, d_mu, scale, nullptr, ld_zq, d_colmap, qmax, d_zb, 64,
+                     np_zb * 64, h_overflow, d_zq16, d_esc_idx, d_esc_val, esc_cap, h_nesc);
 }
 
 int grid_norm_zquant_kb_q16(grid_ctx *ctx, const grid_depth16 *q, int64_t n, int64_t ld, const int32_t *d_sel,

@@ -189,6 +189,16 @@ class HipOps:
                  ld_zq, ptr(colmap), qmax, ptr(zb), np_zb, C.byref(of))
         return of.value
 
+    def zquant16(self, q, n, ld, sel, r, rm, mu, scale, zq16, ld_zq, colmap, qmax, zb, np_zb, esc_idx, esc_val):
+        """As zquant with the step-4 output as int16 codes plus an escape list
+        for the rare values outside them.  Returns (overflow bits, escapes);
+        bit 1 = the list overflowed (the caller reruns with int32)."""
+        of, ne = C.c_int32(), C.c_int64()
+        call("grid_norm_zquant_kb16", self.ctx, ptr(q), n, ld, ptr(sel), r, ptr(rm), ptr(mu), scale, ptr(zq16),
+             ld_zq, ptr(colmap), qmax, ptr(zb), np_zb, ptr(esc_idx), ptr(esc_val),
+             0 if esc_idx is None else esc_idx.numel(), C.byref(ne), C.byref(of))
+        return of.value, ne.value
+
     def gram(self, zb, np_, kpad, qmax, gram):
         """Exact Gram of the K-blocked panel (first kpad columns)."""
         call("grid_knn_gram_kb", self.ctx, ptr(zb), np_, kpad, qmax, ptr(gram))
@@ -219,7 +229,7 @@ class Steps47:
     """
 
     def __init__(self, ops, alloc, n, m_total, col0, m_local, *, k=10, n_nbr=300, top_frac=0.1, zmax=2.0,
-                 sigma2_max=1000.0, frac_r=1.0, min_nbr=1, n_iters=100, comm=None, phase_lane=None):
+                 sigma2_max=1000.0, frac_r=1.0, min_nbr=1, n_iters=100, comm=None, phase_lane=None, zq16=True):
         """``phase_lane``: optional (ops, torch.cuda.Stream) pair on which step
         7 runs, ordered after this pass's dipCN by an event; the next pass's
         dipCN waits for it.  Phasing is one workgroup for ~6 ms, so on its own
@@ -255,7 +265,15 @@ class Steps47:
         self.sel = a.empty(ml1, I4)
         self.r3 = a.empty(max(self.mlmax, 1), F8)
         self.colmap = a.empty(ml1, I4)
-        self.zq = a.empty((n1, ml1), I4)                 # step-4 output: exact hundredths
+        # step-4 output, exact hundredths: int16 codes (GRID_ZQ16_*, half the
+        # HBM writes) when the ops support them, int32 otherwise or when a
+        # pass has |z| > 327.66 (zq_int32() gives the int32 form either way)
+        self.zq16 = a.empty((n1, ml1), U2) if zq16 and hasattr(ops, "zquant16") else None
+        self.zq = None if self.zq16 is not None else a.empty((n1, ml1), I4)
+        self.zq_is16, self.nesc = False, 0
+        if self.zq16 is not None:                        # escapes: |z| > 327.65 (rare)
+            cap = min(n1 * ml1, max(1 << 20, (n1 * ml1) >> 12))
+            self.esc_idx, self.esc_val = a.empty(cap, I8), a.empty(cap, I4)
         self.np_ = pad_to(n1, 256)
         self.kpad = pad_to(ml1, 64)
         # step-5 input panel (bf16), K-blocked [kpad/64][np][64]: one K-step of a
@@ -294,6 +312,18 @@ class Steps47:
     def set_reads(self, reads):
         self.reads = self.A.upload(np.asarray(reads, F8))
         self.has = self.A.upload(np.ones(max(self.n, 1), dtype=U1))
+
+    def zq_int32(self):
+        """The step-4 output of the last pass as int32 hundredths
+        (GRID_ZQ_NAN / GRID_ZQ_NEG0 sentinels), whichever form it was written in."""
+        if not self.zq_is16:
+            return self.zq
+        z = self.zq16.to(self.A.torch.int32)
+        z[self.zq16 == _abi.ZQ16_NAN] = _abi.ZQ_NAN
+        z[self.zq16 == _abi.ZQ16_NEG0] = _abi.ZQ_NEG0
+        if self.nesc:
+            z.view(-1)[self.esc_idx[: self.nesc]] = self.esc_val[: self.nesc]
+        return z
 
     # ---------------------------------------------------------------- helpers
     def _read(self, b, i):
@@ -384,8 +414,17 @@ class Steps47:
         self.ruse_loc = o.colmap_range(self.r3, r_loc, smin, smax, self.colmap)
         self._mark("select_sort")
         # ---- z-scores: exact hundredths (step-4 output) + clipped bf16 panel ----
-        if o.zquant(q, n, ld, self.sel, r_loc, self.rm, self.mu, scale, self.zq, max(ml, 1), self.colmap,
-                    self.qmax, self.zb, self.np_):
+        of, self.zq_is16 = 0, False
+        if self.zq16 is not None and not isinstance(q, Depth16) and ld % 4 == 0:
+            of, self.nesc = o.zquant16(q, n, ld, self.sel, r_loc, self.rm, self.mu, scale, self.zq16, max(ml, 1),
+                                       self.colmap, self.qmax, self.zb, self.np_, self.esc_idx, self.esc_val)
+            self.zq_is16 = not of
+        if not self.zq_is16 and not (of & 1):
+            if self.zq is None:
+                self.zq = self.A.empty(tuple(self.zq16.shape), I4)
+            of = o.zquant(q, n, ld, self.sel, r_loc, self.rm, self.mu, scale, self.zq, max(ml, 1), self.colmap,
+                          self.qmax, self.zb, self.np_)
+        if of & 1:
             raise _abi.GridNativeError("z-score outside the int32 hundredths range")
         self._mark("zquant")
         # ---- step 5: exact Gram (MFMA) -> all-reduce -> top-k ----

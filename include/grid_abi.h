@@ -158,6 +158,26 @@ int grid_norm_zquant_kb(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t ld
                         const int32_t *d_colmap, int32_t qmax, uint16_t *d_zb, int64_t np_zb,
                         int32_t *h_overflow);
 
+/* The same with the step-4 output compacted to int16 (half the HBM writes):
+ * d_zq16[i*ld_zq + s] = the hundredths v when GRID_ZQ16_MIN <= v <=
+ * GRID_ZQ16_MAX, GRID_ZQ16_NAN / GRID_ZQ16_NEG0 for the sentinels, and
+ * GRID_ZQ16_ESC for any other v, which is recorded exactly in the escape list
+ * (d_esc_idx[e] = i*ld_zq + s, d_esc_val[e] = v; *h_nesc = entries, in no
+ * particular order).  Bit 0 of *h_overflow as above; bit 1 = more than
+ * esc_cap escapes (the list holds the first esc_cap; the caller reruns
+ * grid_norm_zquant_kb with int32 output).  Needs ld % 4 == 0. */
+#define GRID_ZQ16_NAN (-32768)
+#define GRID_ZQ16_NEG0 (-32767)
+#define GRID_ZQ16_ESC (-32766)
+#define GRID_ZQ16_MIN (-32765)
+#define GRID_ZQ16_MAX 32767
+int grid_norm_zquant_kb16(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t ld,
+                          const int32_t *d_sel, int64_t r, const double *d_rowmean,
+                          const double *d_mu, double scale, int16_t *d_zq16, int64_t ld_zq,
+                          const int32_t *d_colmap, int32_t qmax, uint16_t *d_zb, int64_t np_zb,
+                          int64_t *d_esc_idx, int32_t *d_esc_val, int64_t esc_cap, int64_t *h_nesc,
+                          int32_t *h_overflow);
+
 int grid_norm_zquant_kb_q16(grid_ctx *ctx, const grid_depth16 *q, int64_t n, int64_t ld,
                             const int32_t *d_sel, int64_t r, const double *d_rowmean,
                             const double *d_mu, double scale, int32_t *d_zq, int64_t ld_zq,

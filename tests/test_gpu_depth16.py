@@ -132,7 +132,7 @@ def test_chain_q16_equals_int32(dev):
         st.set_phasing_graph(off, nbr, w)
         st.run(src, ld)
         torch.cuda.synchronize()
-        res[name] = [t.cpu().numpy() for t in (st.rm[:n], st.mu[:m], st.var[:m], st.zq[:n, : st.r_loc],
+        res[name] = [t.cpu().numpy() for t in (st.rm[:n], st.mu[:m], st.var[:m], st.zq_int32()[:n, : st.r_loc],
                                                st.idx_out[:n], st.d2[:n], st.dip[:n], st.hap[: 2 * n])]
     for a, b in zip(res["i32"], res["q16"]):
         assert np.array_equal(a, b, equal_nan=True)

@@ -60,7 +60,7 @@ def run_chain(rank, world, comm, lane):
     ml = c1 - c0
     return {
         "rm": st.rm[:N].cpu().numpy(), "mu": st.mu[:ml].cpu().numpy(), "var": st.var[:ml].cpu().numpy(),
-        "zq": st.zq[:N, : st.r_loc].cpu().numpy(), "idx": st.idx_out[:N].cpu().numpy(),
+        "zq": st.zq_int32()[:N, : st.r_loc].cpu().numpy(), "idx": st.idx_out[:N].cpu().numpy(),
         "d2": st.d2[:N].cpu().numpy(), "dip": st.dip[:N].cpu().numpy(), "hap": st.hap[: 2 * N].cpu().numpy(),
         "imp": st.imp[: 2 * N].cpu().numpy(), "scale": st.scale, "ruse": st.ruse_loc,
     }

@@ -51,7 +51,7 @@ def run_chain(rank, world, comm):
     ml = c1 - c0
     return {
         "rm": st.rm.numpy()[:N].copy(), "mu": st.mu.numpy()[:ml].copy(), "var": st.var.numpy()[:ml].copy(),
-        "sel": (st.sel.numpy()[: st.r_loc] + c0).copy(), "zq": st.zq.numpy()[:N, : st.r_loc].copy(),
+        "sel": (st.sel.numpy()[: st.r_loc] + c0).copy(), "zq": st.zq_int32().numpy()[:N, : st.r_loc].copy(),
         "idx": st.idx_out.numpy()[:N].copy(), "d2": st.d2.numpy()[:N].copy(), "dip": st.dip.numpy()[:N].copy(),
         "hap": st.hap.numpy()[: 2 * N].copy(), "imp": st.imp.numpy()[: 2 * N].copy(), "scale": st.scale,
         "ruse": st.ruse_loc,

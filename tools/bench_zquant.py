@@ -35,18 +35,29 @@ st.set_phasing_graph(off, nbr, w)
 st.run(q, a.m)
 torch.cuda.synchronize()
 of = C.c_int32()
-cases = {"full": (st.zq, st.zb), "no_zq": (None, st.zb), "no_zb": (st.zq, None), "read_only": (None, None)}
+zq32 = torch.empty((a.n, st.r_loc), dtype=torch.int32, device="cuda")
+zq16 = torch.empty((a.n, st.r_loc), dtype=torch.int16, device="cuda")
+cases = {"full16": (zq16, st.zb), "full": (zq32, st.zb), "no_zq": (None, st.zb), "no_zb": (zq32, None),
+         "read_only": (None, None)}
 res = {}
 for rep in range(a.reps):
     for name, (zq, zb) in cases.items():
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        call("grid_norm_zquant_kb", dev.ctx, q.data_ptr(), a.n, a.m, ptr(st.sel), st.r_loc, ptr(st.rm), ptr(st.mu),
-             st.scale, ptr(zq), a.m, ptr(st.colmap), st.qmax, ptr(zb), st.np_, C.byref(of))
+        if name == "full16":
+            ne = C.c_int64()
+            call("grid_norm_zquant_kb16", dev.ctx, q.data_ptr(), a.n, a.m, ptr(st.sel), st.r_loc, ptr(st.rm),
+                 ptr(st.mu), st.scale, ptr(zq), st.r_loc, ptr(st.colmap), st.qmax, ptr(zb), st.np_,
+                 ptr(st.esc_idx), ptr(st.esc_val), st.esc_idx.numel(), C.byref(ne), C.byref(of))
+            nesc = ne.value
+        else:
+            call("grid_norm_zquant_kb", dev.ctx, q.data_ptr(), a.n, a.m, ptr(st.sel), st.r_loc, ptr(st.rm),
+                 ptr(st.mu), st.scale, ptr(zq), st.r_loc, ptr(st.colmap), st.qmax, ptr(zb), st.np_, C.byref(of))
         e1.record()
         torch.cuda.synchronize()
         res.setdefault(name, []).append(e0.elapsed_time(e1))
 R = st.r_loc
 for name, t in res.items():
     print(f"{name}: min {min(t):.2f} ms  median {np.median(t):.2f} ms", flush=True)
+print(f"escapes (int16 form): {nesc}")
 print(f"bytes: q {a.n * a.m * 4 / 1e9:.1f} GB, zq {a.n * R * 4 / 1e9:.1f} GB, zb {st.np_ * st.kpad * 2 / 1e9:.1f} GB")
