@@ -720,8 +720,11 @@ __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, 
   __shared__ ZT s_zq[4][256 + 64];
   __shared__ uint16_t s_zb[4][256 + 64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t j0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
-  const int64_t r0 = (int64_t)blockIdx.y * rpw;
+  // blockIdx.x = row group (fastest): consecutive workgroups share the column
+  // block's sidx / colmap / mc32 reads in L2 instead of re-fetching them per
+  // row group (-11 GB of L2 fills per launch at the bench shape)
+  const int64_t j0 = ((int64_t)blockIdx.y * 256 + threadIdx.x) * 4;
+  const int64_t r0 = (int64_t)blockIdx.x * rpw;
   const int64_t r1 = (r0 + rpw < n) ? r0 + rpw : n;
   const bool full4 = j0 + 4 <= ld;
   // rows i0 .. i0+ZR-1 of this thread's 4 columns (rows past r1 re-read row r0)
@@ -1052,8 +1055,8 @@ static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, int64_
     LAUNCHCHK();
     const char *ge = getenv("GRID_ZQUANT_GROUPS");
     const int rpw = ZR * ((ge && atoi(ge) > 0) ? atoi(ge) : Z6G);
-    REQUIRE(ceil_div(n, rpw) <= 65535, "n too large for one launch");
-    const dim3 g6((unsigned)ceil_div(ceil_div(ld, 4), 256), (unsigned)ceil_div(n, rpw));
+    REQUIRE(ceil_div(ceil_div(ld, 4), 256) <= 65535, "ld too large for one launch");
+    const dim3 g6((unsigned)ceil_div(n, rpw), (unsigned)ceil_div(ceil_div(ld, 4), 256));
     if (d_zq16) {
       auto k16 = rpw > ZR ? k_zquant6<true, int16_t> : k_zquant6<false, int16_t>;
       hipLaunchKernelGGL(k16, g6, dim3(256), 0, ctx->stream, d_q, n, ld, sidx, d_rm, rinv, mus, sq, rsq, mc32, scale,
