@@ -243,6 +243,9 @@ __device__ __forceinline__ void load_row(const int32_t *__restrict__ q, const Q1
   } else if constexpr (VW == 4) {
     int4 t = *reinterpret_cast<const int4 *>(q + i * ld + j0);
     v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  } else if constexpr (VW == 2) {
+    int2 t = *reinterpret_cast<const int2 *>(q + i * ld + j0);
+    v[0] = t.x; v[1] = t.y;
   } else {
 #pragma unroll
     for (int c = 0; c < VW; c++) v[c] = q[i * ld + j0 + c];
@@ -255,7 +258,7 @@ __device__ __forceinline__ int32_t q_at(const int32_t *__restrict__ q, const Q16
   else return q[i * ld + j];
 }
 
-template <int VW, bool S16>
+template <int VW, bool S16, int CUN = CU>
 __global__ __launch_bounds__(256) void k_col_means(const int32_t *__restrict__ q, Q16 s16, int64_t n, int64_t m,
                                                    int64_t ld, const double *__restrict__ rm,
                                                    const double *__restrict__ rinv, double *__restrict__ mu) {
@@ -278,12 +281,12 @@ __global__ __launch_bounds__(256) void k_col_means(const int32_t *__restrict__ q
 #pragma unroll
   for (int c = 0; c < VW; c++) { acc[c] = 0.0; cnt[c] = 0; }
   int64_t i = 0;
-  for (; i + CU <= n; i += CU) {
-    int32_t v[CU][VW];
+  for (; i + CUN <= n; i += CUN) {
+    int32_t v[CUN][VW];
 #pragma unroll
-    for (int u = 0; u < CU; u++) load_row<VW, S16>(q, s16, i + u, ld, j0, v[u]);
+    for (int u = 0; u < CUN; u++) load_row<VW, S16>(q, s16, i + u, ld, j0, v[u]);
 #pragma unroll
-    for (int u = 0; u < CU; u++) {
+    for (int u = 0; u < CUN; u++) {
       const double r = rm[i + u], ri = rinv[i + u];
 #pragma unroll
       for (int c = 0; c < VW; c++) {
@@ -305,7 +308,7 @@ __global__ __launch_bounds__(256) void k_col_means(const int32_t *__restrict__ q
   for (int c = 0; c < VW; c++) mu[j0 + c] = acc[c] / (double)cnt[c];   // 0/0 -> NaN (numpy)
 }
 
-template <int VW, bool S16>
+template <int VW, bool S16, int CUN = CU>
 __global__ __launch_bounds__(256) void k_col_vars(const int32_t *__restrict__ q, Q16 s16, int64_t n, int64_t m,
                                                   int64_t ld, const double *__restrict__ rm,
                                                   const double *__restrict__ rinv,
@@ -335,12 +338,12 @@ __global__ __launch_bounds__(256) void k_col_vars(const int32_t *__restrict__ q,
 #pragma unroll
   for (int c = 0; c < VW; c++) { acc[c] = 0.0; mj[c] = mu[j0 + c]; }
   int64_t i = 0;
-  for (; i + CU <= n; i += CU) {
-    int32_t v[CU][VW];
+  for (; i + CUN <= n; i += CUN) {
+    int32_t v[CUN][VW];
 #pragma unroll
-    for (int u = 0; u < CU; u++) load_row<VW, S16>(q, s16, i + u, ld, j0, v[u]);
+    for (int u = 0; u < CUN; u++) load_row<VW, S16>(q, s16, i + u, ld, j0, v[u]);
 #pragma unroll
-    for (int u = 0; u < CU; u++) {
+    for (int u = 0; u < CUN; u++) {
       const double r = rm[i + u], ri = rinv[i + u];
 #pragma unroll
       for (int c = 0; c < VW; c++) {
@@ -980,13 +983,22 @@ static int col_stats_impl(grid_ctx *ctx, bool vars, const int32_t *d_q, const Q1
   char *rest;
   int rc = recip_rows(ctx, d_rm, n, 0, &rinv, &rest);
   if (rc) return rc;
-  const int vw = (s16.q || vec4_ok(d_q, ld)) ? 4 : 1;
+  // int32: 1 column per thread (47 k waves at the bench shape, ~6 rounds of
+  // resident waves; 4 per thread left a 2.3-round tail: 14.5 vs 13.7 ms)
+  const char *cv = getenv("GRID_COL_VW"), *cu = getenv("GRID_COL_CU");
+  const int want = cv ? atoi(cv) : 1;
+  const bool cu16 = cu && atoi(cu) == 16;
+  const int vw = s16.q ? 4 : vec4_ok(d_q, ld) ? (want == 4 ? 4 : want == 1 ? 1 : 2) : 1;
   const dim3 grid((unsigned)ceil_div(ceil_div(m, vw), 256));
   if (!vars) {
-    auto kern = s16.q ? k_col_means<4, true> : vw == 4 ? k_col_means<4, false> : k_col_means<1, false>;
+    auto kern = s16.q ? k_col_means<4, true>
+                : vw == 4 ? k_col_means<4, false> : vw == 2 ? k_col_means<2, false>
+                : cu16 ? k_col_means<1, false, 16> : k_col_means<1, false>;
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, ctx->stream, d_q, s16, n, m, ld, d_rm, rinv, d_out);
   } else {
-    auto kern = s16.q ? k_col_vars<4, true> : vw == 4 ? k_col_vars<4, false> : k_col_vars<1, false>;
+    auto kern = s16.q ? k_col_vars<4, true>
+                : vw == 4 ? k_col_vars<4, false> : vw == 2 ? k_col_vars<2, false>
+                : cu16 ? k_col_vars<1, false, 16> : k_col_vars<1, false>;
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, ctx->stream, d_q, s16, n, m, ld, d_rm, rinv, d_mu, d_out,
                        d_ratio);
   }
