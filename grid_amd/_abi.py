@@ -358,20 +358,28 @@ PACK_CAP = 16
 HI_UNIT_WEIGHTS, HI_LEGACY = 1, 2     # grid_hi_phase flags
 
 
-def hi_schedule(off: np.ndarray, nbr: np.ndarray, w: np.ndarray):
-    """Level schedule + schedule-ordered packed neighbour lists (host C++)."""
+def hi_schedule(off: np.ndarray, nbr: np.ndarray, w: np.ndarray, packed_w: bool = True):
+    """Level schedule + schedule-ordered packed neighbour lists (host C++).
+    ``packed_w=False``: with unit weights the packed weights (2/3 of the packed
+    bytes) are not built and pk_w is None (pass NULL: the kernels read 1.0)."""
     order, loff, nl = hi_levels(off, nbr)
     n = len(order)
     off = np.ascontiguousarray(off, dtype=np.int64)
+    unit = len(w) == 0 or bool(np.all(np.asarray(w) == 1.0))
+    flags = HI_UNIT_WEIGHTS if unit else 0
     nbr = np.ascontiguousarray(nbr if len(nbr) else np.zeros(1), dtype=np.int32)
     w = np.ascontiguousarray(w if len(w) else np.zeros(1), dtype=np.float64)
-    pk_nbr = np.zeros((max(n, 1), 2, PACK_CAP), dtype=np.int32)
-    pk_w = np.zeros((max(n, 1), 2, PACK_CAP), dtype=np.float64)
+    pk_nbr = np.empty((max(n, 1), 2, PACK_CAP), dtype=np.int32)
+    skip_w = unit and not packed_w
+    pk_w = None if skip_w else np.empty((max(n, 1), 2, PACK_CAP), dtype=np.float64)
     pk_cnt = np.zeros((max(n, 1), 2), dtype=np.int32)
     call("grid_hi_pack", n, off.ctypes.data, nbr.ctypes.data, w.ctypes.data, order.ctypes.data if n else None,
-         PACK_CAP, pk_nbr.ctypes.data, pk_w.ctypes.data, pk_cnt.ctypes.data)
+         PACK_CAP, pk_nbr.ctypes.data, None if skip_w else pk_w.ctypes.data, pk_cnt.ctypes.data)
+    if n == 0:
+        pk_nbr[:] = 0
+        if pk_w is not None:
+            pk_w[:] = 0
     lens = np.diff(off) if len(off) > 1 else np.zeros(1, np.int64)
-    flags = HI_UNIT_WEIGHTS if (len(w) == 0 or bool(np.all(np.asarray(w) == 1.0))) else 0
     return order, loff, nl, pk_nbr, pk_w, pk_cnt, flags, int(lens.max()) if lens.size else 0
 
 

@@ -141,11 +141,16 @@ __device__ __forceinline__ void ph_fetch(int e, int e1, const int32_t *__restric
     it.nb[0][t] = a.x; it.nb[0][t + 1] = a.y; it.nb[0][t + 2] = a.z; it.nb[0][t + 3] = a.w;
     it.nb[1][t] = b.x; it.nb[1][t + 1] = b.y; it.nb[1][t + 2] = b.z; it.nb[1][t + 3] = b.w;
   }
+  if (pk_w) {
 #pragma unroll
-  for (int t = 0; t < CAP; t += 2) {
-    double2 a = *reinterpret_cast<const double2 *>(pw + t), b = *reinterpret_cast<const double2 *>(pw + CAP + t);
-    it.wt[0][t] = a.x; it.wt[0][t + 1] = a.y;
-    it.wt[1][t] = b.x; it.wt[1][t + 1] = b.y;
+    for (int t = 0; t < CAP; t += 2) {
+      double2 a = *reinterpret_cast<const double2 *>(pw + t), b = *reinterpret_cast<const double2 *>(pw + CAP + t);
+      it.wt[0][t] = a.x; it.wt[0][t + 1] = a.y;
+      it.wt[1][t] = b.x; it.wt[1][t + 1] = b.y;
+    }
+  } else {                            // unit weights, not packed (grid_hi_pack with pk_w NULL)
+#pragma unroll
+    for (int t = 0; t < CAP; t++) it.wt[0][t] = it.wt[1][t] = 1.0;
   }
   it.c0 = c.x < 0 ? CAP + 1 : c.x;     // > CAP: read the CSR in the loop fallback
   it.c1 = c.y < 0 ? CAP + 1 : c.y;
@@ -632,17 +637,17 @@ int grid_dipcn(grid_ctx *ctx, int64_t n, const double *d_reads, const uint8_t *d
 
 int grid_hi_pack(int64_t n, const int64_t *off, const int32_t *nbr, const double *w, const int32_t *order,
                  int32_t cap, int32_t *pk_nbr, double *pk_w, int32_t *pk_cnt) {
-  REQUIRE(n >= 0 && off && order && pk_nbr && pk_w && pk_cnt, "bad args");
+  REQUIRE(n >= 0 && off && order && pk_nbr && pk_cnt, "bad args");
   REQUIRE(cap == CAP, "pack capacity must be %d", CAP);
   for (int64_t e = 0; e < n; e++) {
     const int64_t i = order[e];
     for (int h = 0; h < 2; h++) {
       const int64_t o = off[2 * i + h], c = off[2 * i + h + 1] - o;
       int32_t *pn = pk_nbr + (e * 2 + h) * CAP;
-      double *pw = pk_w + (e * 2 + h) * CAP;
-      for (int t = 0; t < CAP; t++) {
-        pn[t] = (t < c) ? nbr[o + t] : 0;
-        pw[t] = (t < c) ? w[o + t] : 0.0;
+      for (int t = 0; t < CAP; t++) pn[t] = (t < c) ? nbr[o + t] : 0;
+      if (pk_w) {                     // NULL: unit weights, the kernels do not read them
+        double *pw = pk_w + (e * 2 + h) * CAP;
+        for (int t = 0; t < CAP; t++) pw[t] = (t < c) ? w[o + t] : 0.0;
       }
       pk_cnt[e * 2 + h] = c <= CAP ? (int32_t)c : -1;
     }

@@ -219,16 +219,26 @@ def phase_batch(dev: Device, loci, min_nbr: int, n_iters: int):
     (irr [n], off [2n+1], nbr, w) per locus (CSR as csr_from_lists).  Returns
     a list of (hap [2n], imp [2n], mean) equal to phase() per locus."""
     import ctypes as C
-    sched, descs, keep, outs = [], [], [], []
+    import os
+    from concurrent.futures import ThreadPoolExecutor
+    descs, keep, outs = [], [], []
     flags_all, max_list, max_n, max_nlev = _abi.HI_UNIT_WEIGHTS, 0, 0, 0
-    for irr, off, nbr, w in loci:
-        order, loff, nl, pk_nbr, pk_w, pk_cnt, flags, ml = _abi.hi_schedule(off, nbr, w)
+    legacy = _legacy_flag()
+    # per-locus schedules in parallel (the C++ schedule / pack calls release the GIL)
+    with ThreadPoolExecutor(max(1, min(16, os.cpu_count() or 1))) as ex:
+        full = list(ex.map(lambda l: _abi.hi_schedule(l[1], l[2], l[3], packed_w=bool(legacy)), loci))
+    sched = []
+    for (irr, off, nbr, w), (order, loff, nl, pk_nbr, pk_w, pk_cnt, flags, ml) in zip(loci, full):
         flags_all &= flags
         max_list, max_n, max_nlev = max(max_list, ml), max(max_n, len(irr)), max(max_nlev, nl)
         sched.append((order, loff, nl, pk_nbr, pk_w, pk_cnt))
+    if not flags_all and not legacy:   # some locus has weights: every locus needs its packed weights
+        sched = [(o, lf, nl, pn, pw if pw is not None else _abi.hi_schedule(l[1], l[2], l[3])[4], pc)
+                 for l, (o, lf, nl, pn, pw, pc) in zip(loci, sched)]
     for (irr, off, nbr, w), (order, loff, nl, pk_nbr, pk_w, pk_cnt) in zip(loci, sched):
         n = len(irr)
-        b = [dev.upload(np.ascontiguousarray(a)) for a in
+        # pk_w None: unit weights, not packed -> NULL in the descriptor (read as 1.0)
+        b = [None if a is None else dev.upload(np.ascontiguousarray(a)) for a in
              (np.asarray(irr if n else np.zeros(1), F8), np.asarray(off, I8),
               np.asarray(nbr if len(nbr) else np.zeros(1), I4), np.asarray(w if len(w) else np.zeros(1), F8),
               np.asarray(order if n else np.zeros(1), I4), np.asarray(loff, I4), pk_nbr, pk_w, pk_cnt)]
@@ -236,14 +246,14 @@ def phase_batch(dev: Device, loci, min_nbr: int, n_iters: int):
         keep += b
         outs.append((n, hap, imp, mean))
         descs.append(_abi.HiLocus(n, b[0].ptr, b[1].ptr, b[2].ptr, b[3].ptr, b[4].ptr, b[5].ptr, nl, 0, b[6].ptr,
-                                  b[7].ptr, b[8].ptr, hap.ptr, imp.ptr, mean.ptr))
+                                  None if b[7] is None else b[7].ptr, b[8].ptr, hap.ptr, imp.ptr, mean.ptr))
     if not descs:
         return []
     arr = (_abi.HiLocus * len(descs))(*descs)
     d_arr = dev.alloc(C.sizeof(arr), np.uint8)
     call("grid_h2d", dev.ctx, d_arr.ptr, C.addressof(arr), C.sizeof(arr))
     call("grid_hi_phase_batch", dev.ctx, len(descs), d_arr.ptr, max_n, max_nlev, min_nbr, n_iters,
-         flags_all | _legacy_flag(), max_list)
+         flags_all | legacy, max_list)
     res = []
     for n, hap, imp, mean in outs:
         res.append((hap.numpy()[: 2 * n], imp.numpy()[: 2 * n], float(mean.numpy()[0]) if n else 0.0))

@@ -236,7 +236,8 @@ int grid_hi_levels(int64_t n, const int64_t *h_off, const int32_t *h_nbr, int32_
                    int32_t *h_level_off, int32_t *h_nlevels);
 /* Host: schedule-ordered packed neighbour lists for the kernel (cap = 16 per
  * haplotype; longer lists are flagged -1 in pk_cnt and read from the CSR).
- * pk_nbr [n][2][cap], pk_w [n][2][cap], pk_cnt [n][2]. */
+ * pk_nbr [n][2][cap], pk_w [n][2][cap], pk_cnt [n][2].  pk_w may be NULL when
+ * every weight is 1.0 (GRID_HI_UNIT_WEIGHTS kernels do not read it). */
 int grid_hi_pack(int64_t n, const int64_t *h_off, const int32_t *h_nbr, const double *h_w,
                  const int32_t *h_order, int32_t cap, int32_t *h_pk_nbr, double *h_pk_w,
                  int32_t *h_pk_cnt);
@@ -276,7 +277,7 @@ typedef struct grid_hi_locus {
   int32_t nlev;
   int32_t reserved;
   const int32_t *pk_nbr;           /* grid_hi_pack output, schedule order */
-  const double *pk_w;
+  const double *pk_w;              /* NULL allowed when every weight of the locus is 1.0 */
   const int32_t *pk_cnt;
   double *hap;                     /* [2n] out */
   double *imp;                     /* [2n] out */

@@ -65,15 +65,16 @@ prep_s = time.perf_counter() - t0
 # the phasing launch alone (device time) on the prepared batch: rerun with events
 def device_ms():
     import ctypes as C
-    sched = [_abi.hi_schedule(off, nbr, w) for _, off, nbr, w in loci]
+    sched = [_abi.hi_schedule(off, nbr, w, packed_w=False) for _, off, nbr, w in loci]
     keep, descs = [], []
     for (irr, off, nbr, w), (order, loff, nl, pk_nbr, pk_w, pk_cnt, flags, ml) in zip(loci, sched):
-        b = [dev.upload(np.ascontiguousarray(x)) for x in (irr, off, nbr.astype(np.int32), w, order.astype(np.int32),
-                                                          loff.astype(np.int32), pk_nbr, pk_w, pk_cnt)]
+        b = [None if x is None else dev.upload(np.ascontiguousarray(x))
+             for x in (irr, off, nbr.astype(np.int32), w, order.astype(np.int32), loff.astype(np.int32), pk_nbr,
+                       pk_w, pk_cnt)]
         outs = [dev.alloc(2 * len(irr), np.float64), dev.alloc(2 * len(irr), np.float64), dev.alloc(1, np.float64)]
         keep += b + outs
-        descs.append(_abi.HiLocus(len(irr), *[x.ptr for x in b[:6]], nl, 0, *[x.ptr for x in b[6:]],
-                                  *[x.ptr for x in outs]))
+        pk = [None if x is None else x.ptr for x in b[6:]]     # pk_w None: unit weights, not packed
+        descs.append(_abi.HiLocus(len(irr), *[x.ptr for x in b[:6]], nl, 0, *pk, *[x.ptr for x in outs]))
     arr = (_abi.HiLocus * len(descs))(*descs)
     d = dev.alloc(C.sizeof(arr), np.uint8)
     _abi.call("grid_h2d", dev.ctx, d.ptr, C.addressof(arr), C.sizeof(arr))
