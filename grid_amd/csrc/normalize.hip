@@ -677,6 +677,7 @@ __device__ __forceinline__ int wave_max_i32(int v) {
 }
 
 constexpr int Z6G = 1;   // default row groups of ZR rows per workgroup (per-column setup amortised)
+constexpr int Z6NT = 1;   // default for GRID_ZQUANT_NT: streaming q loads (NT stores measured slower)
 
 // ZT = int16_t: the compact step-4 output (GRID_ZQ16_* codes).  A value
 // outside [GRID_ZQ16_MIN, GRID_ZQ16_MAX] is written as GRID_ZQ16_ESC and
@@ -710,7 +711,10 @@ __device__ __forceinline__ ZT zq_code(int32_t o, int64_t flat, const ZEsc &e, in
   }
 }
 
-template <bool LOOP, class ZT>
+// NT bit 0: streaming (nontemporal) loads of q, read once per launch (reads
+// 10.15 -> 9.77 ms at the bench shape).  Bit 1, nontemporal stores of both
+// outputs, measured slower (18.5 -> 21.1 ms) and is not instantiated.
+template <bool LOOP, class ZT, int NT>
 __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, int64_t n, int64_t ld,
                                                  const int32_t *__restrict__ sidx,
                                                  const double *__restrict__ rm, const double *__restrict__ rinv,
@@ -736,7 +740,13 @@ __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, 
     for (int u = 0; u < ZR; u++) {
       const int64_t i = (i0 + u < r1) ? i0 + u : r0;
       if (full4) {
-        v[u] = *reinterpret_cast<const int4 *>(q + i * ld + j0);
+        if constexpr (NT & 1) {
+          typedef int v4i __attribute__((ext_vector_type(4)));
+          const v4i t = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(q + i * ld + j0));
+          v[u] = make_int4(t.x, t.y, t.z, t.w);
+        } else {
+          v[u] = *reinterpret_cast<const int4 *>(q + i * ld + j0);
+        }
       } else {
         v[u].x = (j0 + 0 < ld) ? q[i * ld + j0 + 0] : GRID_MISSING;
         v[u].y = (j0 + 1 < ld) ? q[i * ld + j0 + 1] : GRID_MISSING;
@@ -830,8 +840,10 @@ __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, 
 #pragma unroll
         for (int m = 0; m < 4; m++) {
           const ZT val = s_zq[wv][lane + 64 * m];
-          if (64 * m + 64 <= nS) zrow[lane + 64 * m] = val;              // whole chunk (wave-uniform)
-          else if (lane + 64 * m < nS) zrow[lane + 64 * m] = val;
+          if (lane + 64 * m < nS) {
+            if constexpr (NT & 2) __builtin_nontemporal_store(val, &zrow[lane + 64 * m]);
+            else zrow[lane + 64 * m] = val;
+          }
         }
       }
       if (zb) {
@@ -839,7 +851,10 @@ __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, 
 #pragma unroll
         for (int m = 0; m < 4; m++) {
           const uint16_t val = s_zb[wv][lane + 64 * m];
-          if (lane + 64 * m < nC && val != 0xFFFFu) brow[zoff[m]] = val;
+          if (lane + 64 * m < nC && val != 0xFFFFu) {
+            if constexpr (NT & 2) __builtin_nontemporal_store(val, &brow[zoff[m]]);
+            else brow[zoff[m]] = val;
+          }
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the next row's writes
@@ -1067,14 +1082,19 @@ static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, int64_
     LAUNCHCHK();
     const char *ge = getenv("GRID_ZQUANT_GROUPS");
     const int rpw = ZR * ((ge && atoi(ge) > 0) ? atoi(ge) : Z6G);
+    const char *ntv = getenv("GRID_ZQUANT_NT");
+    const int nt = ntv ? atoi(ntv) : Z6NT;
+    REQUIRE(nt == 0 || nt == 1, "GRID_ZQUANT_NT must be 0 or 1 (got %d)", nt);
     REQUIRE(ceil_div(ceil_div(ld, 4), 256) <= 65535, "ld too large for one launch");
     const dim3 g6((unsigned)ceil_div(n, rpw), (unsigned)ceil_div(ceil_div(ld, 4), 256));
     if (d_zq16) {
-      auto k16 = rpw > ZR ? k_zquant6<true, int16_t> : k_zquant6<false, int16_t>;
+      auto k16 = nt ? (rpw > ZR ? k_zquant6<true, int16_t, 1> : k_zquant6<false, int16_t, 1>)
+                    : (rpw > ZR ? k_zquant6<true, int16_t, 0> : k_zquant6<false, int16_t, 0>);
       hipLaunchKernelGGL(k16, g6, dim3(256), 0, ctx->stream, d_q, n, ld, sidx, d_rm, rinv, mus, sq, rsq, mc32, scale,
                          d_zq16, ld_zq, d_colmap, qmax, d_zb, ld_zb, kbs, d_of, rpw, esc);
     } else {
-      auto k32 = rpw > ZR ? k_zquant6<true, int32_t> : k_zquant6<false, int32_t>;
+      auto k32 = nt ? (rpw > ZR ? k_zquant6<true, int32_t, 1> : k_zquant6<false, int32_t, 1>)
+                    : (rpw > ZR ? k_zquant6<true, int32_t, 0> : k_zquant6<false, int32_t, 0>);
       hipLaunchKernelGGL(k32, g6, dim3(256), 0, ctx->stream, d_q, n, ld, sidx, d_rm, rinv, mus, sq, rsq, mc32, scale,
                          d_zq, ld_zq, d_colmap, qmax, d_zb, ld_zb, kbs, d_of, rpw, esc);
     }
