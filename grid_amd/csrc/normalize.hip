@@ -226,7 +226,8 @@ constexpr int CU = 8;   // rows unrolled per iteration in the column kernels
 
 // VW adjacent columns per thread, sequential over rows: int4 loads of int32
 // (VW == 4), or one 8-B load of 4 compact uint16 values (S16).
-template <int VW, bool S16>
+constexpr bool COL_NT = true;   // default for GRID_COL_NT
+template <int VW, bool S16, bool NTL = false>
 __device__ __forceinline__ void load_row(const int32_t *__restrict__ q, const Q16 &s16, int64_t i, int64_t ld,
                                          int64_t j0, int32_t (&v)[VW]) {
   if constexpr (S16) {
@@ -248,7 +249,10 @@ __device__ __forceinline__ void load_row(const int32_t *__restrict__ q, const Q1
     v[0] = t.x; v[1] = t.y;
   } else {
 #pragma unroll
-    for (int c = 0; c < VW; c++) v[c] = q[i * ld + j0 + c];
+    for (int c = 0; c < VW; c++) {
+      if constexpr (NTL) v[c] = __builtin_nontemporal_load(q + i * ld + j0 + c);   // streamed once
+      else v[c] = q[i * ld + j0 + c];
+    }
   }
 }
 template <bool S16>
@@ -258,7 +262,7 @@ __device__ __forceinline__ int32_t q_at(const int32_t *__restrict__ q, const Q16
   else return q[i * ld + j];
 }
 
-template <int VW, bool S16, int CUN = CU>
+template <int VW, bool S16, int CUN = CU, bool NTL = false>
 __global__ __launch_bounds__(256) void k_col_means(const int32_t *__restrict__ q, Q16 s16, int64_t n, int64_t m,
                                                    int64_t ld, const double *__restrict__ rm,
                                                    const double *__restrict__ rinv, double *__restrict__ mu) {
@@ -284,7 +288,7 @@ __global__ __launch_bounds__(256) void k_col_means(const int32_t *__restrict__ q
   for (; i + CUN <= n; i += CUN) {
     int32_t v[CUN][VW];
 #pragma unroll
-    for (int u = 0; u < CUN; u++) load_row<VW, S16>(q, s16, i + u, ld, j0, v[u]);
+    for (int u = 0; u < CUN; u++) load_row<VW, S16, NTL>(q, s16, i + u, ld, j0, v[u]);
 #pragma unroll
     for (int u = 0; u < CUN; u++) {
       const double r = rm[i + u], ri = rinv[i + u];
@@ -297,7 +301,7 @@ __global__ __launch_bounds__(256) void k_col_means(const int32_t *__restrict__ q
   }
   for (; i < n; i++) {
     int32_t v[VW];
-    load_row<VW, S16>(q, s16, i, ld, j0, v);
+    load_row<VW, S16, NTL>(q, s16, i, ld, j0, v);
 #pragma unroll
     for (int c = 0; c < VW; c++) {
       double y;
@@ -308,7 +312,7 @@ __global__ __launch_bounds__(256) void k_col_means(const int32_t *__restrict__ q
   for (int c = 0; c < VW; c++) mu[j0 + c] = acc[c] / (double)cnt[c];   // 0/0 -> NaN (numpy)
 }
 
-template <int VW, bool S16, int CUN = CU>
+template <int VW, bool S16, int CUN = CU, bool NTL = false>
 __global__ __launch_bounds__(256) void k_col_vars(const int32_t *__restrict__ q, Q16 s16, int64_t n, int64_t m,
                                                   int64_t ld, const double *__restrict__ rm,
                                                   const double *__restrict__ rinv,
@@ -341,7 +345,7 @@ __global__ __launch_bounds__(256) void k_col_vars(const int32_t *__restrict__ q,
   for (; i + CUN <= n; i += CUN) {
     int32_t v[CUN][VW];
 #pragma unroll
-    for (int u = 0; u < CUN; u++) load_row<VW, S16>(q, s16, i + u, ld, j0, v[u]);
+    for (int u = 0; u < CUN; u++) load_row<VW, S16, NTL>(q, s16, i + u, ld, j0, v[u]);
 #pragma unroll
     for (int u = 0; u < CUN; u++) {
       const double r = rm[i + u], ri = rinv[i + u];
@@ -357,7 +361,7 @@ __global__ __launch_bounds__(256) void k_col_vars(const int32_t *__restrict__ q,
   }
   for (; i < n; i++) {
     int32_t v[VW];
-    load_row<VW, S16>(q, s16, i, ld, j0, v);
+    load_row<VW, S16, NTL>(q, s16, i, ld, j0, v);
 #pragma unroll
     for (int c = 0; c < VW; c++) {
       double y;
@@ -1003,17 +1007,19 @@ static int col_stats_impl(grid_ctx *ctx, bool vars, const int32_t *d_q, const Q1
   const char *cv = getenv("GRID_COL_VW"), *cu = getenv("GRID_COL_CU");
   const int want = cv ? atoi(cv) : 1;
   const bool cu16 = cu && atoi(cu) == 16;
+  const char *cn = getenv("GRID_COL_NT");   // streaming (nontemporal) loads, 1-column path (A/B)
+  const bool nt = cn ? atoi(cn) != 0 : COL_NT;
   const int vw = s16.q ? 4 : vec4_ok(d_q, ld) ? (want == 4 ? 4 : want == 1 ? 1 : 2) : 1;
   const dim3 grid((unsigned)ceil_div(ceil_div(m, vw), 256));
   if (!vars) {
     auto kern = s16.q ? k_col_means<4, true>
                 : vw == 4 ? k_col_means<4, false> : vw == 2 ? k_col_means<2, false>
-                : cu16 ? k_col_means<1, false, 16> : k_col_means<1, false>;
+                : cu16 ? k_col_means<1, false, 16> : nt ? k_col_means<1, false, CU, true> : k_col_means<1, false>;
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, ctx->stream, d_q, s16, n, m, ld, d_rm, rinv, d_out);
   } else {
     auto kern = s16.q ? k_col_vars<4, true>
                 : vw == 4 ? k_col_vars<4, false> : vw == 2 ? k_col_vars<2, false>
-                : cu16 ? k_col_vars<1, false, 16> : k_col_vars<1, false>;
+                : cu16 ? k_col_vars<1, false, 16> : nt ? k_col_vars<1, false, CU, true> : k_col_vars<1, false>;
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, ctx->stream, d_q, s16, n, m, ld, d_rm, rinv, d_mu, d_out,
                        d_ratio);
   }
