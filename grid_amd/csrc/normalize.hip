@@ -23,7 +23,9 @@ __device__ __forceinline__ double qval(int32_t q) {
 // ---- full 8192-element blocks: one 256-thread workgroup per (row, block) ----
 // 64 leaves x 8 chains = 512 chains, 2 per thread; leaf results combined in
 // the fixed binary tree of pairwise(8192).
-// SRC: 0 = int32 (int4 loads), 1 = int32 (scalar loads), 2 = compact uint16 (s16)
+// SRC: 0 = int32 (int4 loads), 1 = int32 (scalar loads), 2 = compact uint16 (s16),
+// 3 = int32 (streaming / nontemporal int4 loads; GRID_ROWBLK_NT A/B)
+constexpr bool ROWBLK_NT = true;   // default for GRID_ROWBLK_NT
 template <int SRC>
 __global__ __launch_bounds__(256) void k_row_blocks_full(const int32_t *__restrict__ q, Q16 s16, int64_t ld,
                                                          int64_t nblk_full, int64_t nblk,
@@ -64,6 +66,10 @@ __global__ __launch_bounds__(256) void k_row_blocks_full(const int32_t *__restri
       int4 v;
       if (SRC == 0) {
         v = src[e4];
+      } else if (SRC == 3) {
+        typedef int v4i __attribute__((ext_vector_type(4)));
+        const v4i t = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(src) + e4);
+        v = make_int4(t.x, t.y, t.z, t.w);
       } else {
         v.x = srcp[4 * e4]; v.y = srcp[4 * e4 + 1]; v.z = srcp[4 * e4 + 2]; v.w = srcp[4 * e4 + 3];
       }
@@ -945,7 +951,10 @@ static int row_blocks_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, in
   int64_t nblk = ceil_div(m, BLK), nfull = m / BLK;
   if (nfull > 0) {
     REQUIRE(n <= 65535, "n > 65535 rows per launch");
-    auto kern = c16 ? k_row_blocks_full<2> : vec4_ok(d_q, ld) ? k_row_blocks_full<0> : k_row_blocks_full<1>;
+    const char *rn = getenv("GRID_ROWBLK_NT");
+    const bool nt = rn ? atoi(rn) != 0 : ROWBLK_NT;
+    auto kern = c16 ? k_row_blocks_full<2>
+              : vec4_ok(d_q, ld) ? (nt ? k_row_blocks_full<3> : k_row_blocks_full<0>) : k_row_blocks_full<1>;
     hipLaunchKernelGGL(kern, dim3((unsigned)nfull, (unsigned)n), dim3(256), 0, ctx->stream, d_q, s16, ld, nfull, nblk,
                        d_bsum, d_bcnt);
     LAUNCHCHK();
