@@ -1,22 +1,34 @@
 #!/usr/bin/env python3
 """Benchmark: GRiD steps 4-7 end to end on MI355X (BASELINE.json metric).
 
-One "step" = one pass of the device-resident steps 4-7 chain
-(grid_amd/fused.py) over the BASELINE config-2 cohort: 3,202 samples x
-3,000,000 bins (hg38 @ 1 kb), k = 10 neighbours, n_iters = 100, synthetic
-data generated in HBM before timing.  value = samples / s (whole job).
+One "step" = one pass of the device chain of steps 4-7 (grid_amd/fused.py)
+over a synthetic cohort, k = 10 neighbours, n_iters = 100.  value =
+samples / s (whole job).
 
-Multi-GPU (torch.distributed.run, one rank per GPU, RCCL): the same cohort is
-bin-sharded in 8192-aligned ranges (strong scaling); the Gram all-reduce is
-the only data-path collective.
+  * default: BASELINE config 2, 3,202 samples x 3,000,000 bins (hg38 @ 1 kb),
+    the depth matrix generated in HBM before timing (resident, 38 GB);
+  * --samples 50000 (config 3) / --bins 30000000 (config 4): the matrix does
+    not fit (600 GB / 6 TB int32), so the bin axis is STREAMED: every pass
+    regenerates its 8192-aligned chunk on the device (grid_amd.fused.
+    SynthSource), inside the timed region, and the step-4 output is written
+    chunk by chunk (fused mode).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+Multi-GPU: one rank per GPU over RCCL.  ``--gpus N`` without an external
+launcher starts ``torch.distributed.run`` with N ranks as a child process
+before anything touches the GPU.  The cohort is bin-sharded in 8192-aligned
+ranges (strong scaling); the data-path collectives are the all-gathers of
+row-block partials and ratios and ONE reduce-scatter of the int64 Gram by
+row blocks.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--samples N] [--bins M]
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -73,15 +85,18 @@ def synth_reads_and_ibs(n, seed=SEED, per_hap=10):
     return reads, off, nbr, np.ones(len(nbr))
 
 
-def cpu_baseline(q_host, n, m_total, reads, off, nbr, w, k, n_iters):
+def cpu_baseline(q_host, n_total, m_total, k, n_iters, seed=SEED):
     """The oracle (NumPy restatement of the reference, oracle/) timed on this
-    host on a bounded column sample of the same cohort; normalisation and
-    k-NN (linear in bins) are scaled to the full bin count."""
+    host on a bounded sample of the same cohort: the first ns samples x ms
+    bins (q_host).  Each stage is scaled by its complexity to the full
+    workload: normalisation by (n m) / (ns ms), k-NN by (n^2 m) / (ns^2 ms),
+    dipCN and phasing by n / ns."""
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from oracle import steps
     from oracle.npsum import nanmean_rows
-    ms = q_host.shape[1]
-    mat = q_host / 100.0
+    ns, ms = q_host.shape
+    reads, off, nbr, w = synth_reads_and_ibs(ns, seed)
+    mat = np.where(q_host == -(2 ** 31), np.nan, q_host / 100.0)
     t0 = time.perf_counter()
     raw = nanmean_rows(mat)
     z, ratios, mu, var, scale = steps.normalize_matrix(mat)
@@ -90,27 +105,60 @@ def cpu_baseline(q_host, n, m_total, reads, off, nbr, w, k, n_iters):
     t1 = time.perf_counter()
     r3 = np.round(np.array([ratios[j] for j in sel]), 3)
     idx, ruse = steps.filter_regions_by_variance(r3, 1.0, 1000.0)
-    qz = np.clip(np.rint(zs[:, idx] * 100), -200, 200).astype(np.int64)
+    qz = np.clip(np.rint(np.nan_to_num(zs[:, idx], nan=0.0) * 100), -200, 200).astype(np.int64)
     nb = steps.knn_exact(qz, k)
     t2 = time.perf_counter()
-    ids = [f"S{i:06d}" for i in range(n)]
-    sc = {ids[i]: float(f"{raw[i]:.2f}") for i in range(n)}
-    nbrs = {ids[i]: [(ids[j], sc[ids[j]]) for j, _ in nb[i]] for i in range(n)}
-    rd = {ids[i]: float(reads[i]) for i in range(n)}
+    ids = [f"S{i:06d}" for i in range(ns)]
+    sc = {ids[i]: float(f"{raw[i]:.2f}") for i in range(ns)}
+    nbrs = {ids[i]: [(ids[j], sc[ids[j]]) for j, _ in nb[i]] for i in range(ns)}
+    rd = {ids[i]: float(reads[i]) for i in range(ns)}
     dip = steps.dipcn(nbrs, sc, rd, 300)
     t3 = time.perf_counter()
     irr = [v for _, v in dip]
-    hn = [[(int(nbr[t]), float(w[t])) for t in range(off[h], off[h + 1])] for h in range(2 * n)]
+    hn = [[(int(nbr[t]), float(w[t])) for t in range(off[h], off[h + 1])] for h in range(2 * ns)]
     hap, mean = steps.run_phasing(irr, hn, 1, n_iters)
-    _ = [steps.compute_imp(i, hap, hn, mean) for i in range(n)]
+    _ = [steps.compute_imp(i, hap, hn, mean) for i in range(ns)]
     t4 = time.perf_counter()
-    f = m_total / ms
-    total = (t1 - t0) * f + (t2 - t1) * f + (t3 - t2) + (t4 - t3)
+    fn, fm = n_total / ns, m_total / ms
+    total = (t1 - t0) * fn * fm + (t2 - t1) * fn * fn * fm + (t3 - t2) * fn + (t4 - t3) * fn
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    return {"value": n / total, "unit": "samples/s", "cores": threads, "kind": "port",
-            "sample": (f"oracle steps 4-7 on {n} samples x {ms} bins of the same cohort "
-                       f"(normalise {t1 - t0:.2f}s + kNN {t2 - t1:.2f}s scaled x{f:.1f} to {m_total} bins; "
-                       f"dipCN {t3 - t2:.2f}s, phasing {t4 - t3:.2f}s unscaled)")}
+    return {"value": n_total / total, "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": (f"oracle steps 4-7 on the first {ns} samples x {ms} bins of the same cohort, scaled to "
+                       f"{n_total} x {m_total}: normalise {t1 - t0:.2f}s x{fn * fm:.1f}, kNN {t2 - t1:.2f}s "
+                       f"x{fn * fn * fm:.1f}, dipCN {t3 - t2:.2f}s x{fn:.1f}, phasing {t4 - t3:.2f}s x{fn:.1f} "
+                       f"(extrapolated; host memory bounds the reference well below this shape)")}
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(gpus):
+    """One rank per GPU: torch.distributed.run as a CHILD process (this
+    process has not touched the GPU), exit with its status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
+
+
+def plan_memory(n, ml, world, budget):
+    """Resident (one chunk) when the whole shard fits the HBM budget, else the
+    widest 8192-multiple chunk that does.  Returns (chunk or None, bytes)."""
+    np_ = -(-max(n, 1) // 256) * 256
+    fixed = np_ * np_ * 8 * (1 + (1.0 / world if world > 1 else 0.0)) + n * (-(-ml // 8192)) * 24 + ml * 64
+    per_col_resident = n * 4 + n * 2 + np_ * 2            # q int32 + z int16 + bf16 panel
+    if fixed + per_col_resident * ml <= budget:
+        return None, fixed + per_col_resident * ml
+    per_col = n * 4 + n * 2 + np_ * 2                     # chunk buffers: q, z, panel
+    chunk = int((budget - fixed) // per_col) // 8192 * 8192
+    if chunk < 8192:
+        raise SystemExit(f"bench: {n} samples do not fit the HBM budget ({budget / 1e9:.0f} GB)")
+    return min(chunk, -(-ml // 8192) * 8192), fixed + per_col * chunk
 
 
 def main():
@@ -122,18 +170,29 @@ def main():
     ap.add_argument("--bins", type=int, default=3_000_000)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--n-iters", type=int, default=100)
+    ap.add_argument("--chunk", type=int, default=0, help="bins per streamed chunk (multiple of 8192); "
+                    "0 = resident when the shard fits, else the widest chunk that fits")
+    ap.add_argument("--hbm-budget-gb", type=float, default=250.0)
+    ap.add_argument("--cpu-samples", type=int, default=4096)
     ap.add_argument("--cpu-bins", type=int, default=16384)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-overlap", action="store_true", help="run step 7 inline on the main stream")
+    ap.add_argument("--traffic-json", default=TRAFFIC_JSON,
+                    help="rocprofv3 PMC summary (tools/pmc_traffic.py) of this same command, for roofline.traffic")
     ap.add_argument("--depth-format", choices=["int32", "q16"], default="int32",
-                    help="depth matrix in HBM: int32 hundredths (default) or the compact uint16 + escapes form "
-                         "(half the bytes; measured slower: the step-4 passes are not byte-bound)")
+                    help="resident depth matrix in HBM: int32 hundredths (default) or the compact uint16 + escapes "
+                         "form (half the bytes; measured slower: the step-4 passes are not byte-bound)")
     args = ap.parse_args()
 
-    import torch
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
     # GRID_BENCH_SHARE_GPU=1 (rehearsal only): ranks share the visible GPUs
     # round-robin, with GRID_DIST_BACKEND=gloo since RCCL needs one GPU per rank
     if os.environ.get("GRID_BENCH_SHARE_GPU") == "1":
@@ -152,7 +211,7 @@ def main():
         comm = TorchComm(dist)
 
     from grid_amd import _abi
-    from grid_amd.fused import Depth16, HipOps, Steps47, TorchAlloc, shard_range
+    from grid_amd.fused import Depth16, HipOps, Steps47, SynthSource, TorchAlloc, shard_range
 
     dev = _abi.Device(local)
     dev.set_stream(torch.cuda.current_stream())
@@ -160,7 +219,17 @@ def main():
     c0, c1 = shard_range(m, rank, world)
     ml = c1 - c0
     talloc = TorchAlloc(local)
-    if args.depth_format == "q16":
+    ops = HipOps(dev)
+    if args.chunk:
+        chunk, _ = args.chunk, None
+    else:
+        chunk, _ = plan_memory(n, ml, world, args.hbm_budget_gb * 1e9)
+    streamed = chunk is not None and chunk < ml
+    if streamed:
+        if args.depth_format != "int32":
+            raise SystemExit("bench: the compact depth form is resident-only")
+        q, ldq = SynthSource(ops, SEED, n, c0, NCL), None
+    elif args.depth_format == "q16":
         # compact depth matrix: uint16 hundredths + escape table (half the HBM
         # bytes of the four step-4 passes; same int32 values after decoding)
         q = Depth16.synth(talloc, dev.ctx, SEED, n, ml, c0, NCL)
@@ -179,8 +248,9 @@ def main():
         pstream = torch.cuda.Stream()
         pdev.set_stream(pstream)
         lane = (HipOps(pdev), pstream)
-    st = Steps47(HipOps(dev), talloc, n, m, c0, ml, k=args.k, n_nbr=300, top_frac=0.1, zmax=2.0,
-                 sigma2_max=1000.0, frac_r=1.0, min_nbr=1, n_iters=args.n_iters, comm=comm, phase_lane=lane)
+    st = Steps47(ops, talloc, n, m, c0, ml, k=args.k, n_nbr=300, top_frac=0.1, zmax=2.0, sigma2_max=1000.0,
+                 frac_r=1.0, min_nbr=1, n_iters=args.n_iters, comm=comm, phase_lane=lane,
+                 chunk=chunk if streamed else None, keep_z=not streamed)
     st.set_reads(reads)
     st.set_phasing_graph(off, nbr, w)
 
@@ -189,13 +259,13 @@ def main():
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
     t0 = time.perf_counter()
+    gms, glaunch = 0.0, 0
+    gram_pairs = []
     for s in range(args.steps):
-        st.run(q, ldq, gram_events=ev[s])
+        st.run(q, ldq, time_gram=True)
+        gram_pairs += st.gram_evs
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -204,22 +274,31 @@ def main():
     if dist:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
-    gram_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    gms = sum(a.elapsed_time(b) for a, b in gram_pairs) / max(args.steps, 1)      # Gram ms per step
+    glaunch = len(gram_pairs) // max(args.steps, 1)
     st.run(q, ldq, profile=True)              # untimed pass: per-stage device times
     torch.cuda.synchronize()
     stages = {k: round(v, 3) for k, v in st.stage_ms().items()}
 
     valid = int(st.valid[:n].sum().item())
     traffic, tsrc = None, None
-    tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), TRAFFIC_JSON)
+    tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), args.traffic_json)
     if os.path.exists(tpath):
-        tk = json.load(open(tpath))["kernels"]
-        hits = [v for k, v in tk.items() if k.startswith(GRAM_KERNEL)]
-        if hits and n == 3202 and m == 3_000_000 and world == 1:
-            traffic, tsrc = hits[0]["traffic_bytes"], TRAFFIC_JSON
-    flops = 2.0 * n * n * st.ruse_loc                       # 2 N^2 R_use per launch
-    nt, ni = st.np_ // 128, st.np_ // 256            # k_gram8: 256x128 tiles (I, j >= 2I)
-    executed = 2.0 * sum(nt - 2 * i for i in range(ni)) * 256 * 128 * (-(-st.ruse_loc // 64) * 64)
+        tj = json.load(open(tpath))
+        shape_ok = tj.get("bench", {}).get("samples", 3202) == n and tj.get("bench", {}).get("bins", 3_000_000) == m
+        hits = [v for kk, v in tj["kernels"].items() if kk.startswith(GRAM_KERNEL)]
+        if hits and shape_ok and world == 1 and not streamed:
+            traffic, tsrc = hits[0]["traffic_bytes"], args.traffic_json
+    ruse = st.ruse_loc
+    flops = 2.0 * n * n * ruse                          # 2 N^2 R_use per step (this rank)
+    nt, ni = st.np_ // 128, st.np_ // 256               # k_gram8: 256x128 tiles (I, j >= 2I)
+    ntiles = sum(nt - 2 * i for i in range(ni))
+    executed = 2.0 * ntiles * 256 * 128 * sum(-(-u // 64) * 64 for u in st.chunk_used)
+    gsec = gms * 1e-3
+    streamed_note = (f", bin-streamed in {st.nch} chunks of {chunk} bins regenerated on the device every pass "
+                     f"(inside the timed region), step-4 output written per chunk") if streamed else ""
+    cfgname = {(3202, 3_000_000): "BASELINE config 2", (50_000, 3_000_000): "BASELINE config 3 shape",
+               (50_000, 30_000_000): "BASELINE config 4 shape"}.get((n, m), "custom")
     out = {
         "metric": METRIC,
         "value": n * args.steps / elapsed,
@@ -233,32 +312,34 @@ def main():
         "vs_baseline": None,
         "dtype": "f64 (statistics) + bf16-MFMA exact-integer (k-NN)",
         "data": "synthetic (counter-based cohort generated in HBM; 26 ancestry clusters)",
-        "config": {"workload": f"BASELINE config 2: {n} samples x {m} bins (hg38 @ 1 kb), k={args.k}, "
-                               f"n_iters={args.n_iters}", "samples": n, "bins": m, "k": args.k,
-                   "n_iters": args.n_iters, "parallelism": f"bin-sharded x{world}",
-                   "depth_format": args.depth_format,
-                   "selected_regions": None, "R_use_rank0": st.ruse_loc, "dipcn_valid": valid,
-                   "phasing_levels": st.nlev},
+        "config": {"workload": f"{cfgname}: {n} samples x {m} bins, k={args.k}, n_iters={args.n_iters}, "
+                               f"{world} GPU(s){streamed_note}",
+                   "samples": n, "bins": m, "k": args.k, "n_iters": args.n_iters,
+                   "parallelism": f"bin-sharded x{world}", "depth_format": args.depth_format,
+                   "streamed": streamed, "chunk_bins": chunk if streamed else None, "chunks": st.nch,
+                   "selected_regions": st.r_loc if world == 1 else None, "R_use_rank0": ruse,
+                   "dipcn_valid": valid, "phasing_levels": st.nlev},
         "stages_ms": stages,
-        "roofline": {"kernel": "k_gram (exact bf16-MFMA Gram)", "bound": "mfma",
-                     "achieved": flops / (gram_ms * 1e-3) / 1e12, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": flops / (gram_ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS,
+        "roofline": {"kernel": "k_gram8 (exact bf16-MFMA Gram)", "bound": "mfma",
+                     "achieved": flops / gsec / 1e12, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": flops / gsec / 1e12 / PEAK_BF16_TFLOPS,
                      "traffic": traffic, "traffic_source": tsrc,
-                     "hbm_gbs": traffic / (gram_ms * 1e-3) / 1e9 if traffic else None,
-                     "hbm_frac": traffic / (gram_ms * 1e-3) / 1e9 / PEAK_HBM_GBS if traffic else None,
-                     "gram_ms": gram_ms,
-                     "executed_mfma_tflops": executed / (gram_ms * 1e-3) / 1e12,
-                     "flops_def": "2*N^2*R_use per launch (SURVEY 8d); executed = the 256x128 upper-triangle "
-                                  "tiles k_gram8 computes"},
+                     "hbm_gbs": traffic * glaunch / gsec / 1e9 if traffic else None,
+                     "hbm_frac": traffic * glaunch / gsec / 1e9 / PEAK_HBM_GBS if traffic else None,
+                     "gram_ms": gms, "gram_launches_per_step": glaunch,
+                     "executed_mfma_tflops": executed / gsec / 1e12,
+                     "executed_frac": executed / gsec / 1e12 / PEAK_BF16_TFLOPS,
+                     "flops_def": "2*N^2*R_use per step on this rank (SURVEY 8d), over the summed HIP-event time "
+                                  "of its Gram launches; executed = the 256x128 upper-triangle tiles k_gram8 "
+                                  "computes (the symmetric half is not executed)"},
     }
-    out["config"]["selected_regions"] = st.r_loc if world == 1 else None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        ms = min(args.cpu_bins, ml)
-        qs = torch.empty((n, ms), dtype=torch.int32, device="cuda")   # same cells, int32 form
-        _abi.call("grid_synth_depth", dev.ctx, SEED, n, ms, ms, c0, NCL, qs.data_ptr())
+        ns, ms = min(args.cpu_samples, n), min(args.cpu_bins, ml)
+        qs = torch.empty((ns, ms), dtype=torch.int32, device="cuda")   # same cells, int32 form
+        _abi.call("grid_synth_depth", dev.ctx, SEED, ns, ms, ms, c0, NCL, qs.data_ptr())
         qh = qs.cpu().numpy()
         del qs
-        out["cpu_baseline"] = cpu_baseline(qh, n, m, reads, off, nbr, w, args.k, args.n_iters)
+        out["cpu_baseline"] = cpu_baseline(qh, n, m, args.k, args.n_iters)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

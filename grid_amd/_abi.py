@@ -58,9 +58,19 @@ _SIGS = {
     "grid_norm_zquant_kb16": [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _f64, _vp, _i64, _vp, _i32,
                               _vp, _i64, _vp, _vp, _i64, C.POINTER(_i64), C.POINTER(_i32)],
     "grid_norm_zfull": [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _f64, _vp],
+    "grid_verify_zquant": [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _f64, _vp, _i64, _vp, _i32, _vp, _i64, _vp],
     "grid_knn_gram": [_vp, _vp, _i64, _i64, _i64, _i32, _vp],
     "grid_knn_gram_kb": [_vp, _vp, _i64, _i64, _i32, _vp],
     "grid_knn_topk": [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _vp, _vp, _vp],
+    "grid_knn_mirror": [_vp, _vp, _i64],
+    "grid_knn_diag": [_vp, _vp, _i64, _i64, _vp],
+    "grid_knn_topk_rows": [_vp, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp],
+    "grid_knn_topk_d2": [_vp, _vp, _i64, _f64, _i64, _i64, _i64, _i64, _vp, _vp, _vp],
+    "grid_knn_dist_i32": [_vp, _vp, _i64, _i64, _i64, _vp, _i64],
+    "grid_knn_dist_f64": [_vp, _vp, _i64, _i64, _i64, _vp, _i64],
+    "grid_knn_panel_i32": [_vp, _vp, _i64, _i64, _vp, _i64, _i32, _vp, _i64, _i64],
+    "grid_knn_gather_i32": [_vp, _vp, _i64, _i64, _vp, _i64, _i32, _vp],
+    "grid_knn_gather_f64": [_vp, _vp, _i64, _i64, _vp, _i64, _f64, _vp],
     "grid_dipcn": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, C.POINTER(_i32)],
     "grid_hi_levels": [_i64, _vp, _vp, _vp, _vp, C.POINTER(_i32)],
     "grid_hi_pack": [_i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp],

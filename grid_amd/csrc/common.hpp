@@ -21,7 +21,7 @@ struct grid_ctx {
   int32_t *aux_tiles_host = nullptr;   // host copy of the uploaded tile list (re-upload check)
   int aux_tiles_n = 0;
 };
-constexpr size_t GRID_AUX_BYTES = 1 << 20;
+constexpr size_t GRID_AUX_BYTES = 4 << 20;   // Gram tile list (<= 512 Ki tiles) + round counters
 
 void grid_set_error(const char *fmt, ...);
 int grid_scratch(grid_ctx *ctx, size_t bytes, void **p);

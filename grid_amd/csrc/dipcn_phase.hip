@@ -668,14 +668,19 @@ int grid_hi_phase(grid_ctx *ctx, int64_t n, const double *d_irr, const int64_t *
   const bool unitw = flags & GRID_HI_UNIT_WEIGHTS;
   if (lds2 <= 120 * 1024 && !(flags & GRID_HI_LEGACY)) {
     // register-pipelined kernel; CAPT covers the longest list when it can
-    // GRID_PHASE_PROBE (timing probes, wrong results): 1 = no list prefetch, 2 = no arithmetic
-    const char *pe = getenv("GRID_PHASE_PROBE");
-    const int probe = pe ? atoi(pe) : 0;
     auto kern = unitw ? (max_list <= 8 ? k_phase2<true, 8> : k_phase2<true, 16>)
                       : (max_list <= 8 ? k_phase2<false, 8> : k_phase2<false, 16>);
+#ifdef GRID_PROBES
+    // tools build only -- GRID_PHASE_PROBE timing probes (wrong results):
+    // 1 = no list prefetch, 2 = no arithmetic, 3 = neither
+    const char *pe = getenv("GRID_PHASE_PROBE");
+    const int probe = pe ? atoi(pe) : 0;
     if (probe == 1) kern = k_phase2<true, 16, 1>;
     if (probe == 2) kern = k_phase2<true, 16, 2>;
     if (probe == 3) kern = k_phase2<true, 16, 3>;
+#else
+    const int probe = 0;
+#endif
     static bool attr2[7] = {false, false, false, false, false, false, false};
     const int slot = probe ? 3 + probe : (unitw ? 2 : 0) + (max_list <= 8 ? 0 : 1);
     if (!attr2[slot]) {

@@ -8,13 +8,16 @@
 //     products, kept below 2^24 so every fp32 partial is an exact integer;
 //   * they are then flushed into int32 accumulators (exact while a K-slice
 //     stays below 2^31 / qmax^2 products);
-//   * each workgroup owns one output tile (256x128 in k_gram6, the default;
-//     128x128 in the k_gram_dma fallback) of one K-slice and adds its int32
+//   * each workgroup owns one 256x128 output tile (k_gram8, persistent; the
+//     128x128 k_gram_dma covers np % 256 != 0) of one K-slice and adds its int32
 //     tile into the int64 Gram with integer atomics (order-free, exact).
+// The upper tiles are mirrored into the lower triangle (k_mirror) so a row of
+// G is contiguous for the row top-k and the multi-GPU reduce-scatter.
 // d2(i,j) = G_ii + G_jj - 2 G_ij is then exact, and neighbours are ordered by
 // (d2, j).  That equals sklearn's order wherever exact distances differ.
 #include "common.hpp"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace {
@@ -87,10 +90,7 @@ __global__ __launch_bounds__(NT, 2) void k_gram_dma(const uint16_t *__restrict__
   const int slice = wid / ntiles;
   int t = wid - slice * ntiles;
   int ti = 0, tj;
-  if (blocked == 2) {            // timing probe only (wrong results): every tile reads panel 0
-    tile_blocked(t, nt, ti, tj);
-    ti = tj = 0;
-  } else if (blocked) {
+  if (blocked) {
     tile_blocked(t, nt, ti, tj);
   } else {
     while (t >= nt - ti) { t -= nt - ti; ti++; }
@@ -253,6 +253,7 @@ __host__ __device__ void tile_blocked6(int t, int nt, int ni, int &I, int &tj) {
   I = 0; tj = 0;
 }
 
+#ifdef GRID_PROBES   // k_gram6: tools build only (tools/bench_gram.py A/B and timing probes)
 // One workgroup's pass over K-steps [s0, s1) of output tile (I, tj): fp32
 // MFMA chunks flushed exactly into iacc (which the caller keeps or drains).
 template <int MODE, int SPLIT, int MB, int GS>
@@ -418,6 +419,8 @@ __device__ __forceinline__ void g6_run(const uint16_t *__restrict__ z, int64_t l
 #undef G6_FLUSH
 }
 
+#endif  // GRID_PROBES
+
 // Drain iacc into the int64 Gram (order-free integer atomics) and clear it.
 template <int MB>
 __device__ __forceinline__ void g6_atomics(int32_t (&iacc)[MB][2][16], int I, int tj, int64_t np_,
@@ -448,6 +451,7 @@ __device__ __forceinline__ void g6_zero(f32x16 (&acc)[MB][2], int32_t (&iacc)[MB
       for (int r = 0; r < 16; r++) { acc[a][b][r] = 0.0f; iacc[a][b][r] = 0; }
 }
 
+#ifdef GRID_PROBES
 // MODE 0: production.  Timing probes (wrong results, tools/bench_gram.py):
 // 1 every tile reads the same panels (all L2 hits); 2 = 1 without the flush;
 // 4 = 1 with half the fragment reads; 5 = 1 without any global loads;
@@ -478,6 +482,8 @@ __global__ __launch_bounds__(MB == 2 ? 512 : 256, 1) void k_gram6(const uint16_t
   g6_run<MODE, SPLIT, MB, GS>(z, ld, I, tj, s0, s1, smem, acc, iacc);
   g6_atomics<MB>(iacc, I, tj, np_, gram);
 }
+
+#endif  // GRID_PROBES
 
 // Default Gram kernel (k_gram8): persistent, one 512-thread workgroup per CU,
 // XCD x = blockIdx % 8 (placement is a performance assumption only; results
@@ -683,9 +689,14 @@ __device__ __forceinline__ void g8_run(const uint16_t *__restrict__ z, int64_t l
 #undef G8_FLUSH
 }
 
+// kx = the number of K-ranges the XCDs split the K axis into (8, 4, 2 or 1):
+// XCD x runs K-range x % kx of the tile groups g = x / kx (mod 8 / kx).  A
+// small cohort (fewer tile groups than XCDs) splits K eight ways; a large one
+// gives every XCD whole tile groups over the full K range, so each output tile
+// is flushed with int64 atomics only once per int32-exact unit (sps_max steps).
 template <int MODE, bool BL, int FL>
 __global__ __launch_bounds__(512, 1) void k_gram8(const uint16_t *__restrict__ z, int64_t ld,
-                                                  const int32_t *__restrict__ tiles, int ntiles, int kc,
+                                                  const int32_t *__restrict__ tiles, int ntiles, int kc, int kx,
                                                   int64_t nsteps, int lag, int spin_ticks,
                                                   int64_t np_, unsigned long long *__restrict__ gram,
                                                   unsigned *__restrict__ rounds) {
@@ -694,17 +705,24 @@ __global__ __launch_bounds__(512, 1) void k_gram8(const uint16_t *__restrict__ z
   const int bid = blockIdx.x;
   const int xcd = bid & 7, l = bid >> 3;
   const int per = nwg >> 3;                       // workgroups per XCD (grid is a multiple of 8)
-  const int64_t xs0 = nsteps * xcd / 8, xs1 = nsteps * (xcd + 1) / 8;
+  const int kr = xcd % kx, gx = 8 / kx, xg = xcd / kx;
+  const int64_t xs0 = nsteps * kr / kx, xs1 = nsteps * (kr + 1) / kx;
   const int64_t xlen = xs1 - xs0;
-  const int64_t units = (int64_t)ntiles * kc;
+  // this XCD's tile groups: g = xg, xg + gx, ...; only the last group overall
+  // can be partial, so every group but this XCD's last holds per * kc units
+  const int64_t ngroups = ((int64_t)ntiles + per - 1) / per;
+  const int64_t ngx = ngroups > xg ? (ngroups - xg + gx - 1) / gx : 0;
+  const int64_t glast = xg + (ngx - 1) * gx;
+  const int64_t lastsz = ngx > 0 ? min((int64_t)per, (int64_t)ntiles - glast * per) : 0;
+  const int64_t units = ngx > 0 ? ((ngx - 1) * per + lastsz) * kc : 0;
   for (int64_t r = 0;; r++) {
     const int64_t u = r * per + l;
     if (u >= units) break;
     // unit -> (group, chunk, tile)
-    const int64_t g = u / ((int64_t)per * kc);
-    const int64_t gbase = g * per;
+    const int64_t gl = u / ((int64_t)per * kc);
+    const int64_t gbase = (xg + gl * gx) * per;
     const int gsz = (int)min((int64_t)per, (int64_t)ntiles - gbase);
-    const int64_t v = u - g * (int64_t)per * kc;
+    const int64_t v = u - gl * (int64_t)per * kc;
     const int c = (int)(v / gsz);
     const int t = (int)(gbase + v % gsz);
     const int32_t tv = tiles[t];
@@ -732,36 +750,200 @@ __global__ __launch_bounds__(512, 1) void k_gram8(const uint16_t *__restrict__ z
   }
 }
 
-
-constexpr int SELCAP = 4096;
-
-__device__ __forceinline__ int64_t gram_at(const int64_t *g, int64_t np_, int64_t i, int64_t j) {
-  return ((i >> 7) <= (j >> 7)) ? g[i * np_ + j] : g[j * np_ + i];
+// ---- symmetric completion and row access ------------------------------------
+// The Gram kernels write the upper 128-tiles only.  k_mirror fills every 64x64
+// block (a, b), a > b, with the transpose of block (b, a) through LDS, so the
+// reads and the writes are whole 512-B row segments; afterwards row i of the
+// Gram is contiguous, which is what the row top-k and the multi-GPU
+// reduce-scatter by row blocks read.
+__global__ __launch_bounds__(256) void k_mirror(int64_t *__restrict__ g, int64_t np_) {
+  __shared__ int64_t t[64][65];
+  const int64_t p = blockIdx.x;                   // strict lower triangle of 64-blocks, row-major
+  int64_t a = (int64_t)((sqrt(8.0 * (double)p + 1.0) + 1.0) * 0.5);
+  while (a * (a - 1) / 2 > p) a--;
+  while ((a + 1) * a / 2 <= p) a++;
+  const int64_t b = p - a * (a - 1) / 2;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll 4
+  for (int r = ty; r < 64; r += 4) t[r][tx] = g[(b * 64 + r) * np_ + a * 64 + tx];
+  __syncthreads();
+#pragma unroll 4
+  for (int r = ty; r < 64; r += 4) g[(a * 64 + r) * np_ + b * 64 + tx] = t[tx][r];
 }
 
-__global__ __launch_bounds__(256) void k_topk(const int64_t *__restrict__ g, int64_t n, int64_t np_,
-                                              int64_t k, int64_t row0, int32_t *__restrict__ idx,
-                                              int64_t *__restrict__ d2o, int32_t *__restrict__ cnto) {
+__global__ void k_diag(const int64_t *__restrict__ g, int64_t np_, int64_t n, int64_t *__restrict__ nrm) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < n) nrm[j] = g[j * np_ + j];
+}
+
+// Neighbour keys: (d2 << 20) | j, unique per row, ordered by (d2, j); j < 2^20.
+// GramKey: exact integer d2 = G_ii + G_jj - 2 G_ij from full Gram rows
+// (the MFMA path).  D2Key: rows of precomputed d2 (the direct-difference path),
+// keyed on floor(d2 * scale) -- exact integers when scale = 1 and d2 < 2^44
+// (integer hundredths), a 44-bit fixed-point prefix of fp64 distances
+// otherwise -- with the emitted distance re-read from the row.
+struct GramKey {
+  const int64_t *row;
+  const int64_t *nrm;
+  int64_t gii;
+  typedef int64_t out_t;
+  __device__ __forceinline__ unsigned long long key(int64_t j) const {
+    return ((unsigned long long)(gii + nrm[j] - 2 * row[j]) << 20) | (unsigned long long)j;
+  }
+  __device__ __forceinline__ void load4(int64_t j, int64_t st, unsigned long long (&kk)[4]) const {
+    int64_t gv[4], nv[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) { gv[u] = row[j + u * st]; nv[u] = nrm[j + u * st]; }
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+      kk[u] = ((unsigned long long)(gii + nv[u] - 2 * gv[u]) << 20) | (unsigned long long)(j + u * st);
+  }
+  __device__ __forceinline__ int64_t value(unsigned long long key) const { return (int64_t)(key >> 20); }
+};
+struct D2Key {
+  const double *row;
+  double scale;
+  typedef double out_t;
+  __device__ __forceinline__ unsigned long long key(int64_t j) const {
+    return ((unsigned long long)(row[j] * scale) << 20) | (unsigned long long)j;
+  }
+  __device__ __forceinline__ void load4(int64_t j, int64_t st, unsigned long long (&kk)[4]) const {
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) v[u] = row[j + u * st];
+#pragma unroll
+    for (int u = 0; u < 4; u++) kk[u] = ((unsigned long long)(v[u] * scale) << 20) | (unsigned long long)(j + u * st);
+  }
+  __device__ __forceinline__ double value(unsigned long long key) const { return row[key & 0xFFFFFull]; }
+};
+
+__device__ __forceinline__ GramKey make_src(const int64_t *rows, int64_t ld, const int64_t *nrm, double,
+                                            int64_t orow, int64_t i) {
+  return GramKey{rows + orow * ld, nrm, nrm[i]};
+}
+__device__ __forceinline__ D2Key make_src(const double *rows, int64_t ld, const int64_t *, double scale,
+                                          int64_t orow, int64_t) {
+  return D2Key{rows + orow * ld, scale};
+}
+
+// Write the ktake smallest keys of row i (ascending in s[0..ktake)) with self
+// dropped and the first k kept (find_neighbors.py:216-225).
+template <class Src>
+__device__ __forceinline__ void topk_emit(const Src &src, const unsigned long long *s, int64_t ktake, int64_t i,
+                                          int64_t k, int64_t orow, int32_t *__restrict__ idx,
+                                          typename Src::out_t *__restrict__ d2o, int32_t *__restrict__ cnto) {
+  int64_t w = 0;
+  bool self = false;
+  for (int64_t e = 0; e < ktake; e++) {
+    const int64_t j = (int64_t)(s[e] & 0xFFFFFull);
+    if (j == i && !self) { self = true; continue; }
+    if (w < k) {
+      idx[orow * k + w] = (int32_t)j;
+      d2o[orow * k + w] = src.value(s[e]);
+      w++;
+    }
+  }
+  for (int64_t e = w; e < k; e++) {      // unused slots: idx -1, d2 0
+    idx[orow * k + e] = -1;
+    d2o[orow * k + e] = 0;
+  }
+  cnto[orow] = (int32_t)w;
+}
+
+// Row top-(k+1), k + 1 <= K1 (BASELINE: k = 10): ONE pass over the row.  Every
+// lane keeps the K1 smallest keys of its strided share sorted in registers
+// (branch-free insertion, taken only when a key beats the lane's largest);
+// each wave then extracts its ktake smallest by wave-wide minimum rounds, and
+// one lane merges the four waves' sorted lists.
+template <int K1, class T>
+__global__ __launch_bounds__(256) void k_topk_small(const T *__restrict__ rows, int64_t ld,
+                                                    const int64_t *__restrict__ nrm, double scale, int64_t n,
+                                                    int64_t k, int64_t row0, int32_t *__restrict__ idx,
+                                                    void *__restrict__ d2o, int32_t *__restrict__ cnto) {
+  __shared__ unsigned long long s_w[4][K1];
+  __shared__ unsigned long long s_m[4 * K1];
+  const int64_t orow = blockIdx.x, i = row0 + orow;
+  const auto src = make_src(rows, ld, nrm, scale, orow, i);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t ktake = (k + 1 < n) ? k + 1 : n;
+  unsigned long long L[K1];
+#pragma unroll
+  for (int t = 0; t < K1; t++) L[t] = ~0ull;
+  auto insert = [&](unsigned long long key) {
+    if (key < L[K1 - 1]) {
+#pragma unroll
+      for (int t = 0; t < K1; t++) {
+        const unsigned long long lo = key < L[t] ? key : L[t];
+        key = key < L[t] ? L[t] : key;
+        L[t] = lo;
+      }
+    }
+  };
+  int64_t j = tid;
+  for (; j + 3 * 256 < n; j += 4 * 256) {       // four loads of each kind in flight
+    unsigned long long kk[4];
+    src.load4(j, 256, kk);
+#pragma unroll
+    for (int u = 0; u < 4; u++) insert(kk[u]);
+  }
+  for (; j < n; j += 256) insert(src.key(j));
+  // wave: the ktake smallest of its 64 sorted lists, ascending
+  for (int64_t e = 0; e < ktake; e++) {
+    unsigned long long m = L[0];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long x = __shfl_xor(m, o, 64);
+      m = x < m ? x : m;
+    }
+    if (lane == 0) s_w[wv][e] = m;
+    const bool pop = L[0] == m;                  // keys are unique: one lane (or none once exhausted)
+#pragma unroll
+    for (int t = 0; t + 1 < K1; t++) L[t] = pop ? L[t + 1] : L[t];
+    L[K1 - 1] = pop ? ~0ull : L[K1 - 1];
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int p[4] = {0, 0, 0, 0};
+    for (int64_t e = 0; e < ktake; e++) {
+      int bw = 0;
+      unsigned long long bv = ~0ull;
+#pragma unroll
+      for (int w = 0; w < 4; w++) {
+        const unsigned long long v = p[w] < ktake ? s_w[w][p[w]] : ~0ull;
+        if (v < bv) { bv = v; bw = w; }
+      }
+      p[bw]++;
+      s_m[e] = bv;
+    }
+    topk_emit(src, s_m, ktake, i, k, orow, idx, (typename decltype(src)::out_t *)d2o, cnto);
+  }
+}
+
+// Row top-(k+1) for larger k: 8-pass radix select on the packed keys over the
+// (coalesced) row, then a bitonic sort of the <= SELCAP survivors.
+constexpr int SELCAP = 4096;
+
+template <class T>
+__global__ __launch_bounds__(256) void k_topk_radix(const T *__restrict__ rows, int64_t ld,
+                                                    const int64_t *__restrict__ nrm, double scale, int64_t n,
+                                                    int64_t k, int64_t row0, int32_t *__restrict__ idx,
+                                                    void *__restrict__ d2o, int32_t *__restrict__ cnto) {
   __shared__ unsigned hist[256];
   __shared__ unsigned long long s_prefix;
   __shared__ long long s_rank;
   __shared__ unsigned long long sel[SELCAP];
-  __shared__ int s_nsel, s_self;
-  const int64_t i = row0 + blockIdx.x;
+  __shared__ int s_nsel;
+  const int64_t orow = blockIdx.x, i = row0 + orow;
+  const auto src = make_src(rows, ld, nrm, scale, orow, i);
   const int tid = threadIdx.x;
   const int64_t ktake = (k + 1 < n) ? k + 1 : n;
-  const int64_t gii = g[i * np_ + i];
-  auto key = [&](int64_t j) -> unsigned long long {
-    int64_t d2 = gii + g[j * np_ + j] - 2 * gram_at(g, np_, i, j);
-    return ((unsigned long long)d2 << 20) | (unsigned long long)j;
-  };
   unsigned long long prefix = 0, mask = 0;
   long long rank = ktake - 1;
   for (int shift = 56; shift >= 0; shift -= 8) {
     hist[tid] = 0;
     __syncthreads();
     for (int64_t j = tid; j < n; j += 256) {
-      unsigned long long kk = key(j);
+      const unsigned long long kk = src.key(j);
       if ((kk & mask) == prefix) atomicAdd(&hist[(kk >> shift) & 255], 1u);
     }
     __syncthreads();
@@ -782,57 +964,123 @@ __global__ __launch_bounds__(256) void k_topk(const int64_t *__restrict__ g, int
     mask |= 0xFFull << shift;
     __syncthreads();
   }
-  const unsigned long long T = prefix;   // the ktake-th smallest key (keys unique)
-  if (tid == 0) { s_nsel = 0; s_self = -1; }
+  const unsigned long long T_ = prefix;   // the ktake-th smallest key (keys unique)
+  if (tid == 0) s_nsel = 0;
   for (int e = tid; e < SELCAP; e += 256) sel[e] = ~0ull;
   __syncthreads();
   for (int64_t j = tid; j < n; j += 256) {
-    unsigned long long kk = key(j);
-    if (kk <= T) {
-      int p = atomicAdd(&s_nsel, 1);
+    const unsigned long long kk = src.key(j);
+    if (kk <= T_) {
+      const int p = atomicAdd(&s_nsel, 1);
       if (p < SELCAP) sel[p] = kk;
     }
   }
   __syncthreads();
   int cap = 1;
   while (cap < ktake) cap <<= 1;
-  // bitonic sort of sel[0..cap)
   for (int size = 2; size <= cap; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       for (int e = tid; e < cap; e += 256) {
-        int p = e ^ stride;
+        const int p = e ^ stride;
         if (p > e) {
-          bool up = (e & size) == 0;
-          unsigned long long a = sel[e], b = sel[p];
+          const bool up = (e & size) == 0;
+          const unsigned long long a = sel[e], b = sel[p];
           if ((a > b) == up) { sel[e] = b; sel[p] = a; }
         }
       }
       __syncthreads();
     }
   }
-  for (int e = tid; e < ktake; e += 256)
-    if ((int64_t)(sel[e] & 0xFFFFFull) == i) s_self = e;
-  __syncthreads();
-  const int selfpos = s_self;
-  const int64_t orow = i - row0;
-  for (int e = tid; e < ktake; e += 256) {
-    int64_t j = (int64_t)(sel[e] & 0xFFFFFull);
-    if (e == selfpos) continue;
-    int64_t pos = e - ((selfpos >= 0 && e > selfpos) ? 1 : 0);
-    if (pos < k) {
-      idx[orow * k + pos] = (int32_t)j;
-      d2o[orow * k + pos] = (int64_t)(sel[e] >> 20);
-    }
+  if (tid == 0) topk_emit(src, sel, ktake, i, k, orow, idx, (typename decltype(src)::out_t *)d2o, cnto);
+}
+
+// ---- general-value k-NN (values that are not bf16-exact) -----------------
+// Panel of the MFMA path from int32 hundredths: K-blocked bf16 of
+// clip(zq[i][cols[c]], -qmax, qmax), GRID_MISSING -> 0 (find_neighbors.py:57-58).
+__global__ void k_panel_i32(const int32_t *__restrict__ zq, int64_t n, int64_t ld, const int32_t *__restrict__ cols,
+                            int64_t r, int32_t qmax, uint16_t *__restrict__ zb, int64_t np_, int64_t kpad) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = blockIdx.y;
+  if (c >= kpad) return;
+  int32_t v = 0;
+  if (i < n && c < r) {
+    v = zq[i * ld + cols[c]];
+    v = v == GRID_MISSING ? 0 : min(max(v, -qmax), qmax);        // np.clip order: max, then min
   }
-  {
-    int64_t c = ktake - (selfpos >= 0 ? 1 : 0);
-    c = c < k ? c : k;
-    for (int64_t e = c + tid; e < k; e += 256) {   // unused slots: idx -1, d2 0
-      idx[orow * k + e] = -1;
-      d2o[orow * k + e] = 0;
+  zb[(c >> 6) * np_ * 64 + i * 64 + (c & 63)] = (uint16_t)(__float_as_uint((float)v) >> 16);
+}
+// Column gather + clip into a dense [n][r] matrix for the direct-difference
+// kernels: int32 hundredths (exact path) or fp64 values clip(q/100, +-zmax)
+// (np.clip on float(text) values, :57; NaN -> 0, :58).
+__global__ void k_gather_i32(const int32_t *__restrict__ zq, int64_t n, int64_t ld, const int32_t *__restrict__ cols,
+                             int64_t r, int32_t qmax, int32_t *__restrict__ out) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = blockIdx.y;
+  if (c >= r) return;
+  const int32_t v = zq[i * ld + cols[c]];
+  out[i * r + c] = v == GRID_MISSING ? 0 : min(max(v, -qmax), qmax);
+}
+__global__ void k_gather_f64(const int32_t *__restrict__ zq, int64_t n, int64_t ld, const int32_t *__restrict__ cols,
+                             int64_t r, double zmax, double *__restrict__ out) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = blockIdx.y;
+  if (c >= r) return;
+  const int32_t v = zq[i * ld + cols[c]];
+  const double x = (double)v / 100.0;                           // float("%.2f" text)
+  const double lo = -zmax, y = x < lo ? lo : x;                  // np.clip: maximum(x, -zmax) ...
+  out[i * r + c] = v == GRID_MISSING ? 0.0 : (y > zmax ? zmax : y);   // ... then minimum(., zmax)
+}
+
+// d2[i][j] = sum_k (z_ik - z_jk)^2 for the upper 64-tiles (i-tile <= j-tile),
+// sequential over k: exact int64 for integer hundredths (stored as fp64, exact
+// below 2^53; the caller checks the bound), a fixed-order fp64 sum (no FMA
+// contraction: -ffp-contract=off) for general values.  64x64 tile per
+// 256-thread workgroup, 4x4 outputs per thread, 32-column K slabs in LDS.
+template <class T, class ACC>
+__global__ __launch_bounds__(256) void k_dist(const T *__restrict__ z, int64_t ld, int64_t n, int64_t r,
+                                              double *__restrict__ d2, int64_t np_, int64_t nb) {
+  __shared__ T As[32][64 + 1], Bs[32][64 + 1];
+  int64_t p = blockIdx.x, bi = 0;
+  while (p >= nb - bi) { p -= nb - bi; bi++; }
+  const int64_t bj = bi + p;
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  ACC acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; a++)
+#pragma unroll
+    for (int b = 0; b < 4; b++) acc[a][b] = 0;
+  for (int64_t k0 = 0; k0 < r; k0 += 32) {
+    // 64 rows x 32 columns per operand: thread loads 8 elements of each
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int e = tid + u * 256, row = e >> 5, kk = e & 31;
+      const int64_t ia = bi * 64 + row, ib = bj * 64 + row, kc = k0 + kk;
+      As[kk][row] = (ia < n && kc < r) ? z[ia * ld + kc] : (T)0;
+      Bs[kk][row] = (ib < n && kc < r) ? z[ib * ld + kc] : (T)0;
     }
-    if (tid == 0) cnto[orow] = (int32_t)c;
+    __syncthreads();
+#pragma unroll 4
+    for (int kk = 0; kk < 32; kk++) {
+      T av[4], bv[4];
+#pragma unroll
+      for (int a = 0; a < 4; a++) av[a] = As[kk][ty * 4 + a];
+#pragma unroll
+      for (int b = 0; b < 4; b++) bv[b] = Bs[kk][tx * 4 + b];
+#pragma unroll
+      for (int a = 0; a < 4; a++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          const ACC d = (ACC)av[a] - (ACC)bv[b];
+          acc[a][b] = acc[a][b] + d * d;
+        }
+    }
+    __syncthreads();
   }
+#pragma unroll
+  for (int a = 0; a < 4; a++)
+#pragma unroll
+    for (int b = 0; b < 4; b++)
+      d2[(bi * 64 + ty * 4 + a) * np_ + bj * 64 + tx * 4 + b] = (double)acc[a][b];
 }
 
 }  // namespace
@@ -841,19 +1089,25 @@ extern "C" {
 
 // Launch k_gram8 (persistent, XCD-paced): the tile table lives in ctx->aux.
 static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t nsteps, int64_t ld,
-                        int64_t q2, int64_t sps_max, bool blocked, int variant, int64_t *d_gram) {
+                        int64_t q2, int64_t sps_max, bool blocked, int mode, int64_t *d_gram) {
   const int nt = (int)(np_ / BM), ni = (int)(np_ / BM3);
   int nt6 = 0;
   for (int i = 0; i < ni; i++) nt6 += nt - 2 * i;
-  REQUIRE((size_t)nt6 * 4 <= GRID_AUX_BYTES / 2, "too many Gram tiles");
+  REQUIRE((size_t)nt6 * 4 <= GRID_AUX_BYTES / 2, "too many Gram tiles (np %lld)", (long long)np_);
   if (ctx->aux_tiles_n != nt6 || !ctx->aux_tiles_host) {
     delete[] ctx->aux_tiles_host;
     ctx->aux_tiles_host = new int32_t[nt6];
-    for (int t = 0; t < nt6; t++) {
-      int I = 0, tj = 0;
-      tile_blocked6(t, nt, ni, I, tj);
-      ctx->aux_tiles_host[t] = (I << 16) | tj;
+    // tile_blocked6 order, enumerated incrementally (one pass over the groups)
+    int t = 0;
+    for (int bi = 0; bi * GI6 < ni; bi++) {
+      const int i0 = bi * GI6, i1 = std::min(ni, i0 + GI6);
+      for (int bj = (2 * i0) / GJ6; bj * GJ6 < nt; bj++) {
+        const int j0 = bj * GJ6, j1 = std::min(nt, j0 + GJ6);
+        for (int i = i0; i < i1; i++)
+          for (int j = std::max(j0, 2 * i); j < j1; j++) ctx->aux_tiles_host[t++] = (i << 16) | j;
+      }
     }
+    REQUIRE(t == nt6, "tile enumeration");
     HIPCHK(hipMemcpyAsync(ctx->aux, ctx->aux_tiles_host, (size_t)nt6 * 4, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     ctx->aux_tiles_n = nt6;
@@ -861,38 +1115,77 @@ static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_
   unsigned *rounds = (unsigned *)((char *)ctx->aux + GRID_AUX_BYTES / 2);
   HIPCHK(hipMemsetAsync(rounds, 0, 8 * 16 * 4, ctx->stream));
   const int per = ctx->ncu >= 8 ? ctx->ncu / 8 : 1;
-  const int64_t xlen = ceil_div(nsteps, 8);   // longest XCD range
-  // chunks per XCD: each chunk <= sps_max steps; pick the count that wastes
-  // the fewest workgroup-rounds
-  const int64_t kcmin = ceil_div(xlen, sps_max);
-  int64_t kc = kcmin, best = -1;
-  for (int64_t c = kcmin; c < kcmin + 32; c++) {
-    const int64_t units = (int64_t)nt6 * c;
-    const int64_t waste = ceil_div(units, per) * per - units;
-    // waste fraction compared as waste/units (cross-multiplied)
-    if (best < 0 || waste * (nt6 * kc) < best * units) { best = waste; kc = c; }
+  const int64_t ngroups = ceil_div(nt6, per);
+  // (kx, kc): cost = the longest XCD's sequential K-steps per workgroup
+  // (rounds x steps per unit); the fewest K-ranges within 1 % of the best
+  // cost (fewer int64 flushes), then the chunk count that wastes least
+  int64_t bkx = 8, bkc = 1;
+  double bcost = -1.0;
+  for (int kx = 8; kx >= 1; kx >>= 1) {
+    const int gx = 8 / kx;
+    const int64_t xlen = ceil_div(nsteps, kx);
+    const int64_t kcmin = ceil_div(xlen, sps_max);
+    for (int64_t kc = kcmin; kc < kcmin + 32; kc++) {
+      int64_t worst = 0;
+      for (int xg = 0; xg < gx; xg++) {
+        const int64_t ngx = ngroups > xg ? (ngroups - xg + gx - 1) / gx : 0;
+        if (ngx == 0) continue;
+        const int64_t glast = xg + (ngx - 1) * gx;
+        const int64_t lastsz = std::min((int64_t)per, (int64_t)nt6 - glast * per);
+        const int64_t units = ((ngx - 1) * per + lastsz) * kc;
+        worst = std::max(worst, ceil_div(units, per));
+      }
+      const double cost = (double)worst * (double)ceil_div(xlen, kc);
+      if (bcost < 0 || cost < bcost * 0.99 || (kx < bkx && cost <= bcost * 1.01) ||
+          (kx == bkx && cost < bcost)) {
+        bcost = cost;
+        bkx = kx;
+        bkc = kc;
+      }
+    }
   }
+  // performance knobs only (results are exact for any value)
   const char *le = getenv("GRID_GRAM_LAG"), *se = getenv("GRID_GRAM_SPIN"), *ke = getenv("GRID_GRAM_KC");
+  const char *xe = getenv("GRID_GRAM_KX");
   const int lag = le ? atoi(le) : 1, spin = se ? atoi(se) : 20000;
-  if (ke) kc = atoi(ke) > kc ? atoi(ke) : kc;
+  if (xe && (atoi(xe) == 1 || atoi(xe) == 2 || atoi(xe) == 4 || atoi(xe) == 8)) {
+    bkx = atoi(xe);
+    bkc = ceil_div(ceil_div(nsteps, bkx), sps_max);
+  }
+  if (ke && atoi(ke) > bkc) bkc = atoi(ke);
+  REQUIRE(ceil_div(ceil_div(nsteps, bkx), bkc) <= sps_max, "Gram K chunk exceeds the int32-exact length");
   // fp32 chunks of 384 products while 384 qmax^2 <= 2^24 (qmax <= 209), else 192
   const int fl = 384 * q2 <= (1ll << 24) ? 1 : 2;
-  // variants: 21 production; 22 / 23 / 24 = probes MODE 5 / 6 / 1 (wrong results)
-  // (measured alternatives that lost: register-staged loads + ds_write_b128,
-  // 37.4 vs 31.1 ms; DMA issue spread over the sub-steps, no change)
-  const int mode = variant == 22 ? 5 : variant == 23 ? 6 : variant == 24 ? 1 : 0;
+#ifdef GRID_PROBES
 #define G8_PICK(BLV)                                                                            \
   (mode == 5 ? (fl == 1 ? k_gram8<5, BLV, 1> : k_gram8<5, BLV, 2>)                              \
    : mode == 6 ? (fl == 1 ? k_gram8<6, BLV, 1> : k_gram8<6, BLV, 2>)                            \
    : mode == 1 ? (fl == 1 ? k_gram8<1, BLV, 1> : k_gram8<1, BLV, 2>)                            \
    : (fl == 1 ? k_gram8<0, BLV, 1> : k_gram8<0, BLV, 2>))
+#else
+  (void)mode;
+#define G8_PICK(BLV) (fl == 1 ? k_gram8<0, BLV, 1> : k_gram8<0, BLV, 2>)
+#endif
   auto kern = blocked ? G8_PICK(true) : G8_PICK(false);
 #undef G8_PICK
   hipLaunchKernelGGL(kern, dim3((unsigned)(8 * per)), dim3(512), 0, ctx->stream, d_zb, ld,
-                     (const int32_t *)ctx->aux, nt6, (int)kc, nsteps, lag, spin, np_,
+                     (const int32_t *)ctx->aux, nt6, (int)bkc, (int)bkx, nsteps, lag, spin, np_,
                      (unsigned long long *)d_gram, rounds);
   LAUNCHCHK();
   return GRID_OK;
+}
+
+// Product builds run the production kernels only; the tools build
+// (make probes: -DGRID_PROBES, libgridhip_probes.so) maps GRID_GRAM_VARIANT to
+// the A/B kernels and the timing probes of tools/bench_gram.py (the probes
+// give wrong results by design).
+static int gram_variant() {
+#ifdef GRID_PROBES
+  const char *ve = getenv("GRID_GRAM_VARIANT");
+  return ve ? atoi(ve) : 21;
+#else
+  return 21;
+#endif
 }
 
 int grid_knn_gram(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t kpad, int64_t ld,
@@ -911,12 +1204,11 @@ int grid_knn_gram(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t kpad
   int64_t sps_max = ((1ll << 31) - 1) / (q2 * BK);
   const int nt = (int)(np_ / BM);
   const int ntiles = nt * (nt + 1) / 2;
-  // GRID_GRAM_VARIANT: A/B switch and timing probes for tools/bench_gram.py
-  // (21 = k_gram8, the default; 6 = k_gram6 grid; 2 / 4 = k_gram_dma)
-  const char *ve = getenv("GRID_GRAM_VARIANT");
-  const int variant = ve ? atoi(ve) : 21;
+  const int variant = gram_variant();
   if (variant >= 21 && np_ % BM3 == 0)
-    return launch_gram8(ctx, d_zb, np_, nsteps, ld, q2, sps_max, false, variant, d_gram);
+    return launch_gram8(ctx, d_zb, np_, nsteps, ld, q2, sps_max, false, variant == 22 ? 5 : variant == 23 ? 6
+                                                                                : variant == 24 ? 1 : 0, d_gram);
+#ifdef GRID_PROBES
   if (variant >= 6 && np_ % BM3 == 0) {
     // 256x128 tiles; 4-step fp32 chunks stay exact: 4 * 64 * qmax^2 < 2^24 for qmax <= 256
     const int ni = (int)(np_ / BM3);
@@ -935,8 +1227,12 @@ int grid_knn_gram(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t kpad
               : (variant == 18 && g6ok) ? k_gram6<6, 1, 2, 6> : k_gram6<0, 1, 2, 4>;
     hipLaunchKernelGGL(kern, dim3((unsigned)(nsl6 * nt6)), dim3(512), 0, ctx->stream, d_zb, ld, nt, ni, nt6,
                        nsteps, (int)sps6, np_, (unsigned long long *)d_gram);
-  } else {
-    // np % 256 != 0 (or variants 2 / 4): 128x128 tiles, one K-slice per workgroup
+    LAUNCHCHK();
+    return GRID_OK;
+  }
+#endif
+  {
+    // np % 256 != 0: 128x128 tiles, one K-slice per workgroup
     int64_t target_slices = ceil_div(2048, ntiles);
     int64_t sps = ceil_div(nsteps, target_slices);
     if (sps > sps_max) sps = sps_max;
@@ -961,26 +1257,145 @@ int grid_knn_gram_kb(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t k
   if (kpad == 0) return GRID_OK;
   const int64_t q2 = (int64_t)(qmax > 0 ? qmax : 1) * (qmax > 0 ? qmax : 1);
   const int64_t sps_max = ((1ll << 31) - 1) / (q2 * BK);
-  const char *ve = getenv("GRID_GRAM_VARIANT");
-  const int variant = (ve && atoi(ve) >= 21) ? atoi(ve) : 21;
-  return launch_gram8(ctx, d_zb, np_, kpad / BK, np_ * BK, q2, sps_max, true, variant, d_gram);
+  const int variant = gram_variant();
+  const int mode = variant == 22 ? 5 : variant == 23 ? 6 : variant == 24 ? 1 : 0;
+  return launch_gram8(ctx, d_zb, np_, kpad / BK, np_ * BK, q2, sps_max, true, mode, d_gram);
 }
 
+int grid_knn_mirror(grid_ctx *ctx, int64_t *d_gram, int64_t np_) {
+  REQUIRE(ctx && d_gram && np_ > 0 && np_ % 64 == 0, "np (%lld) must be a positive multiple of 64",
+          (long long)np_);
+  const int64_t nb = np_ / 64, pairs = nb * (nb - 1) / 2;
+  if (pairs == 0) return GRID_OK;
+  REQUIRE(pairs < (1ll << 31), "np too large");
+  hipLaunchKernelGGL(k_mirror, dim3((unsigned)pairs), dim3(256), 0, ctx->stream, d_gram, np_);
+  LAUNCHCHK();
+  return GRID_OK;
+}
 
-int grid_knn_topk(grid_ctx *ctx, const int64_t *d_gram, int64_t n, int64_t np_, int64_t k, int64_t row0,
-                  int64_t nrows, int32_t *d_idx, int64_t *d_d2, int32_t *d_cnt) {
-  REQUIRE(ctx && d_gram && n > 0 && np_ >= n && k >= 0, "bad args");
+int grid_knn_diag(grid_ctx *ctx, const int64_t *d_gram, int64_t np_, int64_t n, int64_t *d_norms) {
+  REQUIRE(ctx && d_gram && d_norms && n >= 0 && np_ >= n, "bad args");
+  if (n == 0) return GRID_OK;
+  hipLaunchKernelGGL(k_diag, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, ctx->stream, d_gram, np_, n, d_norms);
+  LAUNCHCHK();
+  return GRID_OK;
+}
+
+static int topk_checks(int64_t n, int64_t ld, int64_t k, int64_t row0, int64_t nrows) {
+  REQUIRE(n > 0 && ld >= n && k >= 0, "bad args");
   REQUIRE(n <= (1 << 20), "n > 2^20 samples not supported by the packed key");
   REQUIRE(k + 1 <= SELCAP, "num_neighbors + 1 must be <= %d", SELCAP);
   REQUIRE(row0 >= 0 && nrows >= 0 && row0 + nrows <= n, "bad row block");
+  REQUIRE(nrows < (1ll << 31), "too many rows");
+  return GRID_OK;
+}
+
+int grid_knn_topk_rows(grid_ctx *ctx, const int64_t *d_rows, int64_t ld, const int64_t *d_norms, int64_t n,
+                       int64_t k, int64_t row0, int64_t nrows, int32_t *d_idx, int64_t *d_d2, int32_t *d_cnt) {
+  REQUIRE(ctx && d_rows && d_norms, "bad args");
+  int rc = topk_checks(n, ld, k, row0, nrows);
+  if (rc) return rc;
   if (nrows == 0 || k == 0) {
     if (nrows) HIPCHK(hipMemsetAsync(d_cnt, 0, nrows * 4, ctx->stream));
     return GRID_OK;
   }
-  hipLaunchKernelGGL(k_topk, dim3((unsigned)nrows), dim3(256), 0, ctx->stream, d_gram, n, np_, k, row0, d_idx,
-                     d_d2, d_cnt);
+  const int64_t ktake = k + 1 < n ? k + 1 : n;
+  auto kern = ktake <= 16 ? k_topk_small<16, int64_t> : ktake <= 32 ? k_topk_small<32, int64_t>
+                                                                      : k_topk_radix<int64_t>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)nrows), dim3(256), 0, ctx->stream, d_rows, ld, d_norms, 1.0, n, k, row0,
+                     d_idx, (void *)d_d2, d_cnt);
   LAUNCHCHK();
   return GRID_OK;
+}
+
+int grid_knn_topk_d2(grid_ctx *ctx, const double *d_d2rows, int64_t ld, double key_scale, int64_t n, int64_t k,
+                     int64_t row0, int64_t nrows, int32_t *d_idx, double *d_d2, int32_t *d_cnt) {
+  REQUIRE(ctx && d_d2rows && key_scale > 0.0, "bad args");
+  int rc = topk_checks(n, ld, k, row0, nrows);
+  if (rc) return rc;
+  if (nrows == 0 || k == 0) {
+    if (nrows) HIPCHK(hipMemsetAsync(d_cnt, 0, nrows * 4, ctx->stream));
+    return GRID_OK;
+  }
+  const int64_t ktake = k + 1 < n ? k + 1 : n;
+  auto kern = ktake <= 16 ? k_topk_small<16, double> : ktake <= 32 ? k_topk_small<32, double>
+                                                                     : k_topk_radix<double>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)nrows), dim3(256), 0, ctx->stream, d_d2rows, ld,
+                     (const int64_t *)nullptr, key_scale, n, k, row0, d_idx, (void *)d_d2, d_cnt);
+  LAUNCHCHK();
+  return GRID_OK;
+}
+
+int grid_knn_panel_i32(grid_ctx *ctx, const int32_t *d_zq, int64_t n, int64_t ld, const int32_t *d_cols, int64_t r,
+                       int32_t qmax, uint16_t *d_zb, int64_t np_, int64_t kpad) {
+  REQUIRE(ctx && d_zq && d_zb && n >= 0 && r >= 0 && (r == 0 || d_cols), "bad args");
+  REQUIRE(np_ >= n && np_ % 64 == 0 && np_ <= 65535 && kpad >= r && kpad % 64 == 0, "bad panel shape");
+  REQUIRE(qmax >= 0 && qmax <= 256, "qmax must be in [0, 256] (bf16-exact)");
+  if (kpad == 0) return GRID_OK;
+  hipLaunchKernelGGL(k_panel_i32, dim3((unsigned)ceil_div(kpad, 256), (unsigned)np_), dim3(256), 0, ctx->stream,
+                     d_zq, n, ld, d_cols, r, qmax, d_zb, np_, kpad);
+  LAUNCHCHK();
+  return GRID_OK;
+}
+
+int grid_knn_gather_i32(grid_ctx *ctx, const int32_t *d_zq, int64_t n, int64_t ld, const int32_t *d_cols, int64_t r,
+                        int32_t qmax, int32_t *d_out) {
+  REQUIRE(ctx && d_zq && d_out && n >= 0 && n <= 65535 && r >= 0 && (r == 0 || d_cols) && qmax >= 0, "bad args");
+  if (n == 0 || r == 0) return GRID_OK;
+  hipLaunchKernelGGL(k_gather_i32, dim3((unsigned)ceil_div(r, 256), (unsigned)n), dim3(256), 0, ctx->stream, d_zq, n,
+                     ld, d_cols, r, qmax, d_out);
+  LAUNCHCHK();
+  return GRID_OK;
+}
+
+int grid_knn_gather_f64(grid_ctx *ctx, const int32_t *d_zq, int64_t n, int64_t ld, const int32_t *d_cols, int64_t r,
+                        double zmax, double *d_out) {
+  REQUIRE(ctx && d_zq && d_out && n >= 0 && n <= 65535 && r >= 0 && (r == 0 || d_cols), "bad args");
+  if (n == 0 || r == 0) return GRID_OK;
+  hipLaunchKernelGGL(k_gather_f64, dim3((unsigned)ceil_div(r, 256), (unsigned)n), dim3(256), 0, ctx->stream, d_zq, n,
+                     ld, d_cols, r, zmax, d_out);
+  LAUNCHCHK();
+  return GRID_OK;
+}
+
+static int dist_launch(grid_ctx *ctx, const void *d_z, bool is_int, int64_t n, int64_t r, int64_t ld, double *d_d2,
+                       int64_t np_) {
+  REQUIRE(ctx && d_z && d_d2 && n >= 0 && r >= 0 && ld >= r && np_ >= n && np_ % 64 == 0, "bad args");
+  const int64_t nb = np_ / 64, tiles = nb * (nb + 1) / 2;
+  if (tiles == 0) return GRID_OK;
+  REQUIRE(tiles < (1ll << 31), "np too large");
+  if (is_int)
+    hipLaunchKernelGGL((k_dist<int32_t, int64_t>), dim3((unsigned)tiles), dim3(256), 0, ctx->stream,
+                       (const int32_t *)d_z, ld, n, r, d_d2, np_, nb);
+  else
+    hipLaunchKernelGGL((k_dist<double, double>), dim3((unsigned)tiles), dim3(256), 0, ctx->stream,
+                       (const double *)d_z, ld, n, r, d_d2, np_, nb);
+  LAUNCHCHK();
+  return grid_knn_mirror(ctx, (int64_t *)d_d2, np_);
+}
+
+int grid_knn_dist_i32(grid_ctx *ctx, const int32_t *d_z, int64_t n, int64_t r, int64_t ld, double *d_d2,
+                      int64_t np_) {
+  return dist_launch(ctx, d_z, true, n, r, ld, d_d2, np_);
+}
+
+int grid_knn_dist_f64(grid_ctx *ctx, const double *d_z, int64_t n, int64_t r, int64_t ld, double *d_d2,
+                      int64_t np_) {
+  return dist_launch(ctx, d_z, false, n, r, ld, d_d2, np_);
+}
+
+int grid_knn_topk(grid_ctx *ctx, int64_t *d_gram, int64_t n, int64_t np_, int64_t k, int64_t row0,
+                  int64_t nrows, int32_t *d_idx, int64_t *d_d2, int32_t *d_cnt) {
+  REQUIRE(ctx && d_gram && n > 0 && np_ >= n && np_ % 64 == 0 && k >= 0, "bad args");
+  int rc = grid_knn_mirror(ctx, d_gram, np_);
+  if (rc) return rc;
+  void *s = nullptr;
+  rc = grid_scratch(ctx, (size_t)n * 8, &s);
+  if (rc) return rc;
+  int64_t *nrm = (int64_t *)s;
+  rc = grid_knn_diag(ctx, d_gram, np_, n, nrm);
+  if (rc) return rc;
+  return grid_knn_topk_rows(ctx, d_gram + row0 * np_, np_, nrm, n, k, row0, nrows, d_idx, d_d2, d_cnt);
 }
 
 }  // extern "C"

@@ -902,6 +902,62 @@ __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, 
   if (of) atomicOr(overflow, of);
 }
 
+// Independent check of the step-4 output and the step-5 panel (tests): every
+// selected cell recomputed with plain IEEE fp64 operations in the reference's
+// order -- x = q/100 (float("%.2f" text)), y = x/rowmean, z = ((y - mu) /
+// sqrt(mu)) * scale (normalize_mosdepth.py:440-470) -- quantised with the
+// "%.2f" rule (round_dec_k, "-0.00"), and compared with the int16 code and
+// the K-blocked bf16 panel entry.  Missing cells and rows with a zero/NaN
+// mean are counted as skipped (their codes are fixed sentinels).
+// cnt: [0] z-code mismatches, [1] panel mismatches, [2] skipped cells.
+__global__ __launch_bounds__(256) void k_zverify(const int32_t *__restrict__ q, int64_t ld,
+                                                 const int32_t *__restrict__ sel, int64_t r,
+                                                 const double *__restrict__ rm, const double *__restrict__ mu,
+                                                 double scale, const int16_t *__restrict__ zq16, int64_t ld_zq,
+                                                 const int32_t *__restrict__ colmap, int32_t qmax,
+                                                 const uint16_t *__restrict__ zb, int64_t np_zb,
+                                                 unsigned long long *__restrict__ cnt) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = blockIdx.y;
+  unsigned long long bad_z = 0, bad_b = 0, skip = 0;
+  if (s < r) {
+    const int64_t j = sel[s];
+    const int32_t v = q[i * ld + j];
+    const double rmi = rm[i], m = mu[j];
+    if (v == GRID_MISSING || !(rmi != 0.0 && rmi == rmi) || !(m > 0.0)) {
+      skip = 1;
+    } else {
+      const double x = (double)v / 100.0;
+      const double y = x / rmi;
+      const double z = ((y - m) / sqrt(m)) * scale;
+      const double kd = round_dec_k(z, 100.0);
+      const int32_t o = (int32_t)kd;
+      int32_t code;
+      if (o == 0 && signbit(z)) code = GRID_ZQ16_NEG0;
+      else if (o < GRID_ZQ16_MIN || o > GRID_ZQ16_MAX) code = GRID_ZQ16_ESC;
+      else code = o;
+      bad_z = zq16[i * ld_zq + s] != (int16_t)code;
+      const int32_t c = colmap ? colmap[s] : (int32_t)s;
+      if (zb && c >= 0) {
+        const int32_t w = o > qmax ? qmax : (o < -qmax ? -qmax : o);
+        const uint16_t want = (uint16_t)(__float_as_uint((float)w) >> 16);
+        bad_b = zb[(int64_t)(c >> 6) * np_zb * 64 + i * 64 + (c & 63)] != want;
+      }
+    }
+  }
+  // one atomic per wave and counter
+  for (int o = 32; o > 0; o >>= 1) {
+    bad_z += __shfl_xor(bad_z, o, 64);
+    bad_b += __shfl_xor(bad_b, o, 64);
+    skip += __shfl_xor(skip, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (bad_z) atomicAdd(cnt + 0, bad_z);
+    if (bad_b) atomicAdd(cnt + 1, bad_b);
+    if (skip) atomicAdd(cnt + 2, skip);
+  }
+}
+
 // Full fp64 z matrix (normalize_matrix's returned array, :458 and :470):
 // transformed where mu > 0, x/rm*scale elsewhere, NaN for missing cells.
 __global__ __launch_bounds__(256) void k_zfull(const int32_t *__restrict__ q, int64_t n, int64_t m, int64_t ld,
@@ -923,6 +979,28 @@ __global__ __launch_bounds__(256) void k_zfull(const int32_t *__restrict__ q, in
 }  // namespace
 
 extern "C" {
+
+int grid_verify_zquant(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t ld, const int32_t *d_sel, int64_t r,
+                       const double *d_rm, const double *d_mu, double scale, const int16_t *d_zq16, int64_t ld_zq,
+                       const int32_t *d_colmap, int32_t qmax, const uint16_t *d_zb, int64_t np_zb,
+                       int64_t *h_counts) {
+  REQUIRE(ctx && d_q && d_sel && d_rm && d_mu && d_zq16 && h_counts && n >= 0 && n <= 65535 && r >= 0, "bad args");
+  REQUIRE(!d_zb || (np_zb >= n && np_zb % 64 == 0), "bad panel");
+  void *sc = nullptr;
+  int rc = grid_scratch(ctx, 64, &sc);
+  if (rc) return rc;
+  HIPCHK(hipMemsetAsync(sc, 0, 24, ctx->stream));
+  if (n > 0 && r > 0) {
+    hipLaunchKernelGGL(k_zverify, dim3((unsigned)ceil_div(r, 256), (unsigned)n), dim3(256), 0, ctx->stream, d_q, ld,
+                       d_sel, r, d_rm, d_mu, scale, d_zq16, ld_zq, d_colmap, qmax, d_zb, np_zb,
+                       (unsigned long long *)sc);
+    LAUNCHCHK();
+  }
+  HIPCHK(hipMemcpyAsync(ctx->pinned, sc, 24, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  for (int k = 0; k < 3; k++) h_counts[k] = (int64_t)((unsigned long long *)ctx->pinned)[k];
+  return GRID_OK;
+}
 
 int grid_norm_zfull(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t m, int64_t ld, const double *d_rm,
                     const double *d_mu, double scale, double *d_z) {
@@ -1013,9 +1091,15 @@ static int col_stats_impl(grid_ctx *ctx, bool vars, const int32_t *d_q, const Q1
   if (rc) return rc;
   // int32: 1 column per thread (47 k waves at the bench shape, ~6 rounds of
   // resident waves; 4 per thread left a 2.3-round tail: 14.5 vs 13.7 ms)
+#ifdef GRID_PROBES
+  // tools build only: column-width / workgroup-shape alternatives (A/B)
   const char *cv = getenv("GRID_COL_VW"), *cu = getenv("GRID_COL_CU");
   const int want = cv ? atoi(cv) : 1;
   const bool cu16 = cu && atoi(cu) == 16;
+#else
+  const int want = 1;
+  const bool cu16 = false;
+#endif
   const char *cn = getenv("GRID_COL_NT");   // streaming (nontemporal) loads, 1-column path (A/B)
   const bool nt = cn ? atoi(cn) != 0 : COL_NT;
   const int vw = s16.q ? 4 : vec4_ok(d_q, ld) ? (want == 4 ? 4 : want == 1 ? 1 : 2) : 1;
@@ -1088,7 +1172,11 @@ static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, int64_
   hipLaunchKernelGGL(k_zprep, dim3((unsigned)ceil_div(r, 256)), dim3(256), 0, ctx->stream, d_sel, r, d_mu, scale, mus,
                      sq, rsq, mc32);
   LAUNCHCHK();
-  const char *zv = getenv("GRID_ZQUANT_VARIANT");   // 4 = the selected-column kernel (A/B)
+#ifdef GRID_PROBES
+  const char *zv = getenv("GRID_ZQUANT_VARIANT");   // tools build: 4 = the selected-column kernel (A/B)
+#else
+  const char *zv = nullptr;
+#endif
   REQUIRE(!d_zq16 || (!s16.q && vec4_ok(d_q, ld)), "int16 z output needs the int32 depth layout (ld % 4 == 0)");
   if (d_zq16 || (!s16.q && vec4_ok(d_q, ld) && !(zv && atoi(zv) == 4))) {
     int32_t *sidx = (int32_t *)(rest + 4 * rb);

@@ -136,12 +136,16 @@ def sigma2_min(dev: Device, r3: DevBuf, r: int, frac_r: float):
 
 
 def knn(dev: Device, zb: DevBuf, n: int, np_: int, kpad: int, ld: int, qmax: int, k: int,
-        r_use: int):
-    """Exact k-NN on the bf16 hundredths panel: returns (idx, d2, cnt) numpy."""
+        r_use: int, kblocked: bool = False):
+    """Exact k-NN on a bf16 hundredths panel (row-major [np][ld], or
+    K-blocked [kpad/64][np][64]): returns (idx, d2 hundredths^2, cnt) numpy."""
     if 4 * qmax * qmax * max(r_use, 1) >= 2 ** 44:
         raise GridNativeError("R_use too large for the packed distance key")
     gram = dev.zeros((np_, np_), I8)
-    call("grid_knn_gram", dev.ctx, zb.ptr, np_, kpad, ld, qmax, gram.ptr)
+    if kblocked:
+        call("grid_knn_gram_kb", dev.ctx, zb.ptr, np_, kpad, qmax, gram.ptr)
+    else:
+        call("grid_knn_gram", dev.ctx, zb.ptr, np_, kpad, ld, qmax, gram.ptr)
     kk = max(k, 1)
     idx, d2, cnt = dev.alloc((n, kk), I4), dev.alloc((n, kk), I8), dev.alloc(n, I4)
     call("grid_knn_topk", dev.ctx, gram.ptr, n, np_, k, 0, n, idx.ptr, d2.ptr, cnt.ptr)
@@ -149,17 +153,104 @@ def knn(dev: Device, zb: DevBuf, n: int, np_: int, kpad: int, ld: int, qmax: int
 
 
 def knn_from_hundredths(dev: Device, zq: np.ndarray, k: int, qmax: int):
-    """Host (n x R_use) int hundredths, already clipped, NaN -> 0."""
-    n, r = zq.shape
+    """Host (n x R_use) int hundredths, already clipped to +-qmax, NaN -> 0:
+    (idx, exact d2 in hundredths^2, cnt)."""
+    zq = np.ascontiguousarray(zq, dtype=np.int32)
+    return _knn_zq(dev, zq, np.arange(zq.shape[1], dtype=np.int32), k, qmax / 100.0, False)
+
+
+def _dist_key_scale(bound: float) -> float:
+    """Power-of-two key scale so floor(d2 * scale) < 2^44 (1 while exact
+    integer distances fit: they then stay exact)."""
+    if bound < 2.0 ** 44:
+        return 1.0
+    return math.ldexp(1.0, 43 - math.frexp(bound)[1])
+
+
+def _knn_zq(dev: Device, zq: np.ndarray, cols: np.ndarray, k: int, zmax: float, values: bool):
+    """Step 5 on integer hundredths zq [n][ld] (GRID_MISSING = NaN) restricted
+    to columns ``cols``, clipped to +-zmax (find_neighbors.py:57-58).  Path:
+      * zmax = q/100, q <= 256: bf16-exact MFMA Gram (k_gram8) + row top-k;
+      * zmax = q/100, q > 256: exact int64 direct-difference distances;
+      * otherwise (clips are not hundredths): fixed-order fp64 distances.
+    Returns (idx, d2, cnt); d2 is float64 in value^2 units when ``values``,
+    else int64 hundredths^2 (integer paths only)."""
+    zq = np.ascontiguousarray(zq, dtype=np.int32)
+    n, ld = zq.shape
+    r = len(cols)
+    kk = max(k, 1)
     if n == 0:
-        return np.zeros((0, max(k, 1)), I4), np.zeros((0, max(k, 1)), I8), np.zeros(0, I4)
-    np_ = pad_to(max(n, 1), 256)
-    kpad = pad_to(max(r, 1), 64)
-    zf = np.zeros((np_, kpad), dtype=np.float32)
-    zf[:n, :r] = zq
-    zbits = (zf.view(np.uint32) >> 16).astype(np.uint16)     # exact for |v| <= 256
-    zb = dev.upload(zbits)
-    return knn(dev, zb, n, np_, kpad, kpad, qmax, k, r)
+        return np.zeros((0, kk), I4), np.zeros((0, kk), F8 if values else I8), np.zeros(0, I4)
+    q = int(round(zmax * 100))
+    hundredths = q / 100.0 == zmax and 0 <= q < 2 ** 30
+    dz = dev.upload(zq)
+    dcols = dev.upload(np.ascontiguousarray(cols if r else np.zeros(1), dtype=I4))
+    np_ = pad_to(n, 256)
+    if hundredths and q <= 256:
+        kpad = pad_to(max(r, 1), 64)
+        zb = dev.alloc((kpad // 64, np_, 64), U2)
+        call("grid_knn_panel_i32", dev.ctx, dz.ptr, n, ld, dcols.ptr, r, q, zb.ptr, np_, kpad)
+        del dz
+        idx, d2, cnt = knn(dev, zb, n, np_, kpad, kpad, q, k, r, kblocked=True)
+        return idx, (d2 / 10000.0 if values else d2), cnt
+    d2m = dev.alloc((np_, np_), F8)
+    if hundredths:
+        if 4.0 * q * q * max(r, 1) >= 2.0 ** 53:
+            raise GridNativeError("zmax too large for exact int64 distances stored as fp64")
+        g = dev.alloc((n, max(r, 1)), I4)
+        call("grid_knn_gather_i32", dev.ctx, dz.ptr, n, ld, dcols.ptr, r, q, g.ptr)
+        del dz
+        call("grid_knn_dist_i32", dev.ctx, g.ptr, n, r, max(r, 1), d2m.ptr, np_)
+        scale = _dist_key_scale(4.0 * q * q * max(r, 1))
+        unit = 10000.0
+    else:
+        g = dev.alloc((n, max(r, 1)), F8)
+        call("grid_knn_gather_f64", dev.ctx, dz.ptr, n, ld, dcols.ptr, r, float(zmax), g.ptr)
+        del dz
+        call("grid_knn_dist_f64", dev.ctx, g.ptr, n, r, max(r, 1), d2m.ptr, np_)
+        scale = _dist_key_scale(4.0 * zmax * zmax * max(r, 1) + 1.0)
+        unit = 1.0
+    del g
+    idx, d2, cnt = dev.alloc((n, kk), I4), dev.alloc((n, kk), F8), dev.alloc(n, I4)
+    call("grid_knn_topk_d2", dev.ctx, d2m.ptr, np_, scale, n, k, 0, n, idx.ptr, d2.ptr, cnt.ptr)
+    d2h = d2.numpy()
+    if values:
+        return idx.numpy(), d2h / unit, cnt.numpy()
+    if unit != 10000.0:
+        raise GridNativeError("integer distances requested from the fp64 path")
+    return idx.numpy(), d2h.astype(I8), cnt.numpy()
+
+
+def knn_from_zq(dev: Device, zq: np.ndarray, cols: np.ndarray, k: int, zmax: float):
+    """find_neighbors.py:57-65 + find_neighbors_sklearn on the step-4
+    hundredths: (idx, squared distances in value^2 units, cnt)."""
+    return _knn_zq(dev, zq, cols, k, zmax, True)
+
+
+def knn_values(dev: Device, data: np.ndarray, k: int):
+    """find_neighbors_sklearn (:179-227) on an arbitrary float64 matrix (already
+    clipped / NaN-free): exact integer paths when every value is a hundredth,
+    the fp64 direct-difference path otherwise.  (idx, d2 values, cnt)."""
+    data = np.ascontiguousarray(data, dtype=F8)
+    n, r = data.shape
+    kk = max(k, 1)
+    if n == 0:
+        return np.zeros((0, kk), I4), np.zeros((0, kk), F8), np.zeros(0, I4)
+    if not np.all(np.isfinite(data)):
+        raise GridNativeError("find_neighbors_sklearn: NaN/inf in the data matrix (sklearn rejects it too)")
+    qv = np.rint(data * 100.0)
+    if np.array_equal(qv / 100.0, data) and (qv.size == 0 or np.abs(qv).max() < 2 ** 30):
+        qmax = int(np.abs(qv).max()) if qv.size else 0
+        return _knn_zq(dev, qv.astype(np.int32), np.arange(r, dtype=np.int32), k, qmax / 100.0, True)
+    np_ = pad_to(n, 256)
+    dz = dev.upload(data)
+    d2m = dev.alloc((np_, np_), F8)
+    call("grid_knn_dist_f64", dev.ctx, dz.ptr, n, r, r, d2m.ptr, np_)
+    m = float(np.abs(data).max()) if data.size else 0.0
+    scale = _dist_key_scale(4.0 * m * m * max(r, 1) + 1.0)
+    idx, d2, cnt = dev.alloc((n, kk), I4), dev.alloc((n, kk), F8), dev.alloc(n, I4)
+    call("grid_knn_topk_d2", dev.ctx, d2m.ptr, np_, scale, n, k, 0, n, idx.ptr, d2.ptr, cnt.ptr)
+    return idx.numpy(), d2.numpy(), cnt.numpy()
 
 
 # ------------------------------------------------------------------ step 6 --
@@ -190,14 +281,10 @@ def csr_from_lists(hap_nbrs):
     return off, nbr, w
 
 
-def _legacy_flag() -> int:
-    """GRID_PHASE_LEGACY=1 selects the previous phasing kernel (A/B tests)."""
-    import os
-    return _abi.HI_LEGACY if os.environ.get("GRID_PHASE_LEGACY") == "1" else 0
-
-
 def phase(dev: Device, irr: np.ndarray, off: np.ndarray, nbr: np.ndarray, w: np.ndarray, min_nbr: int,
-          n_iters: int):
+          n_iters: int, legacy: bool = False):
+    """``legacy`` selects the per-neighbour LDS kernel (k_phase) that larger
+    loci run anyway (A/B tests; same results)."""
     n = len(irr)
     if n == 0:
         return np.zeros(0), np.zeros(0), 0.0
@@ -209,11 +296,11 @@ def phase(dev: Device, irr: np.ndarray, off: np.ndarray, nbr: np.ndarray, w: np.
     hap, imp, mean = dev.alloc(2 * n, F8), dev.alloc(2 * n, F8), dev.alloc(1, F8)
     call("grid_hi_phase", dev.ctx, n, bufs[0].ptr, bufs[1].ptr, bufs[2].ptr, bufs[3].ptr, min_nbr, n_iters,
          bufs[4].ptr, bufs[5].ptr, nl, bufs[6].ptr, bufs[7].ptr, bufs[8].ptr, hap.ptr, imp.ptr, mean.ptr,
-         flags | _legacy_flag(), max_list)
+         flags | (_abi.HI_LEGACY if legacy else 0), max_list)
     return hap.numpy(), imp.numpy(), float(mean.numpy()[0])
 
 
-def phase_batch(dev: Device, loci, min_nbr: int, n_iters: int):
+def phase_batch(dev: Device, loci, min_nbr: int, n_iters: int, legacy: bool = False):
     """Batched phasing + imputation of L independent loci in one launch (one
     workgroup per locus; BASELINE config 5).  ``loci``: sequence of
     (irr [n], off [2n+1], nbr, w) per locus (CSR as csr_from_lists).  Returns
@@ -223,7 +310,7 @@ def phase_batch(dev: Device, loci, min_nbr: int, n_iters: int):
     from concurrent.futures import ThreadPoolExecutor
     descs, keep, outs = [], [], []
     flags_all, max_list, max_n, max_nlev = _abi.HI_UNIT_WEIGHTS, 0, 0, 0
-    legacy = _legacy_flag()
+    legacy = _abi.HI_LEGACY if legacy else 0
     # per-locus schedules in parallel (the C++ schedule / pack calls release the GIL)
     with ThreadPoolExecutor(max(1, min(16, os.cpu_count() or 1))) as ex:
         full = list(ex.map(lambda l: _abi.hi_schedule(l[1], l[2], l[3], packed_w=bool(legacy)), loci))

@@ -1,10 +1,21 @@
 """Device-resident chain of steps 4-7 with preallocated HBM buffers.
 
 Same arithmetic as the drop-in step modules, without the text files in
-between: the normalised matrix stays in HBM as exact hundredths (int32, the
-step-4 output) plus the clipped bf16 panel that step 5 reads, the neighbour
-lists feed the dipCN kernel directly, and the dipCN values feed phasing.
-``bench.py`` and ``__graft_entry__.smoke()`` drive it.
+between: the normalised matrix stays in HBM as exact hundredths (int16 codes,
+the step-4 output) plus the clipped bf16 panel that step 5 reads, the
+neighbour lists feed the dipCN kernel directly, and the dipCN values feed
+phasing.  ``bench.py`` and ``__graft_entry__.smoke()`` drive it.
+
+Bin-axis streaming (BASELINE configs 3-4: a 50k x 3M int32 depth matrix is
+600 GB, more than one GPU's 288 GB): a rank's columns are processed in
+8192-aligned CHUNKS in three passes over the depth source -- (A) row-block
+partial sums, (B) column means / variances (after the row means), (D) z
+quantisation + the exact Gram of the chunk's panel, accumulated in int64
+across chunks (integer sums: any order is exact).  The global median /
+selection threshold / sigma2 bound (C) sit between B and D.  Every statistic
+is the one-chunk value bit for bit: row sums keep NumPy's 8192-block order,
+column statistics are per column.  The source is a resident matrix, a host
+array, or the synthetic generator (``SynthSource``: regenerated per pass).
 
 Multi-GPU: the bin (column) axis is sharded in 8192-aligned ranges
 (``shard_range``), strong scaling of one cohort.  Exactness across shards:
@@ -14,14 +25,16 @@ Multi-GPU: the bin (column) axis is sharded in 8192-aligned ranges
   * column statistics need no communication (sequential over all rows,
     locally); the median and the selection threshold come from all-gathered
     ratio vectors, sorted identically on every rank;
-  * the Gram matrix is an integer sum over bins: per-rank partials are
-    combined with ONE all-reduce (int64 sum: order-free, exact);
-  * top-k by row blocks, then an all-gather of the neighbour lists; dipCN and
-    phasing are replicated (tiny / sequential per locus).
+  * the Gram matrix is an integer sum over bins: each rank mirrors its
+    partial Gram to full rows and ONE reduce-scatter (int64 sum: order-free,
+    exact) leaves rank r the complete rows [r*np/W, (r+1)*np/W); the norms
+    G_jj come from an all-reduce of the partial diagonals (n int64);
+  * top-k on the rank's rows, then an all-gather of the neighbour lists;
+    dipCN and phasing are replicated (tiny / sequential per locus).
 
 The chain is written against an ``ops`` object.  The product always uses
 ``HipOps`` (libgridhip.so kernels); tests substitute a CPU restatement to
-check the sharding logic under torch.distributed/gloo.
+check the chunking and sharding logic under torch.distributed/gloo.
 """
 from __future__ import annotations
 
@@ -125,6 +138,16 @@ class TorchComm:
         self.dist.all_reduce(t)
         return t
 
+    def reduce_scatter_sum(self, out, t):
+        """out (rank's block) = sum over ranks of t's rank-th equal block."""
+        if self.host and t.is_cuda:
+            h = out.cpu()
+            self.dist.reduce_scatter_tensor(h, t.contiguous().cpu())
+            out.copy_(h)
+            return out
+        self.dist.reduce_scatter_tensor(out, t.contiguous())
+        return out
+
 
 class HipOps:
     """The chain's compute steps as libgridhip.so kernels (include/grid_abi.h)."""
@@ -203,8 +226,18 @@ class HipOps:
         """Exact Gram of the K-blocked panel (first kpad columns)."""
         call("grid_knn_gram_kb", self.ctx, ptr(zb), np_, kpad, qmax, ptr(gram))
 
-    def topk(self, gram, n, np_, k, row0, nrows, idx, d2, cnt):
-        call("grid_knn_topk", self.ctx, ptr(gram), n, np_, k, row0, nrows, ptr(idx), ptr(d2), ptr(cnt))
+    def mirror(self, gram, np_):
+        call("grid_knn_mirror", self.ctx, ptr(gram), np_)
+
+    def diag(self, gram, np_, n, norms):
+        call("grid_knn_diag", self.ctx, ptr(gram), np_, n, ptr(norms))
+
+    def topk_rows(self, rows, ld, norms, n, k, row0, nrows, idx, d2, cnt):
+        call("grid_knn_topk_rows", self.ctx, ptr(rows), ld, ptr(norms), n, k, row0, nrows, ptr(idx), ptr(d2),
+             ptr(cnt))
+
+    def synth(self, seed, n, m, ld, col0, ncl, out):
+        call("grid_synth_depth", self.ctx, seed, n, m, ld, col0, ncl, ptr(out))
 
     def dipcn(self, n, reads, has, scale, nbr, nscale, ncnt, ld, n_nbr, out, valid):
         call("grid_dipcn", self.ctx, n, ptr(reads), ptr(has), ptr(scale), ptr(nbr), ptr(nscale), ptr(ncnt), ld,
@@ -220,16 +253,61 @@ class HipOps:
         return _abi.hi_schedule(off, nbr, w)
 
 
+class SynthSource:
+    """Depth source: the bench cohort (csrc/synth_model.hpp) regenerated on
+    the device for every pass over a chunk -- the stand-in for data arriving
+    in HBM when the matrix does not fit (BASELINE configs 3-4).  Local column
+    c of the rank is global bin col0 + c."""
+
+    def __init__(self, ops, seed, n, col0, ncl):
+        self.ops, self.seed, self.n, self.col0, self.ncl = ops, seed, n, col0, ncl
+
+    def fill(self, a, b, out, ldo):
+        self.ops.synth(self.seed, self.n, b - a, ldo, self.col0 + a, self.ncl, out)
+
+
+class HostSource:
+    """Depth source: an int32 hundredths matrix in host memory, copied to the
+    device one column slab per chunk (pinned staging, H2D)."""
+
+    def __init__(self, q):
+        self.q = q
+
+    def fill(self, a, b, out, ldo):
+        import torch
+        w = b - a
+        slab = torch.from_numpy(np.ascontiguousarray(self.q[:, a:b]))
+        dst = out.view(-1)[: self.q.shape[0] * ldo].view(self.q.shape[0], ldo)
+        dst[:, :w].copy_(slab.pin_memory() if dst.is_cuda else slab, non_blocking=False)
+
+
+def chunk_ranges(m_local: int, chunk: int | None):
+    """Local column ranges [a, b) of the passes: whole 8192-blocks per chunk."""
+    if not chunk or chunk >= m_local:
+        return [(0, m_local)]
+    assert chunk % BLOCK == 0, "chunk must be a multiple of 8192 columns"
+    return [(a, min(a + chunk, m_local)) for a in range(0, m_local, chunk)]
+
+
 class Steps47:
     """One rank's share of the steps 4-7 chain for an n x m cohort.
 
-    Inputs: q [n][ld] int32 hundredths of this rank's columns (global offset
-    col0, a multiple of 8192), reads [n] f64 for every sample, and the IBS
-    hap-neighbour CSR of the cohort (its GS level schedule is derived once).
+    Inputs: the depth matrix of this rank's columns (global offset col0, a
+    multiple of 8192) -- resident [n][ld] int32 hundredths, a Depth16, or a
+    source with ``fill(a, b, out, ld)`` (``SynthSource``, ``HostSource``) --
+    reads [n] f64 for every sample, and the IBS hap-neighbour CSR of the
+    cohort (its GS level schedule is derived once).
+
+    ``chunk``: columns per pass chunk (a multiple of 8192; None = the whole
+    range in one chunk).  ``keep_z``: keep the whole step-4 output in HBM
+    (``zq_int32()``); False writes each chunk's z into a chunk buffer that is
+    overwritten by the next chunk (the fused mode of configs 3-4, SURVEY H7;
+    ``on_z_chunk(zq16, ld, s0, s1, esc_idx, esc_val)`` may consume it).
     """
 
     def __init__(self, ops, alloc, n, m_total, col0, m_local, *, k=10, n_nbr=300, top_frac=0.1, zmax=2.0,
-                 sigma2_max=1000.0, frac_r=1.0, min_nbr=1, n_iters=100, comm=None, phase_lane=None, zq16=True):
+                 sigma2_max=1000.0, frac_r=1.0, min_nbr=1, n_iters=100, comm=None, phase_lane=None, zq16=True,
+                 chunk=None, keep_z=True, on_z_chunk=None):
         """``phase_lane``: optional (ops, torch.cuda.Stream) pair on which step
         7 runs, ordered after this pass's dipCN by an event; the next pass's
         dipCN waits for it.  Phasing is one workgroup for ~6 ms, so on its own
@@ -246,6 +324,9 @@ class Steps47:
         self.sigma2_max, self.frac_r = sigma2_max, frac_r
         self.min_nbr, self.n_iters = min_nbr, n_iters
         self.qmax = qmax_for_zmax(zmax)
+        self.chunks = chunk_ranges(m_local, chunk)
+        self.nch = len(self.chunks)
+        self.keep_z, self.on_z_chunk = keep_z or self.nch == 1, on_z_chunk
         a = alloc
         n1 = max(n, 1)
         widths = [shard_range(m_total, r, self.world) for r in range(self.world)]
@@ -254,6 +335,14 @@ class Steps47:
         self.nblk_max = -(-self.mlmax // BLOCK)
         self.bsum = a.empty((n1, max(self.nblk_l, 1)), F8)
         self.bcnt = a.empty((n1, max(self.nblk_l, 1)), I4)
+        cw = max(b - a_ for a_, b in self.chunks)             # widest chunk
+        if self.nch > 1:
+            nbc = -(-cw // BLOCK)
+            self.bsum_c, self.bcnt_c = a.empty(n1 * nbc, F8), a.empty(n1 * nbc, I4)
+        # chunk buffer of the depth matrix (streamed / chunked sources), ld % 4 == 0
+        self.ldc = pad_to(max(cw, 1), 4)
+        self.qc = None
+        self.qc_holds = None                                  # chunk index the buffer holds
         if self.world > 1:
             self.bsum_pad = a.empty((n1, max(self.nblk_max, 1)), F8)
             self.bcnt_pad = a.empty((n1, max(self.nblk_max, 1)), I4)
@@ -268,21 +357,27 @@ class Steps47:
         # step-4 output, exact hundredths: int16 codes (GRID_ZQ16_*, half the
         # HBM writes) when the ops support them, int32 otherwise or when a
         # pass has |z| > 327.66 (zq_int32() gives the int32 form either way)
-        self.zq16 = a.empty((n1, ml1), U2) if zq16 and hasattr(ops, "zquant16") else None
-        self.zq = None if self.zq16 is not None else a.empty((n1, ml1), I4)
+        zw = ml1 if self.keep_z else cw
+        self.zq16 = a.empty((n1, zw), U2) if zq16 and hasattr(ops, "zquant16") else None
+        self.zq = None if self.zq16 is not None else a.empty((n1, zw), I4)
         self.zq_is16, self.nesc = False, 0
         if self.zq16 is not None:                        # escapes: |z| > 327.65 (rare)
-            cap = min(n1 * ml1, max(1 << 20, (n1 * ml1) >> 12))
+            cap = min(n1 * zw, max(1 << 20, (n1 * zw) >> 10))
             self.esc_idx, self.esc_val = a.empty(cap, I8), a.empty(cap, I4)
         self.np_ = pad_to(n1, 256)
-        self.kpad = pad_to(ml1, 64)
+        self.np_rs = pad_to(self.np_, self.world)         # Gram rows: equal blocks for the reduce-scatter
+        self.kpad = pad_to(cw, 64)
         # step-5 input panel (bf16), K-blocked [kpad/64][np][64]: one K-step of a
         # row panel is contiguous for the Gram kernel's DMA
         self.zb = a.empty((self.kpad // 64, self.np_, 64), U2)
         self.zb.zero_()                                  # pad rows stay zero
-        self.gram = a.empty((self.np_, self.np_), I8)
+        self.gram = a.empty((self.np_rs, self.np_), I8)   # row stride np; rows >= np stay zero
+        self.norms = a.empty(self.np_, I8)
+        self.norms.zero_()
         kk = max(k, 1)
-        self.rows_per = -(-n // self.world)
+        self.rows_per = self.np_rs // self.world
+        if self.world > 1:
+            self.grow = a.empty((self.rows_per, self.np_), I8)
         self.idx_l = a.empty((self.rows_per, kk), I4)
         self.d2_l = a.empty((self.rows_per, kk), I8)
         self.cnt_l = a.empty(self.rows_per, I4)
@@ -294,6 +389,7 @@ class Steps47:
         self.imp = a.empty(2 * n1, F8)
         self.mean = a.empty(1, F8)
         self.marks = None
+        self.gram_evs = None
 
     # ------------------------------------------------------------------ inputs
     def set_phasing_graph(self, off, nbr, w):
@@ -315,15 +411,13 @@ class Steps47:
 
     def zq_int32(self):
         """The step-4 output of the last pass as int32 hundredths
-        (GRID_ZQ_NAN / GRID_ZQ_NEG0 sentinels), whichever form it was written in."""
+        (GRID_ZQ_NAN / GRID_ZQ_NEG0 sentinels), whichever form it was written
+        in (keep_z mode: the whole [n][r] output)."""
+        if not self.keep_z:
+            raise ValueError("keep_z=False: the step-4 output was streamed chunk by chunk")
         if not self.zq_is16:
             return self.zq
-        z = self.zq16.to(self.A.torch.int32)
-        z[self.zq16 == _abi.ZQ16_NAN] = _abi.ZQ_NAN
-        z[self.zq16 == _abi.ZQ16_NEG0] = _abi.ZQ_NEG0
-        if self.nesc:
-            z.view(-1)[self.esc_idx[: self.nesc]] = self.esc_val[: self.nesc]
-        return z
+        return zq16_to_int32(self.A.torch, self.zq16, self.esc_idx[: self.nesc], self.esc_val[: self.nesc])
 
     # ---------------------------------------------------------------- helpers
     def _read(self, b, i):
@@ -359,16 +453,54 @@ class Steps47:
             out[name] = out.get(name, 0.0) + a.elapsed_time(b)
         return out
 
+    def gram_ms(self):
+        """Device time of the Gram launches of the last run(time_gram=True)
+        (ms, summed over chunks) and the launch count."""
+        return sum(a.elapsed_time(b) for a, b in self.gram_evs), len(self.gram_evs)
+
+    def _chunk_q(self, q, ld, ci):
+        """(buffer, ld) holding the depth of local columns chunks[ci]."""
+        a, b = self.chunks[ci]
+        resident = hasattr(q, "data_ptr") or isinstance(q, Depth16)
+        if resident and self.nch == 1:
+            return q, ld
+        if isinstance(q, Depth16):
+            raise _abi.GridNativeError("the compact depth form is resident-only (one chunk)")
+        if self.qc_holds == ci:
+            return self.qc, self.ldc
+        if self.qc is None:
+            self.qc = self.A.empty(max(self.n, 1) * self.ldc, I4)
+        if resident:                                     # a resident matrix read in chunks (tests)
+            dst = self.qc[: self.n * self.ldc].view(self.n, self.ldc)
+            dst[:, : b - a].copy_(q[: self.n, a:b])
+        else:
+            q.fill(a, b, self.qc, self.ldc)
+        self.qc_holds = ci
+        return self.qc, self.ldc
+
     # -------------------------------------------------------------------- run
-    def run(self, q, ld, gram_events=None, profile=False):
-        """One pass of steps 4-7.  ``q``: buffer [n][ld] int32 (this shard).
-        ``gram_events``: optional (start, end) torch.cuda.Event pair recorded
-        around the Gram kernel (same stream as every kernel here)."""
+    def run(self, q, ld=None, time_gram=False, profile=False):
+        """One pass of steps 4-7.  ``q``: the depth source of this shard (see
+        the class docstring; ``ld`` = row stride of a resident matrix).
+        ``time_gram``: record HIP events around every Gram launch (on the
+        stream every kernel here runs on; read with gram_ms())."""
         o, n, ml = self.ops, self.n, self.ml
         self.marks = [] if profile else None
+        self.gram_evs = [] if time_gram else None
+        self.qc_holds = None                     # every pass reads its source afresh
+        order = list(range(self.nch))
         self._mark("start")
-        # ---- step 4: row means from 8192-block pairwise partials ----
-        o.row_blocks(q, n, ml, ld, self.bsum, self.bcnt)
+        # ---- pass A: 8192-block pairwise partial sums per row ----
+        for ci in order:
+            a, b = self.chunks[ci]
+            qc, ldc = self._chunk_q(q, ld, ci)
+            if self.nch == 1:
+                o.row_blocks(qc, n, b - a, ldc, self.bsum, self.bcnt)
+            else:
+                nb, b0 = -(-(b - a) // BLOCK), a // BLOCK
+                o.row_blocks(qc, n, b - a, ldc, self.bsum_c, self.bcnt_c)
+                self.bsum[:n, b0:b0 + nb].copy_(self.bsum_c[: n * nb].view(n, nb))
+                self.bcnt[:n, b0:b0 + nb].copy_(self.bcnt_c[: n * nb].view(n, nb))
         nblk_tot, bsum, bcnt = self.nblk_l, self.bsum, self.bcnt
         if self.comm is not None:
             self.bsum_pad.zero_()
@@ -381,11 +513,15 @@ class Steps47:
             nblk_tot = self.world * self.nblk_max
         o.row_means(bsum, bcnt, n, nblk_tot, self.rm)
         self._mark("row_means")
-        # ---- column statistics (local, exact) ----
-        o.col_means(q, n, ml, ld, self.rm, self.mu)
-        o.col_vars(q, n, ml, ld, self.rm, self.mu, self.var, self.ratio)
+        # ---- pass B: column statistics (local, exact); the chunk the buffer
+        # still holds goes first ----
+        for ci in reversed(order):
+            a, b = self.chunks[ci]
+            qc, ldc = self._chunk_q(q, ld, ci)
+            o.col_means(qc, n, b - a, ldc, self.rm, self.mu[a:b])
+            o.col_vars(qc, n, b - a, ldc, self.rm, self.mu[a:b], self.var[a:b], self.ratio[a:b])
         self._mark("col_stats")
-        # ---- median -> scale; sorted(...)[int(top_frac*n)] -> selection ----
+        # ---- pass C: median -> scale; sorted(...)[int(top_frac*n)] -> selection ----
         rall, rlen = self._gather_padded(self.ratio, ml, self.mlmax, float("nan"))
         nvalid = o.sort_valid(rall, rlen, self.sorted)
         scale, r_loc = 1.0, 0
@@ -412,39 +548,54 @@ class Steps47:
         else:
             smin, smax = -math.inf, math.inf
         self.ruse_loc = o.colmap_range(self.r3, r_loc, smin, smax, self.colmap)
+        sb, kb = self._chunk_bounds(r_loc)
         self._mark("select_sort")
-        # ---- z-scores: exact hundredths (step-4 output) + clipped bf16 panel ----
-        of, self.zq_is16 = 0, False
-        if self.zq16 is not None and not isinstance(q, Depth16) and ld % 4 == 0:
-            of, self.nesc = o.zquant16(q, n, ld, self.sel, r_loc, self.rm, self.mu, scale, self.zq16, max(ml, 1),
-                                       self.colmap, self.qmax, self.zb, self.np_, self.esc_idx, self.esc_val)
-            self.zq_is16 = not of
-        if not self.zq_is16 and not (of & 1):
-            if self.zq is None:
-                self.zq = self.A.empty(tuple(self.zq16.shape), I4)
-            of = o.zquant(q, n, ld, self.sel, r_loc, self.rm, self.mu, scale, self.zq, max(ml, 1), self.colmap,
-                          self.qmax, self.zb, self.np_)
-        if of & 1:
-            raise _abi.GridNativeError("z-score outside the int32 hundredths range")
-        self._mark("zquant")
-        # ---- step 5: exact Gram (MFMA) -> all-reduce -> top-k ----
+        # ---- pass D: z (step-4 output) + clipped bf16 panel per chunk, the
+        # exact Gram accumulated over chunks (MFMA) ----
         self.gram.zero_()
-        kpad_used = pad_to(max(self.ruse_loc, 1), 64)
-        if kpad_used > self.ruse_loc and n > 0:
-            # columns colmap did not write this pass (all in the last K-block)
-            self.zb[kpad_used // 64 - 1, :n, self.ruse_loc % 64:].zero_()
-        if gram_events:
-            gram_events[0].record()
-        o.gram(self.zb, self.np_, kpad_used, self.qmax, self.gram)
-        if gram_events:
-            gram_events[1].record()
-        self._mark("gram")
+        self.nesc, self.zq_is16 = 0, self.zq16 is not None
+        self.chunk_used = []
+        for ci in order:
+            a, b = self.chunks[ci]
+            s0, s1 = sb[ci], sb[ci + 1]
+            used = kb[ci + 1] - kb[ci]
+            self.chunk_used.append(used)
+            qc, ldc = self._chunk_q(q, ld, ci)
+            if self.nch == 1:
+                sel_c, cm_c = self.sel, self.colmap
+            else:
+                sel_c = (self.sel[s0:s1] - a).to(self.sel.dtype)
+                cmv = self.colmap[s0:s1]
+                cm_c = self.A.torch.where(cmv >= 0, cmv - kb[ci], cmv).to(self.colmap.dtype)
+            self._zquant(q, qc, ldc, a, b, s0, s1, sel_c, cm_c)
+            if used == 0 or n == 0:
+                continue
+            kpad_c = pad_to(used, 64)
+            if kpad_c > used:
+                # columns colmap did not write this chunk (all in its last K-block)
+                self.zb[kpad_c // 64 - 1, :n, used % 64:].zero_()
+            if self.gram_evs is not None:
+                import torch
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
+            o.gram(self.zb, self.np_, kpad_c, self.qmax, self.gram)
+            if self.gram_evs is not None:
+                ev[1].record()
+                self.gram_evs.append(ev)
+        self._mark("zquant_gram")
+        # ---- step 5: full rows (mirror), reduce-scatter by row blocks, top-k ----
+        o.mirror(self.gram, self.np_)
+        o.diag(self.gram, self.np_, n, self.norms)
         if self.comm is not None:
-            self.comm.all_reduce_sum(self.gram)
-            self._mark("allreduce")
+            self.comm.all_reduce_sum(self.norms)
+            self.comm.reduce_scatter_sum(self.grow, self.gram)
+            rows = self.grow
+            self._mark("reduce_scatter")
+        else:
+            rows = self.gram
         r0 = min(self.rank * self.rows_per, n)
         nr = max(min(n - r0, self.rows_per), 0)
-        o.topk(self.gram, n, self.np_, self.k, r0, nr, self.idx_l, self.d2_l, self.cnt_l)
+        o.topk_rows(rows, self.np_, self.norms, n, self.k, r0, nr, self.idx_l, self.d2_l, self.cnt_l)
         if self.comm is not None:
             kk = max(self.k, 1)
             idx = self.comm.all_gather(self.idx_l).view(-1, kk)[:n].contiguous()
@@ -455,9 +606,10 @@ class Steps47:
         self._mark("topk")
         # ---- step 6: dipCN (scales as printed "%.2f", neighbour gather) ----
         lane = None if profile else self.phase_lane
-        if lane is not None and self.ev_phase is not None:
+        if self.ev_phase is not None:
             import torch
             torch.cuda.current_stream().wait_event(self.ev_phase)   # previous pass's phasing read dip
+            self.ev_phase = None
         o.round_decimals(self.rm, n, 2, self.scale2)
         o.gather(self.scale2, idx, n * max(self.k, 1), self.nscale)
         if o.dipcn(n, self.reads, self.has, self.scale2, idx, self.nscale, cnt, max(self.k, 1), self.n_nbr,
@@ -480,3 +632,66 @@ class Steps47:
                     self.imp, self.mean)
         self._mark("phase")
         self.idx_out, self.cnt_out = idx, cnt
+
+    def _chunk_bounds(self, r_loc):
+        """Per chunk: the range [sb[c], sb[c+1]) of selected indices whose
+        columns lie in it (sel ascends) and kb[c] = panel columns used before
+        it (colmap ranks ascend)."""
+        if self.nch == 1:
+            return [0, r_loc], [0, self.ruse_loc]
+        torch = self.A.torch
+        sel = self.sel[:r_loc]
+        cuts = torch.tensor([a for a, _ in self.chunks[1:]], dtype=sel.dtype, device=sel.device)
+        inner = torch.searchsorted(sel, cuts) if r_loc else torch.zeros_like(cuts, dtype=torch.int64)
+        used = torch.cumsum((self.colmap[:r_loc] >= 0).to(torch.int64), 0) if r_loc else None
+        kin = used[(inner - 1).clamp(min=0)] * (inner > 0) if r_loc else torch.zeros_like(inner)
+        sb = [0] + [int(x) for x in inner.tolist()] + [r_loc]
+        kb = [0] + [int(x) for x in kin.tolist()] + [self.ruse_loc]
+        return sb, kb
+
+    def _zquant(self, q, qc, ldc, a, b, s0, s1, sel_c, cm_c):
+        """z of the chunk's selected columns [s0, s1): the step-4 output (int16
+        codes + escapes, or int32) and the bf16 panel columns colmap says."""
+        o, n, rc = self.ops, self.n, s1 - s0
+        if rc == 0:
+            return
+        mu_c = self.mu[a:b]
+        if self.keep_z:
+            zcol, ld_zq = s0, max(self.ml, 1)
+        else:
+            zcol, ld_zq = 0, rc
+        if self.zq_is16 and not isinstance(q, Depth16) and ldc % 4 == 0:
+            e0 = self.nesc
+            cap = self.esc_idx.numel() - e0
+            zt = self.zq16.view(-1)[zcol:]
+            of, ne = o.zquant16(qc, n, ldc, sel_c, rc, self.rm, mu_c, self.scale, zt, ld_zq, cm_c, self.qmax, self.zb,
+                                self.np_, self.esc_idx[e0:], self.esc_val[e0:])
+            if of & 1:
+                raise _abi.GridNativeError("z-score outside the int32 hundredths range")
+            if not of & 2:
+                if ne and zcol:
+                    self.esc_idx[e0:e0 + ne] += zcol             # flat index in the whole output
+                self.nesc = e0 + ne
+                if not self.keep_z and self.on_z_chunk is not None:
+                    self.on_z_chunk(self.zq16, ld_zq, s0, s1, self.esc_idx[e0:e0 + ne], self.esc_val[e0:e0 + ne])
+                return
+            if self.nch > 1:
+                raise _abi.GridNativeError(f"more than {cap} int16 escapes (|z| > 327.65) in one chunk")
+            self.zq_is16 = False                                  # one chunk: rerun with int32 output
+        if self.zq is None:
+            self.zq = self.A.empty(tuple(self.zq16.shape), I4)
+        of = o.zquant(qc if not isinstance(q, Depth16) else q, n, ldc, sel_c, rc, self.rm, mu_c, self.scale,
+                      self.zq.view(-1)[zcol:], ld_zq, cm_c, self.qmax, self.zb, self.np_)
+        if of & 1:
+            raise _abi.GridNativeError("z-score outside the int32 hundredths range")
+
+
+def zq16_to_int32(torch, zq16, esc_idx, esc_val):
+    """int16 step-4 codes (+ escapes) -> int32 hundredths with the
+    GRID_ZQ_NAN / GRID_ZQ_NEG0 sentinels."""
+    z = zq16.to(torch.int32)
+    z[zq16 == _abi.ZQ16_NAN] = _abi.ZQ_NAN
+    z[zq16 == _abi.ZQ16_NEG0] = _abi.ZQ_NEG0
+    if esc_idx.numel():
+        z.view(-1)[esc_idx] = esc_val
+    return z

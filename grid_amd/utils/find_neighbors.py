@@ -2,10 +2,16 @@
 
 Drop-in for grid/utils/find_neighbors.py.  The reference calls scikit-learn's
 brute-force Euclidean ArgKmin (:207-213).  Here the clipped z-scores, which
-the normalised file holds as exact hundredths, become an integer bf16 panel
-in HBM; the Gram matrix is computed exactly on the MFMA pipe and the k+1
-nearest are selected per row on the GPU (grid_amd/csrc/knn.hip).  Neighbour
-order equals sklearn's wherever exact distances differ.
+the normalised file holds as exact hundredths, are uploaded once as int32 and
+turned on the device into (grid_amd/engine.py _knn_zq):
+  * zmax = q/100 with q <= 256 (the default 2.0): an integer bf16 panel whose
+    Gram matrix is computed exactly on the MFMA pipe;
+  * zmax = q/100 with q > 256: exact int64 direct-difference distances;
+  * any other zmax (clipped values are not hundredths): fixed-order fp64
+    direct-difference distances;
+and the k+1 nearest are selected per row on the GPU (grid_amd/csrc/knn.hip).
+On the integer paths the neighbour order equals sklearn's wherever exact
+distances differ (sklearn's own tie order is undefined).
 """
 from __future__ import annotations
 
@@ -49,7 +55,7 @@ def _read_normalized_q(input_file):
     grammar goes through the general line parser below."""
     try:
         ids, sc, _means, ratios, zq = _abi.read_normalized_gz(input_file)
-        return ids, {i: float(v) for i, v in zip(ids, sc)}, zq.astype(np.int64), ratios
+        return ids, {i: float(v) for i, v in zip(ids, sc)}, zq, ratios
     except _abi.GridNativeError as e:
         if e.code != _abi.GRID_EUNSUPPORTED:
             raise
@@ -69,7 +75,9 @@ def _read_normalized_q_py(input_file):
             rows.append([_hundredths(v) for v in p[2:]])
     r = len(rows[0]) if rows else 0
     zq = np.array(rows, dtype=np.int64).reshape(len(rows), r) if rows else np.zeros((0, 0), np.int64)
-    return ids, scales, zq, ratios
+    if zq.size and (zq[zq != _abi.MISSING].max(initial=0) >= 2 ** 31 or zq.min() < _abi.MISSING):
+        raise ValueError("normalised z value outside the int32 hundredths range")
+    return ids, scales, zq.astype(np.int32), ratios
 
 
 def filter_regions_by_variance(sigma2ratios, frac_r: float = 1.0, sigma2_max: float = 1000.0, console=None):
@@ -91,20 +99,15 @@ def filter_regions_by_variance(sigma2ratios, frac_r: float = 1.0, sigma2_max: fl
     return idx, len(idx)
 
 
-def find_neighbors_sklearn(data_matrix, individuals, n_neighbors: int = 500, zmax: float = 2.0):
+def find_neighbors_sklearn(data_matrix, individuals, n_neighbors: int = 500):
     """:179-227 API: {id: [(neighbour_id, squared distance), ...]} computed on
-    the GPU.  ``data_matrix`` must hold exact hundredths within +-zmax (the
-    state after find_neighbors' clip, :57-58)."""
+    the GPU for any finite float64 matrix (engine.knn_values: exact integer
+    paths when every value is a hundredth, fixed-order fp64 otherwise)."""
     data = np.asarray(data_matrix, dtype=np.float64)
-    q = np.rint(data * 100.0)
-    if not np.array_equal(q / 100.0, data):
-        raise _abi.GridNativeError("find_neighbors_sklearn: values must be exact hundredths")
-    qmax = int(np.max(np.abs(q))) if q.size else 0
-    qmax = max(qmax, engine.qmax_for_zmax(zmax))
-    if qmax > 256:
-        raise _abi.GridNativeError("values exceed the exact bf16 range (|v| <= 2.56)")
-    idx, d2, cnt = engine.knn_from_hundredths(get_device(), q.astype(np.int64), n_neighbors, qmax)
-    return {ind: [(individuals[int(idx[i, t])], int(d2[i, t]) / 10000.0) for t in range(cnt[i])]
+    if data.ndim != 2:
+        raise ValueError("data_matrix must be 2-D")
+    idx, d2, cnt = engine.knn_values(get_device(), data, int(n_neighbors))
+    return {ind: [(individuals[int(idx[i, t])], float(d2[i, t])) for t in range(cnt[i])]
             for i, ind in enumerate(individuals)}
 
 
@@ -140,17 +143,16 @@ def find_neighbors(config, console):
 
     ids, scales, zq, ratios = _read_normalized_q(input_file)
     N = len(ids)
-    qmax = engine.qmax_for_zmax(float(zmax))
-    # clip (:57) and NaN -> 0 (:58), on exact hundredths
-    zc = np.where(zq == _abi.MISSING, 0, np.clip(zq, -qmax, qmax))
     valid, R_use = filter_regions_by_variance(ratios, frac_r=frac_r, sigma2_max=sigma2_max, console=console)
-    zc = zc[:, valid] if zc.size else zc.reshape(N, 0)
 
+    # clip (:57), NaN -> 0 (:58) and the column filter (:171) run on the device
+    # over the int32 hundredths (no host copies of the matrix)
     with progress_bar(console, total=N, description="Finding neighbors...") as (progress, task):
-        idx, d2, cnt = engine.knn_from_hundredths(get_device(config), zc, int(n_neighbors), qmax)
+        idx, d2, cnt = engine.knn_from_zq(get_device(config), zq.reshape(N, -1) if N else zq,
+                                          np.asarray(valid, dtype=np.int32), int(n_neighbors), float(zmax))
         progress.advance(task, N)
 
-    nbrs = {ind: [(ids[int(idx[i, t])], int(d2[i, t]) / 10000.0) for t in range(cnt[i])]
+    nbrs = {ind: [(ids[int(idx[i, t])], float(d2[i, t])) for t in range(cnt[i])]
             for i, ind in enumerate(ids)}
     save_neighbors(nbrs, scales, output_file, zmax, R_use)
     log(console, f"Saved neighbors to {output_file}", style="success")

@@ -184,6 +184,15 @@ int grid_norm_zquant_kb_q16(grid_ctx *ctx, const grid_depth16 *q, int64_t n, int
                             const int32_t *d_colmap, int32_t qmax, uint16_t *d_zb, int64_t np_zb,
                             int32_t *h_overflow);
 
+/* Verification (tests): recompute every selected cell with plain IEEE fp64
+ * in the reference's order and the "%.2f" rule, compare with the int16 codes
+ * (d_zq16[i*ld_zq + s]) and, if d_zb, the K-blocked bf16 panel at colmap[s].
+ * h_counts[3]: z mismatches, panel mismatches, skipped (missing) cells. */
+int grid_verify_zquant(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t ld, const int32_t *d_sel,
+                       int64_t r, const double *d_rm, const double *d_mu, double scale,
+                       const int16_t *d_zq16, int64_t ld_zq, const int32_t *d_colmap, int32_t qmax,
+                       const uint16_t *d_zb, int64_t np_zb, int64_t *h_counts);
+
 /* The full fp64 matrix normalize_matrix returns (:458, :470): z[i*m+j] =
  * ((y-mu)/sqrt(mu))*scale where mu > 0, y*scale elsewhere, NaN if missing. */
 int grid_norm_zfull(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t m, int64_t ld,
@@ -204,12 +213,54 @@ int grid_knn_gram(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t kpad
  * layout: one K-step of a row panel is contiguous); np % 256 == 0. */
 int grid_knn_gram_kb(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t kpad, int32_t qmax,
                      int64_t *d_gram);
-/* Per row i < n: the min(k+1, n) smallest (d2, j) with
- * d2 = G_ii + G_jj - 2 G_ij, self dropped, first k kept (find_neighbors.py
- * :205-225).  d_idx/d_d2: [n][k]; d_cnt[i] = entries written; unused
- * slots hold idx -1, d2 0.
- * row0/nrows select a row block (multi-GPU); n is the total sample count. */
-int grid_knn_topk(grid_ctx *ctx, const int64_t *d_gram, int64_t n, int64_t np_, int64_t k,
+/* Lower triangle from the upper: every 64x64 block (a, b), a > b, of the
+ * [np][np] Gram becomes the transpose of block (b, a), so row i is contiguous
+ * (np % 64 == 0).  Idempotent. */
+int grid_knn_mirror(grid_ctx *ctx, int64_t *d_gram, int64_t np_);
+/* d_norms[j] = G_jj (= ||z_j||^2) for j < n. */
+int grid_knn_diag(grid_ctx *ctx, const int64_t *d_gram, int64_t np_, int64_t n, int64_t *d_norms);
+/* Row top-k on complete Gram rows: d_rows[r*ld + j] = G(row0 + r, j) for
+ * j < n (a mirrored Gram, or one rank's row block after the multi-GPU
+ * reduce-scatter), d_norms[j] = G_jj.  Per row i = row0 + r: the min(k+1, n)
+ * smallest (d2, j) with d2 = G_ii + G_jj - 2 G_ij, self dropped, first k kept
+ * (find_neighbors.py:205-225).  d_idx/d_d2: [nrows][k]; d_cnt[r] = entries
+ * written; unused slots hold idx -1, d2 0.  n is the total sample count. */
+int grid_knn_topk_rows(grid_ctx *ctx, const int64_t *d_rows, int64_t ld, const int64_t *d_norms,
+                       int64_t n, int64_t k, int64_t row0, int64_t nrows, int32_t *d_idx,
+                       int64_t *d_d2, int32_t *d_cnt);
+/* General values (not bf16-exact: |hundredths| > 256, or not hundredths at
+ * all, e.g. zmax = 2.005 clips): direct-difference distances
+ * d2[i][j] = sum_k (z_ik - z_jk)^2, sequential over k, for all pairs (the
+ * lower triangle mirrored), into d_d2 [np][np] fp64:
+ *   grid_knn_dist_i32: z integer hundredths, exact int64 sums (the caller
+ *     keeps 4 max|z|^2 r < 2^53 so the fp64 store is exact; |z| < 2^30);
+ *   grid_knn_dist_f64: z fp64 values, fixed-order fp64 sums (no FMA).
+ * d_z: [n][ld] row-major; np % 64 == 0. */
+int grid_knn_dist_i32(grid_ctx *ctx, const int32_t *d_z, int64_t n, int64_t r, int64_t ld, double *d_d2,
+                      int64_t np_);
+int grid_knn_dist_f64(grid_ctx *ctx, const double *d_z, int64_t n, int64_t r, int64_t ld, double *d_d2,
+                      int64_t np_);
+/* Row top-k on d2 rows (d_d2rows[r*ld + j] = d2(row0 + r, j)), ordered by
+ * (floor(d2 * key_scale), j) with floor(d2 * key_scale) < 2^44: key_scale =
+ * 1 keeps exact integer distances exact; d_d2 receives the d2 values. */
+int grid_knn_topk_d2(grid_ctx *ctx, const double *d_d2rows, int64_t ld, double key_scale, int64_t n,
+                     int64_t k, int64_t row0, int64_t nrows, int32_t *d_idx, double *d_d2,
+                     int32_t *d_cnt);
+/* Step-5 inputs from the step-4 hundredths (find_neighbors.py:57-58,171):
+ * columns d_cols[0..r) of d_zq [n][ld], clipped to +-qmax (+-zmax) with
+ * GRID_MISSING -> 0, as the K-blocked bf16 panel of grid_knn_gram_kb
+ * ([kpad/64][np][64], zero padded; qmax <= 256), as dense int32 [n][r], or
+ * as fp64 values clip(q/100, +-zmax) [n][r]. */
+int grid_knn_panel_i32(grid_ctx *ctx, const int32_t *d_zq, int64_t n, int64_t ld, const int32_t *d_cols,
+                       int64_t r, int32_t qmax, uint16_t *d_zb, int64_t np_, int64_t kpad);
+int grid_knn_gather_i32(grid_ctx *ctx, const int32_t *d_zq, int64_t n, int64_t ld, const int32_t *d_cols,
+                        int64_t r, int32_t qmax, int32_t *d_out);
+int grid_knn_gather_f64(grid_ctx *ctx, const int32_t *d_zq, int64_t n, int64_t ld, const int32_t *d_cols,
+                        int64_t r, double zmax, double *d_out);
+/* grid_knn_mirror + grid_knn_diag + grid_knn_topk_rows on rows [row0,
+ * row0 + nrows) of a Gram whose upper tiles are written (the lower triangle
+ * is filled in place). */
+int grid_knn_topk(grid_ctx *ctx, int64_t *d_gram, int64_t n, int64_t np_, int64_t k,
                   int64_t row0, int64_t nrows, int32_t *d_idx, int64_t *d_d2, int32_t *d_cnt);
 
 /* ---------------------------------------------------- step 6: diploid CN

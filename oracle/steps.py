@@ -145,6 +145,26 @@ def knn_exact(zq: np.ndarray, n_neighbors: int):
     return res
 
 
+def knn_direct_f64(data: np.ndarray, n_neighbors: int):
+    """find_neighbors_sklearn semantics on general fp64 values, restated as the
+    direct-difference distance d2_ij = sum_k (x_ik - x_jk)^2 accumulated
+    sequentially in k (np.cumsum is sequential), ordered by (d2, j).  This is
+    the arithmetic grid_knn_dist_f64 performs, so d2 values compare bit for
+    bit; sklearn (find_neighbors.py:207-213) computes the same distances up to
+    its fp64 rounding (GEMM trick).  Returns per-row lists of (index, d2)."""
+    x = np.asarray(data, dtype=np.float64)
+    N = x.shape[0]
+    k = min(n_neighbors + 1, N)
+    res = []
+    for i in range(N):
+        d = (x[i][None, :] - x) ** 2
+        d2 = np.cumsum(d, axis=1)[:, -1] if x.shape[1] else np.zeros(N)
+        order = np.lexsort((np.arange(N), d2))[:k]
+        lst = [(int(j), float(d2[j])) for j in order if j != i][:n_neighbors]
+        res.append(lst)
+    return res
+
+
 def neighbor_lines(ids, scales, nbrs, R_use):
     """save_neighbors text (find_neighbors.py:258-267); d2 in 1e-4 units."""
     if R_use == 0:

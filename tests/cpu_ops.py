@@ -19,12 +19,22 @@ def _np(t):
 
 
 class NumpyOps:
+    @staticmethod
+    def _mat(q, n, m, ld):
+        """[n][m] view of a matrix buffer with row stride ld (2-D or flat)."""
+        a = _np(q).reshape(-1)
+        return a[: (n - 1) * ld + m].reshape(-1)[np.arange(n)[:, None] * ld + np.arange(m)[None, :]] if n else \
+            np.zeros((0, m), a.dtype)
+
     def row_blocks(self, q, n, m, ld, bsum, bcnt):
-        qa = _np(q)[:n, :m]
+        qa = self._mat(q, n, m, ld)
         x = np.where(qa == MISSING, 0.0, qa / 100.0)
+        nblk = -(-m // 8192)
+        bs = _np(bsum).reshape(-1)[: n * nblk].reshape(n, nblk)     # kernel layout: [n][ceil(m/8192)]
+        bc = _np(bcnt).reshape(-1)[: n * nblk].reshape(n, nblk)
         for b, s in enumerate(row_block_sums(x)):
-            _np(bsum)[:n, b] = s
-            _np(bcnt)[:n, b] = (qa[:, b * 8192:(b + 1) * 8192] != MISSING).sum(axis=1)
+            bs[:, b] = s
+            bc[:, b] = (qa[:, b * 8192:(b + 1) * 8192] != MISSING).sum(axis=1)
 
     def row_means(self, bsum, bcnt, n, nblk, rm):
         bs, bc = _np(bsum)[:n, :nblk], _np(bcnt)[:n, :nblk]
@@ -34,20 +44,20 @@ class NumpyOps:
         with np.errstate(all="ignore"):
             _np(rm)[:n] = acc / bc.sum(axis=1).astype(np.float64)
 
-    def _y(self, q, n, m, rm):
-        qa = _np(q)[:n, :m]
+    def _y(self, q, n, m, ld, rm):
+        qa = self._mat(q, n, m, ld)
         r = _np(rm)[:n]
         rs = np.where(r == 0, np.nan, r)
         with np.errstate(all="ignore"):
             return np.where(qa == MISSING, np.nan, (qa / 100.0) / rs[:, None])
 
     def col_means(self, q, n, m, ld, rm, mu):
-        y = self._y(q, n, m, rm)
+        y = self._y(q, n, m, ld, rm)
         with np.errstate(all="ignore"):
             _np(mu)[:m] = col_sum(np.nan_to_num(y, nan=0.0)) / (~np.isnan(y)).sum(axis=0)
 
     def col_vars(self, q, n, m, ld, rm, mu, var, ratio):
-        y = self._y(q, n, m, rm)
+        y = self._y(q, n, m, ld, rm)
         mj = _np(mu)[:m]
         with np.errstate(all="ignore"):
             d = y - mj[None, :]
@@ -88,7 +98,7 @@ class NumpyOps:
         if r == 0:
             return 0
         js = _np(sel)[:r]
-        qa = _np(q)[:n][:, js]
+        qa = self._mat(q, n, int(js.max()) + 1, ld)[:, js]
         rr = _np(rm)[:n]
         mj = _np(mu)[js]
         with np.errstate(all="ignore"):
@@ -104,8 +114,8 @@ class NumpyOps:
                     t = f"{v:.2f}"
                     k = int(t.replace(".", ""))
                     out[i, s] = NEG0 if (k == 0 and t.startswith("-")) else k
-        zqa = _np(zq)
-        zqa[:n, :r] = out
+        zqa = _np(zq).reshape(-1)                # row stride ld_zq (flat views allowed)
+        zqa[(np.arange(n)[:, None] * ld_zq + np.arange(r)[None, :]).reshape(-1)] = out.reshape(-1)
         cm = _np(colmap)[:r]
         clip = np.where((out == MISSING) | (out == NEG0), 0, np.clip(out, -qmax, qmax)).astype(np.float32)
         bits = (clip.view(np.uint32) >> 16).astype(np.uint16).view(np.int16)
@@ -116,17 +126,30 @@ class NumpyOps:
         return 0
 
     def gram(self, zb, np_, kpad, qmax, gram):
+        """Upper 128-tiles only, like the HIP kernels (the lower triangle is
+        the mirror's job)."""
         zr = _np(zb)[: kpad // 64, :np_].transpose(1, 0, 2).reshape(np_, kpad)
         bits = zr.view(np.uint16).astype(np.uint32) << 16
         z = bits.view(np.float32).astype(np.float64)
-        _np(gram)[:np_, :np_] += (z @ z.T).astype(np.int64)
+        g = (z @ z.T).astype(np.int64)
+        t = np.arange(np_) // 128
+        _np(gram)[:np_, :np_] += np.where(t[:, None] <= t[None, :], g, 0)
 
-    def topk(self, gram, n, np_, k, row0, nrows, idx, d2, cnt):
-        g = _np(gram)
-        dg = np.diag(g)[:n]
+    def mirror(self, gram, np_):
+        g = _np(gram)[:np_, :np_]
+        b = np.arange(np_) // 64
+        low = b[:, None] > b[None, :]
+        g[low] = g.T[low]
+
+    def diag(self, gram, np_, n, norms):
+        _np(norms)[:n] = np.diag(_np(gram)[:n, :n])
+
+    def topk_rows(self, rows, ld, norms, n, k, row0, nrows, idx, d2, cnt):
+        g = _np(rows).reshape(-1)
+        dg = _np(norms)[:n]
         for r in range(nrows):
             i = row0 + r
-            d = dg[i] + dg - 2 * g[i, :n]
+            d = dg[i] + dg - 2 * g[r * ld: r * ld + n]
             order = np.lexsort((np.arange(n), d))[: min(k + 1, n)]
             lst = [(int(j), int(d[j])) for j in order if j != i][:k]
             _np(idx)[r, :] = -1

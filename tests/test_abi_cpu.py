@@ -86,3 +86,26 @@ def test_level_schedule_reproduces_gauss_seidel():
     exp, _ = steps.run_phasing(irr, hn, 1, 9)
     got = _run_levels(irr, hn, 1, 9)
     assert np.array_equal(np.array(got), np.array(exp), equal_nan=True)
+
+
+PROBE_SELECTORS = (b"GRID_GRAM_VARIANT", b"GRID_PHASE_PROBE", b"GRID_ZQUANT_VARIANT", b"GRID_COL_VW",
+                   b"GRID_COL_CU", b"GRID_PHASE_LEGACY")
+
+
+def test_product_library_has_no_probe_selectors():
+    """The timing probes (wrong results by design) and A/B kernels are built
+    only into libgridhip_probes.so (make probes, -DGRID_PROBES): the product
+    library contains none of the environment variables that select them, so
+    no environment can change its results.  The remaining getenv knobs are
+    performance-only (tests/test_gpu_kernels.py checks results under them)."""
+    from grid_amd import _abi
+    blob = open(_abi.LIB_PATH, "rb").read()
+    for s in PROBE_SELECTORS:
+        assert s not in blob, s
+    knobs = set(re.findall(rb"GRID_[A-Z0-9_]+", blob))
+    allowed = {b"GRID_GRAM_LAG", b"GRID_GRAM_SPIN", b"GRID_GRAM_KC", b"GRID_GRAM_KX", b"GRID_ROWBLK_NT",
+               b"GRID_COL_NT", b"GRID_ZQUANT_NT", b"GRID_ZQUANT_GROUPS", b"GRID_LOADER_THREADS"}
+    env_like = {k for k in knobs if k not in (b"GRID_OK",)}
+    # every GRID_* string in the binary is either an allowed knob or a message token, never a probe selector
+    assert not (env_like & set(PROBE_SELECTORS))
+    assert allowed & env_like                     # the knobs are present (sanity of the scan)

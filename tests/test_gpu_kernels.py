@@ -172,16 +172,22 @@ def test_gram_kblocked_multi_slice(dev, qmax):
             assert np.array_equal(got[blk], ref[blk]), (ti, tj)
 
 
-@pytest.mark.parametrize("variant", ["2", "4", "6", "11", "16", "21"])
-def test_gram_variants_multi_slice(dev, variant, monkeypatch):
-    """Every Gram kernel variant on a shape with several int32 K-slices, a
+@pytest.mark.parametrize("np_,knobs", [(768, {}), (640, {}), (768, {"GRID_GRAM_KX": "1"}),
+                                       (768, {"GRID_GRAM_KX": "2", "GRID_GRAM_KC": "5"}),
+                                       (768, {"GRID_GRAM_KX": "4", "GRID_GRAM_LAG": "3"}),
+                                       (768, {"GRID_GRAM_KX": "8", "GRID_GRAM_SPIN": "0"})])
+def test_gram_variants_multi_slice(dev, np_, knobs, monkeypatch):
+    """The product Gram paths on a shape with several int32 K-slices, a
     partial last slice (remainder steps not a multiple of 4) and a partial
-    256-row block, against a float64 product (exact: |sums| < 2^53)."""
+    256-row block, against a float64 product (exact: |sums| < 2^53): k_gram8
+    (np % 256 == 0) under every K-split / chunk / pacing knob (performance
+    knobs: results must not change), and k_gram_dma (np % 256 != 0)."""
     from grid_amd._abi import call
-    monkeypatch.setenv("GRID_GRAM_VARIANT", variant)
-    qmax, n, np_ = 200, 600, 768
+    for key, val in knobs.items():
+        monkeypatch.setenv(key, val)
+    qmax, n = 200, 600
     r = 64 * (2 * 838 + 7)
-    rng = np.random.default_rng(int(variant))
+    rng = np.random.default_rng(np_ + len(knobs))
     q = np.zeros((np_, r), dtype=np.int64)
     q[:n] = rng.integers(-qmax, qmax + 1, size=(n, r))
     zf = (q.astype(np.float32).view(np.uint32) >> 16).astype(np.uint16)
@@ -195,6 +201,8 @@ def test_gram_variants_multi_slice(dev, variant, monkeypatch):
         for tj in range(ti, np_ // 128):
             blk = (slice(ti * 128, (ti + 1) * 128), slice(tj * 128, (tj + 1) * 128))
             assert np.array_equal(got[blk], ref[blk]), (ti, tj)
+    call("grid_knn_mirror", dev.ctx, g.ptr, np_)
+    assert np.array_equal(g.numpy(), ref)
 
 
 def test_dipcn_random(dev):
@@ -255,12 +263,10 @@ def test_phasing_random(dev, n, seed):
 
 @pytest.mark.parametrize("weighted,maxlen,legacy", [(False, 6, False), (True, 6, False), (True, 14, False),
                                                     (False, 40, False), (True, 40, False), (True, 14, True)])
-def test_phasing_kernel_variants(dev, weighted, maxlen, legacy, monkeypatch):
+def test_phasing_kernel_variants(dev, weighted, maxlen, legacy):
     """Register capacities 8/16, unit and general weights, lists longer than
     the packed capacity (CSR loop), and the legacy kernel, vs the oracle."""
     from grid_amd import engine
-    if legacy:
-        monkeypatch.setenv("GRID_PHASE_LEGACY", "1")
     rng = np.random.default_rng(maxlen * 2 + weighted)
     n = 700
     irr = rng.uniform(0.1, 4.0, n)
@@ -275,7 +281,7 @@ def test_phasing_kernel_variants(dev, weighted, maxlen, legacy, monkeypatch):
             lst.append((min(2 * j + int(rng.integers(0, 2)), 2 * n - 1), wt))
         hn.append(lst)
     off, nbr, w = engine.csr_from_lists(hn)
-    hap, imp, mean = engine.phase(dev, irr, off, nbr, w, 1, 15)
+    hap, imp, mean = engine.phase(dev, irr, off, nbr, w, 1, 15, legacy=legacy)
     eh, em = steps.run_phasing(list(irr), hn, 1, 15)
     assert np.array_equal(hap, np.array(eh), equal_nan=True)
     assert mean == em or (np.isnan(mean) and np.isnan(em))

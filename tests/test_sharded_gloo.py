@@ -38,16 +38,17 @@ def cohort():
     return q, reads, offs, np.array(nbr, dtype=np.int32), np.ones(len(nbr))
 
 
-def run_chain(rank, world, comm):
-    from grid_amd.fused import Steps47, TorchAlloc, shard_range
+def run_chain(rank, world, comm, chunk=None, source="resident"):
+    from grid_amd.fused import HostSource, Steps47, TorchAlloc, shard_range
     from tests.cpu_ops import NumpyOps
     q, reads, off, nbr, w = cohort()
     c0, c1 = shard_range(M, rank, world)
     qs = torch.from_numpy(np.ascontiguousarray(q[:, c0:c1]))
-    st = Steps47(NumpyOps(), TorchAlloc("cpu"), N, M, c0, c1 - c0, k=K, n_nbr=3, n_iters=ITERS, comm=comm)
+    st = Steps47(NumpyOps(), TorchAlloc("cpu"), N, M, c0, c1 - c0, k=K, n_nbr=3, n_iters=ITERS, comm=comm,
+                 chunk=chunk)
     st.set_reads(reads)
     st.set_phasing_graph(off, nbr, w)
-    st.run(qs, c1 - c0)
+    st.run(HostSource(qs.numpy()) if source == "host" else qs, c1 - c0)
     ml = c1 - c0
     return {
         "rm": st.rm.numpy()[:N].copy(), "mu": st.mu.numpy()[:ml].copy(), "var": st.var.numpy()[:ml].copy(),
@@ -58,11 +59,11 @@ def run_chain(rank, world, comm):
     }
 
 
-def _worker(rank, world, port, out_path):
+def _worker(rank, world, port, out_path, chunk):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from grid_amd.fused import TorchComm
-    res = run_chain(rank, world, TorchComm(dist))
+    res = run_chain(rank, world, TorchComm(dist), chunk=chunk)
     np.savez(f"{out_path}.{rank}.npz", **{k: np.asarray(v) for k, v in res.items()})
     dist.barrier()
     dist.destroy_process_group()
@@ -93,11 +94,21 @@ def test_single_rank_matches_oracle(single):
     assert single["sel"].tolist() == steps.select_high_variance_regions(ratios, 0.1)
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_equals_single(single, world, tmp_path):
+@pytest.mark.parametrize("chunk,source", [(8192, "resident"), (16384, "host"), (8192, "host")])
+def test_streamed_equals_single(single, chunk, source):
+    """Bin-axis streaming (3-4 chunks, the last one partial) gives the
+    one-chunk chain's results bit for bit, from a resident matrix read in
+    chunks and from a host source copied slab by slab."""
+    res = run_chain(0, 1, None, chunk=chunk, source=source)
+    for key in ("rm", "mu", "var", "sel", "zq", "idx", "d2", "dip", "hap", "imp", "ruse", "scale"):
+        assert np.array_equal(np.asarray(res[key]), np.asarray(single[key]), equal_nan=True), key
+
+
+@pytest.mark.parametrize("world,chunk", [(2, None), (3, None), (2, 8192)])
+def test_sharded_equals_single(single, world, chunk, tmp_path):
     port = _free_port()
     out = str(tmp_path / "res")
-    mp.start_processes(_worker, args=(world, port, out), nprocs=world, join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(world, port, out, chunk), nprocs=world, join=True, start_method="spawn")
     parts = [dict(np.load(f"{out}.{r}.npz")) for r in range(world)]
     for key in ("rm", "idx", "d2", "dip", "hap", "imp"):
         for p in parts:

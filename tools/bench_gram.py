@@ -11,6 +11,9 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# timing probes and A/B kernels live in the tools build only (make -C grid_amd/csrc probes)
+os.environ.setdefault("GRID_AMD_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                    "grid_amd", "_lib", "libgridhip_probes.so"))
 from grid_amd import _abi  # noqa: E402
 
 ap = argparse.ArgumentParser()
