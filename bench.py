@@ -172,7 +172,7 @@ def main():
     ap.add_argument("--n-iters", type=int, default=100)
     ap.add_argument("--chunk", type=int, default=0, help="bins per streamed chunk (multiple of 8192); "
                     "0 = resident when the shard fits, else the widest chunk that fits")
-    ap.add_argument("--hbm-budget-gb", type=float, default=250.0)
+    ap.add_argument("--hbm-budget-gb", type=float, default=200.0)
     ap.add_argument("--cpu-samples", type=int, default=4096)
     ap.add_argument("--cpu-bins", type=int, default=16384)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -254,8 +254,15 @@ def main():
     st.set_reads(reads)
     st.set_phasing_graph(off, nbr, w)
 
-    for _ in range(args.warmup):
+    def note(msg):
+        if rank == 0:
+            print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+    note(f"{n} x {m}, shard {ml} bins, {st.nch} chunk(s); warmup {args.warmup}, steps {args.steps}")
+    for w_ in range(args.warmup):
         st.run(q, ldq)
+        torch.cuda.synchronize()
+        note(f"warmup {w_} done")
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -266,7 +273,10 @@ def main():
     for s in range(args.steps):
         st.run(q, ldq, time_gram=True)
         gram_pairs += st.gram_evs
+        if st.nch > 1:                          # long streamed steps: progress for the watchdog
+            note(f"step {s} queued")
     torch.cuda.synchronize()
+    note("timed steps done")
     if dist:
         dist.barrier()
     t1 = time.perf_counter()

@@ -159,10 +159,11 @@ def knn_from_hundredths(dev: Device, zq: np.ndarray, k: int, qmax: int):
     return _knn_zq(dev, zq, np.arange(zq.shape[1], dtype=np.int32), k, qmax / 100.0, False)
 
 
-def _dist_key_scale(bound: float) -> float:
-    """Power-of-two key scale so floor(d2 * scale) < 2^44 (1 while exact
-    integer distances fit: they then stay exact)."""
-    if bound < 2.0 ** 44:
+def _dist_key_scale(bound: float, integer: bool) -> float:
+    """Power-of-two key scale with floor(d2 * scale) < 2^44 for d2 <= bound:
+    1 for exact integer distances that fit (they then stay exact), else the
+    finest scale (fp64 distances keep 44 significant bits of the largest)."""
+    if integer and bound < 2.0 ** 44:
         return 1.0
     return math.ldexp(1.0, 43 - math.frexp(bound)[1])
 
@@ -201,14 +202,14 @@ def _knn_zq(dev: Device, zq: np.ndarray, cols: np.ndarray, k: int, zmax: float, 
         call("grid_knn_gather_i32", dev.ctx, dz.ptr, n, ld, dcols.ptr, r, q, g.ptr)
         del dz
         call("grid_knn_dist_i32", dev.ctx, g.ptr, n, r, max(r, 1), d2m.ptr, np_)
-        scale = _dist_key_scale(4.0 * q * q * max(r, 1))
+        scale = _dist_key_scale(4.0 * q * q * max(r, 1), True)
         unit = 10000.0
     else:
         g = dev.alloc((n, max(r, 1)), F8)
         call("grid_knn_gather_f64", dev.ctx, dz.ptr, n, ld, dcols.ptr, r, float(zmax), g.ptr)
         del dz
         call("grid_knn_dist_f64", dev.ctx, g.ptr, n, r, max(r, 1), d2m.ptr, np_)
-        scale = _dist_key_scale(4.0 * zmax * zmax * max(r, 1) + 1.0)
+        scale = _dist_key_scale(4.0 * zmax * zmax * max(r, 1) + 1.0, False)
         unit = 1.0
     del g
     idx, d2, cnt = dev.alloc((n, kk), I4), dev.alloc((n, kk), F8), dev.alloc(n, I4)
@@ -247,7 +248,7 @@ def knn_values(dev: Device, data: np.ndarray, k: int):
     d2m = dev.alloc((np_, np_), F8)
     call("grid_knn_dist_f64", dev.ctx, dz.ptr, n, r, r, d2m.ptr, np_)
     m = float(np.abs(data).max()) if data.size else 0.0
-    scale = _dist_key_scale(4.0 * m * m * max(r, 1) + 1.0)
+    scale = _dist_key_scale(4.0 * m * m * max(r, 1) + 1.0, False)
     idx, d2, cnt = dev.alloc((n, kk), I4), dev.alloc((n, kk), F8), dev.alloc(n, I4)
     call("grid_knn_topk_d2", dev.ctx, d2m.ptr, np_, scale, n, k, 0, n, idx.ptr, d2.ptr, cnt.ptr)
     return idx.numpy(), d2.numpy(), cnt.numpy()

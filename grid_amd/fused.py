@@ -677,7 +677,7 @@ class Steps47:
                 return
             if self.nch > 1:
                 raise _abi.GridNativeError(f"more than {cap} int16 escapes (|z| > 327.65) in one chunk")
-            self.zq_is16 = False                                  # one chunk: rerun with int32 output
+        self.zq_is16 = False            # int32 output: no int16 codes (compact / unaligned input, or escapes)
         if self.zq is None:
             self.zq = self.A.empty(tuple(self.zq16.shape), I4)
         of = o.zquant(qc if not isinstance(q, Depth16) else q, n, ldc, sel_c, rc, self.rm, mu_c, self.scale,
