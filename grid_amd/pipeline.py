@@ -56,7 +56,10 @@ def run_wgs_pipeline(console=False, config=None, **args):
 
     if cfg["compute_haploid_genotypes"].get("run") == True:  # noqa: E712
         try:
-            from .utils.hi_inference import hi_inference
-            hi_inference(cfg, console)
+            from .utils.hi_inference import hi_inference, hi_inference_loci
+            if cfg["compute_haploid_genotypes"].get("loci_file"):
+                hi_inference_loci(cfg, console)      # many regions (BASELINE config 5)
+            else:
+                hi_inference(cfg, console)
         except Exception as e:
             log(console, f"Failed to compute haploid CNV calls: {e}", style="danger")

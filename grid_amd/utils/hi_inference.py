@@ -241,6 +241,166 @@ def _compute_imp(i, hap_IRRs, hap_nbrs, mean_IRRs):
     return i0, i1
 
 
+def _write_haploid(output_file, IDs, IRRs, hap, imp):
+    """The step-7 output table (:329-337)."""
+    with open_maybe_gz(output_file, "wt") as fout:
+        fout.write("ID\tIRRs\thap1phased\thap2phased\thap1imp\thap2imp\n")
+        for i in range(len(IRRs)):
+            fout.write(f"{IDs[i]}\t{IRRs[i]:.2f}\t{hap[2*i]:.2f}\t{hap[2*i+1]:.2f}\t"
+                       f"{imp[2*i]:.2f}\t{imp[2*i+1]:.2f}\n")
+
+
+# ---------------------------------------------------------------------------
+# Multi-locus step (BASELINE config 5): the reference runs step 7 once per
+# region config (chrom/start_bp/end_bp, :300-301).  A loci table such as
+# files/734_possible_coding_vntr_regions.IBD2R_gt_0.25.uniq.txt lists the
+# regions; every locus is the reference's single-locus step with that
+# region's inputs, and all of a rank's loci are phased in ONE batched launch
+# (grid_hi_phase_batch, one workgroup per locus).  Loci are dealt round-robin
+# over the ranks of a torch.distributed job (no data-path collective: loci
+# are independent); every rank writes its own loci's files.
+
+LOCI_COLS = {"chrom": ("CHR", "CHROM", "#CHROM", "CHROMOSOME"),
+             "start": ("BP_START_HG38", "BP_START", "START", "START_BP"),
+             "end": ("BP_END_HG38", "BP_END", "END", "END_BP"),
+             "gene": ("GENE", "NAME", "ID")}
+
+
+def read_loci_file(path):
+    """Loci table: a tab/space-separated header naming the chromosome, start,
+    end and (optional) name columns (the 734-region file's CHR,
+    BP_START_HG38, BP_END_HG38, GENE), one region per line.  Returns a list of
+    dicts {chrom, start, end, gene, index}."""
+    loci = []
+    with open_maybe_gz(path) as f:
+        header = None
+        for line in f:
+            line = line.rstrip("\r\n")
+            if not line.strip():
+                continue
+            p = line.split("\t") if "\t" in line else line.split()
+            if header is None:
+                up = [c.strip().upper() for c in p]
+                header = {}
+                for key, names in LOCI_COLS.items():
+                    for nm in names:
+                        if nm in up:
+                            header[key] = up.index(nm)
+                            break
+                missing = [k for k in ("chrom", "start", "end") if k not in header]
+                if missing:
+                    raise ValueError(f"loci file {path}: no column for {', '.join(missing)} in the header")
+                continue
+            try:
+                rec = {"chrom": p[header["chrom"]].strip(), "start": int(p[header["start"]]),
+                       "end": int(p[header["end"]])}
+            except (IndexError, ValueError) as e:
+                raise ValueError(f"loci file {path}: bad line {line!r}") from e
+            rec["gene"] = p[header["gene"]].strip() if "gene" in header and header["gene"] < len(p) else \
+                f"{rec['chrom']}_{rec['start']}_{rec['end']}"
+            rec["index"] = len(loci)
+            loci.append(rec)
+    return loci
+
+
+def _locus_path(template, locus, **kw):
+    """A per-locus path: ``template`` with {chrom} {start} {end} {gene}
+    {index} {locus} (and the step's own keys) substituted."""
+    return Path(str(template).format(chrom=locus["chrom"], start=locus["start"], end=locus["end"],
+                                     gene=locus["gene"], index=locus["index"],
+                                     locus=f"{locus['chrom']}_{locus['start']}_{locus['end']}_{locus['gene']}", **kw))
+
+
+def _rank_world(comm=None):
+    if comm is not None:
+        return comm.get_rank(), comm.get_world_size()
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_rank(), dist.get_world_size()
+    except ImportError:
+        pass
+    return 0, 1
+
+
+def hi_inference_loci(config, console, comm=None):
+    """Step 7 over every region of ``compute_haploid_genotypes.loci_file``.
+
+    Per-locus inputs and outputs are path templates ({chrom} {start} {end}
+    {gene} {index} {locus}; {output_dir} {prefix} {dip_prefix} {type} too):
+      * ``dip_cn_file`` (default ``{output_dir}/{dip_prefix}.{locus}.{type}``,
+        {locus} = ``{chrom}_{start}_{end}_{gene}``: gene names repeat in the
+        734-region table, regions do not),
+      * ``ibs_output`` / ``ibd_output`` (a template, or one shared file: the
+        IBD loader filters and weights segments by each locus' region, as
+        the reference does with start_bp/end_bp),
+      * ``loci_output`` (default ``{output_dir}/{prefix}.{locus}.{type}``).
+    Each output file is what the reference's hi_inference writes for a
+    config with that locus' chrom/start_bp/end_bp.  ``comm``: a
+    torch.distributed-like object (get_rank/get_world_size); by default the
+    initialised default process group, if any.  Returns the loci this rank
+    phased (dicts with their output paths)."""
+    try:
+        hc = config.get("compute_haploid_genotypes", {})
+        prefix = hc.get("output_file_prefix", "haploid_genotypes")
+        ftype = config.get("output_file_type", "tsv")
+        output_dir = config.get("output_dir", ".")
+        dip_prefix = config["compute_diploid_genotypes"].get("output_file_prefix")
+        method = hc.get("method", "ibs").lower()
+        MIN_NBR = hc.get("min_neighbors", 1)
+        MAX_NBR = hc.get("max_neighbors", 10)
+        N_ITERS = hc.get("n_iters", 100)
+        loci_file = hc["loci_file"]
+        keys = dict(output_dir=output_dir, prefix=prefix, dip_prefix=dip_prefix, type=ftype)
+        dip_t = hc.get("dip_cn_file", "{output_dir}/{dip_prefix}.{locus}.{type}")
+        out_t = hc.get("loci_output", "{output_dir}/{prefix}.{locus}.{type}")
+        if method not in ("ibs", "ibd"):
+            raise ValueError(f"unknown method '{method}', must be 'ibs' or 'ibd'")
+        nbr_t = hc.get("ibs_output" if method == "ibs" else "ibd_output")
+        if not nbr_t:
+            raise ValueError(f"{method}_output required for method='{method}'")
+    except Exception as e:
+        log(console, f"Config error: {e}", style="danger")
+        return None
+
+    loci = read_loci_file(loci_file)
+    outs = [_locus_path(out_t, lc, **keys) for lc in loci]
+    if len(set(outs)) != len(outs):
+        log(console, "Config error: loci_output names collide (add {index} or {start} to the template)",
+            style="danger")
+        return None
+    rank, world = _rank_world(comm)
+    mine = [lc for lc in loci if lc["index"] % world == rank]
+    log(console, f"Phasing {len(mine)} of {len(loci)} loci on rank {rank}/{world} ({method})")
+
+    def load(lc):
+        IDs, IRRs, IDtoInd = _read_dip_cn_file(_locus_path(dip_t, lc, **keys))
+        src = _locus_path(nbr_t, lc, **keys)
+        if method == "ibs":
+            csr = _load_ibs_csr(src, IDtoInd, MAX_NBR)
+        else:
+            csr = _load_ibd_csr(src, IDtoInd, MAX_NBR, lc["start"], lc["end"],
+                                min_length=hc.get("min_length", 0.5), min_match=hc.get("min_match", 0.70),
+                                weighted=hc.get("weighted", False), weight_scale=hc.get("weight_scale", 1_000_000))
+        return IDs, IRRs, csr
+
+    # the loaders are host C++ that release the GIL: parse loci in parallel
+    import os
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max(1, min(16, os.cpu_count() or 1))) as ex:
+        inputs = list(ex.map(load, mine))
+    res = engine.phase_batch(get_device(config), [(np.asarray(irr, dtype=np.float64), *csr)
+                                                   for _, irr, csr in inputs], MIN_NBR, N_ITERS)
+    done = []
+    for lc, (IDs, IRRs, _), (hap, imp, _mean) in zip(mine, inputs, res):
+        out = outs[lc["index"]]
+        out.parent.mkdir(parents=True, exist_ok=True)
+        _write_haploid(out, IDs, IRRs, hap, imp)
+        done.append(dict(lc, output=str(out), samples=len(IRRs)))
+    log(console, f"Haploid genotypes of {len(done)} loci written (rank {rank})", style="success")
+    return done
+
+
 def hi_inference(config, console):
     """Step entry point (:253-339)."""
     try:
@@ -284,9 +444,5 @@ def hi_inference(config, console):
         return
 
     hap, imp, _ = _phase_device_csr(IRRs, *csr, MIN_NBR, N_ITERS, console, get_device(config))
-    with open_maybe_gz(output_file, "wt") as fout:
-        fout.write("ID\tIRRs\thap1phased\thap2phased\thap1imp\thap2imp\n")
-        for i in range(N):
-            fout.write(f"{IDs[i]}\t{IRRs[i]:.2f}\t{hap[2*i]:.2f}\t{hap[2*i+1]:.2f}\t"
-                       f"{imp[2*i]:.2f}\t{imp[2*i+1]:.2f}\n")
+    _write_haploid(output_file, IDs, IRRs, hap, imp)
     log(console, f"Haploid genotypes written to {output_file}", style="success")

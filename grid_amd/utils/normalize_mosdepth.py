@@ -338,7 +338,16 @@ def ingest_py(individuals, mosdepth_dir, chromosome, start, end, excluded, min_d
         rec = per[ind]
         js = np.fromiter((col[r] for r in rows[ind]), dtype=np.int64, count=len(rows[ind]))
         d = np.fromiter((rec[r] for r in rows[ind]), dtype=np.float64, count=len(rows[ind]))
-        q[i, js] = to_hundredths(d)
+        try:
+            q[i, js] = to_hundredths(d)
+        except UnsupportedDepth as e:
+            # mosdepth prints "%.2f"; other text is not supported by the exact
+            # integer path: fail before any GPU work, naming file and value
+            nan = np.isnan(d)
+            bad = d[~nan & (np.rint(np.where(nan, 0.0, d) * 100.0) / 100.0 != np.where(nan, 0.0, d))]
+            where = find_bed_gz_for_individual(ind, mosdepth_dir)
+            raise UnsupportedDepth(f"{where}: {e}; first offending depth {bad[0]!r}" if len(bad) else
+                                   f"{where}: {e}") from None
     return ids, regions, q
 
 

@@ -147,7 +147,7 @@ def test_exotic_text_falls_back_identically(tmp_path, capsys):
             nm.ingest_native(inds, d, None, None, None, {}, 20, 100, 2)
         if k == "decimals":
             # the reference keeps 30.125 in the matrix -> the int32 path refuses it
-            with pytest.raises(nm.UnsupportedDepth):
+            with pytest.raises(nm.UnsupportedDepth, match=r"B\.regions\.bed\.gz.*30\.125"):
                 nm.ingest(inds, d, None, None, None, {}, 20, 100, 2)
             continue
         got = nm.ingest(inds, d, None, None, None, {}, 20, 100, 2)
