@@ -458,8 +458,10 @@ class Steps47:
         (ms, summed over chunks) and the launch count."""
         return sum(a.elapsed_time(b) for a, b in self.gram_evs), len(self.gram_evs)
 
-    def _chunk_q(self, q, ld, ci):
-        """(buffer, ld) holding the depth of local columns chunks[ci]."""
+    def _chunk_q(self, q, ld, ci, stage):
+        """(buffer, ld) holding the depth of local columns chunks[ci].  With
+        profile marks on, a fill from a streamed source is timed as stage
+        "source" (the time before it goes to ``stage``)."""
         a, b = self.chunks[ci]
         resident = hasattr(q, "data_ptr") or isinstance(q, Depth16)
         if resident and self.nch == 1:
@@ -470,11 +472,13 @@ class Steps47:
             return self.qc, self.ldc
         if self.qc is None:
             self.qc = self.A.empty(max(self.n, 1) * self.ldc, I4)
+        self._mark(stage)
         if resident:                                     # a resident matrix read in chunks (tests)
             dst = self.qc[: self.n * self.ldc].view(self.n, self.ldc)
             dst[:, : b - a].copy_(q[: self.n, a:b])
         else:
             q.fill(a, b, self.qc, self.ldc)
+        self._mark("source")
         self.qc_holds = ci
         return self.qc, self.ldc
 
@@ -493,7 +497,7 @@ class Steps47:
         # ---- pass A: 8192-block pairwise partial sums per row ----
         for ci in order:
             a, b = self.chunks[ci]
-            qc, ldc = self._chunk_q(q, ld, ci)
+            qc, ldc = self._chunk_q(q, ld, ci, "row_means")
             if self.nch == 1:
                 o.row_blocks(qc, n, b - a, ldc, self.bsum, self.bcnt)
             else:
@@ -517,7 +521,7 @@ class Steps47:
         # still holds goes first ----
         for ci in reversed(order):
             a, b = self.chunks[ci]
-            qc, ldc = self._chunk_q(q, ld, ci)
+            qc, ldc = self._chunk_q(q, ld, ci, "col_stats")
             o.col_means(qc, n, b - a, ldc, self.rm, self.mu[a:b])
             o.col_vars(qc, n, b - a, ldc, self.rm, self.mu[a:b], self.var[a:b], self.ratio[a:b])
         self._mark("col_stats")
@@ -560,7 +564,7 @@ class Steps47:
             s0, s1 = sb[ci], sb[ci + 1]
             used = kb[ci + 1] - kb[ci]
             self.chunk_used.append(used)
-            qc, ldc = self._chunk_q(q, ld, ci)
+            qc, ldc = self._chunk_q(q, ld, ci, "zquant_gram")
             if self.nch == 1:
                 sel_c, cm_c = self.sel, self.colmap
             else:

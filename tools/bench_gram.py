@@ -25,7 +25,7 @@ ap.add_argument("--qmax", type=int, default=200)
 ap.add_argument("--ld-extra", type=int, default=0, help="extra bf16 columns of row padding (row stride)")
 a = ap.parse_args()
 
-np_ = -(-a.n // 128) * 128
+np_ = -(-a.n // 256) * 256
 kpad = -(-a.k // 64) * 64
 dev = _abi.Device(0)
 dev.set_stream(torch.cuda.current_stream())
@@ -45,7 +45,14 @@ if any(v.startswith("kb") for v in a.variants.split(",")):
 res = {}
 flops = 2.0 * a.n * a.n * a.k
 for rep in range(a.reps):
-    for v in a.variants.split(","):
+    for vv in a.variants.split(","):
+        # "kb21:LAG=2:KC=9" -> variant kb21 with GRID_GRAM_LAG=2, GRID_GRAM_KC=9 (performance knobs)
+        v, *knobs = vv.split(":")
+        for kv in ("LAG", "SPIN", "KC", "KX"):
+            os.environ.pop("GRID_GRAM_" + kv, None)
+        for kv in knobs:
+            key, val = kv.split("=")
+            os.environ["GRID_GRAM_" + key] = val
         os.environ["GRID_GRAM_VARIANT"] = v[2:] if v.startswith("kb") else v
         gram.zero_()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -57,13 +64,13 @@ for rep in range(a.reps):
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1)
-        res.setdefault(v, []).append(ms)
+        res.setdefault(vv, []).append(ms)
         if rep == 0:
             # check a few upper-triangle tiles against a float64 product on the GPU
             zz = zb[:256, :kpad].view(torch.bfloat16).double()
             ref = (zz @ zz.T).long()
             ok = torch.equal(gram[:128, :256], ref[:128, :256])
-            print(f"variant {v}: tile check {'OK' if ok else 'MISMATCH'}", flush=True)
+            print(f"variant {vv}: tile check {'OK' if ok else 'MISMATCH'}", flush=True)
 for v, t in res.items():
     ms = min(t)
     print(f"variant {v}: min {ms:.2f} ms  median {np.median(t):.2f} ms  "
