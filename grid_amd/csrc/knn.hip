@@ -517,7 +517,8 @@ __global__ __launch_bounds__(MB == 2 ? 512 : 256, 1) void k_gram6(const uint16_t
 //     qmax <= 209) or 3b and 12 + 3b (FL = 2: 192 products, qmax <= 256).
 // MODE 0 production; timing probes (wrong results, tools/bench_gram.py):
 // 1 = every tile reads panel 0 (L2-resident loads), 5 = no global loads,
-// 6 = no global loads and no flush.
+// 6 = no global loads and no flush, 7 = no MFMAs (DMA + LDS reads + barriers),
+// 8 = DMA + barriers only (no LDS reads, no MFMAs).
 template <int OFF>
 __device__ __forceinline__ uint4 lds_rd(uint32_t addr) {
   uint4 v;
@@ -583,7 +584,7 @@ __device__ __forceinline__ void g8_run(const uint16_t *__restrict__ z, int64_t l
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lptr_t)(B_ + 1024), 16, vo1, so_, 0, 0);    \
   } while (0)
 #define G8_READ(FR, SL, s_)                                                                    \
-  do {                                                                                         \
+  if (MODE != 8) do {                                                                          \
     FR[0] = lds_rd<(s_) * 256>(ad[SL][0]);                                                     \
     FR[1] = lds_rd<(s_) * 256>(ad[SL][1]);                                                     \
     FR[2] = lds_rd<(s_) * 256>(ad[SL][2]);                                                     \
@@ -592,7 +593,7 @@ __device__ __forceinline__ void g8_run(const uint16_t *__restrict__ z, int64_t l
   // MFMAs of A blocks [m0, m1) at in-group sub-step c_; block b = 2m + nn starts
   // a new fp32 chunk (after flushing the old one) at sub-steps = FSP b (mod FCYC)
 #define G8_MFMA(FR, c_, m0, m1, STAG)                                                          \
-  do {                                                                                         \
+  if (MODE != 7 && MODE != 8) do {                                                             \
     _Pragma("unroll") for (int m = m0; m < m1; m++)                                            \
       _Pragma("unroll") for (int nn = 0; nn < 2; nn++) {                                       \
         if ((STAG) && ((c_) % FCYC) == FSP * (m * 2 + nn)) {                                   \
@@ -1161,6 +1162,7 @@ static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_
   (mode == 5 ? (fl == 1 ? k_gram8<5, BLV, 1> : k_gram8<5, BLV, 2>)                              \
    : mode == 6 ? (fl == 1 ? k_gram8<6, BLV, 1> : k_gram8<6, BLV, 2>)                            \
    : mode == 1 ? (fl == 1 ? k_gram8<1, BLV, 1> : k_gram8<1, BLV, 2>)                            \
+   : mode == 7 ? k_gram8<7, BLV, 1> : mode == 8 ? k_gram8<8, BLV, 1>                            \
    : (fl == 1 ? k_gram8<0, BLV, 1> : k_gram8<0, BLV, 2>))
 #else
   (void)mode;
@@ -1258,7 +1260,8 @@ int grid_knn_gram_kb(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t k
   const int64_t q2 = (int64_t)(qmax > 0 ? qmax : 1) * (qmax > 0 ? qmax : 1);
   const int64_t sps_max = ((1ll << 31) - 1) / (q2 * BK);
   const int variant = gram_variant();
-  const int mode = variant == 22 ? 5 : variant == 23 ? 6 : variant == 24 ? 1 : 0;
+  const int mode = variant == 22 ? 5 : variant == 23 ? 6 : variant == 24 ? 1 : variant == 25 ? 7
+                 : variant == 26 ? 8 : 0;
   return launch_gram8(ctx, d_zb, np_, kpad / BK, np_ * BK, q2, sps_max, true, mode, d_gram);
 }
 
