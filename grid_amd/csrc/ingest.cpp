@@ -43,6 +43,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "fastgz.hpp"
 #include "grid_abi.h"
 
 void grid_set_error(const char *fmt, ...);
@@ -159,6 +160,61 @@ inline bool has_high_byte(const char *p, size_t n) {
   return (acc & 0x8080808080808080ull) != 0;
 }
 
+// Whole file into out when it is at most 1 GiB (the libdeflate path holds the
+// compressed and inflated bytes at once; bigger files stream through zlib).
+bool read_small_file(const char *path, std::string &out) {
+  FILE *f = fopen(path, "rb");
+  if (!f) return false;
+  bool ok = fseek(f, 0, SEEK_END) == 0;
+  const long n = ok ? ftell(f) : -1;
+  ok = ok && n > 0 && n <= (1L << 30) && fseek(f, 0, SEEK_SET) == 0;
+  if (ok) {
+    out.resize((size_t)n);
+    ok = fread(&out[0], 1, (size_t)n, f) == (size_t)n;
+  }
+  fclose(f);
+  return ok;
+}
+
+// The line mosdepth writes, "CHROM\tSTART\tEND\tDEPTH" with CHROM printable
+// ASCII without spaces, START/END 1-18 digits and DEPTH D{1,15}(.D{0,2})?,
+// parsed in one pass; false sends the line to the general parser (which
+// decides every other form).  Same values as that parser on these lines.
+inline bool canonical_line(const char *ls, const char *le, const char *&f0e, int64_t &s, int64_t &e,
+                           int64_t &q) {
+  const char *c = ls;
+  while (c < le && (unsigned char)(*c - 0x21) < 0x5e) c++;
+  if (c == ls || c == le || *c != '\t') return false;
+  f0e = c++;
+  int64_t v[2];
+  for (int k = 0; k < 2; k++) {
+    const char *d = c;
+    int64_t x = 0;
+    while (c < le && (unsigned char)(*c - '0') < 10) x = x * 10 + (*c++ - '0');
+    if (c == d || c - d > 18 || c == le || *c != '\t') return false;
+    v[k] = x;
+    c++;
+  }
+  const char *d = c;
+  int64_t ip = 0;
+  while (c < le && (unsigned char)(*c - '0') < 10) ip = ip * 10 + (*c++ - '0');
+  if (c == d || c - d > 15) return false;
+  int64_t fp = 0;
+  if (c < le) {
+    if (*c != '.') return false;
+    c++;
+    const char *f = c;
+    while (c < le && (unsigned char)(*c - '0') < 10) fp = fp * 10 + (*c++ - '0');
+    if (c != le || c - f > 2) return false;
+    if (c - f == 1) fp *= 10;
+  }
+  q = ip * 100 + fp;
+  if (q > 2147483647LL) return false;   // the general parser classifies it
+  s = v[0];
+  e = v[1];
+  return true;
+}
+
 struct Rec {
   int64_t s, e;
   int32_t q;
@@ -177,13 +233,6 @@ void parse_file(const char *path, const Opts &o, std::vector<Rec> &rec, FileRecs
     if (nm == 0) return;                                   // empty file: no lines
     if (nm < 2 || mg[0] != 0x1f || mg[1] != 0x8b) { fr.status = FS_FAILED; fr.why = "not a gzip file"; return; }
   }
-  gzFile f = gzopen(path, "rb");
-  if (!f) { fr.status = FS_FAILED; fr.why = "cannot open"; return; }
-  gzbuffer(f, 1 << 18);
-  const size_t CH = 1 << 22;
-  std::vector<char> buf(CH + 1);
-  size_t have = 0;
-  bool eof = false;
   const char *pre = o.prefix.c_str();
   const size_t npre = o.prefix.size();
   // chromosome-field cache for the mask lookup
@@ -191,6 +240,122 @@ void parse_file(const char *path, const Opts &o, std::vector<Rec> &rec, FileRecs
   const std::vector<int64_t> *lastmask = nullptr;
   bool lastvalid = false;
   int64_t lineno = 0;
+  // Parse the complete lines of [p, end) (and a final unterminated one when
+  // eof); p is left at the first unconsumed byte.  false: fr holds the verdict.
+  auto lines = [&](char *&p, char *end, bool eof) -> bool {
+    for (;;) {
+      char *nl = (char *)memchr(p, '\n', (size_t)(end - p));
+      if (!nl) {
+        if (!eof) break;       // need more bytes for this line
+        if (p == end) break;   // nothing left
+        nl = end;              // last line without '\n'
+      }
+      lineno++;
+      char *ls = p, *le = nl;
+      p = nl < end ? nl + 1 : end;
+      // raw-line prefix test (the line still has its '\n' in Python; the
+      // prefix never contains one)
+      if (npre) {
+        if ((size_t)(le - ls) < npre || memcmp(ls, pre, npre) != 0) continue;
+      }
+      int64_t s, e, q;
+      const char *fs[4], *fe[4];
+      if (canonical_line(ls, le, fe[0], s, e, q)) {
+        fs[0] = ls;
+        goto parsed;
+      }
+      // byte classes: only printable ASCII and tabs take the fast path
+      for (const char *c = ls; c < le; c++) {
+        const unsigned char u = (unsigned char)*c;
+        if (u == '\t') continue;
+        if (u <= 0x20 || u >= 0x7f) {
+          fr.status = FS_EXOTIC;
+          fr.why = "line " + std::to_string(lineno) + ": whitespace/control/non-ASCII byte";
+          return false;
+        }
+      }
+      // strip(): leading/trailing tabs
+      while (ls < le && *ls == '\t') ls++;
+      while (le > ls && le[-1] == '\t') le--;
+      {
+        int nf = 0;
+        const char *c = ls;
+        while (nf < 4) {
+          const char *t = (const char *)memchr(c, '\t', (size_t)(le - c));
+          fs[nf] = c;
+          fe[nf] = t ? t : le;
+          nf++;
+          if (!t) break;
+          c = t + 1;
+        }
+        if (nf < 4) continue;
+        int r1 = parse_int(fs[1], fe[1], &s);
+        int r2 = r1 == 0 ? parse_int(fs[2], fe[2], &e) : 0;
+        int r3 = (r1 == 0 && r2 == 0) ? parse_depth(fs[3], fe[3], &q) : 0;
+        const int r = r1 ? r1 : r2 ? r2 : r3;
+        if (r == 2) {
+          fr.status = FS_EXOTIC;
+          fr.why = "line " + std::to_string(lineno) + ": number outside the strict grammar";
+          return false;
+        }
+        if (r == 1) {   // ValueError in the reference -> whole sample dropped
+          fr.status = FS_FAILED;
+          fr.why = "line " + std::to_string(lineno) + ": invalid number";
+          return false;
+        }
+        if (q > 2147483647LL || q < -2147483647LL) {
+          fr.status = FS_EXOTIC;
+          fr.why = "line " + std::to_string(lineno) + ": depth outside the int32 hundredths range";
+          return false;
+        }
+      }
+    parsed:
+      if (q <= 0) continue;   // depth > 0 (both branches)
+      if (o.window && !(e >= o.start && s <= o.end)) continue;
+      if (!o.mask.empty()) {
+        const size_t l0 = (size_t)(fe[0] - fs[0]);
+        if (!lastvalid || !(lastc.size() == l0 && memcmp(lastc.data(), fs[0], l0) == 0)) {
+          lastc.assign(fs[0], l0);
+          std::string nc = (l0 >= 3 && memcmp(fs[0], "chr", 3) == 0) ? lastc : "chr" + lastc;
+          auto it = o.mask.find(nc);
+          lastmask = it == o.mask.end() ? nullptr : &it->second;
+          lastvalid = true;
+        }
+        if (masked(lastmask, s, e)) continue;
+      }
+      rec.push_back({s, e, (int32_t)q});
+    }
+    return true;
+  };
+  // Fast path: the whole file inflated at once by libdeflate (fastgz.hpp).  Any
+  // failure there (corrupt/truncated stream, no library, a file too large to
+  // hold) falls through to the streaming zlib reader, which decides the verdict.
+  {
+    std::string whole;
+    if (read_small_file(path, whole)) {
+      std::string text;
+      if (fastgz::gunzip_all((const unsigned char *)whole.data(), whole.size(), text)) {
+        std::string().swap(whole);
+        // Python decodes the whole file as UTF-8 text: a byte >= 0x80 anywhere
+        // (even in a line the chromosome filter skips) leaves the fast path
+        if (has_high_byte(text.data(), text.size())) {
+          fr.status = FS_EXOTIC;
+          fr.why = "non-ASCII byte";
+          return;
+        }
+        char *p = text.empty() ? nullptr : &text[0];
+        lines(p, p + text.size(), true);
+        return;
+      }
+    }
+  }
+  gzFile f = gzopen(path, "rb");
+  if (!f) { fr.status = FS_FAILED; fr.why = "cannot open"; return; }
+  gzbuffer(f, 1 << 18);
+  const size_t CH = 1 << 22;
+  std::vector<char> buf(CH + 1);
+  size_t have = 0;
+  bool eof = false;
   while (!eof || have) {
     if (!eof) {
       const int got = gzread(f, buf.data() + have, (unsigned)(CH - have));
@@ -218,85 +383,7 @@ void parse_file(const char *path, const Opts &o, std::vector<Rec> &rec, FileRecs
     }
     char *p = buf.data();
     char *end = p + have;
-    for (;;) {
-      char *nl = (char *)memchr(p, '\n', (size_t)(end - p));
-      if (!nl) {
-        if (!eof) break;       // need more bytes for this line
-        if (p == end) break;   // nothing left
-        nl = end;              // last line without '\n'
-      }
-      lineno++;
-      char *ls = p, *le = nl;
-      p = nl < end ? nl + 1 : end;
-      // raw-line prefix test (the line still has its '\n' in Python; the
-      // prefix never contains one)
-      if (npre) {
-        if ((size_t)(le - ls) < npre || memcmp(ls, pre, npre) != 0) continue;
-      }
-      // byte classes: only printable ASCII and tabs take the fast path
-      for (const char *c = ls; c < le; c++) {
-        const unsigned char u = (unsigned char)*c;
-        if (u == '\t') continue;
-        if (u <= 0x20 || u >= 0x7f) {
-          fr.status = FS_EXOTIC;
-          fr.why = "line " + std::to_string(lineno) + ": whitespace/control/non-ASCII byte";
-          gzclose(f);
-          return;
-        }
-      }
-      // strip(): leading/trailing tabs
-      while (ls < le && *ls == '\t') ls++;
-      while (le > ls && le[-1] == '\t') le--;
-      const char *fs[4], *fe[4];
-      int nf = 0;
-      const char *c = ls;
-      while (nf < 4) {
-        const char *t = (const char *)memchr(c, '\t', (size_t)(le - c));
-        fs[nf] = c;
-        fe[nf] = t ? t : le;
-        nf++;
-        if (!t) break;
-        c = t + 1;
-      }
-      if (nf < 4) continue;
-      int64_t s, e, q;
-      int r1 = parse_int(fs[1], fe[1], &s);
-      int r2 = r1 == 0 ? parse_int(fs[2], fe[2], &e) : 0;
-      int r3 = (r1 == 0 && r2 == 0) ? parse_depth(fs[3], fe[3], &q) : 0;
-      const int r = r1 ? r1 : r2 ? r2 : r3;
-      if (r == 2) {
-        fr.status = FS_EXOTIC;
-        fr.why = "line " + std::to_string(lineno) + ": number outside the strict grammar";
-        gzclose(f);
-        return;
-      }
-      if (r == 1) {   // ValueError in the reference -> whole sample dropped
-        fr.status = FS_FAILED;
-        fr.why = "line " + std::to_string(lineno) + ": invalid number";
-        gzclose(f);
-        return;
-      }
-      if (q > 2147483647LL || q < -2147483647LL) {
-        fr.status = FS_EXOTIC;
-        fr.why = "line " + std::to_string(lineno) + ": depth outside the int32 hundredths range";
-        gzclose(f);
-        return;
-      }
-      if (q <= 0) continue;   // depth > 0 (both branches)
-      if (o.window && !(e >= o.start && s <= o.end)) continue;
-      if (!o.mask.empty()) {
-        const size_t l0 = (size_t)(fe[0] - fs[0]);
-        if (!lastvalid || !(lastc.size() == l0 && memcmp(lastc.data(), fs[0], l0) == 0)) {
-          lastc.assign(fs[0], l0);
-          std::string nc = (l0 >= 3 && memcmp(fs[0], "chr", 3) == 0) ? lastc : "chr" + lastc;
-          auto it = o.mask.find(nc);
-          lastmask = it == o.mask.end() ? nullptr : &it->second;
-          lastvalid = true;
-        }
-        if (masked(lastmask, s, e)) continue;
-      }
-      rec.push_back({s, e, (int32_t)q});
-    }
+    if (!lines(p, end, eof)) { gzclose(f); return; }
     // keep the partial line
     const size_t rest = (size_t)(end - p);
     if (rest && p != buf.data()) memmove(buf.data(), p, rest);
@@ -399,25 +486,75 @@ bool keys_equal(const std::vector<Key> &a, const std::vector<Key> &b) {
   return memcmp(a.data(), b.data(), a.size() * sizeof(Key)) == 0;
 }
 
-// Add one file's depths into the ordered population sums (file order).
-void accumulate(grid_ingest *h, const FileRecs &fr, std::vector<int64_t> &idx) {
-  const std::vector<Key> &fk = *fr.keys;
-  if (!keys_equal(fk, h->K)) {
-    grow_union(h, fk);
-  }
-  if (keys_equal(fk, h->K)) {
-    for (size_t i = 0; i < fk.size(); i++) {
-      h->sums[i] += (double)fr.q[i] / 100.0;   // float("%.2f" text) == q / 100.0 exactly
-      h->cnts[i] += 1;
+// Ordered fp64 population sums (normalize_mosdepth.py:218-301 adds files in
+// order).  Files whose keys are the union K (the usual case: a cohort's
+// mosdepth files share their bins) are queued and added in column blocks by a
+// thread pool, each block walking the queued files in file order: every
+// column sees the same chain of additions as one file at a time, without a
+// serial pass over K per file.  A file with other keys drains the queue first.
+struct Accum {
+  grid_ingest *h;
+  int threads;
+  std::shared_ptr<const std::vector<Key>> same;   // a keys vector known equal to K
+  std::vector<std::pair<FileRecs *, bool>> run;   // (file, drop its records after adding)
+  std::vector<int64_t> idx;
+
+  void add(FileRecs &fr, bool drop) {
+    const std::vector<Key> &fk = *fr.keys;
+    if (fr.keys != same) {
+      if (!keys_equal(fk, h->K)) {
+        drain();
+        grow_union(h, fk);
+        same.reset();
+      }
+      if (!keys_equal(fk, h->K)) {   // a strict subset of K
+        map_keys(fk, h->K, idx);
+        for (size_t i = 0; i < fk.size(); i++) {
+          h->sums[idx[i]] += (double)fr.q[i] / 100.0;   // float("%.2f" text) == q / 100.0 exactly
+          h->cnts[idx[i]] += 1;
+        }
+        if (drop) release(fr);
+        return;
+      }
+      same = fr.keys;
     }
-  } else {
-    map_keys(fk, h->K, idx);
-    for (size_t i = 0; i < fk.size(); i++) {
-      h->sums[idx[i]] += (double)fr.q[i] / 100.0;
-      h->cnts[idx[i]] += 1;
-    }
+    run.emplace_back(&fr, drop);
+    if (run.size() >= 32) drain();
   }
-}
+
+  static void release(FileRecs &fr) {
+    fr.q.clear();
+    fr.q.shrink_to_fit();
+    fr.keys.reset();
+  }
+
+  void drain() {
+    if (run.empty()) return;
+    const int64_t m = (int64_t)h->K.size(), blk = 32768, nb = (m + blk - 1) / blk;
+    std::atomic<int64_t> nx{0};
+    auto work = [&]() {
+      for (;;) {
+        const int64_t b = nx.fetch_add(1);
+        if (b >= nb) return;
+        const int64_t c0 = b * blk, c1 = std::min(m, c0 + blk);
+        double *sm = h->sums.data();
+        for (const auto &f : run) {
+          const int32_t *q = f.first->q.data();
+          for (int64_t c = c0; c < c1; c++) sm[c] += (double)q[c] / 100.0;
+        }
+        for (int64_t c = c0; c < c1; c++) h->cnts[c] += (int64_t)run.size();
+      }
+    };
+    const int T = (int)std::min<int64_t>(threads, nb);
+    std::vector<std::thread> pool;
+    for (int t = 1; t < T; t++) pool.emplace_back(work);
+    work();
+    for (auto &t : pool) t.join();
+    for (auto &f : run)
+      if (f.second) release(*f.first);
+    run.clear();
+  }
+};
 
 }  // namespace
 
@@ -507,7 +644,7 @@ int grid_ingest_mosdepth(const char *const *paths, int64_t n_files, const char *
   std::vector<std::thread> pool;
   for (int t = 0; t < h->threads; t++) pool.emplace_back(worker);
   std::vector<int64_t> idx;
-  std::vector<std::shared_ptr<const std::vector<Key>>> seen_keys;
+  Accum acc{h.get(), h->threads, nullptr, {}, {}};
   for (int64_t i = 0; i < n_files; i++) {
     {
       std::unique_lock<std::mutex> lk(mu);
@@ -516,18 +653,14 @@ int grid_ingest_mosdepth(const char *const *paths, int64_t n_files, const char *
     FileRecs &fr = h->files[i];
     h->status[i] = fr.status;
     h->why[i] = fr.why;
-    if (fr.status == FS_OK) accumulate(h.get(), fr, idx);
     if (fr.status == FS_OK && keep) {
       int64_t b = (int64_t)fr.q.size() * 4;
       if (fr.keys.use_count() <= 2) b += (int64_t)fr.keys->size() * (int64_t)sizeof(Key);
       if (cached_bytes.load() + b > cache_bytes) keep = false;
       else cached_bytes += b;
     }
-    if (!keep) {
-      fr.q.clear();
-      fr.q.shrink_to_fit();
-      fr.keys.reset();
-    }
+    if (fr.status == FS_OK) acc.add(fr, !keep);
+    else Accum::release(fr);
     {
       std::lock_guard<std::mutex> lk(mu);
       consumed = i + 1;
@@ -535,6 +668,8 @@ int grid_ingest_mosdepth(const char *const *paths, int64_t n_files, const char *
     cv_space.notify_all();
   }
   for (auto &t : pool) t.join();
+  acc.drain();
+  acc.same.reset();
   h->cached = keep;
   if (!keep) {
     for (auto &fr : h->files) { fr.q.clear(); fr.keys.reset(); }
@@ -558,12 +693,18 @@ int grid_ingest_mosdepth(const char *const *paths, int64_t n_files, const char *
   }
   // per-file valid-record counts (needed for the empty-sample filter)
   if (h->cached) {
+    // depends on the keys only: once per distinct (shared) key vector
+    const std::vector<Key> *last = nullptr;
+    int64_t c = 0;
     for (int64_t i = 0; i < n_files; i++) {
       FileRecs &fr = h->files[i];
       if (h->status[i] != FS_OK) continue;
-      map_keys(*fr.keys, h->K, idx);
-      int64_t c = 0;
-      for (size_t t = 0; t < idx.size(); t++) c += h->col_of[idx[t]] >= 0;
+      if (fr.keys.get() != last) {
+        map_keys(*fr.keys, h->K, idx);
+        c = 0;
+        for (size_t t = 0; t < idx.size(); t++) c += h->col_of[idx[t]] >= 0;
+        last = fr.keys.get();
+      }
       h->nvalid[i] = c;
     }
   } else {

@@ -28,16 +28,24 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
 
+#include "fastgz.hpp"
 #include "grid_abi.h"
 
 void grid_set_error(const char *fmt, ...);
 
 namespace {
+
+// "00".."99"
+constexpr char kD2[201] =
+    "00010203040506070809101112131415161718192021222324252627282930313233343536373839"
+    "40414243444546474849505152535455565758596061626364656667686970717273747576777879"
+    "8081828384858687888990919293949596979899";
 
 // Append "%.2f" of integer hundredths x at p (<= 13 bytes); returns the new end.
 inline char *put_hundredths(char *p, int32_t x) {
@@ -45,14 +53,20 @@ inline char *put_hundredths(char *p, int32_t x) {
   if (x == GRID_ZQ_NEG0) { memcpy(p, "-0.00", 5); return p + 5; }
   uint32_t a = (uint32_t)x;
   if (x < 0) { *p++ = '-'; a = 0u - a; }
-  uint32_t ip = a / 100, fp = a % 100;
-  char tmp[12];
-  int t = 0;
-  do { tmp[t++] = (char)('0' + ip % 10); ip /= 10; } while (ip);
-  while (t) *p++ = tmp[--t];
+  uint32_t ip = a / 100, fp = a - ip * 100;
+  if (ip < 10) {
+    *p++ = (char)('0' + ip);
+  } else if (ip < 100) {
+    memcpy(p, kD2 + 2 * ip, 2);
+    p += 2;
+  } else {
+    char tmp[12];
+    int t = 0;
+    do { tmp[t++] = (char)('0' + ip % 10); ip /= 10; } while (ip);
+    while (t) *p++ = tmp[--t];
+  }
   p[0] = '.';
-  p[1] = (char)('0' + fp / 10);
-  p[2] = (char)('0' + fp % 10);
+  memcpy(p + 1, kD2 + 2 * fp, 2);
   return p + 3;
 }
 
@@ -79,19 +93,31 @@ inline uint64_t get_le(const unsigned char *p, int nb) {
 }
 
 // One gzip member of `in` with the 'GR' index subfield.
-bool deflate_member(const std::string &in, int level, int64_t first_row, std::string &out) {
-  z_stream s;
-  memset(&s, 0, sizeof s);
-  if (deflateInit2(&s, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) return false;
-  out.resize(GR_HDR + deflateBound(&s, in.size()) + 8 + 64);
-  s.next_in = (Bytef *)in.data();
-  s.avail_in = (uInt)in.size();
-  s.next_out = (Bytef *)&out[GR_HDR];
-  s.avail_out = (uInt)(out.size() - GR_HDR - 8);
-  const int rc = deflate(&s, Z_FINISH);
-  const size_t clen = out.size() - GR_HDR - 8 - s.avail_out;
-  deflateEnd(&s);
-  if (rc != Z_STREAM_END) return false;
+// The body is libdeflate's when it loads (fastgz.hpp; same text, a different
+// and faster deflate stream), zlib's otherwise.
+bool deflate_member(const char *in, size_t n, int level, int64_t first_row, std::string &out) {
+  size_t clen = 0;
+  uLong crc = 0;
+  if (const size_t bound = fastgz::deflate_bound(n)) {
+    out.resize(GR_HDR + bound + 8);
+    clen = fastgz::deflate_into(in, n, level, &out[GR_HDR], bound);
+    if (clen) crc = fastgz::crc32(in, n);
+  }
+  if (!clen) {
+    z_stream s;
+    memset(&s, 0, sizeof s);
+    if (deflateInit2(&s, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) return false;
+    out.resize(GR_HDR + deflateBound(&s, n) + 8 + 64);
+    s.next_in = (Bytef *)in;
+    s.avail_in = (uInt)n;
+    s.next_out = (Bytef *)&out[GR_HDR];
+    s.avail_out = (uInt)(out.size() - GR_HDR - 8);
+    const int rc = deflate(&s, Z_FINISH);
+    clen = out.size() - GR_HDR - 8 - s.avail_out;
+    deflateEnd(&s);
+    if (rc != Z_STREAM_END) return false;
+    crc = crc32(crc32(0L, Z_NULL, 0), (const Bytef *)in, (uInt)n);
+  }
   const size_t total = GR_HDR + clen + 8;
   unsigned char *h = (unsigned char *)&out[0];
   h[0] = 0x1f; h[1] = 0x8b; h[2] = 8; h[3] = 4;          // deflate, FEXTRA
@@ -102,9 +128,8 @@ bool deflate_member(const std::string &in, int level, int64_t first_row, std::st
   put_le(h + 14, 16, 2);
   put_le(h + 16, total, 8);
   put_le(h + 24, (uint64_t)first_row, 8);
-  const uLong crc = crc32(crc32(0L, Z_NULL, 0), (const Bytef *)in.data(), (uInt)in.size());
   put_le(h + GR_HDR + clen, crc, 4);
-  put_le(h + GR_HDR + clen + 4, (uint64_t)in.size() & 0xffffffffu, 4);
+  put_le(h + GR_HDR + clen + 4, (uint64_t)n & 0xffffffffu, 4);
   out.resize(total);
   return true;
 }
@@ -114,7 +139,10 @@ struct NText {
   int64_t n = 0, r = 0;
   std::vector<std::string> ids;
   std::vector<double> scales, means, ratios;
-  std::vector<int32_t> zq;        // [n][r]
+  std::unique_ptr<int32_t[]> zq;  // [n][r]; uninitialised until parsed (every row is, or the read fails)
+  int threads = 1;
+
+  void alloc_zq() { zq.reset(new int32_t[(size_t)(n * r) + 1]); }
 };
 
 // "%.2f"-grammar token -> hundredths; false if the token leaves the grammar.
@@ -170,10 +198,28 @@ bool parse_rows(NText &t, const char *b, const char *e, int64_t row0, std::strin
     bool ok = true;
     t.scales[row] = parse_float(p, se, ok);
     if (!ok) { why = "bad scale"; return false; }
-    int32_t *z = t.zq.data() + row * t.r;
+    int32_t *z = t.zq.get() + row * t.r;
     int64_t c = 0;
     p = tab ? tab + 1 : le;
     while (tab && p <= le && c < t.r) {
+      // the writer's own form, -?D{1,7}.DD then a tab or the line end, in one
+      // pass; anything else takes the general token parser below
+      {
+        const char *x = p;
+        const bool neg = x < le && *x == '-';
+        x += neg;
+        const char *d = x;
+        uint32_t ip = 0;
+        while (x < le && x - d < 7 && (unsigned char)(*x - '0') < 10) ip = ip * 10 + (uint32_t)(*x++ - '0');
+        if (x != d && le - x >= 3 && x[0] == '.' && (unsigned char)(x[1] - '0') < 10 &&
+            (unsigned char)(x[2] - '0') < 10 && (x + 3 == le || x[3] == '\t')) {
+          const int32_t a = (int32_t)(ip * 100 + (uint32_t)(x[1] - '0') * 10 + (uint32_t)(x[2] - '0'));
+          z[c++] = neg ? -a : a;
+          if (x + 3 == le) break;
+          p = x + 4;
+          continue;
+        }
+      }
       const char *q = (const char *)memchr(p, '\t', (size_t)(le - p));
       const char *te = q ? q : le;
       if (!parse_hundredths(p, te, z[c])) { why = "z value outside the %.2f grammar"; return false; }
@@ -188,10 +234,12 @@ bool parse_rows(NText &t, const char *b, const char *e, int64_t row0, std::strin
   return true;
 }
 
-// Inflate one complete gzip member [p, p + len) (CRC-checked by zlib).
+// Inflate one complete gzip member [p, p + len) (CRC-checked; libdeflate when
+// it loads, zlib for anything it rejects).
 bool inflate_member(const unsigned char *p, size_t len, std::string &out) {
   if (len < 18) return false;
   const size_t isize = (size_t)get_le(p + len - 4, 4);
+  if (fastgz::gunzip_one(p, len, isize, out)) return true;
   out.resize(isize);
   z_stream s;
   memset(&s, 0, sizeof s);
@@ -287,6 +335,8 @@ int grid_write_normalized_gz(const char *path, int64_t n, int64_t r, const char 
   const int64_t window = 2 * T + 2;
   auto worker = [&]() {
     std::string text, gz;
+    std::unique_ptr<char[]> rowbuf;   // row text, written in place (no zero fill)
+    size_t rowcap = 0;
     for (;;) {
       const int64_t k = next.fetch_add(1);
       if (k >= nchunks || failed) return;
@@ -294,8 +344,10 @@ int grid_write_normalized_gz(const char *path, int64_t n, int64_t r, const char 
         std::unique_lock<std::mutex> lk(mu);
         cv_room.wait(lk, [&] { return k < written + window || failed; });
       }
-      text.clear();
+      const char *body = nullptr;
+      size_t blen = 0;
       if (k == 0) {
+        text.clear();
         for (int h = 0; h < 2; h++) {
           // f"{N}\t{R}\t" + "\t".join(values): the tab after R is there even when R == 0
           text += std::to_string(n) + '\t' + std::to_string(r) + '\t';
@@ -307,26 +359,37 @@ int grid_write_normalized_gz(const char *path, int64_t n, int64_t r, const char 
           }
           text += '\n';
         }
+        body = text.data();
+        blen = text.size();
       } else {
         const int64_t r0 = (k - 1) * rpc, r1 = std::min(n, r0 + rpc);
+        size_t need = 0;
+        for (int64_t i = r0; i < r1; i++) need += (size_t)(ide[i] - idb[i]) + 400 + 14 * (size_t)r + 1;
+        if (need > rowcap) {
+          rowbuf.reset(new char[need]);
+          rowcap = need;
+        }
+        char *p = rowbuf.get();
         for (int64_t i = r0; i < r1; i++) {
-          text.append(idb[i], ide[i]);
-          text += '\t';
-          put_fixed(text, raw[i], 2);
-          text += '\t';
+          memcpy(p, idb[i], (size_t)(ide[i] - idb[i]));
+          p += ide[i] - idb[i];
+          *p++ = '\t';
+          text.clear();
+          put_fixed(text, raw[i], 2);   // <= 312 bytes
+          memcpy(p, text.data(), text.size());
+          p += text.size();
+          *p++ = '\t';
           const int32_t *z = zq + i * ld_zq;
-          const size_t at = text.size();
-          text.resize(at + 14 * (size_t)r + 1);
-          char *p = &text[at];
           for (int64_t c = 0; c < r; c++) {
             if (c) *p++ = '\t';
             p = put_hundredths(p, z[c]);
           }
           *p++ = '\n';
-          text.resize((size_t)(p - text.data()));
         }
+        body = rowbuf.get();
+        blen = (size_t)(p - rowbuf.get());
       }
-      if (!deflate_member(text, level, k == 0 ? -1 : (k - 1) * rpc, gz)) failed = true;
+      if (!deflate_member(body, blen, level, k == 0 ? -1 : (k - 1) * rpc, gz)) failed = true;
       {
         std::lock_guard<std::mutex> lk(mu);
         done[k].swap(gz);
@@ -398,7 +461,8 @@ int grid_read_normalized_gz(const char *path, int32_t threads, void **h_out, int
       if (ok) {
         t->ids.resize((size_t)t->n);
         t->scales.assign((size_t)t->n, 0.0);
-        t->zq.assign((size_t)(t->n * t->r), 0);
+        t->alloc_zq();
+        t->threads = std::max(1, (int)threads);
         std::atomic<size_t> next{1};
         std::atomic<int64_t> rows{0};
         std::atomic<bool> bad{false};
@@ -478,7 +542,8 @@ int grid_read_normalized_gz(const char *path, int32_t threads, void **h_out, int
   }
   t->ids.resize((size_t)t->n);
   t->scales.assign((size_t)t->n, 0.0);
-  t->zq.assign((size_t)(t->n * t->r), 0);
+  t->alloc_zq();
+  t->threads = std::max(1, (int)threads);
   // blocks of whole lines -> worker threads
   struct Block { std::string text; int64_t row0; };
   std::deque<Block> q;
@@ -587,7 +652,19 @@ int grid_ntext_fetch(const void *h, char *ids_nl, int64_t ids_cap, double *scale
   if (scales) memcpy(scales, t->scales.data(), t->scales.size() * sizeof(double));
   if (means) memcpy(means, t->means.data(), t->means.size() * sizeof(double));
   if (ratios) memcpy(ratios, t->ratios.data(), t->ratios.size() * sizeof(double));
-  if (zq) memcpy(zq, t->zq.data(), t->zq.size() * sizeof(int32_t));
+  if (zq) {   // threaded copy: the matrix is tens of GB at 50k samples
+    const size_t tot = (size_t)(t->n * t->r), blk = (size_t)1 << 24;
+    const size_t nb = (tot + blk - 1) / blk;
+    std::atomic<size_t> nx{0};
+    auto work = [&]() {
+      for (size_t b; (b = nx.fetch_add(1)) < nb;)
+        memcpy(zq + b * blk, t->zq.get() + b * blk, std::min(blk, tot - b * blk) * sizeof(int32_t));
+    };
+    std::vector<std::thread> pool;
+    for (int i = 1; i < std::min<int>(t->threads, (int)nb); i++) pool.emplace_back(work);
+    work();
+    for (auto &th : pool) th.join();
+  }
   return GRID_OK;
 }
 

@@ -206,3 +206,39 @@ def test_truncated_and_garbage_gzip_drop_sample(tmp_path):
     a, b = _both(d, ["A", "B", "C"])
     _same(a, b)
     assert a[0] == ["A", "C"]
+
+
+_ZLIB_ONLY = r'''
+import sys, numpy as np
+from grid_amd import _abi
+paths = sys.argv[2:]
+ing = _abi.Ingest(paths, None, None, {}, 20, 100, threads=2)
+rof = np.where(ing.status == ing.status[0], np.arange(len(paths)), -1).astype(np.int32)
+np.save(sys.argv[1], np.concatenate([ing.status.astype(np.int32), ing.fill(rof).ravel()]))
+'''
+
+
+def test_libdeflate_and_zlib_paths_agree(tmp_path):
+    """The whole-file libdeflate inflate (fastgz.hpp) and the streaming zlib
+    reader (GRID_NO_LIBDEFLATE=1, a fresh process) give identical matrices,
+    for single- and multi-member files and a truncated one."""
+    import subprocess
+    import sys
+    rng = np.random.default_rng(7)
+    d = tmp_path / "md"
+    d.mkdir()
+    _write(d / "A.regions.bed.gz", _rand_lines(rng, 1500))
+    _write(d / "B.regions.bed.gz", _rand_lines(rng, 1500), members=4)
+    _write(d / "C.regions.bed.gz", _rand_lines(rng, 1500))
+    blob = (d / "C.regions.bed.gz").read_bytes()
+    (d / "C.regions.bed.gz").write_bytes(blob[: len(blob) - 9])            # truncated trailer
+    paths = [str(d / f"{s}.regions.bed.gz") for s in "ABC"]
+    ing = _abi.Ingest(paths, None, None, {}, 20, 100, threads=2)
+    assert ing.status[0] == ing.status[1] != ing.status[2]       # C dropped on both paths
+    rof = np.array([0, 1, -1], dtype=np.int32)
+    fast = np.concatenate([ing.status.astype(np.int32), ing.fill(rof).ravel()])
+    out = tmp_path / "zlib.npy"
+    env = dict(os.environ, GRID_NO_LIBDEFLATE="1")
+    subprocess.run([sys.executable, "-c", _ZLIB_ONLY, str(out), *paths], check=True, env=env,
+                   cwd=os.path.dirname(os.path.dirname(__file__)))
+    assert np.array_equal(fast, np.load(out))
