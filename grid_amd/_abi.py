@@ -95,6 +95,8 @@ _SIGS = {
     "grid_norm_col_vars_q16": [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
     "grid_norm_zquant_kb_q16": [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _f64, _vp, _i64, _vp, _i32,
                                 _vp, _i64, C.POINTER(_i32)],
+    "grid_norm_zquant_kb16_q16": [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _f64, _vp, _i64, _vp, _i32,
+                                  _vp, _i64, _vp, _vp, _i64, C.POINTER(_i64), C.POINTER(_i32)],
     "grid_synth_depth": [_vp, C.c_uint64, _i64, _i64, _i64, _i64, _i32, _vp],
     "grid_format_hundredths": [_vp, _i64, _vp, _i64, C.POINTER(_i64)],
     "grid_ingest_mosdepth": [_vp, _i64, C.c_char_p, C.c_int, _i64, _i64, _i64, _vp, _vp, _vp, _f64, _f64,

@@ -116,6 +116,19 @@ __device__ __attribute__((noinline)) int32_t q16_slow(uint32_t v, int64_t i, int
   }
   return (lo < end && s.ecol[lo] == j) ? s.eval[lo] : GRID_MISSING;
 }
+// The same lookup inlined (no call: a call site makes the compiler keep the
+// caller's live registers across the call ABI); for rarely taken branches of
+// tight loops.
+__device__ __forceinline__ int32_t q16_lookup(int64_t i, int64_t j, const Q16 &s) {
+  int64_t lo = s.eoff[i], hi = s.eoff[i + 1];
+  const int64_t end = hi;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (s.ecol[mid] < j) lo = mid + 1;
+    else hi = mid;
+  }
+  return (lo < end && s.ecol[lo] == j) ? s.eval[lo] : GRID_MISSING;
+}
 __device__ __forceinline__ int32_t q16_val(uint32_t v, int64_t i, int64_t j, const Q16 &s) {
   return v <= GRID_Q16_MAXV ? (int32_t)v : q16_slow(v, i, j, s);
 }

@@ -20,65 +20,17 @@ __device__ __forceinline__ double qval(int32_t q) {
   return q == GRID_MISSING ? 0.0 : div100_exact(q);
 }
 
-// ---- full 8192-element blocks: one 256-thread workgroup per (row, block) ----
-// 64 leaves x 8 chains = 512 chains, 2 per thread; leaf results combined in
-// the fixed binary tree of pairwise(8192).
-// SRC: 0 = int32 (int4 loads), 1 = int32 (scalar loads), 2 = compact uint16 (s16),
-// 3 = int32 (streaming / nontemporal int4 loads; GRID_ROWBLK_NT A/B)
-constexpr bool ROWBLK_NT = true;   // default for GRID_ROWBLK_NT
-template <int SRC>
-__global__ __launch_bounds__(256) void k_row_blocks_full(const int32_t *__restrict__ q, Q16 s16, int64_t ld,
-                                                         int64_t nblk_full, int64_t nblk,
-                                                         double *__restrict__ bsum,
-                                                         int32_t *__restrict__ bcnt) {
-  __shared__ int32_t s_q[64 * LEAF_PAD];
-  __shared__ double s_leaf[64];
-  __shared__ int s_cnt[4];
-  const int64_t b = blockIdx.x;
-  const int64_t row = blockIdx.y;
+// The block's int32 values are in s_q (leaf-padded); cnt = this thread's
+// count of non-missing values.  Leaf chains, the fixed pairwise tree, and
+// the (row, block) outputs.  Ends with every LDS read done (the caller may
+// refill s_q after a __syncthreads()).
+// T / DEC: the LDS element type and its value, dec(code, element) -> double
+// (int32 hundredths: qval; compact codes: decoded in place).
+template <class T, class DEC, int UNR = 16>
+__device__ __forceinline__ void rb_finish(const T *s_q, const DEC &dec, double *s_leaf, int *s_cnt, int cnt,
+                                          int64_t row, int64_t b, int64_t nblk, double *__restrict__ bsum,
+                                          int32_t *__restrict__ bcnt) {
   const int tid = threadIdx.x;
-  int cnt = 0;
-  if constexpr (SRC == 2) {
-    const uint4 *src = reinterpret_cast<const uint4 *>(s16.q + row * ld + b * BLK);
-#pragma unroll
-    for (int it = 0; it < 4; it++) {
-      const int e8 = it * 256 + tid;         // 8-value group within the block
-      const uint4 u = src[e8];
-      const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
-      int32_t v[8];
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const uint32_t c = (wd[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
-        v[k] = q16_val(c, row, b * BLK + e8 * 8 + k, s16);
-        cnt += v[k] != GRID_MISSING;
-      }
-      const int e = e8 * 8;
-      const int leaf = e >> 7, w = e & 127;
-      *reinterpret_cast<int4 *>(&s_q[leaf * LEAF_PAD + w]) = make_int4(v[0], v[1], v[2], v[3]);
-      *reinterpret_cast<int4 *>(&s_q[leaf * LEAF_PAD + w + 4]) = make_int4(v[4], v[5], v[6], v[7]);
-    }
-  } else {
-    const int32_t *srcp = q + row * ld + b * BLK;
-    const int4 *src = reinterpret_cast<const int4 *>(srcp);
-#pragma unroll
-    for (int it = 0; it < 8; it++) {
-      int e4 = it * 256 + tid;                 // int4 index within block
-      int4 v;
-      if (SRC == 0) {
-        v = src[e4];
-      } else if (SRC == 3) {
-        typedef int v4i __attribute__((ext_vector_type(4)));
-        const v4i t = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(src) + e4);
-        v = make_int4(t.x, t.y, t.z, t.w);
-      } else {
-        v.x = srcp[4 * e4]; v.y = srcp[4 * e4 + 1]; v.z = srcp[4 * e4 + 2]; v.w = srcp[4 * e4 + 3];
-      }
-      int e = e4 * 4;
-      int leaf = e >> 7, w = e & 127;
-      *reinterpret_cast<int4 *>(&s_q[leaf * LEAF_PAD + w]) = v;
-      cnt += (v.x != GRID_MISSING) + (v.y != GRID_MISSING) + (v.z != GRID_MISSING) + (v.w != GRID_MISSING);
-    }
-  }
   // wave-level count reduction
   for (int o = 32; o > 0; o >>= 1) cnt += __shfl_down(cnt, o, 64);
   if ((tid & 63) == 0) s_cnt[tid >> 6] = cnt;
@@ -88,10 +40,10 @@ __global__ __launch_bounds__(256) void k_row_blocks_full(const int32_t *__restri
   for (int c = 0; c < 2; c++) {
     int chain = tid + c * 256;
     int leaf = chain >> 3, j = chain & 7;
-    const int32_t *lp = &s_q[leaf * LEAF_PAD + j];
-    double acc = qval(lp[0]);
-#pragma unroll
-    for (int s = 1; s < 16; s++) acc = acc + qval(lp[8 * s]);
+    const T *lp = &s_q[leaf * LEAF_PAD + j];
+    double acc = dec(lp[0], leaf * LEAF + j);
+#pragma unroll(UNR)
+    for (int s = 1; s < 16; s++) acc = acc + dec(lp[8 * s], leaf * LEAF + j + 8 * s);
     r[c] = acc;
   }
   // combine the 8 chains of each leaf (8 consecutive lanes)
@@ -120,6 +72,110 @@ __global__ __launch_bounds__(256) void k_row_blocks_full(const int32_t *__restri
     if (tid == 0) {
       bsum[row * nblk + b] = v5;
       bcnt[row * nblk + b] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+    }
+  }
+}
+
+// ---- full 8192-element blocks: one 256-thread workgroup per (row, block) ----
+// 64 leaves x 8 chains = 512 chains, 2 per thread; leaf results combined in
+// the fixed binary tree of pairwise(8192).
+// SRC: 0 = int32 (int4 loads), 1 = int32 (scalar loads), 3 = int32 (streaming / nontemporal int4 loads; GRID_ROWBLK_NT A/B)
+constexpr bool ROWBLK_NT = true;   // default for GRID_ROWBLK_NT
+template <int SRC>
+__global__ __launch_bounds__(256) void k_row_blocks_full(const int32_t *__restrict__ q, Q16 s16, int64_t ld,
+                                                         int64_t nblk_full, int64_t nblk,
+                                                         double *__restrict__ bsum,
+                                                         int32_t *__restrict__ bcnt) {
+  __shared__ int32_t s_q[64 * LEAF_PAD];
+  __shared__ double s_leaf[64];
+  __shared__ int s_cnt[4];
+  const int64_t b = blockIdx.x;
+  const int64_t row = blockIdx.y;
+  const int tid = threadIdx.x;
+  int cnt = 0;
+  {
+    const int32_t *srcp = q + row * ld + b * BLK;
+    const int4 *src = reinterpret_cast<const int4 *>(srcp);
+#pragma unroll
+    for (int it = 0; it < 8; it++) {
+      int e4 = it * 256 + tid;                 // int4 index within block
+      int4 v;
+      if (SRC == 0) {
+        v = src[e4];
+      } else if (SRC == 3) {
+        typedef int v4i __attribute__((ext_vector_type(4)));
+        const v4i t = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(src) + e4);
+        v = make_int4(t.x, t.y, t.z, t.w);
+      } else {
+        v.x = srcp[4 * e4]; v.y = srcp[4 * e4 + 1]; v.z = srcp[4 * e4 + 2]; v.w = srcp[4 * e4 + 3];
+      }
+      int e = e4 * 4;
+      int leaf = e >> 7, w = e & 127;
+      *reinterpret_cast<int4 *>(&s_q[leaf * LEAF_PAD + w]) = v;
+      cnt += (v.x != GRID_MISSING) + (v.y != GRID_MISSING) + (v.z != GRID_MISSING) + (v.w != GRID_MISSING);
+    }
+  }
+  rb_finish(s_q, [](int32_t v, int) { return qval(v); }, s_leaf, s_cnt, cnt, row, b, nblk, bsum, bcnt);
+}
+
+// ---- compact codes: PB consecutive full blocks per workgroup ----
+// The codes stay uint16 in LDS (17 KiB per block image instead of 35 KiB of
+// decoded int32: twice the resident workgroups, so one workgroup's loads
+// overlap another's chain sums) and are decoded where the chains read them;
+// an escape (rare) is looked up out of line.  PB blocks' codes are loaded up
+// front (PB x 4 uint4 per thread).
+constexpr int RB16_PB = 1;   // default for GRID_ROWBLK16_PB (timing only)
+template <int PB, bool NT>
+__global__ __launch_bounds__(256) void k_row_blocks16(Q16 s16, int64_t ld, int64_t nblk_full, int64_t nblk,
+                                                      double *__restrict__ bsum, int32_t *__restrict__ bcnt) {
+  __shared__ __attribute__((aligned(16))) uint16_t s_q[64 * LEAF_PAD];
+  __shared__ double s_leaf[64];
+  __shared__ int s_cnt[4];
+  const int64_t row = blockIdx.y, b0 = (int64_t)blockIdx.x * PB;
+  const int tid = threadIdx.x;
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  v4u raw[PB][4];
+#pragma unroll
+  for (int h = 0; h < PB; h++) {
+    const v4u *src = reinterpret_cast<const v4u *>(s16.q + row * ld + (b0 + h) * BLK);
+    if (b0 + h < nblk_full) {
+#pragma unroll
+      for (int it = 0; it < 4; it++) {
+        if constexpr (NT) raw[h][it] = __builtin_nontemporal_load(src + it * 256 + tid);
+        else raw[h][it] = src[it * 256 + tid];
+      }
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < PB; h++) {
+    const int64_t b = b0 + h;
+    if (b >= nblk_full) break;                      // workgroup-uniform
+    if (h > 0) __syncthreads();                     // the previous block's LDS reads are done
+    int cnt = 0, special = 0;
+#pragma unroll
+    for (int it = 0; it < 4; it++) {
+      const int e = (it * 256 + tid) * 8;           // first of this thread's 8 codes
+      const v4u u = raw[h][it];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint32_t c = (u[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+        cnt += c != GRID_Q16_MISS;
+        special |= c > GRID_Q16_MAXV;
+      }
+      *reinterpret_cast<v4u *>(&s_q[(e >> 7) * LEAF_PAD + (e & 127)]) = u;
+    }
+    // blocks without a missing cell or an escape (the common case) read the
+    // codes as plain hundredths
+    if (__builtin_expect(!__syncthreads_or(special), 1)) {
+      rb_finish(s_q, [](uint16_t c, int) { return div100_exact((int32_t)c); }, s_leaf, s_cnt, cnt, row, b, nblk,
+                bsum, bcnt);
+    } else {
+      const int64_t c0 = b * BLK;
+      auto dec = [&](uint16_t c, int e) -> double {
+        if (c == GRID_Q16_ESC) return qval(q16_lookup(row, c0 + e, s16));
+        return c == GRID_Q16_MISS ? 0.0 : div100_exact((int32_t)c);
+      };
+      rb_finish<uint16_t, decltype(dec), 1>(s_q, dec, s_leaf, s_cnt, cnt, row, b, nblk, bsum, bcnt);   // rare
     }
   }
 }
@@ -223,9 +279,14 @@ __device__ __forceinline__ bool yval(int32_t qv, double rm, double ri, double &y
   return true;
 }
 
-__global__ void k_recip(const double *__restrict__ v, int64_t n, double *__restrict__ r) {
+// bad (optional): 1 for a row whose mean is 0 or NaN (its cells are skipped),
+// so the column kernels test 8 rows with one 8-byte load
+__global__ void k_recip(const double *__restrict__ v, int64_t n, double *__restrict__ r, uint8_t *__restrict__ bad) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) r[i] = 1.0 / v[i];
+  if (i < n) {
+    r[i] = 1.0 / v[i];
+    if (bad) bad[i] = !(v[i] != 0.0 && v[i] == v[i]);
+  }
 }
 
 constexpr int CU = 8;   // rows unrolled per iteration in the column kernels
@@ -233,18 +294,35 @@ constexpr int CU = 8;   // rows unrolled per iteration in the column kernels
 // VW adjacent columns per thread, sequential over rows: int4 loads of int32
 // (VW == 4), or one 8-B load of 4 compact uint16 values (S16).
 constexpr bool COL_NT = true;   // default for GRID_COL_NT
-template <int VW, bool S16, bool NTL = false>
+constexpr int COL16_VW = 2;     // default for GRID_COL16_VW (compact codes)
+// CHECK = false (compact codes): the raw codes only, so a group of rows can
+// be loaded before any value is inspected; fix16() then decodes the group.
+template <int VW, bool S16, bool NTL = false, bool CHECK = true>
 __device__ __forceinline__ void load_row(const int32_t *__restrict__ q, const Q16 &s16, int64_t i, int64_t ld,
                                          int64_t j0, int32_t (&v)[VW]) {
   if constexpr (S16) {
-    static_assert(VW == 4, "compact rows load 4 columns (8 bytes)");
-    const uint2 u = *reinterpret_cast<const uint2 *>(s16.q + i * ld + j0);
-    v[0] = (int32_t)(u.x & 0xFFFFu); v[1] = (int32_t)(u.x >> 16);
-    v[2] = (int32_t)(u.y & 0xFFFFu); v[3] = (int32_t)(u.y >> 16);
-    // rare: missing cells and escapes (one out-of-line loop, not per element)
-    if (__builtin_expect(max(max(v[0], v[1]), max(v[2], v[3])) > GRID_Q16_MAXV, 0)) {
+    // 2 (VW 1), 4 (VW 2) or 8 (VW 4) bytes of uint16 codes per row
+    static_assert(VW == 1 || VW == 2 || VW == 4, "compact rows load 1, 2 or 4 columns");
+    const uint16_t *p = s16.q + i * ld + j0;
+    if constexpr (VW == 4) {
+      const uint2 u = *reinterpret_cast<const uint2 *>(p);
+      v[0] = (int32_t)(u.x & 0xFFFFu); v[1] = (int32_t)(u.x >> 16);
+      v[2] = (int32_t)(u.y & 0xFFFFu); v[3] = (int32_t)(u.y >> 16);
+    } else if constexpr (VW == 2) {
+      const uint32_t u = NTL ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(p))
+                             : *reinterpret_cast<const uint32_t *>(p);
+      v[0] = (int32_t)(u & 0xFFFFu); v[1] = (int32_t)(u >> 16);
+    } else {
+      v[0] = (int32_t)(NTL ? __builtin_nontemporal_load(p) : *p);
+    }
+    if constexpr (!CHECK) return;
+    // rare: missing cells and escapes (one out-of-line call, not per element)
+    int32_t mx = v[0];
 #pragma unroll
-      for (int k = 0; k < 4; k++)
+    for (int k = 1; k < VW; k++) mx = max(mx, v[k]);
+    if (__builtin_expect(mx > GRID_Q16_MAXV, 0)) {
+#pragma unroll
+      for (int k = 0; k < VW; k++)
         if (v[k] > GRID_Q16_MAXV) v[k] = q16_slow((uint32_t)v[k], i, j0 + k, s16);
     }
   } else if constexpr (VW == 4) {
@@ -261,6 +339,53 @@ __device__ __forceinline__ void load_row(const int32_t *__restrict__ q, const Q1
     }
   }
 }
+// Decode a group of CUN rows of raw compact codes (missing -> GRID_MISSING,
+// escapes looked up); one test of the group's largest code on the fast path.
+template <int CUN, int VW>
+__device__ __forceinline__ void fix16(int32_t (&v)[CUN][VW], int64_t i, int64_t j0, const Q16 &s16) {
+  int32_t mx = v[0][0];
+#pragma unroll
+  for (int u = 0; u < CUN; u++)
+#pragma unroll
+    for (int c = 0; c < VW; c++) mx = max(mx, v[u][c]);
+  if (__builtin_expect(mx > GRID_Q16_MAXV, 0)) {
+#pragma unroll
+    for (int u = 0; u < CUN; u++)
+#pragma unroll
+      for (int c = 0; c < VW; c++)
+        if (v[u][c] > GRID_Q16_MAXV)
+          v[u][c] = v[u][c] == GRID_Q16_MISS ? GRID_MISSING : q16_lookup(i + u, j0 + c, s16);
+  }
+}
+
+// True when every cell of a group of CUN rows is an ordinary depth: no
+// missing cell / escape code and every row mean nonzero and not NaN (rm is
+// the same for all lanes: scalar loads).  Such a group needs no per-cell
+// masks: missing cells and zero rows are rare and take the masked path.
+template <bool S16, int CUN, int VW>
+__device__ __forceinline__ bool plain_group(const int32_t (&v)[CUN][VW], const uint8_t *__restrict__ badg) {
+  static_assert(CUN % 8 == 0, "row groups of whole 8-byte flag words");
+  uint64_t bad = 0;                                   // k_recip's row flags, 8 per load (i % 8 == 0)
+#pragma unroll
+  for (int u = 0; u < CUN; u += 8) bad |= *reinterpret_cast<const uint64_t *>(badg + u);
+  const bool rows = bad == 0;
+  if constexpr (S16) {
+    int32_t mx = v[0][0];
+#pragma unroll
+    for (int u = 0; u < CUN; u++)
+#pragma unroll
+      for (int c = 0; c < VW; c++) mx = max(mx, v[u][c]);
+    return rows && mx <= GRID_Q16_MAXV;
+  } else {
+    int32_t mn = v[0][0];
+#pragma unroll
+    for (int u = 0; u < CUN; u++)
+#pragma unroll
+      for (int c = 0; c < VW; c++) mn = min(mn, v[u][c]);
+    return rows && mn != GRID_MISSING;
+  }
+}
+
 template <bool S16>
 __device__ __forceinline__ int32_t q_at(const int32_t *__restrict__ q, const Q16 &s16, int64_t i, int64_t ld,
                                         int64_t j) {
@@ -271,7 +396,8 @@ __device__ __forceinline__ int32_t q_at(const int32_t *__restrict__ q, const Q16
 template <int VW, bool S16, int CUN = CU, bool NTL = false>
 __global__ __launch_bounds__(256) void k_col_means(const int32_t *__restrict__ q, Q16 s16, int64_t n, int64_t m,
                                                    int64_t ld, const double *__restrict__ rm,
-                                                   const double *__restrict__ rinv, double *__restrict__ mu) {
+                                                   const double *__restrict__ rinv, const uint8_t *__restrict__ rbad,
+                                                   double *__restrict__ mu) {
   const int64_t j0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * VW;
   if (j0 >= m) return;
   if (VW > 1 && j0 + VW > m) {   // ragged tail: scalar path
@@ -294,7 +420,20 @@ __global__ __launch_bounds__(256) void k_col_means(const int32_t *__restrict__ q
   for (; i + CUN <= n; i += CUN) {
     int32_t v[CUN][VW];
 #pragma unroll
-    for (int u = 0; u < CUN; u++) load_row<VW, S16, NTL>(q, s16, i + u, ld, j0, v[u]);
+    for (int u = 0; u < CUN; u++) load_row<VW, S16, NTL, false>(q, s16, i + u, ld, j0, v[u]);
+    if (__builtin_expect(plain_group<S16, CUN, VW>(v, rbad + i), 1)) {
+      // every cell valid (the common case): no per-cell masks or counts
+#pragma unroll
+      for (int u = 0; u < CUN; u++) {
+        const double r = rm[i + u], ri = rinv[i + u];
+#pragma unroll
+        for (int c = 0; c < VW; c++) acc[c] = acc[c] + div_exact(div100_exact(v[u][c]), r, ri);
+      }
+#pragma unroll
+      for (int c = 0; c < VW; c++) cnt[c] += CUN;
+      continue;
+    }
+    if constexpr (S16) fix16<CUN, VW>(v, i, j0, s16);
 #pragma unroll
     for (int u = 0; u < CUN; u++) {
       const double r = rm[i + u], ri = rinv[i + u];
@@ -321,7 +460,7 @@ __global__ __launch_bounds__(256) void k_col_means(const int32_t *__restrict__ q
 template <int VW, bool S16, int CUN = CU, bool NTL = false>
 __global__ __launch_bounds__(256) void k_col_vars(const int32_t *__restrict__ q, Q16 s16, int64_t n, int64_t m,
                                                   int64_t ld, const double *__restrict__ rm,
-                                                  const double *__restrict__ rinv,
+                                                  const double *__restrict__ rinv, const uint8_t *__restrict__ rbad,
                                                   const double *__restrict__ mu, double *__restrict__ var,
                                                   double *__restrict__ ratio) {
   const int64_t j0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * VW;
@@ -351,7 +490,22 @@ __global__ __launch_bounds__(256) void k_col_vars(const int32_t *__restrict__ q,
   for (; i + CUN <= n; i += CUN) {
     int32_t v[CUN][VW];
 #pragma unroll
-    for (int u = 0; u < CUN; u++) load_row<VW, S16, NTL>(q, s16, i + u, ld, j0, v[u]);
+    for (int u = 0; u < CUN; u++) load_row<VW, S16, NTL, false>(q, s16, i + u, ld, j0, v[u]);
+    if (__builtin_expect(plain_group<S16, CUN, VW>(v, rbad + i), 1)) {
+      // every cell valid: y is finite, so dd is NaN only when mu_j is, and
+      // then every term is (the sum is reset to nansum's 0 below)
+#pragma unroll
+      for (int u = 0; u < CUN; u++) {
+        const double r = rm[i + u], ri = rinv[i + u];
+#pragma unroll
+        for (int c = 0; c < VW; c++) {
+          const double d = div_exact(div100_exact(v[u][c]), r, ri) - mj[c];
+          acc[c] = acc[c] + d * d;
+        }
+      }
+      continue;
+    }
+    if constexpr (S16) fix16<CUN, VW>(v, i, j0, s16);
 #pragma unroll
     for (int u = 0; u < CUN; u++) {
       const double r = rm[i + u], ri = rinv[i + u];
@@ -379,6 +533,7 @@ __global__ __launch_bounds__(256) void k_col_vars(const int32_t *__restrict__ q,
   }
 #pragma unroll
   for (int c = 0; c < VW; c++) {
+    if (!(mj[c] == mj[c])) acc[c] = 0.0;           // mu NaN: every term was NaN, nansum = 0
     double vv = acc[c] / (double)(n - 1);
     var[j0 + c] = vv;
     ratio[j0 + c] = (mj[c] > 0.0) ? (100.0 * vv) / mj[c] : qnan;
@@ -724,8 +879,11 @@ __device__ __forceinline__ ZT zq_code(int32_t o, int64_t flat, const ZEsc &e, in
 // NT bit 0: streaming (nontemporal) loads of q, read once per launch (reads
 // 10.15 -> 9.77 ms at the bench shape).  Bit 1, nontemporal stores of both
 // outputs, measured slower (18.5 -> 21.1 ms) and is not instantiated.
-template <bool LOOP, class ZT, int NT>
-__global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, int64_t n, int64_t ld,
+// S16: the compact depth matrix (s16; q unused): one 8-B load of 4 uint16
+// codes per row; a missing code decodes to GRID_MISSING inline, an escape
+// (depth > 655.33, rare) is decoded by the deferred loop like an undecided cell.
+template <bool LOOP, class ZT, int NT, bool S16 = false>
+__global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, Q16 s16, int64_t n, int64_t ld,
                                                  const int32_t *__restrict__ sidx,
                                                  const double *__restrict__ rm, const double *__restrict__ rinv,
                                                  const double *__restrict__ mus, const double *__restrict__ sq,
@@ -749,7 +907,23 @@ __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, 
 #pragma unroll
     for (int u = 0; u < ZR; u++) {
       const int64_t i = (i0 + u < r1) ? i0 + u : r0;
-      if (full4) {
+      if constexpr (S16) {
+        uint2 t = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);     // past ld: missing
+        if (full4) {
+          if constexpr (NT & 1) {
+            typedef unsigned v2u __attribute__((ext_vector_type(2)));
+            const v2u x = __builtin_nontemporal_load(reinterpret_cast<const v2u *>(s16.q + i * ld + j0));
+            t = make_uint2(x.x, x.y);
+          } else {
+            t = *reinterpret_cast<const uint2 *>(s16.q + i * ld + j0);
+          }
+        }
+        const uint32_t c0 = t.x & 0xFFFFu, c1 = t.x >> 16, c2 = t.y & 0xFFFFu, c3 = t.y >> 16;
+        v[u].x = c0 == GRID_Q16_MISS ? GRID_MISSING : (int32_t)c0;
+        v[u].y = c1 == GRID_Q16_MISS ? GRID_MISSING : (int32_t)c1;
+        v[u].z = c2 == GRID_Q16_MISS ? GRID_MISSING : (int32_t)c2;
+        v[u].w = c3 == GRID_Q16_MISS ? GRID_MISSING : (int32_t)c3;
+      } else if (full4) {
         if constexpr (NT & 1) {
           typedef int v4i __attribute__((ext_vector_type(4)));
           const v4i t = __builtin_nontemporal_load(reinterpret_cast<const v4i *>(q + i * ld + j0));
@@ -832,7 +1006,8 @@ __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, 
         // int16 output: a value outside the codes goes to the deferred loop
         // too (it records the escape); those cells store a placeholder here
         const bool esc16 = sizeof(ZT) == 2 && o != GRID_ZQ_NEG0 && (o < GRID_ZQ16_MIN || o > GRID_ZQ16_MAX);
-        const bool defer = sk[k] >= 0 && valid && (!good || esc16);
+        const bool escq = S16 && qv[k] > GRID_Q16_MAXV;      // compact escape code: exact value in the table
+        const bool defer = sk[k] >= 0 && valid && (!good || esc16 || escq);
         int32_t code;
         if constexpr (sizeof(ZT) == 2)
           code = !valid ? GRID_ZQ16_NAN : defer ? 0 : o == GRID_ZQ_NEG0 ? GRID_ZQ16_NEG0 : o;
@@ -880,7 +1055,8 @@ __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, 
         const int64_t i = i0 + u;
         const int32_t sc = sel4(sk, k), cc = sel4(ck, k);
         double y;
-        yval(q[i * ld + j0 + k], rm[i], rinv[i], y);
+        if constexpr (S16) yval(q16_val(s16.q[i * ld + j0 + k], i, j0 + k, s16), rm[i], rinv[i], y);
+        else yval(q[i * ld + j0 + k], rm[i], rinv[i], y);
         const double z = div_exact(y - mus[sc], sq[sc], rsq[sc]) * scale;
         int32_t o = GRID_ZQ_NAN, w = 0;
         if (z == z) {
@@ -1031,10 +1207,20 @@ static int row_blocks_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, in
     REQUIRE(n <= 65535, "n > 65535 rows per launch");
     const char *rn = getenv("GRID_ROWBLK_NT");
     const bool nt = rn ? atoi(rn) != 0 : ROWBLK_NT;
-    auto kern = c16 ? k_row_blocks_full<2>
-              : vec4_ok(d_q, ld) ? (nt ? k_row_blocks_full<3> : k_row_blocks_full<0>) : k_row_blocks_full<1>;
-    hipLaunchKernelGGL(kern, dim3((unsigned)nfull, (unsigned)n), dim3(256), 0, ctx->stream, d_q, s16, ld, nfull, nblk,
-                       d_bsum, d_bcnt);
+    if (c16) {
+      const char *pe = getenv("GRID_ROWBLK16_PB");
+      const int pb = pe ? atoi(pe) : RB16_PB;
+      REQUIRE(pb == 1 || pb == 2 || pb == 4, "GRID_ROWBLK16_PB must be 1, 2 or 4 (got %d)", pb);
+      auto kern = pb == 1 ? (nt ? k_row_blocks16<1, true> : k_row_blocks16<1, false>)
+                : pb == 2 ? (nt ? k_row_blocks16<2, true> : k_row_blocks16<2, false>)
+                          : (nt ? k_row_blocks16<4, true> : k_row_blocks16<4, false>);
+      hipLaunchKernelGGL(kern, dim3((unsigned)ceil_div(nfull, pb), (unsigned)n), dim3(256), 0, ctx->stream, s16, ld,
+                         nfull, nblk, d_bsum, d_bcnt);
+    } else {
+      auto kern = vec4_ok(d_q, ld) ? (nt ? k_row_blocks_full<3> : k_row_blocks_full<0>) : k_row_blocks_full<1>;
+      hipLaunchKernelGGL(kern, dim3((unsigned)nfull, (unsigned)n), dim3(256), 0, ctx->stream, d_q, s16, ld, nfull,
+                         nblk, d_bsum, d_bcnt);
+    }
     LAUNCHCHK();
   }
   if (nblk > nfull) {
@@ -1067,15 +1253,20 @@ int grid_norm_row_means(grid_ctx *ctx, const double *d_bsum, const int32_t *d_bc
   return GRID_OK;
 }
 
-static int recip_rows(grid_ctx *ctx, const double *d_rm, int64_t n, size_t extra, double **rinv, char **rest) {
+// Scratch layout: [256 B flags][rinv: n doubles][bad: n + 64 bytes if wanted][extra] -> *rest
+static int recip_rows(grid_ctx *ctx, const double *d_rm, int64_t n, size_t extra, double **rinv, char **rest,
+                      uint8_t **bad = nullptr) {
   void *s = nullptr;
   size_t nb = (((size_t)n * 8 + 255) & ~size_t(255));
-  int rc = grid_scratch(ctx, 256 + nb + extra, &s);
+  size_t bb = bad ? (((size_t)n + 64 + 255) & ~size_t(255)) : 0;
+  int rc = grid_scratch(ctx, 256 + nb + bb + extra, &s);
   if (rc) return rc;
   *rinv = (double *)((char *)s + 256);
-  *rest = (char *)s + 256 + nb;
+  uint8_t *bp = bad ? (uint8_t *)s + 256 + nb : nullptr;
+  if (bad) *bad = bp;
+  *rest = (char *)s + 256 + nb + bb;
   if (n > 0) {
-    hipLaunchKernelGGL(k_recip, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, ctx->stream, d_rm, n, *rinv);
+    hipLaunchKernelGGL(k_recip, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, ctx->stream, d_rm, n, *rinv, bp);
     LAUNCHCHK();
   }
   return GRID_OK;
@@ -1087,7 +1278,8 @@ static int col_stats_impl(grid_ctx *ctx, bool vars, const int32_t *d_q, const Q1
   if (m == 0) return GRID_OK;
   double *rinv;
   char *rest;
-  int rc = recip_rows(ctx, d_rm, n, 0, &rinv, &rest);
+  uint8_t *rbad;
+  int rc = recip_rows(ctx, d_rm, n, 0, &rinv, &rest, &rbad);
   if (rc) return rc;
   // int32: 1 column per thread (47 k waves at the bench shape, ~6 rounds of
   // resident waves; 4 per thread left a 2.3-round tail: 14.5 vs 13.7 ms)
@@ -1098,22 +1290,33 @@ static int col_stats_impl(grid_ctx *ctx, bool vars, const int32_t *d_q, const Q1
   const bool cu16 = cu && atoi(cu) == 16;
 #else
   const int want = 1;
-  const bool cu16 = false;
+  const char *cu = getenv("GRID_COL16_CU");   // compact codes: 16 rows in flight (timing only)
+  const bool cu16 = s16.q && cu && atoi(cu) == 16;
 #endif
   const char *cn = getenv("GRID_COL_NT");   // streaming (nontemporal) loads, 1-column path (A/B)
   const bool nt = cn ? atoi(cn) != 0 : COL_NT;
-  const int vw = s16.q ? 4 : vec4_ok(d_q, ld) ? (want == 4 ? 4 : want == 1 ? 1 : 2) : 1;
+  // compact codes: GRID_COL16_VW columns per thread (1: 2-B loads, 2: 4-B loads, the default; timing only)
+  const char *c16v = getenv("GRID_COL16_VW");
+  const int vw16 = c16v ? atoi(c16v) : COL16_VW;
+  REQUIRE(vw16 == 1 || vw16 == 2 || vw16 == 4, "GRID_COL16_VW must be 1, 2 or 4 (got %d)", vw16);
+  const int vw = s16.q ? vw16 : vec4_ok(d_q, ld) ? (want == 4 ? 4 : want == 1 ? 1 : 2) : 1;
   const dim3 grid((unsigned)ceil_div(ceil_div(m, vw), 256));
   if (!vars) {
-    auto kern = s16.q ? k_col_means<4, true>
+    auto kern = s16.q ? (vw == 4 ? k_col_means<4, true>
+                         : vw == 2 ? (cu16 ? k_col_means<2, true, 16, true>
+                                      : nt ? k_col_means<2, true, CU, true> : k_col_means<2, true>)
+                                   : (nt ? k_col_means<1, true, CU, true> : k_col_means<1, true>))
                 : vw == 4 ? k_col_means<4, false> : vw == 2 ? k_col_means<2, false>
                 : cu16 ? k_col_means<1, false, 16> : nt ? k_col_means<1, false, CU, true> : k_col_means<1, false>;
-    hipLaunchKernelGGL(kern, grid, dim3(256), 0, ctx->stream, d_q, s16, n, m, ld, d_rm, rinv, d_out);
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, ctx->stream, d_q, s16, n, m, ld, d_rm, rinv, rbad, d_out);
   } else {
-    auto kern = s16.q ? k_col_vars<4, true>
+    auto kern = s16.q ? (vw == 4 ? k_col_vars<4, true>
+                         : vw == 2 ? (cu16 ? k_col_vars<2, true, 16, true>
+                                      : nt ? k_col_vars<2, true, CU, true> : k_col_vars<2, true>)
+                                   : (nt ? k_col_vars<1, true, CU, true> : k_col_vars<1, true>))
                 : vw == 4 ? k_col_vars<4, false> : vw == 2 ? k_col_vars<2, false>
                 : cu16 ? k_col_vars<1, false, 16> : nt ? k_col_vars<1, false, CU, true> : k_col_vars<1, false>;
-    hipLaunchKernelGGL(kern, grid, dim3(256), 0, ctx->stream, d_q, s16, n, m, ld, d_rm, rinv, d_mu, d_out,
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, ctx->stream, d_q, s16, n, m, ld, d_rm, rinv, rbad, d_mu, d_out,
                        d_ratio);
   }
   LAUNCHCHK();
@@ -1177,8 +1380,9 @@ static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, int64_
 #else
   const char *zv = nullptr;
 #endif
-  REQUIRE(!d_zq16 || (!s16.q && vec4_ok(d_q, ld)), "int16 z output needs the int32 depth layout (ld % 4 == 0)");
-  if (d_zq16 || (!s16.q && vec4_ok(d_q, ld) && !(zv && atoi(zv) == 4))) {
+  const bool c16 = s16.q != nullptr;
+  REQUIRE(!d_zq16 || c16 || vec4_ok(d_q, ld), "int16 z output needs the int32 depth layout (ld % 4 == 0)");
+  if (d_zq16 || c16 || (vec4_ok(d_q, ld) && !(zv && atoi(zv) == 4))) {
     int32_t *sidx = (int32_t *)(rest + 4 * rb);
     HIPCHK(hipMemsetAsync(sidx, 0xFF, (size_t)ld * 4, ctx->stream));
     hipLaunchKernelGGL(k_sidx, dim3((unsigned)ceil_div(r, 256)), dim3(256), 0, ctx->stream, d_sel, r, sidx);
@@ -1190,17 +1394,18 @@ static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, int64_
     REQUIRE(nt == 0 || nt == 1, "GRID_ZQUANT_NT must be 0 or 1 (got %d)", nt);
     REQUIRE(ceil_div(ceil_div(ld, 4), 256) <= 65535, "ld too large for one launch");
     const dim3 g6((unsigned)ceil_div(n, rpw), (unsigned)ceil_div(ceil_div(ld, 4), 256));
+#define Z6_PICK(ZT, CS) (nt ? (rpw > ZR ? k_zquant6<true, ZT, 1, CS> : k_zquant6<false, ZT, 1, CS>)                    \
+                            : (rpw > ZR ? k_zquant6<true, ZT, 0, CS> : k_zquant6<false, ZT, 0, CS>))
     if (d_zq16) {
-      auto k16 = nt ? (rpw > ZR ? k_zquant6<true, int16_t, 1> : k_zquant6<false, int16_t, 1>)
-                    : (rpw > ZR ? k_zquant6<true, int16_t, 0> : k_zquant6<false, int16_t, 0>);
-      hipLaunchKernelGGL(k16, g6, dim3(256), 0, ctx->stream, d_q, n, ld, sidx, d_rm, rinv, mus, sq, rsq, mc32, scale,
-                         d_zq16, ld_zq, d_colmap, qmax, d_zb, ld_zb, kbs, d_of, rpw, esc);
+      auto k16 = c16 ? Z6_PICK(int16_t, true) : Z6_PICK(int16_t, false);
+      hipLaunchKernelGGL(k16, g6, dim3(256), 0, ctx->stream, d_q, s16, n, ld, sidx, d_rm, rinv, mus, sq, rsq, mc32,
+                         scale, d_zq16, ld_zq, d_colmap, qmax, d_zb, ld_zb, kbs, d_of, rpw, esc);
     } else {
-      auto k32 = nt ? (rpw > ZR ? k_zquant6<true, int32_t, 1> : k_zquant6<false, int32_t, 1>)
-                    : (rpw > ZR ? k_zquant6<true, int32_t, 0> : k_zquant6<false, int32_t, 0>);
-      hipLaunchKernelGGL(k32, g6, dim3(256), 0, ctx->stream, d_q, n, ld, sidx, d_rm, rinv, mus, sq, rsq, mc32, scale,
-                         d_zq, ld_zq, d_colmap, qmax, d_zb, ld_zb, kbs, d_of, rpw, esc);
+      auto k32 = c16 ? Z6_PICK(int32_t, true) : Z6_PICK(int32_t, false);
+      hipLaunchKernelGGL(k32, g6, dim3(256), 0, ctx->stream, d_q, s16, n, ld, sidx, d_rm, rinv, mus, sq, rsq, mc32,
+                         scale, d_zq, ld_zq, d_colmap, qmax, d_zb, ld_zb, kbs, d_of, rpw, esc);
     }
+#undef Z6_PICK
     LAUNCHCHK();
   } else {
   auto kz = s16.q ? k_zquant4<false, true> : vec4_ok(d_q, ld) ? k_zquant4<true, false> : k_zquant4<false, false>;
@@ -1249,6 +1454,19 @@ int grid_norm_zquant_kb16(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t 
           "grid_norm_zquant_kb16: bad escape list / outputs");
   return zquant_impl(ctx, d_q, kNoQ16, n, ld, d_sel, r, d_rm, d_mu, scale, nullptr, ld_zq, d_colmap, qmax, d_zb, 64,
                      np_zb * 64, h_overflow, d_zq16, d_esc_idx, d_esc_val, esc_cap, h_nesc);
+}
+
+int grid_norm_zquant_kb16_q16(grid_ctx *ctx, const grid_depth16 *q, int64_t n, int64_t ld, const int32_t *d_sel,
+                              int64_t r, const double *d_rm, const double *d_mu, double scale, int16_t *d_zq16,
+                              int64_t ld_zq, const int32_t *d_colmap, int32_t qmax, uint16_t *d_zb,
+                              int64_t np_zb, int64_t *d_esc_idx, int32_t *d_esc_val, int64_t esc_cap,
+                              int64_t *h_nesc, int32_t *h_overflow) {
+  REQUIRE(q16_ok(q, ld), "compact matrix: 16-byte aligned q, ld %% 8 == 0 and escape offsets required");
+  REQUIRE(np_zb >= n && np_zb % 64 == 0, "np_zb must be >= n and a multiple of 64");
+  REQUIRE(d_zq16 && h_overflow && h_nesc && esc_cap >= 0 && (esc_cap == 0 || (d_esc_idx && d_esc_val)),
+          "grid_norm_zquant_kb16_q16: bad escape list / outputs");
+  return zquant_impl(ctx, nullptr, to_q16(q), n, ld, d_sel, r, d_rm, d_mu, scale, nullptr, ld_zq, d_colmap, qmax, d_zb,
+                     64, np_zb * 64, h_overflow, d_zq16, d_esc_idx, d_esc_val, esc_cap, h_nesc);
 }
 
 int grid_norm_zquant_kb_q16(grid_ctx *ctx, const grid_depth16 *q, int64_t n, int64_t ld, const int32_t *d_sel,

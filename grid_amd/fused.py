@@ -217,9 +217,15 @@ class HipOps:
         for the rare values outside them.  Returns (overflow bits, escapes);
         bit 1 = the list overflowed (the caller reruns with int32)."""
         of, ne = C.c_int32(), C.c_int64()
-        call("grid_norm_zquant_kb16", self.ctx, ptr(q), n, ld, ptr(sel), r, ptr(rm), ptr(mu), scale, ptr(zq16),
-             ld_zq, ptr(colmap), qmax, ptr(zb), np_zb, ptr(esc_idx), ptr(esc_val),
-             0 if esc_idx is None else esc_idx.numel(), C.byref(ne), C.byref(of))
+        cap = 0 if esc_idx is None else esc_idx.numel()
+        if isinstance(q, Depth16):
+            call("grid_norm_zquant_kb16_q16", self.ctx, C.byref(q.desc), n, q.ld, ptr(sel), r, ptr(rm), ptr(mu),
+                 scale, ptr(zq16), ld_zq, ptr(colmap), qmax, ptr(zb), np_zb, ptr(esc_idx), ptr(esc_val), cap,
+                 C.byref(ne), C.byref(of))
+        else:
+            call("grid_norm_zquant_kb16", self.ctx, ptr(q), n, ld, ptr(sel), r, ptr(rm), ptr(mu), scale, ptr(zq16),
+                 ld_zq, ptr(colmap), qmax, ptr(zb), np_zb, ptr(esc_idx), ptr(esc_val), cap, C.byref(ne),
+                 C.byref(of))
         return of.value, ne.value
 
     def gram(self, zb, np_, kpad, qmax, gram):
@@ -664,7 +670,7 @@ class Steps47:
             zcol, ld_zq = s0, max(self.ml, 1)
         else:
             zcol, ld_zq = 0, rc
-        if self.zq_is16 and not isinstance(q, Depth16) and ldc % 4 == 0:
+        if self.zq_is16 and (isinstance(q, Depth16) or ldc % 4 == 0):
             e0 = self.nesc
             cap = self.esc_idx.numel() - e0
             zt = self.zq16.view(-1)[zcol:]
@@ -681,7 +687,7 @@ class Steps47:
                 return
             if self.nch > 1:
                 raise _abi.GridNativeError(f"more than {cap} int16 escapes (|z| > 327.65) in one chunk")
-        self.zq_is16 = False            # int32 output: no int16 codes (compact / unaligned input, or escapes)
+        self.zq_is16 = False            # int32 output: no int16 codes (unaligned input, or too many escapes)
         if self.zq is None:
             self.zq = self.A.empty(tuple(self.zq16.shape), I4)
         of = o.zquant(qc if not isinstance(q, Depth16) else q, n, ldc, sel_c, rc, self.rm, mu_c, self.scale,

@@ -183,6 +183,14 @@ int grid_norm_zquant_kb_q16(grid_ctx *ctx, const grid_depth16 *q, int64_t n, int
                             const double *d_mu, double scale, int32_t *d_zq, int64_t ld_zq,
                             const int32_t *d_colmap, int32_t qmax, uint16_t *d_zb, int64_t np_zb,
                             int32_t *h_overflow);
+/* grid_norm_zquant_kb16 on the compact depth matrix (ld % 8 == 0): the same
+ * int16 codes, escape list and panel as on the int32 matrix it encodes. */
+int grid_norm_zquant_kb16_q16(grid_ctx *ctx, const grid_depth16 *q, int64_t n, int64_t ld,
+                              const int32_t *d_sel, int64_t r, const double *d_rowmean,
+                              const double *d_mu, double scale, int16_t *d_zq16, int64_t ld_zq,
+                              const int32_t *d_colmap, int32_t qmax, uint16_t *d_zb, int64_t np_zb,
+                              int64_t *d_esc_idx, int32_t *d_esc_val, int64_t esc_cap, int64_t *h_nesc,
+                              int32_t *h_overflow);
 
 /* Verification (tests): recompute every selected cell with plain IEEE fp64
  * in the reference's order and the "%.2f" rule, compare with the int16 codes

@@ -83,10 +83,17 @@ def test_synth_q16_equals_encoded_synth(dev):
     assert torch.equal(d.ecol[:k], ecol) and torch.equal(d.evals[:k], ev)
 
 
-def test_step4_kernels_q16_equal_int32(dev):
-    from grid_amd import _abi
+@pytest.mark.parametrize("knobs", [{}, {"GRID_COL16_VW": "1", "GRID_ROWBLK16_PB": "1"},
+                                   {"GRID_COL16_VW": "4", "GRID_ROWBLK16_PB": "4", "GRID_ROWBLK_NT": "0",
+                                    "GRID_COL_NT": "0", "GRID_ZQUANT_NT": "0"}])
+def test_step4_kernels_q16_equal_int32(dev, knobs, monkeypatch):
+    """Every q16 kernel variant (columns per thread, blocks per workgroup,
+    streaming loads: timing knobs) gives the int32 kernels' bits, including
+    the int16 step-4 codes and their escape list."""
     from grid_amd.fused import Depth16, HipOps
-    n, m = 300, 2 * 8192 + 517
+    for k_, v_ in knobs.items():
+        monkeypatch.setenv(k_, v_)
+    n, m = 300, 5 * 8192 + 516          # ld % 4 == 0: the int32 layout of the int16 output
     q = random_depths(n, m, 2)
     q[:, 100] = MISSING
     qd = torch.from_numpy(q).cuda()
@@ -111,7 +118,15 @@ def test_step4_kernels_q16_equal_int32(dev):
         kp = -(-r // 64) * 64
         zb = torch.zeros((kp // 64, 512, 64), dtype=torch.int16, device="cuda")
         ops.zquant(src, n, ld, sel, r, rm, mu, 1.7, zq, r, colmap, 200, zb, 512)
-        out[name] = [t.cpu().numpy() for t in (bsum, bcnt, rm, mu, var, ratio, zq, zb)]
+        zq16 = torch.zeros((n, r), dtype=torch.int16, device="cuda")
+        zb16 = torch.zeros_like(zb)
+        eidx = torch.zeros(1 << 16, dtype=torch.int64, device="cuda")
+        eval_ = torch.zeros(1 << 16, dtype=torch.int32, device="cuda")
+        of, ne = ops.zquant16(src, n, ld, sel, r, rm, mu, 1.7, zq16, r, colmap, 200, zb16, 512, eidx, eval_)
+        assert of == 0
+        order = torch.argsort(eidx[:ne])
+        esc = (eidx[:ne][order], eval_[:ne][order])
+        out[name] = [t.cpu().numpy() for t in (bsum, bcnt, rm, mu, var, ratio, zq, zb, zq16, zb16) + esc]
     for a, b in zip(out["i32"], out["q16"]):
         assert np.array_equal(a, b, equal_nan=True)
 
