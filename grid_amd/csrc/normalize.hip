@@ -10,6 +10,8 @@
 // Every arithmetic op is an IEEE fp64 +,-,*,/,sqrt with -ffp-contract=off.
 #include "common.hpp"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int BLK = GRID_BLOCK;       // 8192
@@ -555,6 +557,23 @@ __global__ void k_zprep(const int32_t *__restrict__ sel, int64_t r, const double
 }
 
 constexpr int ZR = 8;    // rows per zquant batch
+
+// The row means / reciprocals of rows i0 .. i0+R-1 (clamped to n-1), all
+// loaded before any is used: a load inside the row loop, behind its
+// "row < r1" exit, cannot be hoisted and costs one scalar-load latency per
+// row (the zquant kernels were bound by that chain, not by memory).
+template <int R>
+__device__ __forceinline__ void load_rows(const double *__restrict__ p, int64_t i0, int64_t n, double (&o)[R]) {
+  if (i0 + R <= n) {
+#pragma unroll
+    for (int u = 0; u < R; u++) o[u] = p[i0 + u];
+  } else {
+#pragma unroll
+    for (int u = 0; u < R; u++) o[u] = p[(i0 + u < n) ? i0 + u : n - 1];
+  }
+}
+
+
 constexpr int ZRB = 1;   // row batches per thread (4 measured slower: 22.6 vs 20.5 ms)
 
 // 4 consecutive selected columns x ZR rows per thread.
@@ -902,8 +921,11 @@ __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, 
   const int64_t r0 = (int64_t)blockIdx.x * rpw;
   const int64_t r1 = (r0 + rpw < n) ? r0 + rpw : n;
   const bool full4 = j0 + 4 <= ld;
-  // rows i0 .. i0+ZR-1 of this thread's 4 columns (rows past r1 re-read row r0)
-  auto load_group = [&](int64_t i0, int4 (&v)[ZR]) {
+  // rows i0 .. i0+ZR-1 of this thread's 4 columns (rows past r1 re-read row
+  // r0), raw: int4 of int32 depths or uint2 of 4 compact codes (decoded per
+  // row where it is used, so a prefetched group costs 2 registers per row)
+  typedef typename std::conditional<S16, uint2, int4>::type RawT;
+  auto load_group = [&](int64_t i0, RawT (&v)[ZR]) {
 #pragma unroll
     for (int u = 0; u < ZR; u++) {
       const int64_t i = (i0 + u < r1) ? i0 + u : r0;
@@ -918,11 +940,7 @@ __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, 
             t = *reinterpret_cast<const uint2 *>(s16.q + i * ld + j0);
           }
         }
-        const uint32_t c0 = t.x & 0xFFFFu, c1 = t.x >> 16, c2 = t.y & 0xFFFFu, c3 = t.y >> 16;
-        v[u].x = c0 == GRID_Q16_MISS ? GRID_MISSING : (int32_t)c0;
-        v[u].y = c1 == GRID_Q16_MISS ? GRID_MISSING : (int32_t)c1;
-        v[u].z = c2 == GRID_Q16_MISS ? GRID_MISSING : (int32_t)c2;
-        v[u].w = c3 == GRID_Q16_MISS ? GRID_MISSING : (int32_t)c3;
+        v[u] = t;
       } else if (full4) {
         if constexpr (NT & 1) {
           typedef int v4i __attribute__((ext_vector_type(4)));
@@ -939,8 +957,17 @@ __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, 
       }
     }
   };
-  int4 v[ZR];
-  load_group(r0, v);                        // in flight while the column setup runs
+  auto decode = [&](const RawT &t, int32_t (&qv)[4]) {
+    if constexpr (S16) {
+      const uint32_t c[4] = {t.x & 0xFFFFu, t.x >> 16, t.y & 0xFFFFu, t.y >> 16};
+#pragma unroll
+      for (int k = 0; k < 4; k++) qv[k] = c[k] == GRID_Q16_MISS ? GRID_MISSING : (int32_t)c[k];
+    } else {
+      qv[0] = t.x; qv[1] = t.y; qv[2] = t.z; qv[3] = t.w;
+    }
+  };
+  RawT nx[ZR];
+  load_group(r0, nx);                       // in flight while the column setup runs
   int32_t sk[4], ck[4];
   float m32[4], c32[4], ac[4];
   if (full4) {
@@ -976,16 +1003,23 @@ __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, 
   const float qf = (float)qmax;
   int of = 0;
   for (int64_t i0 = r0; i0 < r1; i0 += ZR) {
-    if (LOOP && i0 != r0) load_group(i0, v);
+    double rmg[ZR], rig[ZR];
+    load_rows(rm, i0, n, rmg);
+    load_rows(rinv, i0, n, rig);
+    RawT v[ZR];
+#pragma unroll
+    for (int u = 0; u < ZR; u++) v[u] = nx[u];
+    if (LOOP && i0 + ZR < r1) load_group(i0 + ZR, nx);   // the next group's loads fly while this one runs
     uint32_t slowm = 0;
 #pragma unroll
     for (int u = 0; u < ZR; u++) {
       const int64_t i = i0 + u;
       if (i >= r1) break;
-      const double rmi = rm[i], rii = rinv[i];
+      const double rmi = rmg[u], rii = rig[u];
       const bool rowok = rmi != 0.0 && rmi == rmi;
       const float a32 = (float)(0.01 * rii);
-      const int32_t qv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+      int32_t qv[4];
+      decode(v[u], qv);
       // used columns need not be contiguous (any colmap): slots no lane fills
       // keep the marker 0xFFFF (a NaN bf16 the conversion never produces) and
       // are not stored
@@ -1074,6 +1108,254 @@ __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, 
       }
     }
     if (!LOOP) break;
+  }
+  if (of) atomicOr(overflow, of);
+}
+
+// ---- zquant over SELECTED columns of the compact matrix (k_zquant7) --------
+// Thread = 4 consecutive selected indices s0..s0+3 x ZR rows.  Its outputs are
+// contiguous: the 4 int16 codes of a row leave as ONE 8-B store, and when the
+// 4 panel columns colmap[s] are consecutive (and 4-aligned) the 4 bf16 values
+// as one 8-B store in their K-block -- no LDS compaction, and unselected
+// source columns are never computed (k_zquant6 computes and drops them: its
+// LDS round trip and dropped cells made it instruction-bound, ~9.7 ms of its
+// 17.4 at the bench shape with every store removed).  The 4 source columns
+// sel[s] usually lie in the 8 codes at base = sel[s0] & ~3: two aligned 8-B
+// loads per row and a register pick (bfe); other lanes gather per cell.
+// Fast path, acceptance test and deferred exact chain: as zquant_rows.
+// PROBE (tools build only, wrong results): bit 0 no z stores, bit 1 no panel
+// stores, bit 2 no loads (codes from a constant).
+template <int NT, int PROBE = 0>
+__global__ __launch_bounds__(256) void k_zquant7(Q16 s16, int64_t n, int64_t ld, const int32_t *__restrict__ sel,
+                                                 int64_t r, const double *__restrict__ rm,
+                                                 const double *__restrict__ rinv, const double *__restrict__ mus,
+                                                 const double *__restrict__ sq, const double *__restrict__ rsq,
+                                                 const float2 *__restrict__ mc32, double scale,
+                                                 int16_t *__restrict__ zq, int64_t ld_zq,
+                                                 const int32_t *__restrict__ colmap, int32_t qmax,
+                                                 uint16_t *__restrict__ zb, int64_t ld_zb, int64_t kbs,
+                                                 int32_t *__restrict__ overflow, int rpw, ZEsc esc) {
+  const int64_t s0 = ((int64_t)blockIdx.y * 256 + threadIdx.x) * 4;
+  if (s0 >= r) return;
+  const int w = (int)((r - s0) < 4 ? (r - s0) : 4);
+  const int64_t r0 = (int64_t)blockIdx.x * rpw;
+  const int64_t r1 = (r0 + rpw < n) ? r0 + rpw : n;
+  int64_t js[4];
+  int32_t cm[4];
+  float m32[4], c32[4], ac[4];
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const bool ok = c < w;
+    js[c] = sel[ok ? s0 + c : s0];
+    cm[c] = ok ? (colmap ? colmap[s0 + c] : (int32_t)(s0 + c)) : -1;
+    const float2 mc = ok ? mc32[s0 + c] : make_float2(1.0f, 1.0f);
+    m32[c] = mc.x;
+    c32[c] = mc.y;
+    ac[c] = 0x1p-21f * fabsf(mc.y);
+  }
+  // the lane's window: the 12 codes at base (three 8-B loads; the last ones
+  // only while inside the row), enough unless 4 selected columns span > 8
+  const int64_t base = js[0] & ~3ll;
+  const int nwin = base + 12 <= ld ? 12 : base + 8 <= ld ? 8 : 4;
+  int d[4];
+  bool inwin = true;
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    d[c] = (int)(js[c] - base);
+    inwin = inwin && (c >= w || d[c] < nwin);
+  }
+  // byte-permute selectors of code c: the 8-B piece it is not in selects zero
+  // bytes (0x0c), so code = perm(va) | perm(vb) | perm(vc), branch-free
+  uint32_t pa[4], pb[4], pc[4];
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const uint32_t e = (uint32_t)(d[c] & 3), sel2 = (2 * e) | ((2 * e + 1) << 8) | 0x0c0c0000u;
+    const int piece = d[c] >> 2;
+    pa[c] = piece == 0 ? sel2 : 0x0c0c0c0cu;
+    pb[c] = piece == 1 ? sel2 : 0x0c0c0c0cu;
+    pc[c] = piece == 2 ? sel2 : 0x0c0c0c0cu;
+  }
+  typedef unsigned v2u __attribute__((ext_vector_type(2)));
+  auto ld8 = [&](const uint16_t *p) -> v2u {
+    if constexpr (NT & 1) return __builtin_nontemporal_load(reinterpret_cast<const v2u *>(p));
+    else return *reinterpret_cast<const v2u *>(p);
+  };
+  // rows i0 .. i0+ZR-1 (rows past r1 re-read row r0)
+  v2u va[ZR], vb[ZR], vc[ZR];
+#pragma unroll
+  for (int u = 0; u < ZR; u++) {
+    const int64_t i = (r0 + u < r1) ? r0 + u : r0;
+    const uint16_t *p = s16.q + i * ld + base;
+    if constexpr (PROBE & 4) {
+      va[u] = v2u{0x0FA00FA0u + (uint32_t)u, 0x0FA00FA0u};
+      vb[u] = va[u];
+      vc[u] = va[u];
+    } else {
+      va[u] = ld8(p);
+      vb[u] = nwin >= 8 ? ld8(p + 4) : v2u{0xFFFFFFFFu, 0xFFFFFFFFu};
+      vc[u] = nwin >= 12 ? ld8(p + 8) : v2u{0xFFFFFFFFu, 0xFFFFFFFFu};
+    }
+  }
+  double rmg[ZR], rig[ZR];
+  load_rows(rm, r0, n, rmg);
+  load_rows(rinv, r0, n, rig);
+  const bool vec_zq = w == 4 && (ld_zq & 3) == 0 && ((uintptr_t)(zq + s0) & 7) == 0;
+  const bool vec_zb = zb && w == 4 && cm[0] >= 0 && cm[1] == cm[0] + 1 && cm[2] == cm[0] + 2 && cm[3] == cm[0] + 3 &&
+                      (cm[0] & 3) == 0 && ((kbs > 0 ? kbs : ld_zb) & 3) == 0;
+  auto zbi = [&](int64_t i, int64_t c) -> int64_t {
+    return kbs > 0 ? (c >> 6) * kbs + i * 64 + (c & 63) : i * ld_zb + c;
+  };
+  const int64_t zb0 = zbi(0, cm[0] >= 0 ? cm[0] : 0), zbs = kbs > 0 ? 64 : ld_zb;   // panel row 0, row stride
+  const float qf = (float)qmax;
+  uint32_t slowm = 0;
+  int of = 0;
+  // HOT (wave-uniform): every lane has 4 columns, all in its 8-code window,
+  // 8-B stores for both outputs -- no per-cell branches; otherwise the
+  // general body (tail lanes, gathers, element stores)
+  auto rows = [&](auto hot_c) {
+    constexpr bool HOT = decltype(hot_c)::value;
+#pragma unroll
+    for (int u = 0; u < ZR; u++) {
+      const int64_t i = r0 + u;
+      if (i >= r1) break;
+      const double rmi = rmg[u], rii = rig[u];
+      const bool rowok = rmi != 0.0 && rmi == rmi;
+      const float a32 = (float)(0.01 * rii);
+      uint32_t zc[4], bv[4];
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        uint32_t code = __builtin_amdgcn_perm(va[u].y, va[u].x, pa[c]) | __builtin_amdgcn_perm(vb[u].y, vb[u].x, pb[c]) |
+                        __builtin_amdgcn_perm(vc[u].y, vc[u].x, pc[c]);
+        if (!HOT && !inwin && c < w && !(d[c] < nwin)) code = s16.q[i * ld + js[c]];   // gather
+        const bool valid = (HOT || c < w) && rowok && code != GRID_Q16_MISS;
+        const float y = (float)(int32_t)code * a32;
+        const float t = (y - m32[c]) * c32[c];
+        const float kk = rintf(t);
+        const float f = fabsf(t - kk);
+        const float dl = fmaf(ac[c], fabsf(y) + m32[c], 0x1p-21f * fabsf(t));
+        // = min(0.5 - f, |t|) > dl without fminf's operand canonicalisation (t is never NaN)
+        const bool good = (0.5f - f > dl) & (fabsf(t) > dl);
+        const int32_t o = (__float_as_uint(kk) == 0x80000000u) ? GRID_ZQ_NEG0 : (int32_t)kk;
+        const bool esc16 = o != GRID_ZQ_NEG0 && (o < GRID_ZQ16_MIN || o > GRID_ZQ16_MAX);
+        const bool defer = valid && (!good || esc16 || code > GRID_Q16_MAXV);   // escape codes: exact chain
+        const float zf = (valid && !defer) ? __builtin_amdgcn_fmed3f(kk, -qf, qf) + 0.0f : 0.0f;
+        bv[c] = __float_as_uint(zf) >> 16;             // exact bf16 of |v| <= 256
+        const int32_t cd = !valid ? GRID_ZQ16_NAN : defer ? 0 : o == GRID_ZQ_NEG0 ? GRID_ZQ16_NEG0 : o;
+        zc[c] = (uint32_t)cd & 0xFFFFu;
+        slowm |= defer ? (1u << (u * 4 + c)) : 0u;
+      }
+      if (HOT || vec_zq) {
+        *reinterpret_cast<uint2 *>(zq + i * ld_zq + s0) = make_uint2(zc[0] | (zc[1] << 16), zc[2] | (zc[3] << 16));
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+          if (c < w) zq[i * ld_zq + s0 + c] = (int16_t)zc[c];
+      }
+      if (HOT) {
+        *reinterpret_cast<uint2 *>(zb + zb0 + i * zbs) = make_uint2(bv[0] | (bv[1] << 16), bv[2] | (bv[3] << 16));
+      } else if (zb) {
+        if (vec_zb) {
+          *reinterpret_cast<uint2 *>(zb + zbi(i, cm[0])) = make_uint2(bv[0] | (bv[1] << 16), bv[2] | (bv[3] << 16));
+        } else {
+#pragma unroll
+          for (int c = 0; c < 4; c++)
+            if (cm[c] >= 0) zb[zbi(i, cm[c])] = (uint16_t)bv[c];
+        }
+      }
+    }
+  };
+  // HOT body: no per-cell branch or mask.  A code outside the lane's window,
+  // a missing cell or an escape is computed from garbage and DEFERRED (the
+  // exact loop below gathers it); a row with a zero / NaN mean (uniform) is
+  // written as NaN codes directly.
+  auto hot_rows = [&]() {
+    uint32_t outm = 0;                                // this lane's cells outside its 8-code window
+#pragma unroll
+    for (int c = 0; c < 4; c++) outm |= (d[c] < nwin) ? 0u : (1u << c);
+    // first-order error of t (u = 2^-24; a32 = fl(0.01/rm), y = fl(q a32),
+    // m32 = fl(mu), d = fl(y - m32), c32 = fl(100 scale / sqrt(mu)), t = fl(d c32);
+    // the fp64 chain's own error is below 2^-50 relative):
+    //   |t - 100 z| <= |c| (2u y + u m) + 3u |t| + O(u^2)
+    // dl = 2^-23 (1.5 |c| y + |c| m + 2 |t|) = u (3|c|y + 2|c|m + 4|t|) covers it
+    // with a 1.33x margin on every term (zquant_rows' 8u per term deferred ~3x
+    // as many cells to the exact chain at the bench shape)
+    float cy[4], cm2[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      cy[c] = 0x1.8p-23f * fabsf(c32[c]);
+      cm2[c] = 0x1p-23f * fabsf(c32[c]) * m32[c];
+    }
+#pragma unroll
+    for (int u = 0; u < ZR; u++) {
+      const int64_t i = r0 + u;
+      if (i >= r1) break;
+      const double rmi = rmg[u], rii = rig[u];
+      int16_t *zrow = zq + i * ld_zq + s0;
+      uint16_t *brow = zb + zb0 + i * zbs;
+      if (!(rmi != 0.0 && rmi == rmi)) {              // uniform: every cell NaN, panel 0
+        *reinterpret_cast<uint2 *>(zrow) = make_uint2(0x80008000u, 0x80008000u);
+        *reinterpret_cast<uint2 *>(brow) = make_uint2(0u, 0u);
+        continue;
+      }
+      const float a32 = (float)(0.01 * rii);
+      uint32_t zc[4], bv[4], dm = outm;
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const uint32_t code = __builtin_amdgcn_perm(va[u].y, va[u].x, pa[c]) |
+                              __builtin_amdgcn_perm(vb[u].y, vb[u].x, pb[c]) |
+                              __builtin_amdgcn_perm(vc[u].y, vc[u].x, pc[c]);
+        const float y = (float)code * a32;            // y >= 0
+        const float t = (y - m32[c]) * c32[c];
+        const float kk = rintf(t);
+        const float g = 0.5f - fabsf(t - kk);
+        const float dl = fmaf(cy[c], y, fmaf(0x1p-22f, fabsf(t), cm2[c]));
+        const bool good = (g > dl) & (fabsf(t) > dl) & (fabsf(kk) <= 32765.0f) & (code <= GRID_Q16_MAXV);
+        zc[c] = (__float_as_uint(kk) == 0x80000000u) ? (uint32_t)GRID_ZQ16_NEG0 : (uint32_t)(int32_t)kk;
+        bv[c] = __float_as_uint(__builtin_amdgcn_fmed3f(kk, -qf, qf) + 0.0f);   // its high half: exact bf16
+        dm |= good ? 0u : (1u << c);
+      }
+      slowm |= dm << (u * 4);
+      // byte permutes pack the low halves of the codes / the high halves of the floats
+      if (!(PROBE & 1))
+        *reinterpret_cast<uint2 *>(zrow) = make_uint2(__builtin_amdgcn_perm(zc[1], zc[0], 0x05040100u),
+                                                      __builtin_amdgcn_perm(zc[3], zc[2], 0x05040100u));
+      if (!(PROBE & 2))
+        *reinterpret_cast<uint2 *>(brow) = make_uint2(__builtin_amdgcn_perm(bv[1], bv[0], 0x07060302u),
+                                                      __builtin_amdgcn_perm(bv[3], bv[2], 0x07060302u));
+      if (PROBE) slowm = 0;
+    }
+  };
+  // wave-uniform test (lanes past r have returned)
+  const bool hot = __all(w == 4 && vec_zq && vec_zb && zb != nullptr);
+  if (hot) hot_rows();
+  else rows(std::integral_constant<bool, false>());
+  if (__builtin_expect(slowm != 0, 0)) {          // exact fp64 chain (rare), after the fast stores
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll 1
+    while (slowm) {
+      const int e = __builtin_ctz(slowm);
+      slowm &= slowm - 1;
+      const int u = e >> 2, c = e & 3;
+      const int64_t i = r0 + u, sc = s0 + c;
+      const int64_t j = c == 0 ? js[0] : c == 1 ? js[1] : c == 2 ? js[2] : js[3];
+      const int32_t cc = sel4(cm, c);
+      double y;
+      const bool ok = yval(q16_val(s16.q[i * ld + j], i, j, s16), rm[i], rinv[i], y);   // missing: NaN code
+      const double z = ok ? div_exact(y - mus[sc], sq[sc], rsq[sc]) * scale : __builtin_nan("");
+      int32_t o = GRID_ZQ_NAN, v = 0;
+      if (z == z) {
+        double kd = round_dec_k(z, 100.0);
+        if (fabs(kd) >= 2147483000.0) { of |= 1; kd = 0.0; }
+        o = (int32_t)kd;
+        v = o;
+        if (o == 0 && signbit(z)) o = GRID_ZQ_NEG0;
+      }
+      zq[i * ld_zq + sc] = zq_code<int16_t>(o, i * ld_zq + sc, esc, of);
+      if (zb && cc >= 0) {
+        v = v > qmax ? qmax : (v < -qmax ? -qmax : v);
+        zb[zbi(i, cc)] = (uint16_t)(__float_as_uint((float)v) >> 16);
+      }
+    }
   }
   if (of) atomicOr(overflow, of);
 }
@@ -1396,7 +1678,27 @@ static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, int64_
     const dim3 g6((unsigned)ceil_div(n, rpw), (unsigned)ceil_div(ceil_div(ld, 4), 256));
 #define Z6_PICK(ZT, CS) (nt ? (rpw > ZR ? k_zquant6<true, ZT, 1, CS> : k_zquant6<false, ZT, 1, CS>)                    \
                             : (rpw > ZR ? k_zquant6<true, ZT, 0, CS> : k_zquant6<false, ZT, 0, CS>))
-    if (d_zq16) {
+    const char *z7e = getenv("GRID_ZQUANT7");        // compact source, int16 output: 1 (default) = k_zquant7
+    const bool z7 = c16 && d_zq16 && (!z7e || atoi(z7e) != 0);
+    if (z7) {
+      // k_zquant7 reads overlapping 24-B windows: plain loads (the rows' lines
+      // serve neighbouring lanes from L2) unless GRID_ZQUANT_NT=1 (15.7 vs 17.8 ms)
+      const bool nt7 = ntv && atoi(ntv) == 1;
+      REQUIRE(ceil_div(ceil_div(r, 4), 256) <= 65535, "r too large for one launch");
+      const dim3 g7((unsigned)ceil_div(n, ZR), (unsigned)ceil_div(ceil_div(r, 4), 256));   // one row group each
+#ifdef GRID_PROBES
+      const char *pe = getenv("GRID_Z7_PROBE");
+      const int pr = pe ? atoi(pe) : 0;
+#define Z7P(P) (nt7 ? k_zquant7<1, P> : k_zquant7<0, P>)
+      auto k7 = pr == 1 ? Z7P(1) : pr == 2 ? Z7P(2) : pr == 3 ? Z7P(3) : pr == 4 ? Z7P(4) : pr == 7 ? Z7P(7) : Z7P(0);
+#undef Z7P
+#else
+      auto k7 = nt7 ? k_zquant7<1> : k_zquant7<0>;
+#endif
+      hipLaunchKernelGGL(k7, g7, dim3(256), 0, ctx->stream, s16, n, ld, d_sel, r, d_rm,
+                         rinv, mus, sq, rsq, mc32, scale, d_zq16, ld_zq, d_colmap, qmax, d_zb, ld_zb, kbs, d_of,
+                         ZR, esc);
+    } else if (d_zq16) {
       auto k16 = c16 ? Z6_PICK(int16_t, true) : Z6_PICK(int16_t, false);
       hipLaunchKernelGGL(k16, g6, dim3(256), 0, ctx->stream, d_q, s16, n, ld, sidx, d_rm, rinv, mus, sq, rsq, mc32,
                          scale, d_zq16, ld_zq, d_colmap, qmax, d_zb, ld_zb, kbs, d_of, rpw, esc);

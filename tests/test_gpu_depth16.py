@@ -85,8 +85,11 @@ def test_synth_q16_equals_encoded_synth(dev):
 
 @pytest.mark.parametrize("knobs", [{}, {"GRID_COL16_VW": "1", "GRID_ROWBLK16_PB": "1"},
                                    {"GRID_COL16_VW": "4", "GRID_ROWBLK16_PB": "4", "GRID_ROWBLK_NT": "0",
-                                    "GRID_COL_NT": "0", "GRID_ZQUANT_NT": "0"}])
-def test_step4_kernels_q16_equal_int32(dev, knobs, monkeypatch):
+                                    "GRID_COL_NT": "0", "GRID_ZQUANT_NT": "0", "GRID_ZQUANT_GROUPS": "3"},
+                                   {"GRID_COL16_CU": "16", "GRID_ROWBLK16_PB": "2", "GRID_ZQUANT_GROUPS": "5"},
+                                   {"GRID_ZQUANT7": "0"}])
+@pytest.mark.parametrize("pattern", ["every3", "dense"])
+def test_step4_kernels_q16_equal_int32(dev, knobs, pattern, monkeypatch):
     """Every q16 kernel variant (columns per thread, blocks per workgroup,
     streaming loads: timing knobs) gives the int32 kernels' bits, including
     the int16 step-4 codes and their escape list."""
@@ -111,9 +114,20 @@ def test_step4_kernels_q16_equal_int32(dev, knobs, monkeypatch):
         mu, var, ratio = (torch.zeros(m, dtype=torch.float64, device="cuda") for _ in range(3))
         ops.col_means(src, n, m, ld, rm, mu)
         ops.col_vars(src, n, m, ld, rm, mu, var, ratio)
-        sel = torch.arange(0, m, 3, dtype=torch.int32, device="cuda")
+        if pattern == "every3":     # 4 selected columns never share an 8-code window: per-cell gathers
+            sel = torch.arange(0, m, 3, dtype=torch.int32, device="cuda")
+            colmap = torch.arange(len(sel), dtype=torch.int32, device="cuda")
+        else:                       # ~90 % selected, r % 4 != 0, panel holes (colmap -1) and runs
+            keep = np.random.default_rng(5).random(m) < 0.9
+            keep[-3:] = [True, False, True]
+            sel_np = np.flatnonzero(keep).astype(np.int32)
+            if len(sel_np) % 4 == 0:
+                sel_np = sel_np[:-1]
+            hole = np.random.default_rng(6).random(len(sel_np)) < 0.05
+            cm_np = np.where(hole, -1, np.cumsum(~hole) - 1).astype(np.int32)
+            sel = torch.from_numpy(sel_np).cuda()
+            colmap = torch.from_numpy(cm_np).cuda()
         r = len(sel)
-        colmap = torch.arange(r, dtype=torch.int32, device="cuda")
         zq = torch.zeros((n, r), dtype=torch.int32, device="cuda")
         kp = -(-r // 64) * 64
         zb = torch.zeros((kp // 64, 512, 64), dtype=torch.int16, device="cuda")
