@@ -969,7 +969,7 @@ __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, 
   RawT nx[ZR];
   load_group(r0, nx);                       // in flight while the column setup runs
   int32_t sk[4], ck[4];
-  float m32[4], c32[4], ac[4];
+  float m32[4], c32[4], ac[4], cmk[4];
   if (full4) {
     const int4 t = *reinterpret_cast<const int4 *>(sidx + j0);
     sk[0] = t.x; sk[1] = t.y; sk[2] = t.z; sk[3] = t.w;
@@ -985,7 +985,10 @@ __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, 
     const float2 mc = sv >= 0 ? mc32[sv] : make_float2(1.0f, 1.0f);
     m32[k] = mc.x;
     c32[k] = mc.y;
-    ac[k] = 0x1p-21f * fabsf(mc.y);
+    // error bound terms as k_zquant7's, with one more u on y: (float)q rounds
+    // for |q| > 2^24 (k_zquant7's 16-bit codes are exact)
+    ac[k] = 0x1p-22f * fabsf(mc.y);
+    cmk[k] = 0x1p-23f * fabsf(mc.y) * fabsf(mc.x);
     if (sv >= 0) { smin = min(smin, sv); smax = max(smax, sv); }
     if (ck[k] >= 0) { cmin = min(cmin, ck[k]); cmax = max(cmax, ck[k]); }
   }
@@ -1032,7 +1035,7 @@ __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, 
         const float t = (y - m32[k]) * c32[k];
         const float kk = rintf(t);
         const float f = fabsf(t - kk);
-        const float dl = fmaf(ac[k], fabsf(y) + m32[k], 0x1p-21f * fabsf(t));
+        const float dl = fmaf(ac[k], fabsf(y), fmaf(0x1p-22f, fabsf(t), cmk[k]));
         const bool good = fminf(0.5f - f, fabsf(t)) > dl;
         const int32_t o = (__float_as_uint(kk) == 0x80000000u) ? GRID_ZQ_NEG0 : (int32_t)kk;
         const float zf = (valid && good) ? fminf(fmaxf(kk, -qf), qf) + 0.0f : 0.0f;
@@ -1283,7 +1286,7 @@ __global__ __launch_bounds__(256) void k_zquant7(Q16 s16, int64_t n, int64_t ld,
 #pragma unroll
     for (int c = 0; c < 4; c++) {
       cy[c] = 0x1.8p-23f * fabsf(c32[c]);
-      cm2[c] = 0x1p-23f * fabsf(c32[c]) * m32[c];
+      cm2[c] = 0x1p-23f * fabsf(c32[c]) * fabsf(m32[c]);
     }
 #pragma unroll
     for (int u = 0; u < ZR; u++) {
@@ -1304,11 +1307,11 @@ __global__ __launch_bounds__(256) void k_zquant7(Q16 s16, int64_t n, int64_t ld,
         const uint32_t code = __builtin_amdgcn_perm(va[u].y, va[u].x, pa[c]) |
                               __builtin_amdgcn_perm(vb[u].y, vb[u].x, pb[c]) |
                               __builtin_amdgcn_perm(vc[u].y, vc[u].x, pc[c]);
-        const float y = (float)code * a32;            // y >= 0
+        const float y = (float)code * a32;
         const float t = (y - m32[c]) * c32[c];
         const float kk = rintf(t);
         const float g = 0.5f - fabsf(t - kk);
-        const float dl = fmaf(cy[c], y, fmaf(0x1p-22f, fabsf(t), cm2[c]));
+        const float dl = fmaf(cy[c], fabsf(y), fmaf(0x1p-22f, fabsf(t), cm2[c]));   // y < 0 iff the row mean is
         const bool good = (g > dl) & (fabsf(t) > dl) & (fabsf(kk) <= 32765.0f) & (code <= GRID_Q16_MAXV);
         zc[c] = (__float_as_uint(kk) == 0x80000000u) ? (uint32_t)GRID_ZQ16_NEG0 : (uint32_t)(int32_t)kk;
         bv[c] = __float_as_uint(__builtin_amdgcn_fmed3f(kk, -qf, qf) + 0.0f);   // its high half: exact bf16

@@ -96,6 +96,33 @@ def test_zquant_full_bench_cohort_exact(dev):
     assert list(counts) == [0, 0, 0], list(counts)
 
 
+def test_zquant7_full_bench_cohort_exact(dev):
+    """(b) for the compact depth form (k_zquant7, the bench default): the chain
+    on the Depth16 cohort, every selected cell checked against the int32
+    matrix it encodes."""
+    from grid_amd import _abi
+    from grid_amd.fused import Depth16, HipOps, Steps47, TorchAlloc
+    import bench
+    import ctypes as C
+    n, m = 3202, 3_000_000
+    d16 = Depth16.synth(TorchAlloc(0), dev.ctx, bench.SEED, n, m, 0, bench.NCL)
+    reads, off, nbr, w = bench.synth_reads_and_ibs(n)
+    st = Steps47(HipOps(dev), TorchAlloc(0), n, m, 0, m, k=10, n_iters=5)
+    st.set_reads(reads)
+    st.set_phasing_graph(off, nbr, w)
+    st.run(d16, d16.ld)
+    torch.cuda.synchronize()
+    assert st.zq_is16
+    q = torch.empty((n, m), dtype=torch.int32, device="cuda")
+    _abi.call("grid_synth_depth", dev.ctx, bench.SEED, n, m, m, 0, bench.NCL, q.data_ptr())
+    counts = (C.c_int64 * 3)()
+    _abi.call("grid_verify_zquant", dev.ctx, q.data_ptr(), n, m, st.sel.data_ptr(), st.r_loc, st.rm.data_ptr(),
+              st.mu.data_ptr(), st.scale, st.zq16.data_ptr(), m, st.colmap.data_ptr(), st.qmax, st.zb.data_ptr(),
+              st.np_, counts)
+    assert st.r_loc > 2_500_000
+    assert list(counts) == [0, 0, 0], list(counts)
+
+
 def _fmt_code(z):
     t = f"{z:.2f}"
     k = int(t.replace(".", ""))
@@ -139,9 +166,27 @@ def test_zquant_rounding_boundaries(dev):
         sel = np.arange(ld, dtype=np.int32)
         d = {k: dev.upload(v) for k, v in (("q", qq), ("rm", rr), ("mu", mu_arr), ("sel", sel))}
         np_zb = -(-nn // 64) * 64
-        for mode in ("int32", "int16"):
+        for mode in ("int32", "int16", "q16"):
             zb = dev.zeros((1, np_zb, 64), np.uint16)
-            if mode == "int32":
+            if mode == "q16":              # compact source (k_zquant7): the same codes, 8-wide rows
+                import ctypes as C
+                q16 = dev.zeros((nn, 8), np.uint16)
+                eoff = dev.zeros(nn + 1, np.int64)
+                ecol, evl = dev.zeros(1, np.int32), dev.zeros(1, np.int32)
+                need = C.c_int64()
+                _abi.call("grid_q16_encode", dev.ctx, d["q"].ptr, nn, ld, ld, q16.ptr, 8, eoff.ptr, ecol.ptr,
+                          evl.ptr, 1, C.byref(need))
+                desc = _abi.Depth16Desc(q16.ptr, eoff.ptr, ecol.ptr, evl.ptr)
+                zq = dev.alloc((nn, ld), np.int16)
+                ei, ev = dev.alloc(1 << 16, np.int64), dev.alloc(1 << 16, np.int32)
+                of, ne = C.c_int32(), C.c_int64()
+                _abi.call("grid_norm_zquant_kb16_q16", dev.ctx, C.byref(desc), nn, 8, d["sel"].ptr, ld, d["rm"].ptr,
+                          d["mu"].ptr, scale, zq.ptr, ld, None, 200, zb.ptr, np_zb, ei.ptr, ev.ptr, 1 << 16,
+                          C.byref(ne), C.byref(of))
+                assert of.value == 0
+                got = zq.numpy().astype(np.int64)
+                got[got == -32767] = -(2 ** 31) + 1
+            elif mode == "int32":
                 zq = dev.alloc((nn, ld), np.int32)
                 import ctypes as C
                 of = C.c_int32()
