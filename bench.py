@@ -39,7 +39,7 @@ PEAK_BF16_TFLOPS = 2516.6     # 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz (dense
 PEAK_HBM_GBS = 8000.0
 # HBM bytes per Gram launch from the rocprofv3 FETCH_SIZE / WRITE_SIZE passes
 # of this same command (tools/gpu_round.sh -> tools/pmc_traffic.py)
-TRAFFIC_JSON = "profiles/r02o_pmc_traffic.json"
+TRAFFIC_JSON = "profiles/r02q_pmc_traffic.json"
 GRAM_KERNEL = "k_gram8<0, true"
 SEED = 20260821
 NCL = 26
@@ -179,9 +179,10 @@ def main():
     ap.add_argument("--no-overlap", action="store_true", help="run step 7 inline on the main stream")
     ap.add_argument("--traffic-json", default=TRAFFIC_JSON,
                     help="rocprofv3 PMC summary (tools/pmc_traffic.py) of this same command, for roofline.traffic")
-    ap.add_argument("--depth-format", choices=["int32", "q16"], default="int32",
-                    help="resident depth matrix in HBM: int32 hundredths (default) or the compact uint16 + escapes "
-                         "form (half the bytes; measured slower: the step-4 passes are not byte-bound)")
+    ap.add_argument("--depth-format", choices=["auto", "int32", "q16"], default="auto",
+                    help="depth matrix in HBM: the compact uint16 hundredths + escape table (q16: half the bytes of "
+                         "the step-4 passes, same int32 values after decoding) or int32 hundredths; auto = q16 when "
+                         "the shard is resident, int32 chunks when it is streamed")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -225,6 +226,8 @@ def main():
     else:
         chunk, _ = plan_memory(n, ml, world, args.hbm_budget_gb * 1e9)
     streamed = chunk is not None and chunk < ml
+    if args.depth_format == "auto":
+        args.depth_format = "int32" if streamed else "q16"
     if streamed:
         if args.depth_format != "int32":
             raise SystemExit("bench: the compact depth form is resident-only")
