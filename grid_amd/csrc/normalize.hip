@@ -1128,6 +1128,7 @@ __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, 
 // Fast path, acceptance test and deferred exact chain: as zquant_rows.
 // PROBE (tools build only, wrong results): bit 0 no z stores, bit 1 no panel
 // stores, bit 2 no loads (codes from a constant).
+// 106 VGPRs, 4 workgroups per CU (forcing 5 spilled 12 VGPRs: 19.0 vs 15.5 ms).
 template <int NT, int PROBE = 0>
 __global__ __launch_bounds__(256) void k_zquant7(Q16 s16, int64_t n, int64_t ld, const int32_t *__restrict__ sel,
                                                  int64_t r, const double *__restrict__ rm,
@@ -1340,8 +1341,9 @@ __global__ __launch_bounds__(256) void k_zquant7(Q16 s16, int64_t n, int64_t ld,
       slowm &= slowm - 1;
       const int u = e >> 2, c = e & 3;
       const int64_t i = r0 + u, sc = s0 + c;
-      const int64_t j = c == 0 ? js[0] : c == 1 ? js[1] : c == 2 ? js[2] : js[3];
-      const int32_t cc = sel4(cm, c);
+      // re-read (rare path): keeping js / cm live through the row loop costs registers
+      const int64_t j = sel[sc];
+      const int32_t cc = colmap ? colmap[sc] : (int32_t)sc;
       double y;
       const bool ok = yval(q16_val(s16.q[i * ld + j], i, j, s16), rm[i], rinv[i], y);   // missing: NaN code
       const double z = ok ? div_exact(y - mus[sc], sq[sc], rsq[sc]) * scale : __builtin_nan("");
