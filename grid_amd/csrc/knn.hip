@@ -200,6 +200,7 @@ __global__ __launch_bounds__(NT, 2) void k_gram_dma(const uint16_t *__restrict__
 
 constexpr int BM3 = 256, BN3 = 128;
 constexpr int SLOT3 = (BM3 + BN3) * BK * 2;     // 48 KiB
+constexpr int QSA = BM3 * BK * 2, QSB = BN3 * BK * 2;   // quad-row image: A / B slot bytes
 
 __device__ __forceinline__ uint4 lds_read_b128(uint32_t addr) {
   uint4 v;
@@ -526,7 +527,16 @@ __device__ __forceinline__ uint4 lds_rd(uint32_t addr) {
   return v;
 }
 
-template <int MODE, bool BL, int FL>
+// QL (quad-row image, the default): a lane quad of every LDS-DMA piece reads 64
+// contiguous bytes of ONE panel row (the texture path then moves a piece at
+// twice the rate of the pair-row pieces above: 146 vs 75 GB/s per CU from L2,
+// tools/micro/dmapat.hip).  Piece (8-row block b) = [half p (2)][row r (8)][64 B],
+// the 16-B chunk j of a half stored at j ^ (b & 3); A slots at 0/32/64 KiB,
+// B slots at 96/112/128 KiB.  Fragment of sub-step s = chunk 2s + h of row R:
+// base(s & 1) + 512 (s >> 1) (+ slot offset), where the odd base is the even one
+// ^ 32; each ds_read_b128 lane group sees 4 rows x 4 distinct x = b & 3, i.e.
+// 16 distinct 16-B bank slots (conflict-free).
+template <int MODE, bool BL, int FL, bool QL>
 __device__ __forceinline__ void g8_run(const uint16_t *__restrict__ z, int64_t ld, int I, int tj, int64_t s0,
                                        int64_t s1, char *smem, f32x16 (&acc)[2][2],
                                        int32_t (&iacc)[2][2][16]) {
@@ -544,23 +554,44 @@ __device__ __forceinline__ void g8_run(const uint16_t *__restrict__ z, int64_t l
   const uint16_t *pb0 = z + ((int64_t)tj * BN3 + wv * 16) * rs_el;
   const __amdgpu_buffer_rsrc_t rsa0 = __builtin_amdgcn_make_buffer_rsrc((void *)pa0, (short)0, -1, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsb0 = __builtin_amdgcn_make_buffer_rsrc((void *)pb0, (short)0, -1, 0x00020000);
-  const int dr = (lane >> 1) & 7, ds = lane >> 4, dj = lane & 1;
-  const uint32_t v0 = (uint32_t)((dr * rs_el + (2 * ds + dj) * 8) * 2);        // even block
-  const uint32_t v1 = (uint32_t)((dr * rs_el + (2 * ds + (dj ^ 1)) * 8) * 2);  // odd block
   const uint32_t rb8 = (uint32_t)(16 * rs_el);                                 // bytes per 8 rows
-  const uint32_t vo0 = v0, vo1 = v1 + rb8, vo2 = v0 + 2 * rb8, vo3 = v1 + 3 * rb8;
+  uint32_t vo0, vo1, vo2, vo3, vb0, vb1;
+  if constexpr (QL) {
+    const int qr = (lane >> 2) & 7, qp = lane >> 5, qj = lane & 3;
+    auto vq = [&](int x) { return (uint32_t)((qr * rs_el + (4 * qp + (qj ^ x)) * 8) * 2); };
+    vo0 = vq(0); vo1 = vq(1) + rb8; vo2 = vq(2) + 2 * rb8; vo3 = vq(3) + 3 * rb8;
+    const int xb = 2 * (wv & 1);                                               // B blocks 2 wv + t
+    vb0 = vq(xb); vb1 = vq(xb + 1) + rb8;
+  } else {
+    const int dr = (lane >> 1) & 7, ds = lane >> 4, dj = lane & 1;
+    const uint32_t v0 = (uint32_t)((dr * rs_el + (2 * ds + dj) * 8) * 2);        // even block
+    const uint32_t v1 = (uint32_t)((dr * rs_el + (2 * ds + (dj ^ 1)) * 8) * 2);  // odd block
+    vo0 = v0; vo1 = v1 + rb8; vo2 = v0 + 2 * rb8; vo3 = v1 + 3 * rb8;
+    vb0 = vo0; vb1 = vo1;
+  }
   const uint32_t sbase = (uint32_t)(uintptr_t)smem;
   // fragment bases per (slot, fragment): A blocks m = 0, 1; B blocks nn = 0, 1
+  // (QL: per (parity of s, fragment), slot 2 of A separately: offsets < 64 KiB)
   uint32_t ad[3][4];
 #pragma unroll
-  for (int sl = 0; sl < 3; sl++)
+  for (int f = 0; f < 4; f++) {
+    const int R = f < 2 ? wr * 64 + f * 32 + (lane & 31) : wc * 64 + (f - 2) * 32 + (lane & 31);
+    const int rb = R >> 3;
+    if constexpr (QL) {
+      const uint32_t ev = sbase + (f < 2 ? 0 : 3 * QSA) + rb * 1024 + (R & 7) * 64 + (((lane >> 5) ^ (rb & 3)) << 4);
+      ad[0][f] = ev;
+      ad[1][f] = ev ^ 32u;
+      if (f < 2) {                      // A, slot 2: [2][m] even, [2][2 + m] odd
+        ad[2][f] = ev + 2 * QSA;
+        ad[2][f + 2] = (ev ^ 32u) + 2 * QSA;
+      }
+    } else {
 #pragma unroll
-    for (int f = 0; f < 4; f++) {
-      const int R = f < 2 ? wr * 64 + f * 32 + (lane & 31) : wc * 64 + (f - 2) * 32 + (lane & 31);
-      const int rb = R >> 3;
-      ad[sl][f] = sbase + sl * SLOT3 + (f < 2 ? 0 : BM3 * 128) + rb * 1024 + (R & 7) * 32 +
-                  (((lane >> 5) ^ (rb & 1)) << 4);
+      for (int sl = 0; sl < 3; sl++)
+        ad[sl][f] = sbase + sl * SLOT3 + (f < 2 ? 0 : BM3 * 128) + rb * 1024 + (R & 7) * 32 +
+                    (((lane >> 5) ^ (rb & 1)) << 4);
     }
+  }
   const f32x16 zero16 = {};
   uint4 fr0[NF], fr1[NF];
 
@@ -574,21 +605,31 @@ __device__ __forceinline__ void g8_run(const uint16_t *__restrict__ z, int64_t l
         (void *)(pa0 + (int64_t)(step_) * ld), (short)0, -1, 0x00020000) : rsa0;               \
     const __amdgpu_buffer_rsrc_t rsb = BL ? __builtin_amdgcn_make_buffer_rsrc(                 \
         (void *)(pb0 + (int64_t)(step_) * ld), (short)0, -1, 0x00020000) : rsb0;               \
-    char *A_ = smem + (SL) * SLOT3 + wv * 4096;                                                \
-    char *B_ = smem + (SL) * SLOT3 + BM3 * 128 + wv * 2048;                                    \
+    char *A_ = smem + (SL) * (QL ? QSA : SLOT3) + wv * 4096;                                   \
+    char *B_ = smem + (QL ? 3 * QSA + (SL) * QSB : (SL) * SLOT3 + BM3 * 128) + wv * 2048;      \
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lptr_t)(A_), 16, vo0, so_, 0, 0);           \
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lptr_t)(A_ + 1024), 16, vo1, so_, 0, 0);    \
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lptr_t)(A_ + 2048), 16, vo2, so_, 0, 0);    \
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lptr_t)(A_ + 3072), 16, vo3, so_, 0, 0);    \
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lptr_t)(B_), 16, vo0, so_, 0, 0);           \
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lptr_t)(B_ + 1024), 16, vo1, so_, 0, 0);    \
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lptr_t)(B_), 16, vb0, so_, 0, 0);           \
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lptr_t)(B_ + 1024), 16, vb1, so_, 0, 0);    \
   } while (0)
 #define G8_READ(FR, SL, s_)                                                                    \
   if (MODE != 8) do {                                                                          \
-    FR[0] = lds_rd<(s_) * 256>(ad[SL][0]);                                                     \
-    FR[1] = lds_rd<(s_) * 256>(ad[SL][1]);                                                     \
-    FR[2] = lds_rd<(s_) * 256>(ad[SL][2]);                                                     \
-    FR[3] = lds_rd<(s_) * 256>(ad[SL][3]);                                                     \
+    if constexpr (QL) {                                                                        \
+      constexpr int pa_ = (s_) & 1, ia_ = (SL) == 2 ? 2 : pa_, ja_ = (SL) == 2 ? 2 * pa_ : 0;  \
+      constexpr int oa_ = ((SL) == 2 ? 0 : (SL) * QSA) + ((s_) >> 1) * 512;                    \
+      constexpr int ob_ = (SL) * QSB + ((s_) >> 1) * 512;                                      \
+      FR[0] = lds_rd<oa_>(ad[ia_][ja_]);                                                       \
+      FR[1] = lds_rd<oa_>(ad[ia_][ja_ + 1]);                                                   \
+      FR[2] = lds_rd<ob_>(ad[pa_][2]);                                                         \
+      FR[3] = lds_rd<ob_>(ad[pa_][3]);                                                         \
+    } else {                                                                                   \
+      FR[0] = lds_rd<(s_) * 256>(ad[SL][0]);                                                   \
+      FR[1] = lds_rd<(s_) * 256>(ad[SL][1]);                                                   \
+      FR[2] = lds_rd<(s_) * 256>(ad[SL][2]);                                                   \
+      FR[3] = lds_rd<(s_) * 256>(ad[SL][3]);                                                   \
+    }                                                                                          \
   } while (0)
   // MFMAs of A blocks [m0, m1) at in-group sub-step c_; block b = 2m + nn starts
   // a new fp32 chunk (after flushing the old one) at sub-steps = FSP b (mod FCYC)
@@ -695,7 +736,7 @@ __device__ __forceinline__ void g8_run(const uint16_t *__restrict__ z, int64_t l
 // small cohort (fewer tile groups than XCDs) splits K eight ways; a large one
 // gives every XCD whole tile groups over the full K range, so each output tile
 // is flushed with int64 atomics only once per int32-exact unit (sps_max steps).
-template <int MODE, bool BL, int FL>
+template <int MODE, bool BL, int FL, bool QL>
 __global__ __launch_bounds__(512, 1) void k_gram8(const uint16_t *__restrict__ z, int64_t ld,
                                                   const int32_t *__restrict__ tiles, int ntiles, int kc, int kx,
                                                   int64_t nsteps, int lag, int spin_ticks,
@@ -743,7 +784,7 @@ __global__ __launch_bounds__(512, 1) void k_gram8(const uint16_t *__restrict__ z
       f32x16 acc[2][2];
       int32_t iacc[2][2][16];
       g6_zero<2>(acc, iacc);
-      g8_run<MODE, BL, FL>(z, ld, I, tj, s0, s1, smem, acc, iacc);
+      g8_run<MODE, BL, FL, QL>(z, ld, I, tj, s0, s1, smem, acc, iacc);
       g6_atomics<2>(iacc, I, tj, np_, gram);
     }
     __syncthreads();
@@ -1158,17 +1199,21 @@ static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_
   // fp32 chunks of 384 products while 384 qmax^2 <= 2^24 (qmax <= 209), else 192
   const int fl = 384 * q2 <= (1ll << 24) ? 1 : 2;
 #ifdef GRID_PROBES
-#define G8_PICK(BLV)                                                                            \
-  (mode == 5 ? (fl == 1 ? k_gram8<5, BLV, 1> : k_gram8<5, BLV, 2>)                              \
-   : mode == 6 ? (fl == 1 ? k_gram8<6, BLV, 1> : k_gram8<6, BLV, 2>)                            \
-   : mode == 1 ? (fl == 1 ? k_gram8<1, BLV, 1> : k_gram8<1, BLV, 2>)                            \
-   : mode == 7 ? k_gram8<7, BLV, 1> : mode == 8 ? k_gram8<8, BLV, 1>                            \
-   : (fl == 1 ? k_gram8<0, BLV, 1> : k_gram8<0, BLV, 2>))
+#define G8_PICK(BLV, QLV)                                                                       \
+  (mode == 5 ? (fl == 1 ? k_gram8<5, BLV, 1, QLV> : k_gram8<5, BLV, 2, QLV>)                    \
+   : mode == 6 ? (fl == 1 ? k_gram8<6, BLV, 1, QLV> : k_gram8<6, BLV, 2, QLV>)                  \
+   : mode == 1 ? (fl == 1 ? k_gram8<1, BLV, 1, QLV> : k_gram8<1, BLV, 2, QLV>)                  \
+   : mode == 7 ? k_gram8<7, BLV, 1, QLV> : mode == 8 ? k_gram8<8, BLV, 1, QLV>                  \
+   : (fl == 1 ? k_gram8<0, BLV, 1, QLV> : k_gram8<0, BLV, 2, QLV>))
 #else
   (void)mode;
-#define G8_PICK(BLV) (fl == 1 ? k_gram8<0, BLV, 1> : k_gram8<0, BLV, 2>)
+#define G8_PICK(BLV, QLV) (fl == 1 ? k_gram8<0, BLV, 1, QLV> : k_gram8<0, BLV, 2, QLV>)
 #endif
-  auto kern = blocked ? G8_PICK(true) : G8_PICK(false);
+  // LDS image: quad-row pieces (default) or the earlier pair-row pieces (GRID_GRAM_QL=0; timing A/B)
+  const char *qe = getenv("GRID_GRAM_QL");
+  const bool ql = !(qe && atoi(qe) == 0);
+  auto kern = blocked ? (ql ? G8_PICK(true, true) : G8_PICK(true, false))
+                      : (ql ? G8_PICK(false, true) : G8_PICK(false, false));
 #undef G8_PICK
   hipLaunchKernelGGL(kern, dim3((unsigned)(8 * per)), dim3(512), 0, ctx->stream, d_zb, ld,
                      (const int32_t *)ctx->aux, nt6, (int)bkc, (int)bkx, nsteps, lag, spin, np_,
