@@ -1158,9 +1158,14 @@ static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_
   HIPCHK(hipMemsetAsync(rounds, 0, 8 * 16 * 4, ctx->stream));
   const int per = ctx->ncu >= 8 ? ctx->ncu / 8 : 1;
   const int64_t ngroups = ceil_div(nt6, per);
-  // (kx, kc): cost = the longest XCD's sequential K-steps per workgroup
-  // (rounds x steps per unit); the fewest K-ranges within 1 % of the best
-  // cost (fewer int64 flushes), then the chunk count that wastes least
+  // (kx, kc): cost = the longest XCD's sequential work per workgroup in
+  // K-step units: rounds x (steps per unit + UF), where UF prices a unit's
+  // prologue and its int64-atomic flush (256 KiB per workgroup at ~5 GB/s per
+  // CU: ~25-50 us, i.e. tens of K-steps -- without it, short K ranges were cut
+  // into hundreds of units and the flushes doubled the launch); the fewest
+  // K-ranges within 1 % of the best cost, then the chunk count that wastes least
+  const char *ufe = getenv("GRID_GRAM_UF");
+  const double UF = ufe ? atof(ufe) : 40.0;
   int64_t bkx = 8, bkc = 1;
   double bcost = -1.0;
   for (int kx = 8; kx >= 1; kx >>= 1) {
@@ -1177,7 +1182,7 @@ static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_
         const int64_t units = ((ngx - 1) * per + lastsz) * kc;
         worst = std::max(worst, ceil_div(units, per));
       }
-      const double cost = (double)worst * (double)ceil_div(xlen, kc);
+      const double cost = (double)worst * ((double)ceil_div(xlen, kc) + UF);
       if (bcost < 0 || cost < bcost * 0.99 || (kx < bkx && cost <= bcost * 1.01) ||
           (kx == bkx && cost < bcost)) {
         bcost = cost;

@@ -579,6 +579,7 @@ __global__ void k_zprep(const int32_t *__restrict__ sel, int64_t r, const double
 }
 
 constexpr int ZR = 8;    // rows per zquant batch
+constexpr int Z7RGS = 0, Z7CBW = 64;   // k_zquant7 grid walk (see the launch)
 
 // The row means / reciprocals of rows i0 .. i0+R-1 (clamped to n-1), all
 // loaded before any is used: a load inside the row loop, behind its
@@ -1160,11 +1161,32 @@ __global__ __launch_bounds__(256) void k_zquant7(Q16 s16, int64_t n, int64_t ld,
                                                  int16_t *__restrict__ zq, int64_t ld_zq,
                                                  const int32_t *__restrict__ colmap, int32_t qmax,
                                                  uint16_t *__restrict__ zb, int64_t ld_zb, int64_t kbs,
-                                                 int32_t *__restrict__ overflow, int rpw, ZEsc esc) {
-  const int64_t s0 = ((int64_t)blockIdx.y * 256 + threadIdx.x) * 4;
+                                                 int32_t *__restrict__ overflow, int rpw, ZEsc esc,
+                                                 int rgs, int cbw) {
+  // (row group, column block) of this workgroup: the 2-D grid (x = row group) when
+  // rgs == 0, else a 1-D grid walked in super-tiles of rgs row groups x cbw column
+  // blocks (placement only; every (row group, column block) is visited once)
+  int64_t bx = blockIdx.x, by = blockIdx.y;
+  if (rgs > 0) {
+    const int64_t nrg = (n + rpw - 1) / rpw, ncb = ((r + 3) / 4 + 255) / 256;
+    const int64_t L = blockIdx.x, sr = L / (rgs * ncb), brg = sr * rgs;
+    const int64_t h = nrg - brg < rgs ? nrg - brg : rgs;
+    const int64_t rem = L - sr * rgs * ncb, st = rem / (h * cbw), bcb = st * cbw;
+    const int64_t wd = ncb - bcb < cbw ? ncb - bcb : cbw;
+    const int64_t t = rem - st * h * cbw;
+    if (wd == cbw && (cbw & 7) == 0) {   // XCD L % 8 keeps the column blocks bcb + 8 g + (t % 8)
+      const int64_t k = t >> 3;
+      bx = brg + k % h;
+      by = bcb + (k / h) * 8 + (t & 7);
+    } else {
+      bx = brg + t % h;
+      by = bcb + t / h;
+    }
+  }
+  const int64_t s0 = (by * 256 + threadIdx.x) * 4;
   if (s0 >= r) return;
   const int w = (int)((r - s0) < 4 ? (r - s0) : 4);
-  const int64_t r0 = (int64_t)blockIdx.x * rpw;
+  const int64_t r0 = bx * rpw;
   const int64_t r1 = (r0 + rpw < n) ? r0 + rpw : n;
   int64_t js[4];
   int32_t cm[4];
@@ -1712,7 +1734,14 @@ static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, int64_
       // serve neighbouring lanes from L2) unless GRID_ZQUANT_NT=1 (15.7 vs 17.8 ms)
       const bool nt7 = ntv && atoi(ntv) == 1;
       REQUIRE(ceil_div(ceil_div(r, 4), 256) <= 65535, "r too large for one launch");
-      const dim3 g7((unsigned)ceil_div(n, ZR), (unsigned)ceil_div(ceil_div(r, 4), 256));   // one row group each
+      // super-tiles of rgs row groups x cbw column blocks (GRID_Z7_RGS / GRID_Z7_CBW; RGS=0: the 2-D grid,
+      // row groups fastest)
+      const char *rge = getenv("GRID_Z7_RGS"), *cbe = getenv("GRID_Z7_CBW");
+      const int rgs = rge ? atoi(rge) : Z7RGS, cbw = cbe ? atoi(cbe) : Z7CBW;
+      REQUIRE(rgs >= 0 && cbw > 0, "GRID_Z7_RGS must be >= 0 and GRID_Z7_CBW > 0");
+      const int64_t nrg7 = ceil_div(n, ZR), ncb7 = ceil_div(ceil_div(r, 4), 256);
+      REQUIRE(rgs == 0 || nrg7 * ncb7 < (1ll << 31), "zquant grid too large");
+      const dim3 g7 = rgs > 0 ? dim3((unsigned)(nrg7 * ncb7)) : dim3((unsigned)nrg7, (unsigned)ncb7);
 #ifdef GRID_PROBES
       const char *pe = getenv("GRID_Z7_PROBE");
       const int pr = pe ? atoi(pe) : 0;
@@ -1724,7 +1753,7 @@ static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, int64_
 #endif
       hipLaunchKernelGGL(k7, g7, dim3(256), 0, ctx->stream, s16, n, ld, d_sel, r, d_rm,
                          rinv, mus, sq, rsq, mc32, scale, d_zq16, ld_zq, d_colmap, qmax, d_zb, ld_zb, kbs, d_of,
-                         ZR, esc);
+                         ZR, esc, rgs, cbw);
     } else if (d_zq16) {
       auto k16 = c16 ? Z6_PICK(int16_t, true) : Z6_PICK(int16_t, false);
       hipLaunchKernelGGL(k16, g6, dim3(256), 0, ctx->stream, d_q, s16, n, ld, sidx, d_rm, rinv, mus, sq, rsq, mc32,

@@ -27,6 +27,7 @@ ap.add_argument("--m", type=int, default=3_000_000)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--q16", action="store_true", help="compact depth matrix (grid_depth16) as the source")
 ap.add_argument("--groups", default="1", help="comma list of GRID_ZQUANT_GROUPS values to time")
+ap.add_argument("--ldz-align", type=int, default=8, help="step-4 output row stride rounded up to this many columns")
 ap.add_argument("--env", default="", help="semicolon list of K=V[,K=V] settings to time full16 under "
                 "(the tools build's probes, e.g. GRID_Z7_PROBE=3)")
 a = ap.parse_args()
@@ -44,7 +45,7 @@ st.run(q, a.m)
 torch.cuda.synchronize()
 of = C.c_int32()
 zq32 = torch.empty((a.n, st.r_loc), dtype=torch.int32, device="cuda")
-LDZ = -(-st.r_loc // 8) * 8          # the chain's step-4 output row stride is a multiple of 4 (m)
+LDZ = -(-st.r_loc // a.ldz_align) * a.ldz_align          # the chain's step-4 output row stride is a multiple of 4 (m)
 zq16 = torch.empty((a.n, LDZ), dtype=torch.int16, device="cuda")
 if a.q16:
     d16 = Depth16.synth(TorchAlloc(0), dev.ctx, bench.SEED, a.n, a.m, 0, bench.NCL)
