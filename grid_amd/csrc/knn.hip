@@ -731,12 +731,205 @@ __device__ __forceinline__ void g8_run(const uint16_t *__restrict__ z, int64_t l
 #undef G8_FLUSH
 }
 
+// LAY 2 (half-split image): every ring slot holds a K-step as two halves
+// (K chunks 0-3 | 4-7, 64 B of each panel row), region [half p][row][64 B]
+// with the 16-B chunk j of row R stored at j ^ ((R >> 2) & 3).  A DMA piece is
+// 16 rows x 64 B (lane quad = 64 contiguous bytes of one row; ONE voffset VGPR,
+// the piece's rows and half in soffset).  Sub-steps 0-1 read half 0 and 2-3
+// half 1, so each half of slot st is refilled with step st + 3 as soon as
+// every wave has read it: two barriers per step, each followed by 3 pieces
+// per wave (the texture path's work spread over the step instead of one
+// 6-piece burst behind a single barrier), and 2.5 steps of DMA lead.
+// Fragment bases: even / odd sub-steps (odd = even ^ 32), half offsets and
+// slots as immediates (A slot 2 has its own bases: offsets stay < 64 KiB).
+// K32 (tools A/B, LAY 3): the panel K-blocked by 32 columns, [K-half][row][32],
+// so a 16-row half piece is 1 KiB contiguous (whole 128-B lines; with the
+// 64-wide blocks a half piece reads half of every line it touches).
+template <int MODE, bool BL, int FL, bool K32 = false>
+__device__ __forceinline__ void g8h_run(const uint16_t *__restrict__ z, int64_t ld, int I, int tj, int64_t s0,
+                                        int64_t s1, char *smem, f32x16 (&acc)[2][2],
+                                        int32_t (&iacc)[2][2][16]) {
+  constexpr int NF = 4;
+  constexpr int FCYC = 24 / FL, FSP = FCYC / 4;
+  constexpr int HA = QSA / 2, HB = QSB / 2;             // half regions of a slot (A, B)
+  constexpr bool NOLOAD = MODE == 5 || MODE == 6, NOFLUSH = MODE == 6;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int wr = wv >> 1, wc = wv & 1;
+  static_assert(!K32 || BL, "K32 is a K-blocked layout");
+  const int64_t rs_el = K32 ? BK / 2 : BL ? BK : ld;
+  const uint16_t *pa0 = z + ((int64_t)I * BM3 + wv * 32) * rs_el;
+  const uint16_t *pb0 = z + ((int64_t)tj * BN3 + wv * 16) * rs_el;
+  const __amdgpu_buffer_rsrc_t rsa0 = __builtin_amdgcn_make_buffer_rsrc((void *)pa0, (short)0, -1, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb0 = __builtin_amdgcn_make_buffer_rsrc((void *)pb0, (short)0, -1, 0x00020000);
+  const uint32_t vq = (uint32_t)(((lane >> 2) * rs_el + ((lane & 3) ^ ((lane >> 4) & 3)) * 8) * 2);
+  const uint32_t r16 = (uint32_t)(32 * rs_el);         // bytes per 16 rows
+  const uint32_t sbase = (uint32_t)(uintptr_t)smem;
+  uint32_t ad[3][4];
+#pragma unroll
+  for (int f = 0; f < 4; f++) {
+    const int R = f < 2 ? wr * 64 + f * 32 + (lane & 31) : wc * 64 + (f - 2) * 32 + (lane & 31);
+    const uint32_t ev = sbase + (f < 2 ? 0 : 3 * QSA) + R * 64 + ((((lane >> 5) ^ (R >> 2)) & 3) << 4);
+    ad[0][f] = ev;
+    ad[1][f] = ev ^ 32u;
+    if (f < 2) {                      // A, slot 2: [2][m] even, [2][2 + m] odd
+      ad[2][f] = ev + 2 * QSA;
+      ad[2][f + 2] = (ev ^ 32u) + 2 * QSA;
+    }
+  }
+  const f32x16 zero16 = {};
+  uint4 fr0[NF], fr1[NF];
+
+#define H8_WAIT_VM(n_) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(n_) : "memory")
+#define H8_WAIT_LGKM(n_) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(n_) : "memory")
+#define H8_SB() __builtin_amdgcn_sched_barrier(0)
+  // half P of K-step step_ into ring slot SL: A rows wv*32 + {0..15, 16..31}, B rows wv*16 + 0..15
+#define H8_ISSUE(step_, P, SL)                                                                 \
+  if (!NOLOAD) do {                                                                            \
+    const uint32_t so_ = K32 ? 0u : (BL ? 0u : (uint32_t)((step_) * (BK * 2))) + (P) * 64u;    \
+    const int64_t ko_ = K32 ? (2 * (int64_t)(step_) + (P)) * (ld >> 1) : (int64_t)(step_) * ld; \
+    const __amdgpu_buffer_rsrc_t rsa = BL ? __builtin_amdgcn_make_buffer_rsrc(                 \
+        (void *)(pa0 + ko_), (short)0, -1, 0x00020000) : rsa0;                                 \
+    const __amdgpu_buffer_rsrc_t rsb = BL ? __builtin_amdgcn_make_buffer_rsrc(                 \
+        (void *)(pb0 + ko_), (short)0, -1, 0x00020000) : rsb0;                                 \
+    char *A_ = smem + (SL) * QSA + (P) * HA + wv * 2048;                                       \
+    char *B_ = smem + 3 * QSA + (SL) * QSB + (P) * HB + wv * 1024;                             \
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lptr_t)(A_), 16, vq, so_, 0, 0);            \
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lptr_t)(A_ + 1024), 16, vq, so_ + r16, 0, 0); \
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lptr_t)(B_), 16, vq, so_, 0, 0);            \
+  } while (0)
+#define H8_READ(FR, SL, s_)                                                                    \
+  if (MODE != 8) do {                                                                          \
+    constexpr int pa_ = (s_) & 1, ia_ = (SL) == 2 ? 2 : pa_, ja_ = (SL) == 2 ? 2 * pa_ : 0;    \
+    constexpr int oa_ = ((SL) == 2 ? 0 : (SL) * QSA) + ((s_) >> 1) * HA;                       \
+    constexpr int ob_ = (SL) * QSB + ((s_) >> 1) * HB;                                         \
+    FR[0] = lds_rd<oa_>(ad[ia_][ja_]);                                                         \
+    FR[1] = lds_rd<oa_>(ad[ia_][ja_ + 1]);                                                     \
+    FR[2] = lds_rd<ob_>(ad[pa_][2]);                                                           \
+    FR[3] = lds_rd<ob_>(ad[pa_][3]);                                                           \
+  } while (0)
+#define H8_MFMA(FR, c_, m0, m1, STAG)                                                          \
+  if (MODE != 7 && MODE != 8) do {                                                             \
+    _Pragma("unroll") for (int m = m0; m < m1; m++)                                            \
+      _Pragma("unroll") for (int nn = 0; nn < 2; nn++) {                                       \
+        if ((STAG) && ((c_) % FCYC) == FSP * (m * 2 + nn)) {                                   \
+          _Pragma("unroll") for (int r = 0; r < 16; r++) iacc[m][nn][r] += (int32_t)acc[m][nn][r]; \
+          acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(FR[m]), as_bf16x8(FR[2 + nn]), \
+                                                               zero16, 0, 0, 0);               \
+        } else {                                                                               \
+          acc[m][nn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(FR[m]), as_bf16x8(FR[2 + nn]), \
+                                                               acc[m][nn], 0, 0, 0);           \
+        }                                                                                      \
+      }                                                                                        \
+  } while (0)
+  // vmcnt before barrier 1 of step st: the wave's pieces of (st, half 1) have
+  // landed; younger: (st+1, *), (st+2, *) -- 3 pieces per half
+#define H8_VM1(st_, COND)                                                                      \
+  do {                                                                                         \
+    if (!(COND) || (st_) + 2 < s1) H8_WAIT_VM(12);                                             \
+    else if ((st_) + 1 < s1) H8_WAIT_VM(6);                                                    \
+    else H8_WAIT_VM(0);                                                                        \
+  } while (0)
+  // before barrier 2: (st+1, half 0) landed; younger: (st+1, 1), (st+2, *), (st+3, 0)
+#define H8_VM2(st_, COND)                                                                      \
+  do {                                                                                         \
+    if (!(COND) || (st_) + 3 < s1) H8_WAIT_VM(12);                                             \
+    else if ((st_) + 2 < s1) H8_WAIT_VM(9);                                                    \
+    else if ((st_) + 1 < s1) H8_WAIT_VM(3);                                                    \
+    else H8_WAIT_VM(0);                                                                        \
+  } while (0)
+  // K-step st_ in ring slot SL (compile-time), in-group index q_; fr0 holds
+  // its sub-step 0 on entry and the next step's sub-step 0 on exit.
+#define H8_STEP(st_, q_, SL, STAG, COND)                                                       \
+  do {                                                                                         \
+    H8_READ(fr1, SL, 1);                                                                       \
+    H8_WAIT_LGKM(NF); H8_SB();                                                                 \
+    H8_MFMA(fr0, 4 * (q_) + 0, 0, 2, STAG); H8_SB();                                           \
+    H8_WAIT_LGKM(0); H8_VM1(st_, COND);                                                        \
+    __builtin_amdgcn_s_barrier(); H8_SB();                                                     \
+    if (!(COND) || (st_) + 3 < s1) H8_ISSUE((st_) + 3, 0, SL);                                 \
+    H8_READ(fr0, SL, 2);                                                                       \
+    H8_SB();                                                                                   \
+    H8_MFMA(fr1, 4 * (q_) + 1, 0, 2, STAG); H8_SB();                                           \
+    H8_READ(fr1, SL, 3);                                                                       \
+    H8_WAIT_LGKM(NF); H8_SB();                                                                 \
+    H8_MFMA(fr0, 4 * (q_) + 2, 0, 2, STAG); H8_SB();                                           \
+    H8_WAIT_LGKM(0); H8_SB();                                                                  \
+    H8_MFMA(fr1, 4 * (q_) + 3, 0, 1, STAG); H8_SB();                                           \
+    H8_VM2(st_, COND);                                                                         \
+    __builtin_amdgcn_s_barrier(); H8_SB();                                                     \
+    if (!(COND) || (st_) + 3 < s1) H8_ISSUE((st_) + 3, 1, SL);                                 \
+    if (!(COND) || (st_) + 1 < s1) H8_READ(fr0, ((SL) + 1) % 3, 0);                            \
+    H8_SB();                                                                                   \
+    H8_MFMA(fr1, 4 * (q_) + 3, 1, 2, STAG); H8_SB();                                           \
+  } while (0)
+#define H8_FLUSH()                                                                             \
+  do {                                                                                         \
+    _Pragma("unroll") for (int a = 0; a < 2; a++)                                              \
+      _Pragma("unroll") for (int b = 0; b < 2; b++)                                            \
+        _Pragma("unroll") for (int r = 0; r < 16; r++) {                                       \
+          iacc[a][b][r] += (int32_t)acc[a][b][r];                                              \
+          acc[a][b][r] = 0.0f;                                                                 \
+        }                                                                                      \
+  } while (0)
+
+  if (s0 >= s1) return;
+  H8_ISSUE(s0, 0, 0);
+  H8_ISSUE(s0, 1, 0);
+  if (s0 + 1 < s1) { H8_ISSUE(s0 + 1, 0, 1); H8_ISSUE(s0 + 1, 1, 1); }
+  if (s0 + 2 < s1) { H8_ISSUE(s0 + 2, 0, 2); H8_ISSUE(s0 + 2, 1, 2); }
+  // (s0, half 0) landed; younger: (s0, 1) and the two next steps
+  if (s0 + 2 < s1) H8_WAIT_VM(15);
+  else if (s0 + 1 < s1) H8_WAIT_VM(9);
+  else H8_WAIT_VM(3);
+  __builtin_amdgcn_s_barrier();
+  H8_SB();
+  H8_READ(fr0, 0, 0);
+  int64_t st = s0;
+  const int64_t sfull = s0 + ((s1 - s0) / 6) * 6;
+  for (; st < sfull && st + 8 < s1; st += 6) {
+    H8_STEP(st, 0, 0, !NOFLUSH, 0);
+    H8_STEP(st + 1, 1, 1, !NOFLUSH, 0);
+    H8_STEP(st + 2, 2, 2, !NOFLUSH, 0);
+    H8_STEP(st + 3, 3, 0, !NOFLUSH, 0);
+    H8_STEP(st + 4, 4, 1, !NOFLUSH, 0);
+    H8_STEP(st + 5, 5, 2, !NOFLUSH, 0);
+  }
+  for (; st < sfull; st += 6) {
+    H8_STEP(st, 0, 0, !NOFLUSH, 1);
+    H8_STEP(st + 1, 1, 1, !NOFLUSH, 1);
+    H8_STEP(st + 2, 2, 2, !NOFLUSH, 1);
+    H8_STEP(st + 3, 3, 0, !NOFLUSH, 1);
+    H8_STEP(st + 4, 4, 1, !NOFLUSH, 1);
+    H8_STEP(st + 5, 5, 2, !NOFLUSH, 1);
+  }
+  H8_FLUSH();
+  for (int t = 0; st < s1; st++, t++) {
+    const int sl = (int)((st - s0) % 3);
+    if (sl == 0) H8_STEP(st, 0, 0, 0, 1);
+    else if (sl == 1) H8_STEP(st, 0, 1, 0, 1);
+    else H8_STEP(st, 0, 2, 0, 1);
+    if (FL == 2 && t == 2) H8_FLUSH();
+  }
+  H8_FLUSH();
+#undef H8_WAIT_VM
+#undef H8_WAIT_LGKM
+#undef H8_SB
+#undef H8_ISSUE
+#undef H8_READ
+#undef H8_MFMA
+#undef H8_VM1
+#undef H8_VM2
+#undef H8_STEP
+#undef H8_FLUSH
+}
+
 // kx = the number of K-ranges the XCDs split the K axis into (8, 4, 2 or 1):
 // XCD x runs K-range x % kx of the tile groups g = x / kx (mod 8 / kx).  A
 // small cohort (fewer tile groups than XCDs) splits K eight ways; a large one
 // gives every XCD whole tile groups over the full K range, so each output tile
 // is flushed with int64 atomics only once per int32-exact unit (sps_max steps).
-template <int MODE, bool BL, int FL, bool QL>
+template <int MODE, bool BL, int FL, int LAY>
 __global__ __launch_bounds__(512, 1) void k_gram8(const uint16_t *__restrict__ z, int64_t ld,
                                                   const int32_t *__restrict__ tiles, int ntiles, int kc, int kx,
                                                   int64_t nsteps, int lag, int spin_ticks,
@@ -784,7 +977,9 @@ __global__ __launch_bounds__(512, 1) void k_gram8(const uint16_t *__restrict__ z
       f32x16 acc[2][2];
       int32_t iacc[2][2][16];
       g6_zero<2>(acc, iacc);
-      g8_run<MODE, BL, FL, QL>(z, ld, I, tj, s0, s1, smem, acc, iacc);
+      if constexpr (LAY == 2) g8h_run<MODE, BL, FL>(z, ld, I, tj, s0, s1, smem, acc, iacc);
+      else if constexpr (LAY == 3) g8h_run<MODE, BL, FL, BL>(z, ld, I, tj, s0, s1, smem, acc, iacc);
+      else g8_run<MODE, BL, FL, LAY == 1>(z, ld, I, tj, s0, s1, smem, acc, iacc);
       g6_atomics<2>(iacc, I, tj, np_, gram);
     }
     __syncthreads();
@@ -1214,11 +1409,19 @@ static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_
   (void)mode;
 #define G8_PICK(BLV, QLV) (fl == 1 ? k_gram8<0, BLV, 1, QLV> : k_gram8<0, BLV, 2, QLV>)
 #endif
-  // LDS image: quad-row pieces (default) or the earlier pair-row pieces (GRID_GRAM_QL=0; timing A/B)
+  // LDS image (timing A/B, results identical): 1 quad-row pieces (default), 2 half-split ring,
+  // 0 the earlier pair-row pieces (GRID_GRAM_QL)
   const char *qe = getenv("GRID_GRAM_QL");
-  const bool ql = !(qe && atoi(qe) == 0);
-  auto kern = blocked ? (ql ? G8_PICK(true, true) : G8_PICK(true, false))
-                      : (ql ? G8_PICK(false, true) : G8_PICK(false, false));
+  const int lay = qe ? atoi(qe) : 1;
+#ifdef GRID_PROBES
+  REQUIRE(lay >= 0 && lay <= 3 && (lay != 3 || blocked), "GRID_GRAM_QL must be 0, 1, 2 (or 3: K32 panel)");
+  auto kern = blocked ? (lay == 3 ? G8_PICK(true, 3) : lay == 2 ? G8_PICK(true, 2) : lay == 1 ? G8_PICK(true, 1)
+                                                                                     : G8_PICK(true, 0))
+#else
+  REQUIRE(lay >= 0 && lay <= 2, "GRID_GRAM_QL must be 0, 1 or 2");
+  auto kern = blocked ? (lay == 2 ? G8_PICK(true, 2) : lay == 1 ? G8_PICK(true, 1) : G8_PICK(true, 0))
+#endif
+                      : (lay == 2 ? G8_PICK(false, 2) : lay == 1 ? G8_PICK(false, 1) : G8_PICK(false, 0));
 #undef G8_PICK
   hipLaunchKernelGGL(kern, dim3((unsigned)(8 * per)), dim3(512), 0, ctx->stream, d_zb, ld,
                      (const int32_t *)ctx->aux, nt6, (int)bkc, (int)bkx, nsteps, lag, spin, np_,
