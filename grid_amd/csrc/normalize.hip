@@ -580,6 +580,7 @@ __global__ void k_zprep(const int32_t *__restrict__ sel, int64_t r, const double
 
 constexpr int ZR = 8;    // rows per zquant batch
 constexpr int Z7RGS = 0, Z7CBW = 64;   // k_zquant7 grid walk (see the launch)
+constexpr bool Z7W16 = true;           // k_zquant7 16-B loads (see the launch)
 
 // The row means / reciprocals of rows i0 .. i0+R-1 (clamped to n-1), all
 // loaded before any is used: a load inside the row loop, behind its
@@ -1152,7 +1153,11 @@ __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, 
 // PROBE (tools build only, wrong results): bit 0 no z stores, bit 1 no panel
 // stores, bit 2 no loads (codes from a constant).
 // 106 VGPRs, 4 workgroups per CU (forcing 5 spilled 12 VGPRs: 19.0 vs 15.5 ms).
-template <int NT, int PROBE = 0>
+// W16: 16-B loads (the metadata of a lane's 4 columns as int4 / float4, and a
+// 16-code window at sel[s0] & ~7 as two 16-B loads per row instead of three
+// 8-B loads): the texture data path, not HBM, bounds this kernel (PMC: TD busy
+// 99 %, TA 82 %), and it costs per wave-instruction, not per byte.
+template <int NT, int PROBE = 0, bool W16 = false>
 __global__ __launch_bounds__(256) void k_zquant7(Q16 s16, int64_t n, int64_t ld, const int32_t *__restrict__ sel,
                                                  int64_t r, const double *__restrict__ rm,
                                                  const double *__restrict__ rinv, const double *__restrict__ mus,
@@ -1162,7 +1167,7 @@ __global__ __launch_bounds__(256) void k_zquant7(Q16 s16, int64_t n, int64_t ld,
                                                  const int32_t *__restrict__ colmap, int32_t qmax,
                                                  uint16_t *__restrict__ zb, int64_t ld_zb, int64_t kbs,
                                                  int32_t *__restrict__ overflow, int rpw, ZEsc esc,
-                                                 int rgs, int cbw) {
+                                                 int rgs, int cbw, int zblk) {
   // (row group, column block) of this workgroup: the 2-D grid (x = row group) when
   // rgs == 0, else a 1-D grid walked in super-tiles of rgs row groups x cbw column
   // blocks (placement only; every (row group, column block) is visited once)
@@ -1185,26 +1190,49 @@ __global__ __launch_bounds__(256) void k_zquant7(Q16 s16, int64_t n, int64_t ld,
   }
   const int64_t s0 = (by * 256 + threadIdx.x) * 4;
   if (s0 >= r) return;
+  if (zblk) {   // timing probe (tools build): step-4 output blocked [col block][row][1024]
+    zq += by * (n - 1) * 1024;
+    ld_zq = 1024;
+  }
   const int w = (int)((r - s0) < 4 ? (r - s0) : 4);
   const int64_t r0 = bx * rpw;
   const int64_t r1 = (r0 + rpw < n) ? r0 + rpw : n;
   int64_t js[4];
   int32_t cm[4];
   float m32[4], c32[4], ac[4];
+  if (W16 && w == 4) {
+    const int4 sv = *reinterpret_cast<const int4 *>(sel + s0);
+    js[0] = sv.x; js[1] = sv.y; js[2] = sv.z; js[3] = sv.w;
+    if (colmap) {
+      const int4 cv = *reinterpret_cast<const int4 *>(colmap + s0);
+      cm[0] = cv.x; cm[1] = cv.y; cm[2] = cv.z; cm[3] = cv.w;
+    } else {
 #pragma unroll
-  for (int c = 0; c < 4; c++) {
-    const bool ok = c < w;
-    js[c] = sel[ok ? s0 + c : s0];
-    cm[c] = ok ? (colmap ? colmap[s0 + c] : (int32_t)(s0 + c)) : -1;
-    const float2 mc = ok ? mc32[s0 + c] : make_float2(1.0f, 1.0f);
-    m32[c] = mc.x;
-    c32[c] = mc.y;
-    ac[c] = 0x1p-21f * fabsf(mc.y);
+      for (int c = 0; c < 4; c++) cm[c] = (int32_t)(s0 + c);
+    }
+    const float4 m01 = *reinterpret_cast<const float4 *>(mc32 + s0);
+    const float4 m23 = *reinterpret_cast<const float4 *>(mc32 + s0 + 2);
+    m32[0] = m01.x; c32[0] = m01.y; m32[1] = m01.z; c32[1] = m01.w;
+    m32[2] = m23.x; c32[2] = m23.y; m32[3] = m23.z; c32[3] = m23.w;
+#pragma unroll
+    for (int c = 0; c < 4; c++) ac[c] = 0x1p-21f * fabsf(c32[c]);
+  } else {
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const bool ok = c < w;
+      js[c] = sel[ok ? s0 + c : s0];
+      cm[c] = ok ? (colmap ? colmap[s0 + c] : (int32_t)(s0 + c)) : -1;
+      const float2 mc = ok ? mc32[s0 + c] : make_float2(1.0f, 1.0f);
+      m32[c] = mc.x;
+      c32[c] = mc.y;
+      ac[c] = 0x1p-21f * fabsf(mc.y);
+    }
   }
   // the lane's window: the 12 codes at base (three 8-B loads; the last ones
-  // only while inside the row), enough unless 4 selected columns span > 8
-  const int64_t base = js[0] & ~3ll;
-  const int nwin = base + 12 <= ld ? 12 : base + 8 <= ld ? 8 : 4;
+  // only while inside the row), enough unless 4 selected columns span > 8;
+  // W16: the 16 codes at sel[s0] & ~7 (ld % 8 == 0, so 8 always fit)
+  const int64_t base = W16 ? (js[0] & ~7ll) : (js[0] & ~3ll);
+  const int nwin = W16 ? (base + 16 <= ld ? 16 : 8) : (base + 12 <= ld ? 12 : base + 8 <= ld ? 8 : 4);
   int d[4];
   bool inwin = true;
 #pragma unroll
@@ -1214,7 +1242,7 @@ __global__ __launch_bounds__(256) void k_zquant7(Q16 s16, int64_t n, int64_t ld,
   }
   // byte-permute selectors of code c: the 8-B piece it is not in selects zero
   // bytes (0x0c), so code = perm(va) | perm(vb) | perm(vc), branch-free
-  uint32_t pa[4], pb[4], pc[4];
+  uint32_t pa[4], pb[4], pc[4], pd[4];
 #pragma unroll
   for (int c = 0; c < 4; c++) {
     const uint32_t e = (uint32_t)(d[c] & 3), sel2 = (2 * e) | ((2 * e + 1) << 8) | 0x0c0c0000u;
@@ -1222,6 +1250,7 @@ __global__ __launch_bounds__(256) void k_zquant7(Q16 s16, int64_t n, int64_t ld,
     pa[c] = piece == 0 ? sel2 : 0x0c0c0c0cu;
     pb[c] = piece == 1 ? sel2 : 0x0c0c0c0cu;
     pc[c] = piece == 2 ? sel2 : 0x0c0c0c0cu;
+    pd[c] = piece == 3 ? sel2 : 0x0c0c0c0cu;
   }
   typedef unsigned v2u __attribute__((ext_vector_type(2)));
   auto ld8 = [&](const uint16_t *p) -> v2u {
@@ -1229,7 +1258,7 @@ __global__ __launch_bounds__(256) void k_zquant7(Q16 s16, int64_t n, int64_t ld,
     else return *reinterpret_cast<const v2u *>(p);
   };
   // rows i0 .. i0+ZR-1 (rows past r1 re-read row r0)
-  v2u va[ZR], vb[ZR], vc[ZR];
+  v2u va[ZR], vb[ZR], vc[ZR], vd[ZR];
 #pragma unroll
   for (int u = 0; u < ZR; u++) {
     const int64_t i = (r0 + u < r1) ? r0 + u : r0;
@@ -1238,7 +1267,17 @@ __global__ __launch_bounds__(256) void k_zquant7(Q16 s16, int64_t n, int64_t ld,
       va[u] = v2u{0x0FA00FA0u + (uint32_t)u, 0x0FA00FA0u};
       vb[u] = va[u];
       vc[u] = va[u];
+      vd[u] = va[u];
+    } else if constexpr (W16) {
+      typedef unsigned v4u __attribute__((ext_vector_type(4)));
+      const v4u lo = NT & 1 ? __builtin_nontemporal_load(reinterpret_cast<const v4u *>(p))
+                            : *reinterpret_cast<const v4u *>(p);
+      const v4u hi = nwin >= 16 ? (NT & 1 ? __builtin_nontemporal_load(reinterpret_cast<const v4u *>(p + 8))
+                                          : *reinterpret_cast<const v4u *>(p + 8))
+                                : v4u{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+      va[u] = lo.xy; vb[u] = lo.zw; vc[u] = hi.xy; vd[u] = hi.zw;
     } else {
+      vd[u] = v2u{0u, 0u};
       va[u] = ld8(p);
       vb[u] = nwin >= 8 ? ld8(p + 4) : v2u{0xFFFFFFFFu, 0xFFFFFFFFu};
       vc[u] = nwin >= 12 ? ld8(p + 8) : v2u{0xFFFFFFFFu, 0xFFFFFFFFu};
@@ -1273,7 +1312,8 @@ __global__ __launch_bounds__(256) void k_zquant7(Q16 s16, int64_t n, int64_t ld,
 #pragma unroll
       for (int c = 0; c < 4; c++) {
         uint32_t code = __builtin_amdgcn_perm(va[u].y, va[u].x, pa[c]) | __builtin_amdgcn_perm(vb[u].y, vb[u].x, pb[c]) |
-                        __builtin_amdgcn_perm(vc[u].y, vc[u].x, pc[c]);
+                        __builtin_amdgcn_perm(vc[u].y, vc[u].x, pc[c]) |
+                        (W16 ? __builtin_amdgcn_perm(vd[u].y, vd[u].x, pd[c]) : 0u);
         if (!HOT && !inwin && c < w && !(d[c] < nwin)) code = s16.q[i * ld + js[c]];   // gather
         const bool valid = (HOT || c < w) && rowok && code != GRID_Q16_MISS;
         const float y = (float)(int32_t)code * a32;
@@ -1351,7 +1391,8 @@ __global__ __launch_bounds__(256) void k_zquant7(Q16 s16, int64_t n, int64_t ld,
       for (int c = 0; c < 4; c++) {
         const uint32_t code = __builtin_amdgcn_perm(va[u].y, va[u].x, pa[c]) |
                               __builtin_amdgcn_perm(vb[u].y, vb[u].x, pb[c]) |
-                              __builtin_amdgcn_perm(vc[u].y, vc[u].x, pc[c]);
+                              __builtin_amdgcn_perm(vc[u].y, vc[u].x, pc[c]) |
+                              (W16 ? __builtin_amdgcn_perm(vd[u].y, vd[u].x, pd[c]) : 0u);
         const float y = (float)code * a32;
         const float t = (y - m32[c]) * c32[c];
         const float kk = rintf(t);
@@ -1733,6 +1774,11 @@ static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, int64_
       // k_zquant7 reads overlapping 24-B windows: plain loads (the rows' lines
       // serve neighbouring lanes from L2) unless GRID_ZQUANT_NT=1 (15.7 vs 17.8 ms)
       const bool nt7 = ntv && atoi(ntv) == 1;
+      // 16-B loads (GRID_Z7_W16, timing A/B; results identical); needs 16-B aligned operands
+      const char *w16e = getenv("GRID_Z7_W16");
+      const bool w16 = (w16e ? atoi(w16e) != 0 : Z7W16) && (ld % 8) == 0 && ((uintptr_t)s16.q % 16) == 0 &&
+                       ((uintptr_t)d_sel % 16) == 0 && (!d_colmap || ((uintptr_t)d_colmap % 16) == 0) &&
+                       ((uintptr_t)mc32 % 16) == 0;
       REQUIRE(ceil_div(ceil_div(r, 4), 256) <= 65535, "r too large for one launch");
       // super-tiles of rgs row groups x cbw column blocks (GRID_Z7_RGS / GRID_Z7_CBW; RGS=0: the 2-D grid,
       // row groups fastest)
@@ -1740,20 +1786,27 @@ static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, int64_
       const int rgs = rge ? atoi(rge) : Z7RGS, cbw = cbe ? atoi(cbe) : Z7CBW;
       REQUIRE(rgs >= 0 && cbw > 0, "GRID_Z7_RGS must be >= 0 and GRID_Z7_CBW > 0");
       const int64_t nrg7 = ceil_div(n, ZR), ncb7 = ceil_div(ceil_div(r, 4), 256);
+#ifdef GRID_PROBES
+      const char *zbe = getenv("GRID_Z7_ZBLK");     // wrong escape positions: timing only
+      const int zblk = zbe ? atoi(zbe) : 0;
+      REQUIRE(!zblk || ld_zq >= ncb7 * 1024, "GRID_Z7_ZBLK needs ld_zq >= %lld", (long long)(ncb7 * 1024));
+#else
+      const int zblk = 0;
+#endif
       REQUIRE(rgs == 0 || nrg7 * ncb7 < (1ll << 31), "zquant grid too large");
       const dim3 g7 = rgs > 0 ? dim3((unsigned)(nrg7 * ncb7)) : dim3((unsigned)nrg7, (unsigned)ncb7);
 #ifdef GRID_PROBES
       const char *pe = getenv("GRID_Z7_PROBE");
       const int pr = pe ? atoi(pe) : 0;
-#define Z7P(P) (nt7 ? k_zquant7<1, P> : k_zquant7<0, P>)
+#define Z7P(P) (w16 ? (nt7 ? k_zquant7<1, P, true> : k_zquant7<0, P, true>) : (nt7 ? k_zquant7<1, P> : k_zquant7<0, P>))
       auto k7 = pr == 1 ? Z7P(1) : pr == 2 ? Z7P(2) : pr == 3 ? Z7P(3) : pr == 4 ? Z7P(4) : pr == 7 ? Z7P(7) : Z7P(0);
 #undef Z7P
 #else
-      auto k7 = nt7 ? k_zquant7<1> : k_zquant7<0>;
+      auto k7 = w16 ? (nt7 ? k_zquant7<1, 0, true> : k_zquant7<0, 0, true>) : (nt7 ? k_zquant7<1> : k_zquant7<0>);
 #endif
       hipLaunchKernelGGL(k7, g7, dim3(256), 0, ctx->stream, s16, n, ld, d_sel, r, d_rm,
                          rinv, mus, sq, rsq, mc32, scale, d_zq16, ld_zq, d_colmap, qmax, d_zb, ld_zb, kbs, d_of,
-                         ZR, esc, rgs, cbw);
+                         ZR, esc, rgs, cbw, zblk);
     } else if (d_zq16) {
       auto k16 = c16 ? Z6_PICK(int16_t, true) : Z6_PICK(int16_t, false);
       hipLaunchKernelGGL(k16, g6, dim3(256), 0, ctx->stream, d_q, s16, n, ld, sidx, d_rm, rinv, mus, sq, rsq, mc32,
