@@ -581,6 +581,7 @@ __global__ void k_zprep(const int32_t *__restrict__ sel, int64_t r, const double
 constexpr int ZR = 8;    // rows per zquant batch
 constexpr int Z7RGS = 0, Z7CBW = 64;   // k_zquant7 grid walk (see the launch)
 constexpr bool Z7W16 = true;           // k_zquant7 16-B loads (see the launch)
+constexpr bool Z7PAIR = false;         // k_zquant7 paired 16-B stores (see the launch)
 
 // The row means / reciprocals of rows i0 .. i0+R-1 (clamped to n-1), all
 // loaded before any is used: a load inside the row loop, behind its
@@ -1157,8 +1158,8 @@ __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, 
 // 16-code window at sel[s0] & ~7 as two 16-B loads per row instead of three
 // 8-B loads): the texture data path, not HBM, bounds this kernel (PMC: TD busy
 // 99 %, TA 82 %), and it costs per wave-instruction, not per byte.
-template <int NT, int PROBE = 0, bool W16 = false>
-__global__ __launch_bounds__(256) void k_zquant7(Q16 s16, int64_t n, int64_t ld, const int32_t *__restrict__ sel,
+template <int NT, int PROBE = 0, bool W16 = false, bool PAIR = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_zquant7(Q16 s16, int64_t n, int64_t ld, const int32_t *__restrict__ sel,
                                                  int64_t r, const double *__restrict__ rm,
                                                  const double *__restrict__ rinv, const double *__restrict__ mus,
                                                  const double *__restrict__ sq, const double *__restrict__ rsq,
@@ -1356,67 +1357,112 @@ __global__ __launch_bounds__(256) void k_zquant7(Q16 s16, int64_t n, int64_t ld,
   // a missing cell or an escape is computed from garbage and DEFERRED (the
   // exact loop below gathers it); a row with a zero / NaN mean (uniform) is
   // written as NaN codes directly.
-  auto hot_rows = [&]() {
-    uint32_t outm = 0;                                // this lane's cells outside its 8-code window
-#pragma unroll
-    for (int c = 0; c < 4; c++) outm |= (d[c] < nwin) ? 0u : (1u << c);
-    // first-order error of t (u = 2^-24; a32 = fl(0.01/rm), y = fl(q a32),
-    // m32 = fl(mu), d = fl(y - m32), c32 = fl(100 scale / sqrt(mu)), t = fl(d c32);
-    // the fp64 chain's own error is below 2^-50 relative):
-    //   |t - 100 z| <= |c| (2u y + u m) + 3u |t| + O(u^2)
-    // dl = 2^-23 (1.5 |c| y + |c| m + 2 |t|) = u (3|c|y + 2|c|m + 4|t|) covers it
-    // with a 1.33x margin on every term (zquant_rows' 8u per term deferred ~3x
-    // as many cells to the exact chain at the bench shape)
-    float cy[4], cm2[4];
+  // first-order error of t (u = 2^-24; a32 = fl(0.01/rm), y = fl(q a32),
+  // m32 = fl(mu), d = fl(y - m32), c32 = fl(100 scale / sqrt(mu)), t = fl(d c32);
+  // the fp64 chain's own error is below 2^-50 relative):
+  //   |t - 100 z| <= |c| (2u y + u m) + 3u |t| + O(u^2)
+  // dl = 2^-23 (1.5 |c| y + |c| m + 2 |t|) = u (3|c|y + 2|c|m + 4|t|) covers it
+  // with a 1.33x margin on every term (zquant_rows' 8u per term deferred ~3x
+  // as many cells to the exact chain at the bench shape)
+  // HOT row u: the packed int16 codes (z0, z1) and bf16 panel values (b0, b1)
+  // of the lane's 4 cells; undecided cells set their bits in slowm.  A row
+  // with a zero / NaN mean (uniform) is NaN codes and a zero panel.
+  auto hot_row = [&](int u, uint32_t outm, const float (&cy)[4], const float (&cm2)[4], uint32_t &z0,
+                     uint32_t &z1, uint32_t &b0, uint32_t &b1) {
+    const double rmi = rmg[u], rii = rig[u];
+    if (!(rmi != 0.0 && rmi == rmi)) {
+      z0 = z1 = 0x80008000u;
+      b0 = b1 = 0u;
+      return;
+    }
+    const float a32 = (float)(0.01 * rii);
+    uint32_t zc[4], bv[4], dm = outm;
 #pragma unroll
     for (int c = 0; c < 4; c++) {
+      const uint32_t code = __builtin_amdgcn_perm(va[u].y, va[u].x, pa[c]) |
+                            __builtin_amdgcn_perm(vb[u].y, vb[u].x, pb[c]) |
+                            __builtin_amdgcn_perm(vc[u].y, vc[u].x, pc[c]) |
+                            (W16 ? __builtin_amdgcn_perm(vd[u].y, vd[u].x, pd[c]) : 0u);
+      const float y = (float)code * a32;
+      const float t = (y - m32[c]) * c32[c];
+      const float kk = rintf(t);
+      const float g = 0.5f - fabsf(t - kk);
+      const float dl = fmaf(cy[c], fabsf(y), fmaf(0x1p-22f, fabsf(t), cm2[c]));   // y < 0 iff the row mean is
+      const bool good = (g > dl) & (fabsf(t) > dl) & (fabsf(kk) <= 32765.0f) & (code <= GRID_Q16_MAXV);
+      zc[c] = (__float_as_uint(kk) == 0x80000000u) ? (uint32_t)GRID_ZQ16_NEG0 : (uint32_t)(int32_t)kk;
+      bv[c] = __float_as_uint(__builtin_amdgcn_fmed3f(kk, -qf, qf) + 0.0f);   // its high half: exact bf16
+      dm |= good ? 0u : (1u << c);
+    }
+    slowm |= dm << (u * 4);
+    // byte permutes pack the low halves of the codes / the high halves of the floats
+    z0 = __builtin_amdgcn_perm(zc[1], zc[0], 0x05040100u);
+    z1 = __builtin_amdgcn_perm(zc[3], zc[2], 0x05040100u);
+    b0 = __builtin_amdgcn_perm(bv[1], bv[0], 0x07060302u);
+    b1 = __builtin_amdgcn_perm(bv[3], bv[2], 0x07060302u);
+  };
+  auto hot_prep = [&](uint32_t &outm, float (&cy)[4], float (&cm2)[4]) {
+    outm = 0;                                         // this lane's cells outside its code window
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      outm |= (d[c] < nwin) ? 0u : (1u << c);
       cy[c] = 0x1.8p-23f * fabsf(c32[c]);
       cm2[c] = 0x1p-23f * fabsf(c32[c]) * fabsf(m32[c]);
     }
+  };
+  auto hot_rows = [&]() {
+    uint32_t outm;
+    float cy[4], cm2[4];
+    hot_prep(outm, cy, cm2);
 #pragma unroll
     for (int u = 0; u < ZR; u++) {
       const int64_t i = r0 + u;
       if (i >= r1) break;
-      const double rmi = rmg[u], rii = rig[u];
-      int16_t *zrow = zq + i * ld_zq + s0;
-      uint16_t *brow = zb + zb0 + i * zbs;
-      if (!(rmi != 0.0 && rmi == rmi)) {              // uniform: every cell NaN, panel 0
-        *reinterpret_cast<uint2 *>(zrow) = make_uint2(0x80008000u, 0x80008000u);
-        *reinterpret_cast<uint2 *>(brow) = make_uint2(0u, 0u);
-        continue;
-      }
-      const float a32 = (float)(0.01 * rii);
-      uint32_t zc[4], bv[4], dm = outm;
+      uint32_t z0, z1, b0, b1;
+      hot_row(u, outm, cy, cm2, z0, z1, b0, b1);
+      if (!(PROBE & 1)) *reinterpret_cast<uint2 *>(zq + i * ld_zq + s0) = make_uint2(z0, z1);
+      if (!(PROBE & 2)) *reinterpret_cast<uint2 *>(zb + zb0 + i * zbs) = make_uint2(b0, b1);
+      if (PROBE) slowm = 0;
+    }
+  };
+  // PAIRED stores (a full row group): lanes 2k and 2k+1 swap halves with one
+  // DPP move per dword, so the even lane stores 16 B of row u (its 4 cells and
+  // its partner's) and the odd lane 16 B of row u+1: half the store
+  // instructions (the texture path costs per wave-instruction)
+  auto hot_pairs = [&]() {
+    uint32_t outm;
+    float cy[4], cm2[4];
+    hot_prep(outm, cy, cm2);
+    const bool odd = threadIdx.x & 1;
+    auto swp = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false); };
 #pragma unroll
-      for (int c = 0; c < 4; c++) {
-        const uint32_t code = __builtin_amdgcn_perm(va[u].y, va[u].x, pa[c]) |
-                              __builtin_amdgcn_perm(vb[u].y, vb[u].x, pb[c]) |
-                              __builtin_amdgcn_perm(vc[u].y, vc[u].x, pc[c]) |
-                              (W16 ? __builtin_amdgcn_perm(vd[u].y, vd[u].x, pd[c]) : 0u);
-        const float y = (float)code * a32;
-        const float t = (y - m32[c]) * c32[c];
-        const float kk = rintf(t);
-        const float g = 0.5f - fabsf(t - kk);
-        const float dl = fmaf(cy[c], fabsf(y), fmaf(0x1p-22f, fabsf(t), cm2[c]));   // y < 0 iff the row mean is
-        const bool good = (g > dl) & (fabsf(t) > dl) & (fabsf(kk) <= 32765.0f) & (code <= GRID_Q16_MAXV);
-        zc[c] = (__float_as_uint(kk) == 0x80000000u) ? (uint32_t)GRID_ZQ16_NEG0 : (uint32_t)(int32_t)kk;
-        bv[c] = __float_as_uint(__builtin_amdgcn_fmed3f(kk, -qf, qf) + 0.0f);   // its high half: exact bf16
-        dm |= good ? 0u : (1u << c);
-      }
-      slowm |= dm << (u * 4);
-      // byte permutes pack the low halves of the codes / the high halves of the floats
+    for (int u = 0; u < ZR; u += 2) {
+      uint32_t za0, za1, ba0, ba1, zb0_, zb1_, bb0, bb1;
+      hot_row(u, outm, cy, cm2, za0, za1, ba0, ba1);
+      hot_row(u + 1, outm, cy, cm2, zb0_, zb1_, bb0, bb1);
+      const uint32_t rz0 = swp(odd ? za0 : zb0_), rz1 = swp(odd ? za1 : zb1_);
+      const uint32_t rb0 = swp(odd ? ba0 : bb0), rb1 = swp(odd ? ba1 : bb1);
+      const int64_t i = r0 + u + (odd ? 1 : 0);
+      const int64_t sh = odd ? 4 : 0;
       if (!(PROBE & 1))
-        *reinterpret_cast<uint2 *>(zrow) = make_uint2(__builtin_amdgcn_perm(zc[1], zc[0], 0x05040100u),
-                                                      __builtin_amdgcn_perm(zc[3], zc[2], 0x05040100u));
+        *reinterpret_cast<uint4 *>(zq + i * ld_zq + s0 - sh) =
+            odd ? make_uint4(rz0, rz1, zb0_, zb1_) : make_uint4(za0, za1, rz0, rz1);
       if (!(PROBE & 2))
-        *reinterpret_cast<uint2 *>(brow) = make_uint2(__builtin_amdgcn_perm(bv[1], bv[0], 0x07060302u),
-                                                      __builtin_amdgcn_perm(bv[3], bv[2], 0x07060302u));
+        *reinterpret_cast<uint4 *>(zb + zb0 - sh + i * zbs) =
+            odd ? make_uint4(rb0, rb1, bb0, bb1) : make_uint4(ba0, ba1, rb0, rb1);
       if (PROBE) slowm = 0;
     }
   };
   // wave-uniform test (lanes past r have returned)
   const bool hot = __all(w == 4 && vec_zq && vec_zb && zb != nullptr);
-  if (hot) hot_rows();
+  // pairing: the partner lane holds the next 4 columns of both outputs and the
+  // pair's 8 panel columns are 16-B aligned (a disabled partner reads INT_MIN)
+  const int cmp = __builtin_amdgcn_update_dpp((int)0x80000000, cm[0], 0xB1, 0xF, 0xF, false);
+  const bool podd = threadIdx.x & 1;
+  const bool pair = PAIR && hot && r1 - r0 == ZR && (ld_zq & 7) == 0 && ((uintptr_t)zq & 15) == 0 &&
+                    ((kbs > 0 ? kbs : ld_zb) & 7) == 0 && ((uintptr_t)zb & 15) == 0 &&
+                    __all(podd ? cmp == cm[0] - 4 : (cmp == cm[0] + 4 && (cm[0] & 7) == 0));
+  if (pair) hot_pairs();
+  else if (hot) hot_rows();
   else rows(std::integral_constant<bool, false>());
   if (__builtin_expect(slowm != 0, 0)) {          // exact fp64 chain (rare), after the fast stores
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1779,6 +1825,9 @@ static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, int64_
       const bool w16 = (w16e ? atoi(w16e) != 0 : Z7W16) && (ld % 8) == 0 && ((uintptr_t)s16.q % 16) == 0 &&
                        ((uintptr_t)d_sel % 16) == 0 && (!d_colmap || ((uintptr_t)d_colmap % 16) == 0) &&
                        ((uintptr_t)mc32 % 16) == 0;
+      // paired 16-B stores (GRID_Z7_PAIR, timing A/B; results identical; with the 16-B loads)
+      const char *pre = getenv("GRID_Z7_PAIR");
+      const bool pr7 = (pre ? atoi(pre) != 0 : Z7PAIR) && w16;
       REQUIRE(ceil_div(ceil_div(r, 4), 256) <= 65535, "r too large for one launch");
       // super-tiles of rgs row groups x cbw column blocks (GRID_Z7_RGS / GRID_Z7_CBW; RGS=0: the 2-D grid,
       // row groups fastest)
@@ -1798,11 +1847,13 @@ static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, int64_
 #ifdef GRID_PROBES
       const char *pe = getenv("GRID_Z7_PROBE");
       const int pr = pe ? atoi(pe) : 0;
-#define Z7P(P) (w16 ? (nt7 ? k_zquant7<1, P, true> : k_zquant7<0, P, true>) : (nt7 ? k_zquant7<1, P> : k_zquant7<0, P>))
+#define Z7P(P) (w16 ? (pr7 ? k_zquant7<0, P, true, true> : k_zquant7<0, P, true>) : k_zquant7<0, P>)
       auto k7 = pr == 1 ? Z7P(1) : pr == 2 ? Z7P(2) : pr == 3 ? Z7P(3) : pr == 4 ? Z7P(4) : pr == 7 ? Z7P(7) : Z7P(0);
 #undef Z7P
+      if (nt7) k7 = w16 ? k_zquant7<1, 0, true> : k_zquant7<1>;
 #else
-      auto k7 = w16 ? (nt7 ? k_zquant7<1, 0, true> : k_zquant7<0, 0, true>) : (nt7 ? k_zquant7<1> : k_zquant7<0>);
+      auto k7 = w16 ? (pr7 ? k_zquant7<0, 0, true, true> : nt7 ? k_zquant7<1, 0, true> : k_zquant7<0, 0, true>)
+                    : (nt7 ? k_zquant7<1> : k_zquant7<0>);
 #endif
       hipLaunchKernelGGL(k7, g7, dim3(256), 0, ctx->stream, s16, n, ld, d_sel, r, d_rm,
                          rinv, mus, sq, rsq, mc32, scale, d_zq16, ld_zq, d_colmap, qmax, d_zb, ld_zb, kbs, d_of,
