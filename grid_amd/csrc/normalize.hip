@@ -325,10 +325,19 @@ template <int VW, bool S16, bool NTL = false, bool CHECK = true>
 __device__ __forceinline__ void load_row(const int32_t *__restrict__ q, const Q16 &s16, int64_t i, int64_t ld,
                                          int64_t j0, int32_t (&v)[VW]) {
   if constexpr (S16) {
-    // 2 (VW 1), 4 (VW 2) or 8 (VW 4) bytes of uint16 codes per row
-    static_assert(VW == 1 || VW == 2 || VW == 4, "compact rows load 1, 2 or 4 columns");
+    // 2 (VW 1), 4 (VW 2), 8 (VW 4) or 16 (VW 8) bytes of uint16 codes per row
+    static_assert(VW == 1 || VW == 2 || VW == 4 || VW == 8, "compact rows load 1, 2, 4 or 8 columns");
     const uint16_t *p = s16.q + i * ld + j0;
-    if constexpr (VW == 4) {
+    if constexpr (VW == 8) {
+      typedef unsigned v4u __attribute__((ext_vector_type(4)));
+      const v4u u = NTL ? __builtin_nontemporal_load(reinterpret_cast<const v4u *>(p))
+                        : *reinterpret_cast<const v4u *>(p);
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        v[2 * k] = (int32_t)(u[k] & 0xFFFFu);
+        v[2 * k + 1] = (int32_t)(u[k] >> 16);
+      }
+    } else if constexpr (VW == 4) {
       const uint2 u = *reinterpret_cast<const uint2 *>(p);
       v[0] = (int32_t)(u.x & 0xFFFFu); v[1] = (int32_t)(u.x >> 16);
       v[2] = (int32_t)(u.y & 0xFFFFu); v[3] = (int32_t)(u.y >> 16);
@@ -1716,11 +1725,13 @@ static int col_stats_impl(grid_ctx *ctx, bool vars, const int32_t *d_q, const Q1
   // compact codes: GRID_COL16_VW columns per thread (1: 2-B loads, 2: 4-B loads, the default; timing only)
   const char *c16v = getenv("GRID_COL16_VW");
   const int vw16 = c16v ? atoi(c16v) : COL16_VW;
-  REQUIRE(vw16 == 1 || vw16 == 2 || vw16 == 4, "GRID_COL16_VW must be 1, 2 or 4 (got %d)", vw16);
-  const int vw = s16.q ? vw16 : vec4_ok(d_q, ld) ? (want == 4 ? 4 : want == 1 ? 1 : 2) : 1;
+  REQUIRE(vw16 == 1 || vw16 == 2 || vw16 == 4 || vw16 == 8, "GRID_COL16_VW must be 1, 2, 4 or 8 (got %d)", vw16);
+  // 16-B rows (VW 8) need 16-B aligned rows of the compact matrix
+  const int vw = s16.q ? (vw16 == 8 && (ld % 8 != 0 || (uintptr_t)s16.q % 16 != 0) ? 4 : vw16)
+                       : vec4_ok(d_q, ld) ? (want == 4 ? 4 : want == 1 ? 1 : 2) : 1;
   const dim3 grid((unsigned)ceil_div(ceil_div(m, vw), 256));
   if (!vars) {
-    auto kern = s16.q ? (vw == 4 ? k_col_means<4, true>
+    auto kern = s16.q ? (vw == 8 ? (nt ? k_col_means<8, true, CU, true> : k_col_means<8, true>) : vw == 4 ? k_col_means<4, true>
                          : vw == 2 ? (cu16 ? k_col_means<2, true, 16, true>
                                       : nt ? k_col_means<2, true, CU, true> : k_col_means<2, true>)
                                    : (nt ? k_col_means<1, true, CU, true> : k_col_means<1, true>))
@@ -1728,7 +1739,7 @@ static int col_stats_impl(grid_ctx *ctx, bool vars, const int32_t *d_q, const Q1
                 : cu16 ? k_col_means<1, false, 16> : nt ? k_col_means<1, false, CU, true> : k_col_means<1, false>;
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, ctx->stream, d_q, s16, n, m, ld, d_rm, rinv, rbad, d_out);
   } else {
-    auto kern = s16.q ? (vw == 4 ? k_col_vars<4, true>
+    auto kern = s16.q ? (vw == 8 ? (nt ? k_col_vars<8, true, CU, true> : k_col_vars<8, true>) : vw == 4 ? k_col_vars<4, true>
                          : vw == 2 ? (cu16 ? k_col_vars<2, true, 16, true>
                                       : nt ? k_col_vars<2, true, CU, true> : k_col_vars<2, true>)
                                    : (nt ? k_col_vars<1, true, CU, true> : k_col_vars<1, true>))
