@@ -319,6 +319,7 @@ constexpr int CU = 8;   // rows unrolled per iteration in the column kernels
 // (VW == 4), or one 8-B load of 4 compact uint16 values (S16).
 constexpr bool COL_NT = true;   // default for GRID_COL_NT
 constexpr int COL16_VW = 2;     // default for GRID_COL16_VW (compact codes)
+constexpr bool COL_PF = false;  // default for GRID_COL_PF
 // CHECK = false (compact codes): the raw codes only, so a group of rows can
 // be loaded before any value is inspected; fix16() then decodes the group.
 template <int VW, bool S16, bool NTL = false, bool CHECK = true>
@@ -426,7 +427,9 @@ __device__ __forceinline__ int32_t q_at(const int32_t *__restrict__ q, const Q16
   else return q[i * ld + j];
 }
 
-template <int VW, bool S16, int CUN = CU, bool NTL = false>
+// PF: software-pipelined row groups (the next group's loads issued before
+// this group is summed; the summation order is unchanged).
+template <int VW, bool S16, int CUN = CU, bool NTL = false, bool PF = false>
 __global__ __launch_bounds__(256) void k_col_means(const int32_t *__restrict__ q, Q16 s16, int64_t n, int64_t m,
                                                    int64_t ld, const double *__restrict__ rm,
                                                    const double *__restrict__ rinv, const uint8_t *__restrict__ rbad,
@@ -449,11 +452,11 @@ __global__ __launch_bounds__(256) void k_col_means(const int32_t *__restrict__ q
   int64_t cnt[VW];
 #pragma unroll
   for (int c = 0; c < VW; c++) { acc[c] = 0.0; cnt[c] = 0; }
-  int64_t i = 0;
-  for (; i + CUN <= n; i += CUN) {
-    int32_t v[CUN][VW];
+  auto ld_grp = [&](int32_t (&v)[CUN][VW], int64_t i0) {
 #pragma unroll
-    for (int u = 0; u < CUN; u++) load_row<VW, S16, NTL, false>(q, s16, i + u, ld, j0, v[u]);
+    for (int u = 0; u < CUN; u++) load_row<VW, S16, NTL, false>(q, s16, i0 + u, ld, j0, v[u]);
+  };
+  auto do_grp = [&](int32_t (&v)[CUN][VW], int64_t i) {
     if (__builtin_expect(plain_group<S16, CUN, VW>(v, rbad + i), 1)) {
       // every cell valid (the common case): no per-cell masks or counts
 #pragma unroll
@@ -464,7 +467,7 @@ __global__ __launch_bounds__(256) void k_col_means(const int32_t *__restrict__ q
       }
 #pragma unroll
       for (int c = 0; c < VW; c++) cnt[c] += CUN;
-      continue;
+      return;
     }
     if constexpr (S16) fix16<CUN, VW>(v, i, j0, s16);
 #pragma unroll
@@ -475,6 +478,27 @@ __global__ __launch_bounds__(256) void k_col_means(const int32_t *__restrict__ q
         double y;
         if (yval(v[u][c], r, ri, y)) { acc[c] = acc[c] + y; cnt[c]++; }
       }
+    }
+  };
+  const int64_t ng = n / CUN;
+  int64_t i = 0;
+  if constexpr (PF) {
+    // the next group's loads are in flight while this group is summed (same order)
+    int32_t va[CUN][VW], vb[CUN][VW];
+    if (ng > 0) ld_grp(va, 0);
+    for (int64_t g = 0; g < ng; g += 2) {
+      if (g + 1 < ng) ld_grp(vb, (g + 1) * CUN);
+      do_grp(va, g * CUN);
+      if (g + 1 >= ng) break;
+      if (g + 2 < ng) ld_grp(va, (g + 2) * CUN);
+      do_grp(vb, (g + 1) * CUN);
+    }
+    i = ng * CUN;
+  } else {
+    for (; i + CUN <= n; i += CUN) {
+      int32_t v[CUN][VW];
+      ld_grp(v, i);
+      do_grp(v, i);
     }
   }
   for (; i < n; i++) {
@@ -490,7 +514,7 @@ __global__ __launch_bounds__(256) void k_col_means(const int32_t *__restrict__ q
   for (int c = 0; c < VW; c++) mu[j0 + c] = acc[c] / (double)cnt[c];   // 0/0 -> NaN (numpy)
 }
 
-template <int VW, bool S16, int CUN = CU, bool NTL = false>
+template <int VW, bool S16, int CUN = CU, bool NTL = false, bool PF = false>
 __global__ __launch_bounds__(256) void k_col_vars(const int32_t *__restrict__ q, Q16 s16, int64_t n, int64_t m,
                                                   int64_t ld, const double *__restrict__ rm,
                                                   const double *__restrict__ rinv, const uint8_t *__restrict__ rbad,
@@ -519,11 +543,11 @@ __global__ __launch_bounds__(256) void k_col_vars(const int32_t *__restrict__ q,
   double acc[VW], mj[VW];
 #pragma unroll
   for (int c = 0; c < VW; c++) { acc[c] = 0.0; mj[c] = mu[j0 + c]; }
-  int64_t i = 0;
-  for (; i + CUN <= n; i += CUN) {
-    int32_t v[CUN][VW];
+  auto ld_grp = [&](int32_t (&v)[CUN][VW], int64_t i0) {
 #pragma unroll
-    for (int u = 0; u < CUN; u++) load_row<VW, S16, NTL, false>(q, s16, i + u, ld, j0, v[u]);
+    for (int u = 0; u < CUN; u++) load_row<VW, S16, NTL, false>(q, s16, i0 + u, ld, j0, v[u]);
+  };
+  auto do_grp = [&](int32_t (&v)[CUN][VW], int64_t i) {
     if (__builtin_expect(plain_group<S16, CUN, VW>(v, rbad + i), 1)) {
       // every cell valid: y is finite, so dd is NaN only when mu_j is, and
       // then every term is (the sum is reset to nansum's 0 below)
@@ -536,7 +560,7 @@ __global__ __launch_bounds__(256) void k_col_vars(const int32_t *__restrict__ q,
           acc[c] = acc[c] + d * d;
         }
       }
-      continue;
+      return;
     }
     if constexpr (S16) fix16<CUN, VW>(v, i, j0, s16);
 #pragma unroll
@@ -550,6 +574,26 @@ __global__ __launch_bounds__(256) void k_col_vars(const int32_t *__restrict__ q,
           if (dd == dd) acc[c] = acc[c] + dd;      // nansum: NaN (mu NaN) -> 0
         }
       }
+    }
+  };
+  const int64_t ng = n / CUN;
+  int64_t i = 0;
+  if constexpr (PF) {
+    int32_t va[CUN][VW], vb[CUN][VW];
+    if (ng > 0) ld_grp(va, 0);
+    for (int64_t g = 0; g < ng; g += 2) {
+      if (g + 1 < ng) ld_grp(vb, (g + 1) * CUN);
+      do_grp(va, g * CUN);
+      if (g + 1 >= ng) break;
+      if (g + 2 < ng) ld_grp(va, (g + 2) * CUN);
+      do_grp(vb, (g + 1) * CUN);
+    }
+    i = ng * CUN;
+  } else {
+    for (; i + CUN <= n; i += CUN) {
+      int32_t v[CUN][VW];
+      ld_grp(v, i);
+      do_grp(v, i);
     }
   }
   for (; i < n; i++) {
@@ -1720,6 +1764,8 @@ static int col_stats_impl(grid_ctx *ctx, bool vars, const int32_t *d_q, const Q1
   const char *cu = getenv("GRID_COL16_CU");   // compact codes: 16 rows in flight (timing only)
   const bool cu16 = s16.q && cu && atoi(cu) == 16;
 #endif
+  const char *cpf = getenv("GRID_COL_PF");  // software-pipelined row groups, compact 2-column path (A/B)
+  const bool pf = cpf ? atoi(cpf) != 0 : COL_PF;
   const char *cn = getenv("GRID_COL_NT");   // streaming (nontemporal) loads, 1-column path (A/B)
   const bool nt = cn ? atoi(cn) != 0 : COL_NT;
   // compact codes: GRID_COL16_VW columns per thread (1: 2-B loads, 2: 4-B loads, the default; timing only)
@@ -1733,7 +1779,8 @@ static int col_stats_impl(grid_ctx *ctx, bool vars, const int32_t *d_q, const Q1
   if (!vars) {
     auto kern = s16.q ? (vw == 8 ? (nt ? k_col_means<8, true, CU, true> : k_col_means<8, true>) : vw == 4 ? k_col_means<4, true>
                          : vw == 2 ? (cu16 ? k_col_means<2, true, 16, true>
-                                      : nt ? k_col_means<2, true, CU, true> : k_col_means<2, true>)
+                                      : nt ? (pf ? k_col_means<2, true, CU, true, true> : k_col_means<2, true, CU, true>)
+                                           : k_col_means<2, true>)
                                    : (nt ? k_col_means<1, true, CU, true> : k_col_means<1, true>))
                 : vw == 4 ? k_col_means<4, false> : vw == 2 ? k_col_means<2, false>
                 : cu16 ? k_col_means<1, false, 16> : nt ? k_col_means<1, false, CU, true> : k_col_means<1, false>;
@@ -1741,7 +1788,8 @@ static int col_stats_impl(grid_ctx *ctx, bool vars, const int32_t *d_q, const Q1
   } else {
     auto kern = s16.q ? (vw == 8 ? (nt ? k_col_vars<8, true, CU, true> : k_col_vars<8, true>) : vw == 4 ? k_col_vars<4, true>
                          : vw == 2 ? (cu16 ? k_col_vars<2, true, 16, true>
-                                      : nt ? k_col_vars<2, true, CU, true> : k_col_vars<2, true>)
+                                      : nt ? (pf ? k_col_vars<2, true, CU, true, true> : k_col_vars<2, true, CU, true>)
+                                           : k_col_vars<2, true>)
                                    : (nt ? k_col_vars<1, true, CU, true> : k_col_vars<1, true>))
                 : vw == 4 ? k_col_vars<4, false> : vw == 2 ? k_col_vars<2, false>
                 : cu16 ? k_col_vars<1, false, 16> : nt ? k_col_vars<1, false, CU, true> : k_col_vars<1, false>;
