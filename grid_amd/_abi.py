@@ -22,6 +22,7 @@ ZQ_NAN = -(2 ** 31)
 ZQ_NEG0 = -(2 ** 31) + 1
 ZQ16_NAN, ZQ16_NEG0, ZQ16_ESC = -32768, -32767, -32766   # GRID_ZQ16_* (grid_norm_zquant_kb16)
 BLOCK = 8192
+KBW = 32                       # K-block width of the k-NN panel (common.hpp KBW)
 
 _i64, _i32, _f64, _vp = C.c_int64, C.c_int32, C.c_double, C.c_void_p
 

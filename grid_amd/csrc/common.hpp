@@ -21,6 +21,9 @@ struct grid_ctx {
   int32_t *aux_tiles_host = nullptr;   // host copy of the uploaded tile list (re-upload check)
   int aux_tiles_n = 0;
 };
+// K-blocked bf16 panel of the k-NN Gram: [kpad / KBW][np][KBW] (a 16-row
+// half K-step of k_gram8's ring is then 1 KiB contiguous: whole 128-B lines)
+constexpr int KBW = 32;
 constexpr size_t GRID_AUX_BYTES = 4 << 20;   // Gram tile list (<= 512 Ki tiles) + round counters
 
 void grid_set_error(const char *fmt, ...);

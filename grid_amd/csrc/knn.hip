@@ -1244,7 +1244,7 @@ __global__ void k_panel_i32(const int32_t *__restrict__ zq, int64_t n, int64_t l
     v = zq[i * ld + cols[c]];
     v = v == GRID_MISSING ? 0 : min(max(v, -qmax), qmax);        // np.clip order: max, then min
   }
-  zb[(c >> 6) * np_ * 64 + i * 64 + (c & 63)] = (uint16_t)(__float_as_uint((float)v) >> 16);
+  zb[(c / KBW) * np_ * KBW + i * KBW + (c % KBW)] = (uint16_t)(__float_as_uint((float)v) >> 16);
 }
 // Column gather + clip into a dense [n][r] matrix for the direct-difference
 // kernels: int32 hundredths (exact path) or fp64 values clip(q/100, +-zmax)
@@ -1409,18 +1409,14 @@ static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_
   (void)mode;
 #define G8_PICK(BLV, QLV) (fl == 1 ? k_gram8<0, BLV, 1, QLV> : k_gram8<0, BLV, 2, QLV>)
 #endif
-  // LDS image (timing A/B, results identical): 1 quad-row pieces (default), 2 half-split ring,
-  // 0 the earlier pair-row pieces (GRID_GRAM_QL)
+  // LDS image.  K-blocked panel ([kpad/KBW][np][KBW], KBW = 32): the half-split
+  // ring (LAY 3).  Row-major panel (timing A/B, results identical): 1 quad-row
+  // pieces (default), 2 half-split ring, 0 the earlier pair-row pieces (GRID_GRAM_QL)
   const char *qe = getenv("GRID_GRAM_QL");
   const int lay = qe ? atoi(qe) : 1;
-#ifdef GRID_PROBES
-  REQUIRE(lay >= 0 && lay <= 3 && (lay != 3 || blocked), "GRID_GRAM_QL must be 0, 1, 2 (or 3: K32 panel)");
-  auto kern = blocked ? (lay == 3 ? G8_PICK(true, 3) : lay == 2 ? G8_PICK(true, 2) : lay == 1 ? G8_PICK(true, 1)
-                                                                                     : G8_PICK(true, 0))
-#else
   REQUIRE(lay >= 0 && lay <= 2, "GRID_GRAM_QL must be 0, 1 or 2");
-  auto kern = blocked ? (lay == 2 ? G8_PICK(true, 2) : lay == 1 ? G8_PICK(true, 1) : G8_PICK(true, 0))
-#endif
+  static_assert(KBW == BK / 2, "k_gram8's K-blocked path reads 32-wide K-blocks");
+  auto kern = blocked ? G8_PICK(true, 3)
                       : (lay == 2 ? G8_PICK(false, 2) : lay == 1 ? G8_PICK(false, 1) : G8_PICK(false, 0));
 #undef G8_PICK
   hipLaunchKernelGGL(kern, dim3((unsigned)(8 * per)), dim3(512), 0, ctx->stream, d_zb, ld,

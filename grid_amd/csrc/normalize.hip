@@ -721,9 +721,9 @@ __device__ __forceinline__ void zquant_rows(const int32_t (&qv)[ZR][4], GETQ get
   const bool vec_zb = zb && w == 4 && cm[0] >= 0 && cm[1] == cm[0] + 1 && cm[2] == cm[0] + 2 &&
                       cm[3] == cm[0] + 3 && ((cm[0] & 3) == 0) && ((ld_zb & 3) == 0);
   // panel element (i, c): row-major i*ld_zb + c, or K-blocked (kbs > 0)
-  // (c >> 6)*kbs + i*64 + (c & 63) as k_gram8 reads it
+  // (c / KBW)*kbs + i*KBW + (c % KBW) as k_gram8 reads it
   auto zbi = [&](int64_t i, int64_t c) -> int64_t {
-    return kbs > 0 ? (c >> 6) * kbs + i * 64 + (c & 63) : i * ld_zb + c;
+    return kbs > 0 ? (c / KBW) * kbs + i * KBW + (c % KBW) : i * ld_zb + c;
   };
   const float qf = (float)qmax;
   float ac[4];
@@ -1075,7 +1075,7 @@ __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, 
   const int nS = Shi >= Slo ? Shi - Slo + 1 : 0, nC = Chi >= Clo ? Chi - Clo + 1 : 0;
   if (nS == 0) return;                      // no selected column in this wave (wave-uniform)
   auto zbi = [&](int64_t i, int64_t c) -> int64_t {
-    return kbs > 0 ? (c >> 6) * kbs + i * 64 + (c & 63) : i * ld_zb + c;
+    return kbs > 0 ? (c / KBW) * kbs + i * KBW + (c % KBW) : i * ld_zb + c;
   };
   // row-invariant panel offsets of this lane's used columns Clo + lane + 64 m
   int64_t zoff[4];
@@ -1147,7 +1147,7 @@ __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, 
         }
       }
       if (zb) {
-        uint16_t *brow = zb + (kbs > 0 ? i * 64 : i * ld_zb);
+        uint16_t *brow = zb + (kbs > 0 ? i * KBW : i * ld_zb);
 #pragma unroll
         for (int m = 0; m < 4; m++) {
           const uint16_t val = s_zb[wv][lane + 64 * m];
@@ -1344,9 +1344,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   const bool vec_zb = zb && w == 4 && cm[0] >= 0 && cm[1] == cm[0] + 1 && cm[2] == cm[0] + 2 && cm[3] == cm[0] + 3 &&
                       (cm[0] & 3) == 0 && ((kbs > 0 ? kbs : ld_zb) & 3) == 0;
   auto zbi = [&](int64_t i, int64_t c) -> int64_t {
-    return kbs > 0 ? (c >> 6) * kbs + i * 64 + (c & 63) : i * ld_zb + c;
+    return kbs > 0 ? (c / KBW) * kbs + i * KBW + (c % KBW) : i * ld_zb + c;
   };
-  const int64_t zb0 = zbi(0, cm[0] >= 0 ? cm[0] : 0), zbs = kbs > 0 ? 64 : ld_zb;   // panel row 0, row stride
+  const int64_t zb0 = zbi(0, cm[0] >= 0 ? cm[0] : 0), zbs = kbs > 0 ? KBW : ld_zb;   // panel row 0, row stride
   const float qf = (float)qmax;
   uint32_t slowm = 0;
   int of = 0;
@@ -1588,7 +1588,7 @@ __global__ __launch_bounds__(256) void k_zverify(const int32_t *__restrict__ q, 
       if (zb && c >= 0) {
         const int32_t w = o > qmax ? qmax : (o < -qmax ? -qmax : o);
         const uint16_t want = (uint16_t)(__float_as_uint((float)w) >> 16);
-        bad_b = zb[(int64_t)(c >> 6) * np_zb * 64 + i * 64 + (c & 63)] != want;
+        bad_b = zb[(int64_t)(c / KBW) * np_zb * KBW + i * KBW + (c % KBW)] != want;
       }
     }
   }
@@ -1961,8 +1961,8 @@ int grid_norm_zquant_kb(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t ld
                         int64_t ld_zq, const int32_t *d_colmap, int32_t qmax, uint16_t *d_zb,
                         int64_t np_zb, int32_t *h_overflow) {
   REQUIRE(np_zb >= n && np_zb % 64 == 0, "np_zb must be >= n and a multiple of 64");
-  return zquant_impl(ctx, d_q, kNoQ16, n, ld, d_sel, r, d_rm, d_mu, scale, d_zq, ld_zq, d_colmap, qmax, d_zb, 64,
-                     np_zb * 64, h_overflow);
+  return zquant_impl(ctx, d_q, kNoQ16, n, ld, d_sel, r, d_rm, d_mu, scale, d_zq, ld_zq, d_colmap, qmax, d_zb, KBW,
+                     np_zb * KBW, h_overflow);
 }
 
 int grid_norm_zquant_kb16(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t ld, const int32_t *d_sel,
@@ -1973,8 +1973,8 @@ int grid_norm_zquant_kb16(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t 
   REQUIRE(np_zb >= n && np_zb % 64 == 0, "np_zb must be >= n and a multiple of 64");
   REQUIRE(d_zq16 && h_overflow && h_nesc && esc_cap >= 0 && (esc_cap == 0 || (d_esc_idx && d_esc_val)),
           "grid_norm_zquant_kb16: bad escape list / outputs");
-  return zquant_impl(ctx, d_q, kNoQ16, n, ld, d_sel, r, d_rm, d_mu, scale, nullptr, ld_zq, d_colmap, qmax, d_zb, 64,
-                     np_zb * 64, h_overflow, d_zq16, d_esc_idx, d_esc_val, esc_cap, h_nesc);
+  return zquant_impl(ctx, d_q, kNoQ16, n, ld, d_sel, r, d_rm, d_mu, scale, nullptr, ld_zq, d_colmap, qmax, d_zb, KBW,
+                     np_zb * KBW, h_overflow, d_zq16, d_esc_idx, d_esc_val, esc_cap, h_nesc);
 }
 
 int grid_norm_zquant_kb16_q16(grid_ctx *ctx, const grid_depth16 *q, int64_t n, int64_t ld, const int32_t *d_sel,
@@ -1987,7 +1987,7 @@ int grid_norm_zquant_kb16_q16(grid_ctx *ctx, const grid_depth16 *q, int64_t n, i
   REQUIRE(d_zq16 && h_overflow && h_nesc && esc_cap >= 0 && (esc_cap == 0 || (d_esc_idx && d_esc_val)),
           "grid_norm_zquant_kb16_q16: bad escape list / outputs");
   return zquant_impl(ctx, nullptr, to_q16(q), n, ld, d_sel, r, d_rm, d_mu, scale, nullptr, ld_zq, d_colmap, qmax, d_zb,
-                     64, np_zb * 64, h_overflow, d_zq16, d_esc_idx, d_esc_val, esc_cap, h_nesc);
+                     KBW, np_zb * KBW, h_overflow, d_zq16, d_esc_idx, d_esc_val, esc_cap, h_nesc);
 }
 
 int grid_norm_zquant_kb_q16(grid_ctx *ctx, const grid_depth16 *q, int64_t n, int64_t ld, const int32_t *d_sel,
@@ -1997,7 +1997,7 @@ int grid_norm_zquant_kb_q16(grid_ctx *ctx, const grid_depth16 *q, int64_t n, int
   REQUIRE(q16_ok(q, ld), "compact matrix: 16-byte aligned q, ld %% 8 == 0 and escape offsets required");
   REQUIRE(np_zb >= n && np_zb % 64 == 0, "np_zb must be >= n and a multiple of 64");
   return zquant_impl(ctx, nullptr, to_q16(q), n, ld, d_sel, r, d_rm, d_mu, scale, d_zq, ld_zq, d_colmap, qmax, d_zb,
-                     64, np_zb * 64, h_overflow);
+                     KBW, np_zb * KBW, h_overflow);
 }
 
 }  // extern "C"

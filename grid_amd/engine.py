@@ -21,7 +21,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _abi
-from ._abi import BLOCK, Device, DevBuf, GridNativeError, call, ptr
+from ._abi import BLOCK, KBW, Device, DevBuf, GridNativeError, call, ptr
 
 F8, I4, I8, U2, U1 = np.float64, np.int32, np.int64, np.uint16, np.uint8
 
@@ -138,7 +138,7 @@ def sigma2_min(dev: Device, r3: DevBuf, r: int, frac_r: float):
 def knn(dev: Device, zb: DevBuf, n: int, np_: int, kpad: int, ld: int, qmax: int, k: int,
         r_use: int, kblocked: bool = False):
     """Exact k-NN on a bf16 hundredths panel (row-major [np][ld], or
-    K-blocked [kpad/64][np][64]): returns (idx, d2 hundredths^2, cnt) numpy."""
+    K-blocked [kpad/32][np][32]): returns (idx, d2 hundredths^2, cnt) numpy."""
     if 4 * qmax * qmax * max(r_use, 1) >= 2 ** 44:
         raise GridNativeError("R_use too large for the packed distance key")
     gram = dev.zeros((np_, np_), I8)
@@ -189,7 +189,7 @@ def _knn_zq(dev: Device, zq: np.ndarray, cols: np.ndarray, k: int, zmax: float, 
     np_ = pad_to(n, 256)
     if hundredths and q <= 256:
         kpad = pad_to(max(r, 1), 64)
-        zb = dev.alloc((kpad // 64, np_, 64), U2)
+        zb = dev.alloc((kpad // KBW, np_, KBW), U2)
         call("grid_knn_panel_i32", dev.ctx, dz.ptr, n, ld, dcols.ptr, r, q, zb.ptr, np_, kpad)
         del dz
         idx, d2, cnt = knn(dev, zb, n, np_, kpad, kpad, q, k, r, kblocked=True)

@@ -202,7 +202,7 @@ class HipOps:
         return c.value
 
     def zquant(self, q, n, ld, sel, r, rm, mu, scale, zq, ld_zq, colmap, qmax, zb, np_zb):
-        """z hundredths + the K-blocked bf16 panel [kpad/64][np_zb][64]."""
+        """z hundredths + the K-blocked bf16 panel [kpad/32][np_zb][32]."""
         of = C.c_int32()
         if isinstance(q, Depth16):
             call("grid_norm_zquant_kb_q16", self.ctx, C.byref(q.desc), n, q.ld, ptr(sel), r, ptr(rm), ptr(mu), scale,
@@ -373,9 +373,9 @@ class Steps47:
         self.np_ = pad_to(n1, 256)
         self.np_rs = pad_to(self.np_, self.world)         # Gram rows: equal blocks for the reduce-scatter
         self.kpad = pad_to(cw, 64)
-        # step-5 input panel (bf16), K-blocked [kpad/64][np][64]: one K-step of a
+        # step-5 input panel (bf16), K-blocked [kpad/32][np][32]: one K-step of a
         # row panel is contiguous for the Gram kernel's DMA
-        self.zb = a.empty((self.kpad // 64, self.np_, 64), U2)
+        self.zb = a.empty((self.kpad // _abi.KBW, self.np_, _abi.KBW), U2)
         self.zb.zero_()                                  # pad rows stay zero
         self.gram = a.empty((self.np_rs, self.np_), I8)   # row stride np; rows >= np stay zero
         self.norms = a.empty(self.np_, I8)
@@ -583,7 +583,11 @@ class Steps47:
             kpad_c = pad_to(used, 64)
             if kpad_c > used:
                 # columns colmap did not write this chunk (all in its last K-block)
-                self.zb[kpad_c // 64 - 1, :n, used % 64:].zero_()
+                b0 = used // _abi.KBW
+                if used % _abi.KBW:
+                    self.zb[b0, :n, used % _abi.KBW:].zero_()
+                    b0 += 1
+                self.zb[b0:kpad_c // _abi.KBW, :n].zero_()
             if self.gram_evs is not None:
                 import torch
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))

@@ -217,7 +217,7 @@ int grid_norm_zfull(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t m, int
  * d_gram: [np][np] int64, must be zeroed; only tiles (ti <= tj) are written. */
 int grid_knn_gram(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t kpad, int64_t ld,
                   int32_t qmax, int64_t *d_gram);
-/* The same on a K-blocked panel [kpad/64][np][64] (grid_norm_zquant_kb's
+/* The same on a K-blocked panel [kpad/32][np][32] (grid_norm_zquant_kb's
  * layout: one K-step of a row panel is contiguous); np % 256 == 0. */
 int grid_knn_gram_kb(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t kpad, int32_t qmax,
                      int64_t *d_gram);
@@ -257,7 +257,7 @@ int grid_knn_topk_d2(grid_ctx *ctx, const double *d_d2rows, int64_t ld, double k
 /* Step-5 inputs from the step-4 hundredths (find_neighbors.py:57-58,171):
  * columns d_cols[0..r) of d_zq [n][ld], clipped to +-qmax (+-zmax) with
  * GRID_MISSING -> 0, as the K-blocked bf16 panel of grid_knn_gram_kb
- * ([kpad/64][np][64], zero padded; qmax <= 256), as dense int32 [n][r], or
+ * ([kpad/32][np][32], zero padded; qmax <= 256), as dense int32 [n][r], or
  * as fp64 values clip(q/100, +-zmax) [n][r]. */
 int grid_knn_panel_i32(grid_ctx *ctx, const int32_t *d_zq, int64_t n, int64_t ld, const int32_t *d_cols,
                        int64_t r, int32_t qmax, uint16_t *d_zb, int64_t np_, int64_t kpad);

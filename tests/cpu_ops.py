@@ -10,6 +10,8 @@ import numpy as np
 from oracle import steps
 from oracle.npsum import col_sum, row_block_sums
 
+KBW = 32   # K-block width of the k-NN panel (grid_amd._abi.KBW; this module runs without the library)
+
 MISSING = -(2 ** 31)
 NEG0 = -(2 ** 31) + 1
 
@@ -119,16 +121,16 @@ class NumpyOps:
         cm = _np(colmap)[:r]
         clip = np.where((out == MISSING) | (out == NEG0), 0, np.clip(out, -qmax, qmax)).astype(np.float32)
         bits = (clip.view(np.uint32) >> 16).astype(np.uint16).view(np.int16)
-        zba = _np(zb)                      # K-blocked [kpad/64][np_zb][64]
+        zba = _np(zb)                      # K-blocked [kpad/32][np_zb][32]
         for s in range(r):
             if cm[s] >= 0:
-                zba[cm[s] // 64, :n, cm[s] % 64] = bits[:, s]
+                zba[cm[s] // KBW, :n, cm[s] % KBW] = bits[:, s]
         return 0
 
     def gram(self, zb, np_, kpad, qmax, gram):
         """Upper 128-tiles only, like the HIP kernels (the lower triangle is
         the mirror's job)."""
-        zr = _np(zb)[: kpad // 64, :np_].transpose(1, 0, 2).reshape(np_, kpad)
+        zr = _np(zb)[: kpad // KBW, :np_].transpose(1, 0, 2).reshape(np_, kpad)
         bits = zr.view(np.uint16).astype(np.uint32) << 16
         z = bits.view(np.float32).astype(np.float64)
         g = (z @ z.T).astype(np.int64)

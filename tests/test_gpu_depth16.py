@@ -8,6 +8,8 @@ import numpy as np
 import pytest
 import torch
 
+from grid_amd import _abi
+
 pytestmark = pytest.mark.gpu
 
 MISSING = -(2 ** 31)
@@ -130,7 +132,7 @@ def test_step4_kernels_q16_equal_int32(dev, knobs, pattern, monkeypatch):
         r = len(sel)
         zq = torch.zeros((n, r), dtype=torch.int32, device="cuda")
         kp = -(-r // 64) * 64
-        zb = torch.zeros((kp // 64, 512, 64), dtype=torch.int16, device="cuda")
+        zb = torch.zeros((kp // _abi.KBW, 512, _abi.KBW), dtype=torch.int16, device="cuda")
         ops.zquant(src, n, ld, sel, r, rm, mu, 1.7, zq, r, colmap, 200, zb, 512)
         zq16 = torch.zeros((n, r), dtype=torch.int16, device="cuda")
         zb16 = torch.zeros_like(zb)

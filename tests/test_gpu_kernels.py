@@ -10,6 +10,8 @@ import os
 import numpy as np
 import pytest
 
+from grid_amd import _abi
+
 from oracle import steps
 from oracle.npsum import nanmean_rows
 
@@ -159,7 +161,7 @@ def test_gram_kblocked_multi_slice(dev, qmax):
     q[:4] = np.where(rng.random((4, r)) < 0.5, -qmax, qmax)
     q[4] = qmax
     zf = (q.astype(np.float32).view(np.uint32) >> 16).astype(np.uint16)
-    zkb = np.ascontiguousarray(zf.reshape(np_, r // 64, 64).transpose(1, 0, 2))
+    zkb = np.ascontiguousarray(zf.reshape(np_, r // _abi.KBW, _abi.KBW).transpose(1, 0, 2))
     zb = dev.upload(zkb)
     g = dev.zeros((np_, np_), np.int64)
     call("grid_knn_gram_kb", dev.ctx, zb.ptr, np_, r, qmax, g.ptr)

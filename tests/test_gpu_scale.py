@@ -16,6 +16,8 @@ import math
 
 import numpy as np
 import pytest
+
+from grid_amd import _abi
 import torch
 
 pytestmark = pytest.mark.gpu
@@ -45,7 +47,7 @@ def test_gram_3202_multi_chunk(dev, kx, monkeypatch):
         zi[:, : 64 * 50] = qmax                     # worst-case magnitudes in the first chunk
         z[r0:r1] = zi.to(torch.bfloat16).view(torch.int16)
         del zi
-    zkb = z.view(np_, steps_, 64).permute(1, 0, 2).contiguous()
+    zkb = z.view(np_, steps_ * 64 // _abi.KBW, _abi.KBW).permute(1, 0, 2).contiguous()
     gram = torch.zeros((np_, np_), dtype=torch.int64, device="cuda")
     call("grid_knn_gram_kb", dev.ctx, zkb.data_ptr(), np_, kpad, qmax, gram.data_ptr())
     call("grid_knn_mirror", dev.ctx, gram.data_ptr(), np_)
@@ -167,7 +169,7 @@ def test_zquant_rounding_boundaries(dev):
         d = {k: dev.upload(v) for k, v in (("q", qq), ("rm", rr), ("mu", mu_arr), ("sel", sel))}
         np_zb = -(-nn // 64) * 64
         for mode in ("int32", "int16", "q16"):
-            zb = dev.zeros((1, np_zb, 64), np.uint16)
+            zb = dev.zeros((1, np_zb, _abi.KBW), np.uint16)
             if mode == "q16":              # compact source (k_zquant7): the same codes, 8-wide rows
                 import ctypes as C
                 q16 = dev.zeros((nn, 8), np.uint16)

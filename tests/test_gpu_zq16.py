@@ -64,7 +64,7 @@ def test_kb16_codes_equal_int32(dev, scale):
     kp = -(-r // 64) * 64
     out = {}
     for form in ("i32", "i16"):
-        zb = torch.zeros((kp // 64, 512, 64), dtype=torch.int16, device="cuda")
+        zb = torch.zeros((kp // _abi.KBW, 512, _abi.KBW), dtype=torch.int16, device="cuda")
         if form == "i32":
             zq = torch.zeros((n, r), dtype=torch.int32, device="cuda")
             of = ops.zquant(q, n, m, sel, r, rm, mu, scale, zq, r, colmap, 200, zb, 512)
@@ -93,7 +93,7 @@ def test_kb16_escape_overflow_flag(dev):
     ops, rm, mu = stats(dev, q, n, m)
     sel = torch.arange(m, dtype=torch.int32, device="cuda")
     zq = torch.zeros((n, m), dtype=torch.int16, device="cuda")
-    zb = torch.zeros((m // 64, 64, 64), dtype=torch.int16, device="cuda")
+    zb = torch.zeros((m // _abi.KBW, 64, _abi.KBW), dtype=torch.int16, device="cuda")
     ei = torch.zeros(8, dtype=torch.int64, device="cuda")
     ev = torch.zeros(8, dtype=torch.int32, device="cuda")
     of, ne = ops.zquant16(q, n, m, sel, m, rm, mu, 1.0, zq, m, None, 200, zb, 64, ei, ev)

@@ -38,12 +38,10 @@ for r0 in range(0, a.n, 256):
     zb[r0:r1, :kpad] = zi.to(torch.bfloat16).view(torch.int16)
     del zi
 gram = torch.zeros((np_, np_), dtype=torch.int64, device="cuda")
-# "kbNN": variant NN through grid_knn_gram_kb on the K-blocked panel [K-step][row][64]
-zbb = zbb32 = None
-if any(v.startswith("kb") for v in a.variants.split(",")):
-    zbb = zb[:, :kpad].reshape(np_, kpad // 64, 64).permute(1, 0, 2).contiguous()
-if any("QL=3" in v for v in a.variants.split(",")):   # tools build: K-blocked by 32 columns
-    zbb32 = zb[:, :kpad].reshape(np_, kpad // 32, 32).permute(1, 0, 2).contiguous()
+# "kbNN": variant NN through grid_knn_gram_kb on the K-blocked panel [kpad/KBW][row][KBW]
+zbb = None
+if any(v.startswith("kb") for v in a.variants.split(",")):   # K-blocked [kpad/KBW][np][KBW]
+    zbb = zb[:, :kpad].reshape(np_, kpad // _abi.KBW, _abi.KBW).permute(1, 0, 2).contiguous()
 res = {}
 flops = 2.0 * a.n * a.n * a.k
 for rep in range(a.reps):
@@ -60,8 +58,7 @@ for rep in range(a.reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         if v.startswith("kb"):
-            src = zbb32 if "QL=3" in vv else zbb
-            _abi.call("grid_knn_gram_kb", dev.ctx, src.data_ptr(), np_, kpad, a.qmax, gram.data_ptr())
+            _abi.call("grid_knn_gram_kb", dev.ctx, zbb.data_ptr(), np_, kpad, a.qmax, gram.data_ptr())
         else:
             _abi.call("grid_knn_gram", dev.ctx, zb.data_ptr(), np_, kpad, ld, a.qmax, gram.data_ptr())
         e1.record()
