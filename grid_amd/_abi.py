@@ -48,6 +48,8 @@ _SIGS = {
     "grid_norm_col_means": [_vp, _vp, _i64, _i64, _i64, _vp, _vp],
     "grid_norm_col_vars": [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
     "grid_sort_valid": [_vp, _vp, _i64, _vp, C.POINTER(_i64)],
+    "grid_count_valid": [_vp, _vp, _i64, C.POINTER(_i64)],
+    "grid_select_kth": [_vp, _vp, _i64, _vp, _i32, _vp],
     "grid_select_gt": [_vp, _vp, _i64, _f64, _vp, C.POINTER(_i64)],
     "grid_round_decimals": [_vp, _vp, _i64, C.c_int, _vp],
     "grid_gather_f64": [_vp, _vp, _vp, _i64, _vp],

@@ -223,6 +223,145 @@ int grid_sort_valid(grid_ctx *ctx, const double *d_v, int64_t n, double *d_sorte
   return GRID_OK;
 }
 
+// ---- order statistics of the non-NaN values without a sort ------------------
+// The k-th smallest (0-based) of the non-NaN doubles (key = bits with every
+// bit flipped for negatives and the sign bit flipped otherwise, so -0.0 ranks
+// before +0.0; the sort above keeps equal zeros in input order, as sorted()
+// does: a zero may differ in sign only, and every use compares values), by an MSB-first radix
+// SELECT: 8 passes of 8-bit digits, each a histogram of the values whose key
+// prefix matches, then one wave picking the digit that holds rank k.  Reads
+// the vector 8 times (8 x 24 MB at 3 M bins) instead of sorting it.
+struct KthState {
+  uint64_t prefix;
+  int64_t rank;
+};
+constexpr int KTH_MAX = 4;
+
+__device__ __forceinline__ uint64_t dkey(double d) {
+  const uint64_t u = (uint64_t)__double_as_longlong(d);
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+
+__global__ __launch_bounds__(256) void k_kth_hist(const double *__restrict__ v, int64_t n, int nk, int shift,
+                                                  const KthState *__restrict__ st, unsigned *__restrict__ ghist) {
+  __shared__ unsigned h[KTH_MAX][256];
+  for (int t = threadIdx.x; t < KTH_MAX * 256; t += 256) (&h[0][0])[t] = 0;
+  uint64_t pre[KTH_MAX];
+#pragma unroll
+  for (int j = 0; j < KTH_MAX; j++) pre[j] = j < nk ? st[j].prefix : 0;
+  __syncthreads();
+  const int hs = shift + 8;                      // bits above the current digit must match
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const double d = v[i];
+    if (d != d) continue;
+    const uint64_t k = dkey(d);
+    const unsigned dig = (unsigned)(k >> shift) & 255u;
+#pragma unroll
+    for (int j = 0; j < KTH_MAX; j++)
+      if (j < nk && (hs >= 64 || ((k ^ pre[j]) >> hs) == 0)) atomicAdd(&h[j][dig], 1u);
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < nk * 256; t += 256) {
+    const unsigned c = (&h[0][0])[t];
+    if (c) atomicAdd(ghist + t, c);
+  }
+}
+
+// one wave per k: the digit holding rank k, the rank within it; clears the histogram
+__global__ __launch_bounds__(64) void k_kth_pick(int shift, KthState *__restrict__ st, unsigned *__restrict__ ghist) {
+  const int j = blockIdx.x, lane = threadIdx.x;
+  unsigned *hj = ghist + j * 256;
+  unsigned c[4];
+  unsigned s = 0;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    c[q] = hj[lane * 4 + q];
+    s += c[q];
+  }
+  // inclusive prefix over lanes of the 4-bin sums
+  unsigned incl = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  const int64_t rank = st[j].rank;
+  const unsigned excl = incl - s;
+  const bool mine = (int64_t)excl <= rank && rank < (int64_t)incl;
+  if (mine) {
+    int64_t r = rank - excl;
+    int q = 0;
+    while (q < 3 && r >= (int64_t)c[q]) { r -= c[q]; q++; }
+    st[j].prefix |= (uint64_t)(lane * 4 + q) << shift;
+    st[j].rank = r;
+  }
+#pragma unroll
+  for (int q = 0; q < 4; q++) hj[lane * 4 + q] = 0;
+}
+
+__global__ __launch_bounds__(256) void k_count_valid(const double *__restrict__ v, int64_t n,
+                                                     unsigned long long *__restrict__ cnt) {
+  __shared__ unsigned bc;
+  if (threadIdx.x == 0) bc = 0;
+  __syncthreads();
+  unsigned c = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    c += v[i] == v[i];
+  if (c) atomicAdd(&bc, c);
+  __syncthreads();
+  if (threadIdx.x == 0 && bc) atomicAdd(cnt, (unsigned long long)bc);
+}
+
+int grid_count_valid(grid_ctx *ctx, const double *d_v, int64_t n, int64_t *h_nvalid) {
+  REQUIRE(ctx && h_nvalid && n >= 0 && (n == 0 || d_v), "bad args");
+  if (n == 0) { *h_nvalid = 0; return GRID_OK; }
+  void *s = nullptr;
+  int rc = grid_scratch(ctx, 256, &s);
+  if (rc) return rc;
+  unsigned long long *cnt = (unsigned long long *)s;
+  HIPCHK(hipMemsetAsync(cnt, 0, 8, ctx->stream));
+  const int blocks = (int)std::min<int64_t>(ceil_div(n, 256), 8 * ctx->ncu);
+  hipLaunchKernelGGL(k_count_valid, dim3(blocks), dim3(256), 0, ctx->stream, d_v, n, cnt);
+  LAUNCHCHK();
+  HIPCHK(hipMemcpyAsync(ctx->pinned, cnt, 8, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  *h_nvalid = (int64_t)*(unsigned long long *)ctx->pinned;
+  return GRID_OK;
+}
+
+int grid_select_kth(grid_ctx *ctx, const double *d_v, int64_t n, const int64_t *h_ks, int32_t nk, double *h_vals) {
+  REQUIRE(ctx && h_ks && h_vals && n > 0 && d_v && nk >= 1 && nk <= KTH_MAX, "bad args (1 <= nk <= %d)", KTH_MAX);
+  for (int j = 0; j < nk; j++) REQUIRE(h_ks[j] >= 0 && h_ks[j] < n, "k (%lld) out of range", (long long)h_ks[j]);
+  void *s = nullptr;
+  const size_t hbytes = (size_t)KTH_MAX * 256 * 4;
+  int rc = grid_scratch(ctx, 256 + hbytes, &s);
+  if (rc) return rc;
+  KthState *st = (KthState *)s;
+  unsigned *gh = (unsigned *)((char *)s + 256);
+  KthState hs[KTH_MAX];
+  for (int j = 0; j < nk; j++) hs[j] = KthState{0ull, h_ks[j]};
+  std::memcpy(ctx->pinned, hs, sizeof(KthState) * nk);
+  HIPCHK(hipMemcpyAsync(st, ctx->pinned, sizeof(KthState) * nk, hipMemcpyHostToDevice, ctx->stream));
+  HIPCHK(hipMemsetAsync(gh, 0, hbytes, ctx->stream));
+  const int blocks = (int)std::min<int64_t>(ceil_div(n, 256), 4 * ctx->ncu);
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    hipLaunchKernelGGL(k_kth_hist, dim3(blocks), dim3(256), 0, ctx->stream, d_v, n, nk, shift, st, gh);
+    hipLaunchKernelGGL(k_kth_pick, dim3(nk), dim3(64), 0, ctx->stream, shift, st, gh);
+  }
+  LAUNCHCHK();
+  HIPCHK(hipMemcpyAsync(ctx->pinned, st, sizeof(KthState) * nk, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  const KthState *out = (const KthState *)ctx->pinned;
+  for (int j = 0; j < nk; j++) {
+    const uint64_t k = out[j].prefix;
+    const uint64_t u = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k;
+    double d;
+    std::memcpy(&d, &u, 8);
+    h_vals[j] = d;
+  }
+  return GRID_OK;
+}
+
 int grid_select_gt(grid_ctx *ctx, const double *d_v, int64_t n, double thr, int32_t *d_idx,
                    int64_t *h_count) {
   REQUIRE(ctx && h_count && n >= 0, "bad args");

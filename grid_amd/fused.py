@@ -185,6 +185,18 @@ class HipOps:
         call("grid_sort_valid", self.ctx, ptr(v), n, ptr(out), C.byref(nv))
         return nv.value
 
+    def count_valid(self, v, n):
+        nv = C.c_int64()
+        call("grid_count_valid", self.ctx, ptr(v), n, C.byref(nv))
+        return nv.value
+
+    def select_kth(self, v, n, ks):
+        """The ks-th smallest non-NaN values of v[:n] (grid_sort_valid's order)."""
+        kk = (C.c_int64 * len(ks))(*ks)
+        out = (C.c_double * len(ks))()
+        call("grid_select_kth", self.ctx, ptr(v), n, kk, len(ks), out)
+        return list(out)
+
     def select_gt(self, v, n, thr, idx):
         c = C.c_int64()
         call("grid_select_gt", self.ctx, ptr(v), n, thr, ptr(idx), C.byref(c))
@@ -533,16 +545,17 @@ class Steps47:
         self._mark("col_stats")
         # ---- pass C: median -> scale; sorted(...)[int(top_frac*n)] -> selection ----
         rall, rlen = self._gather_padded(self.ratio, ml, self.mlmax, float("nan"))
-        nvalid = o.sort_valid(rall, rlen, self.sorted)
+        # order statistics of the valid ratios (radix select; no sort)
+        nvalid = o.count_valid(rall, rlen)
         scale, r_loc = 1.0, 0
         if nvalid:
-            if nvalid % 2:
-                med = self._read(self.sorted, nvalid // 2)
-            else:
-                med = (self._read(self.sorted, nvalid // 2 - 1) + self._read(self.sorted, nvalid // 2)) / 2.0
+            ks = [nvalid // 2] if nvalid % 2 else [nvalid // 2 - 1, nvalid // 2]
+            ks.append(py_index(nvalid, int(self.top_frac * nvalid)))
+            vals = o.select_kth(rall, rlen, ks)
+            med = vals[0] if nvalid % 2 else (vals[0] + vals[1]) / 2.0
             if med > 0:
                 scale = 1.0 / math.sqrt(med / 100.0)
-            thr = self._read(self.sorted, py_index(nvalid, int(self.top_frac * nvalid)))
+            thr = vals[-1]
             r_loc = o.select_gt(self.ratio, ml, thr, self.sel)
         self.scale, self.r_loc = scale, r_loc
         # ---- step 5 region filter on the "%.3f" ratios (find_neighbors.py:148-171) ----
@@ -551,9 +564,9 @@ class Steps47:
         r3all, r3len = self._gather_padded(self.r3, r_loc, self.mlmax, float("nan"))
         r_tot = r_loc if self.comm is None else self._sum_int(r_loc)
         self.r_tot = r_tot
-        nv = o.sort_valid(r3all, r3len, self.sorted)
+        nv = o.count_valid(r3all, r3len)
         if nv:
-            smin = self._read(self.sorted, min(int(r_tot * (1.0 - self.frac_r)), nv - 1))
+            smin = o.select_kth(r3all, r3len, [min(int(r_tot * (1.0 - self.frac_r)), nv - 1)])[0]
             smax = float(self.sigma2_max)
         else:
             smin, smax = -math.inf, math.inf

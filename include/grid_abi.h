@@ -125,6 +125,15 @@ int grid_norm_col_vars(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t m, 
  * d_sorted must hold n doubles.  (np.median :462 / sorted() :495) */
 int grid_sort_valid(grid_ctx *ctx, const double *d_v, int64_t n, double *d_sorted,
                     int64_t *h_nvalid);
+/* Count of the non-NaN values of d_v (the length grid_sort_valid would report). */
+int grid_count_valid(grid_ctx *ctx, const double *d_v, int64_t n, int64_t *h_nvalid);
+/* h_vals[j] = the h_ks[j]-th smallest (0-based) non-NaN value of d_v, for
+ * 1 <= nk <= 4 ranks 0 <= k < count: the sorted()[k] / np.median reads of
+ * :462 / :495 without sorting (radix select, 8 passes over d_v).  Ranks -0.0
+ * before +0.0 where grid_sort_valid (like sorted()) keeps equal zeros in input
+ * order, so a zero may differ in sign only; every use compares values. */
+int grid_select_kth(grid_ctx *ctx, const double *d_v, int64_t n, const int64_t *h_ks, int32_t nk,
+                    double *h_vals);
 /* Stable compaction of indices j with v[j] > thr (NaN never kept). (:499) */
 int grid_select_gt(grid_ctx *ctx, const double *d_v, int64_t n, double thr, int32_t *d_idx,
                    int64_t *h_count);

@@ -67,6 +67,23 @@ class NumpyOps:
             _np(var)[:m] = v
             _np(ratio)[:m] = np.where(mj > 0, (100.0 * v) / mj, np.nan)
 
+    def count_valid(self, v, n):
+        a = _np(v).reshape(-1)[:n]
+        return int((~np.isnan(a)).sum())
+
+    def select_kth(self, v, n, ks):
+        # grid_select_kth's order: keys with every bit flipped for negatives, the sign bit otherwise
+        a = _np(v).reshape(-1)[:n]
+        u = a[~np.isnan(a)].view(np.uint64)
+        neg = (u >> np.uint64(63)).astype(bool)
+        key = np.sort(np.where(neg, ~u, u | np.uint64(1 << 63)))
+        out = []
+        for k in ks:
+            kk = key[k]
+            uu = kk & np.uint64((1 << 63) - 1) if kk >> np.uint64(63) else ~kk
+            out.append(float(np.array([uu], dtype=np.uint64).view(np.float64)[0]))
+        return out
+
     def sort_valid(self, v, n, out):
         a = _np(v).reshape(-1)[:n]
         s = np.sort(a[~np.isnan(a)])

@@ -323,3 +323,43 @@ def test_phasing_batch_equals_per_locus_oracle(dev, big, weighted, min_nbr):
         assert mean == em
         ei = [steps.compute_imp(i, eh, hn, em) for i in range(len(irr))]
         assert np.array_equal(imp, np.array(ei).reshape(-1), equal_nan=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 7, 4096, 3_000_001])
+def test_select_kth_equals_sorted(dev, n):
+    """grid_select_kth / grid_count_valid (radix select) give grid_sort_valid's
+    values: NaNs skipped, duplicates, negatives.  The sort keeps -0.0 and +0.0
+    as equal keys in input order (as Python's sorted() does) while the select
+    ranks -0.0 first, so a zero may differ in sign only; every use of these
+    values (median > 0, ratio > thr, range tests) compares, so ranks are
+    checked by value with the sign of zero ignored, and exactly otherwise."""
+    import ctypes as C
+    from grid_amd._abi import call
+    rng = np.random.default_rng(n)
+    v = rng.standard_normal(n) * 10.0 ** rng.integers(-3, 4, n)
+    v[rng.random(n) < 0.1] = np.nan
+    v[rng.random(n) < 0.05] = 0.0
+    v[rng.random(n) < 0.05] = -0.0
+    v[rng.random(n) < 0.05] = 3.25                  # duplicates
+    d = dev.upload(v)
+    out = dev.zeros(n, np.float64)
+    nv = C.c_int64()
+    call("grid_sort_valid", dev.ctx, d.ptr, n, out.ptr, C.byref(nv))
+    nc = C.c_int64()
+    call("grid_count_valid", dev.ctx, d.ptr, n, C.byref(nc))
+    assert nc.value == nv.value == int((~np.isnan(v)).sum())
+    if nv.value == 0:
+        return
+    srt = out.numpy()[: nv.value]
+    ks = sorted({0, nv.value - 1, nv.value // 2, max(nv.value // 2 - 1, 0), int(0.9 * nv.value) % nv.value})
+    for i in range(0, len(ks), 4):
+        kk = ks[i:i + 4]
+        karr = (C.c_int64 * len(kk))(*kk)
+        vals = (C.c_double * len(kk))()
+        call("grid_select_kth", dev.ctx, d.ptr, n, karr, len(kk), vals)
+        for k, got in zip(kk, vals):
+            if srt[k] == 0.0:
+                assert got == 0.0, (k, got, srt[k])
+            else:
+                assert np.float64(got).view(np.uint64) == srt[k].view(np.uint64), (k, got, srt[k])
