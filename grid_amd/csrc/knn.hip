@@ -934,8 +934,9 @@ __global__ __launch_bounds__(512, 1) void k_gram8(const uint16_t *__restrict__ z
                                                   const int32_t *__restrict__ tiles, int ntiles, int kc, int kx,
                                                   int64_t nsteps, int lag, int spin_ticks,
                                                   int64_t np_, unsigned long long *__restrict__ gram,
-                                                  unsigned *__restrict__ rounds) {
+                                                  unsigned *__restrict__ rounds, int dyn) {
   __shared__ __attribute__((aligned(1024))) char smem[3 * SLOT3];
+  __shared__ int64_t s_unit;
   const int nwg = gridDim.x;
   const int bid = blockIdx.x;
   const int xcd = bid & 7, l = bid >> 3;
@@ -950,9 +951,21 @@ __global__ __launch_bounds__(512, 1) void k_gram8(const uint16_t *__restrict__ z
   const int64_t glast = xg + (ngx - 1) * gx;
   const int64_t lastsz = ngx > 0 ? min((int64_t)per, (int64_t)ntiles - glast * per) : 0;
   const int64_t units = ngx > 0 ? ((ngx - 1) * per + lastsz) * kc : 0;
+  // dyn: the XCD's workgroups take units in order from a counter instead of
+  // unit r * per + l in round r, so a workgroup that starts late (its CU still
+  // running the phasing lane's kernel) takes fewer units instead of holding
+  // the launch open for its fixed share
   for (int64_t r = 0;; r++) {
-    const int64_t u = r * per + l;
+    int64_t u = r * per + l;
+    if (dyn) {
+      if (threadIdx.x == 0)
+        s_unit = (int64_t)__hip_atomic_fetch_add(rounds + 128 + xcd * 16, 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      u = s_unit;
+    }
     if (u >= units) break;
+    const int64_t ru = u / per;                     // the unit's round (pacing)
     // unit -> (group, chunk, tile)
     const int64_t gl = u / ((int64_t)per * kc);
     const int64_t gbase = (xg + gl * gx) * per;
@@ -963,9 +976,9 @@ __global__ __launch_bounds__(512, 1) void k_gram8(const uint16_t *__restrict__ z
     const int32_t tv = tiles[t];
     const int I = MODE == 1 ? 0 : tv >> 16, tj = MODE == 1 ? 0 : tv & 0xFFFF;
     const int64_t s0 = xs0 + xlen * c / kc, s1 = xs0 + xlen * (c + 1) / kc;
-    // pace: wait (bounded) until the XCD's round r - lag is complete
-    if (r >= lag && threadIdx.x == 0) {
-      const unsigned need = (unsigned)((r - lag + 1) * per);
+    // pace: wait (bounded) until the XCD's round ru - lag is complete
+    if (ru >= lag && threadIdx.x == 0) {
+      const unsigned need = (unsigned)((ru - lag + 1) * per);
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       while (__hip_atomic_load(rounds + xcd * 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
         __builtin_amdgcn_s_sleep(2);
@@ -1350,7 +1363,7 @@ static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_
     ctx->aux_tiles_n = nt6;
   }
   unsigned *rounds = (unsigned *)((char *)ctx->aux + GRID_AUX_BYTES / 2);
-  HIPCHK(hipMemsetAsync(rounds, 0, 8 * 16 * 4, ctx->stream));
+  HIPCHK(hipMemsetAsync(rounds, 0, (128 + 8 * 16) * 4, ctx->stream));   // round and unit counters
   const int per = ctx->ncu >= 8 ? ctx->ncu / 8 : 1;
   const int64_t ngroups = ceil_div(nt6, per);
   // (kx, kc): cost = the longest XCD's sequential work per workgroup in
@@ -1390,6 +1403,8 @@ static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_
   const char *le = getenv("GRID_GRAM_LAG"), *se = getenv("GRID_GRAM_SPIN"), *ke = getenv("GRID_GRAM_KC");
   const char *xe = getenv("GRID_GRAM_KX");
   const int lag = le ? atoi(le) : 1, spin = se ? atoi(se) : 20000;
+  const char *dye = getenv("GRID_GRAM_DYN");      // units from a per-XCD counter (1) or fixed per workgroup (0)
+  const int dyn = dye ? atoi(dye) != 0 : 1;
   if (xe && (atoi(xe) == 1 || atoi(xe) == 2 || atoi(xe) == 4 || atoi(xe) == 8)) {
     bkx = atoi(xe);
     bkc = ceil_div(ceil_div(nsteps, bkx), sps_max);
@@ -1421,7 +1436,7 @@ static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_
 #undef G8_PICK
   hipLaunchKernelGGL(kern, dim3((unsigned)(8 * per)), dim3(512), 0, ctx->stream, d_zb, ld,
                      (const int32_t *)ctx->aux, nt6, (int)bkc, (int)bkx, nsteps, lag, spin, np_,
-                     (unsigned long long *)d_gram, rounds);
+                     (unsigned long long *)d_gram, rounds, dyn);
   LAUNCHCHK();
   return GRID_OK;
 }
