@@ -1211,8 +1211,8 @@ __global__ __launch_bounds__(256) void k_zquant6(const int32_t *__restrict__ q, 
 // 16-code window at sel[s0] & ~7 as two 16-B loads per row instead of three
 // 8-B loads): the texture data path, not HBM, bounds this kernel (PMC: TD busy
 // 99 %, TA 82 %), and it costs per wave-instruction, not per byte.
-template <int NT, int PROBE = 0, bool W16 = false, bool PAIR = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_zquant7(Q16 s16, int64_t n, int64_t ld, const int32_t *__restrict__ sel,
+template <int NT, int PROBE, bool W16, bool PAIR>
+__device__ __forceinline__ void z7_body(Q16 s16, int64_t n, int64_t ld, const int32_t *__restrict__ sel,
                                                  int64_t r, const double *__restrict__ rm,
                                                  const double *__restrict__ rinv, const double *__restrict__ mus,
                                                  const double *__restrict__ sq, const double *__restrict__ rsq,
@@ -1547,6 +1547,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     }
   }
   if (of) atomicOr(overflow, of);
+}
+
+// k_zquant7 at 4 waves per SIMD (<= 128 VGPRs); the paired-store variant
+// also at 3 (its 130 VGPRs spill 9 at 4).
+template <int NT, int PROBE = 0, bool W16 = false, bool PAIR = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_zquant7(Q16 s16, int64_t n, int64_t ld, const int32_t *__restrict__ sel,
+                                                 int64_t r, const double *__restrict__ rm,
+                                                 const double *__restrict__ rinv, const double *__restrict__ mus,
+                                                 const double *__restrict__ sq, const double *__restrict__ rsq,
+                                                 const float2 *__restrict__ mc32, double scale,
+                                                 int16_t *__restrict__ zq, int64_t ld_zq,
+                                                 const int32_t *__restrict__ colmap, int32_t qmax,
+                                                 uint16_t *__restrict__ zb, int64_t ld_zb, int64_t kbs,
+                                                 int32_t *__restrict__ overflow, int rpw, ZEsc esc,
+                                                 int rgs, int cbw, int zblk) {
+  z7_body<NT, PROBE, W16, PAIR>(s16, n, ld, sel, r, rm, rinv, mus, sq, rsq, mc32, scale, zq, ld_zq, colmap, qmax, zb, ld_zb, kbs, overflow, rpw, esc, rgs, cbw, zblk);
+}
+template <int NT, int PROBE = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_zquant7p3(Q16 s16, int64_t n, int64_t ld, const int32_t *__restrict__ sel,
+                                                 int64_t r, const double *__restrict__ rm,
+                                                 const double *__restrict__ rinv, const double *__restrict__ mus,
+                                                 const double *__restrict__ sq, const double *__restrict__ rsq,
+                                                 const float2 *__restrict__ mc32, double scale,
+                                                 int16_t *__restrict__ zq, int64_t ld_zq,
+                                                 const int32_t *__restrict__ colmap, int32_t qmax,
+                                                 uint16_t *__restrict__ zb, int64_t ld_zb, int64_t kbs,
+                                                 int32_t *__restrict__ overflow, int rpw, ZEsc esc,
+                                                 int rgs, int cbw, int zblk) {
+  z7_body<NT, PROBE, true, true>(s16, n, ld, sel, r, rm, rinv, mus, sq, rsq, mc32, scale, zq, ld_zq, colmap, qmax, zb, ld_zb, kbs, overflow, rpw, esc, rgs, cbw, zblk);
 }
 
 // Independent check of the step-4 output and the step-5 panel (tests): every
@@ -1886,7 +1915,8 @@ static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, int64_
                        ((uintptr_t)mc32 % 16) == 0;
       // paired 16-B stores (GRID_Z7_PAIR, timing A/B; results identical; with the 16-B loads)
       const char *pre = getenv("GRID_Z7_PAIR");
-      const bool pr7 = (pre ? atoi(pre) != 0 : Z7PAIR) && w16;
+      const int pr7v = pre ? atoi(pre) : (Z7PAIR ? 1 : 0);   // 2: the pair variant at 3 waves/SIMD
+      const bool pr7 = pr7v != 0 && w16;
       REQUIRE(ceil_div(ceil_div(r, 4), 256) <= 65535, "r too large for one launch");
       // super-tiles of rgs row groups x cbw column blocks (GRID_Z7_RGS / GRID_Z7_CBW; RGS=0: the 2-D grid,
       // row groups fastest)
@@ -1906,12 +1936,14 @@ static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, int64_
 #ifdef GRID_PROBES
       const char *pe = getenv("GRID_Z7_PROBE");
       const int pr = pe ? atoi(pe) : 0;
-#define Z7P(P) (w16 ? (pr7 ? k_zquant7<0, P, true, true> : k_zquant7<0, P, true>) : k_zquant7<0, P>)
+#define Z7P(P) (w16 ? (pr7 ? (pr7v == 2 ? k_zquant7p3<0, P> : k_zquant7<0, P, true, true>) : k_zquant7<0, P, true>) \
+                     : k_zquant7<0, P>)
       auto k7 = pr == 1 ? Z7P(1) : pr == 2 ? Z7P(2) : pr == 3 ? Z7P(3) : pr == 4 ? Z7P(4) : pr == 7 ? Z7P(7) : Z7P(0);
 #undef Z7P
       if (nt7) k7 = w16 ? k_zquant7<1, 0, true> : k_zquant7<1>;
 #else
-      auto k7 = w16 ? (pr7 ? k_zquant7<0, 0, true, true> : nt7 ? k_zquant7<1, 0, true> : k_zquant7<0, 0, true>)
+      auto k7 = w16 ? (pr7 ? (pr7v == 2 ? k_zquant7p3<0, 0> : k_zquant7<0, 0, true, true>)
+                           : nt7 ? k_zquant7<1, 0, true> : k_zquant7<0, 0, true>)
                     : (nt7 ? k_zquant7<1> : k_zquant7<0>);
 #endif
       hipLaunchKernelGGL(k7, g7, dim3(256), 0, ctx->stream, s16, n, ld, d_sel, r, d_rm,

@@ -2,7 +2,7 @@
 # k_zquant7 paired 16-B stores (GRID_Z7_PAIR): timing A/B, then zquant / chain GPU parity tests under PAIR=1.
 set -e
 O=gpurun_out/pair; mkdir -p $O
-timeout -k 10 300 python -u tools/bench_zquant.py --q16 --reps 3 --env "GRID_Z7_PAIR=0;GRID_Z7_PAIR=1;GRID_Z7_PAIR=1,GRID_Z7_PROBE=1;GRID_Z7_PAIR=1,GRID_Z7_PROBE=2" > $O/zq.log 2>&1
+timeout -k 10 300 python -u tools/bench_zquant.py --q16 --reps 3 --env "GRID_Z7_PAIR=0;GRID_Z7_PAIR=1;GRID_Z7_PAIR=2;GRID_Z7_PAIR=0,GRID_Z7_PROBE=3;GRID_Z7_PAIR=1,GRID_Z7_PROBE=3" > $O/zq.log 2>&1
 cat $O/zq.log
 GRID_Z7_PAIR=1 timeout -k 10 400 python -u -m pytest tests/test_gpu_depth16.py tests/test_gpu_zq16.py tests/test_gpu_scale.py tests/test_gpu_streamed.py -m gpu -x -v --timeout 200 --timeout-method thread > $O/pytest.log 2>&1
 echo "pytest PAIR=1: $(tail -1 $O/pytest.log)"
