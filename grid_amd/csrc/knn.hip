@@ -15,6 +15,8 @@
 // G is contiguous for the row top-k and the multi-GPU reduce-scatter.
 // d2(i,j) = G_ii + G_jj - 2 G_ij is then exact, and neighbours are ordered by
 // (d2, j).  That equals sklearn's order wherever exact distances differ.
+#include <vector>
+
 #include "common.hpp"
 
 #include <algorithm>
@@ -440,6 +442,61 @@ __device__ __forceinline__ void g6_atomics(int32_t (&iacc)[MB][2][16], int I, in
         if (v != 0) atomicAdd(gram + (int64_t)row * np_ + col, (unsigned long long)(long long)v);
         iacc[a][b][r] = 0;
       }
+}
+
+// Plain-store flush (k_gram8 partial mode): the unit's int32 tile, row-major
+// [256][128] in its own scratch slot (one 128-B row segment per half-wave
+// store), summed per tile by k_gram_part_reduce after the launch.  A
+// workgroup's 128 KiB of plain stores drain in a few us where its 256 KiB of
+// int64 atomics took tens (atomics run at ~1.3 TB/s chip-wide).
+template <int MB>
+__device__ __forceinline__ void g8_store_part(int32_t (&iacc)[MB][2][16], int32_t *__restrict__ slot) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+#pragma unroll
+  for (int a = 0; a < MB; a++)
+#pragma unroll
+    for (int b = 0; b < 2; b++)
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int row = wr * (32 * MB) + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int col = wc * 64 + b * 32 + (lane & 31);
+        slot[row * BN3 + col] = iacc[a][b][r];
+        iacc[a][b][r] = 0;
+      }
+}
+
+// Slot offsets of the XCDs' unit ranges (partial mode), passed by value.
+struct GramXoff {
+  int64_t x[8];
+};
+
+// gram tile t += the sum (int64, exact in any order) of its units' slots; the
+// units of tile t follow k_gram8's unit -> (group, chunk, tile) map: group
+// g = t / per is run by the XCDs x = (g % gx) * kx + kr (kr < kx), unit
+// u = (g / gx) * per * kc + c * gsz + t % per for chunk c (empty K ranges
+// hold no slot).  One thread per tile element.
+__global__ __launch_bounds__(256) void k_gram_part_reduce(const int32_t *__restrict__ part, GramXoff xo, int per,
+                                                          int kc, int kx, int64_t nsteps, int ntiles,
+                                                          const int32_t *__restrict__ tiles, int64_t np_,
+                                                          int64_t *__restrict__ gram) {
+  const int e = blockIdx.x * 256 + threadIdx.x;            // element of the 256 x 128 tile
+  const int t = blockIdx.y;
+  const int gx = 8 / kx, g = t / per, tl = t % per;
+  const int gsz = min(per, ntiles - g * per);
+  int64_t sum = 0;
+  for (int kr = 0; kr < kx; kr++) {
+    const int x = (g % gx) * kx + kr;
+    const int64_t xs0 = nsteps * kr / kx, xlen = nsteps * (kr + 1) / kx - xs0;
+    for (int c = 0; c < kc; c++) {
+      if (xlen * c / kc == xlen * (c + 1) / kc) continue;
+      const int64_t u = (int64_t)(g / gx) * per * kc + (int64_t)c * gsz + tl;
+      sum += part[(xo.x[x] + u) * (BM3 * BN3) + e];
+    }
+  }
+  const int32_t tv = tiles[t];
+  const int64_t row = (int64_t)(tv >> 16) * BM3 + e / BN3, col = (int64_t)(tv & 0xFFFF) * BN3 + e % BN3;
+  gram[row * np_ + col] += sum;
 }
 
 template <int MB>
@@ -934,7 +991,8 @@ __global__ __launch_bounds__(512, 1) void k_gram8(const uint16_t *__restrict__ z
                                                   const int32_t *__restrict__ tiles, int ntiles, int kc, int kx,
                                                   int64_t nsteps, int lag, int spin_ticks,
                                                   int64_t np_, unsigned long long *__restrict__ gram,
-                                                  unsigned *__restrict__ rounds, int dyn) {
+                                                  unsigned *__restrict__ rounds, int dyn,
+                                                  int32_t *__restrict__ part, GramXoff xoff) {
   __shared__ __attribute__((aligned(1024))) char smem[3 * SLOT3];
   __shared__ int64_t s_unit;
   const int nwg = gridDim.x;
@@ -993,7 +1051,8 @@ __global__ __launch_bounds__(512, 1) void k_gram8(const uint16_t *__restrict__ z
       if constexpr (LAY == 2) g8h_run<MODE, BL, FL>(z, ld, I, tj, s0, s1, smem, acc, iacc);
       else if constexpr (LAY == 3) g8h_run<MODE, BL, FL, BL>(z, ld, I, tj, s0, s1, smem, acc, iacc);
       else g8_run<MODE, BL, FL, LAY == 1>(z, ld, I, tj, s0, s1, smem, acc, iacc);
-      g6_atomics<2>(iacc, I, tj, np_, gram);
+      if (part) g8_store_part<2>(iacc, part + (xoff.x[xcd] + u) * (int64_t)(BM3 * BN3));
+      else g6_atomics<2>(iacc, I, tj, np_, gram);
     }
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_fetch_add(rounds + xcd * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1434,10 +1493,41 @@ static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_
   auto kern = blocked ? G8_PICK(true, 3)
                       : (lay == 2 ? G8_PICK(false, 2) : lay == 1 ? G8_PICK(false, 1) : G8_PICK(false, 0));
 #undef G8_PICK
+  // partial mode (GRID_GRAM_PART_MB > 0: while the slots fit that many MiB; off by default): plain
+  // int32 stores of each unit's tile into its own slot, one reduction launch
+  // after the Gram, in place of the int64 atomics (the atomics were not what bounds the Gram)
+  const char *pme = getenv("GRID_GRAM_PART_MB");
+  const int64_t part_cap = (int64_t)(pme ? atof(pme) : 0.0) << 20;   // measured slower: 29.3 vs 28.3 ms at config 2
+  int32_t *d_part = nullptr;
+  GramXoff xoff{};
+  {
+    const int gx = 8 / (int)bkx;
+    int64_t tot = 0;
+    for (int x = 0; x < 8; x++) {
+      const int xg = x / (int)bkx;
+      const int64_t ngx = ngroups > xg ? (ngroups - xg + gx - 1) / gx : 0;
+      const int64_t glast = xg + (ngx - 1) * gx;
+      const int64_t lastsz = ngx > 0 ? std::min((int64_t)per, (int64_t)nt6 - glast * per) : 0;
+      xoff.x[x] = tot;
+      tot += ngx > 0 ? ((ngx - 1) * per + lastsz) * bkc : 0;
+    }
+    if (mode == 0 && part_cap > 0 && tot * (int64_t)(BM3 * BN3 * 4) <= part_cap) {
+      void *sp = nullptr;
+      int rc = grid_scratch(ctx, (size_t)tot * BM3 * BN3 * 4, &sp);
+      if (rc) return rc;
+      d_part = (int32_t *)sp;
+    }
+  }
   hipLaunchKernelGGL(kern, dim3((unsigned)(8 * per)), dim3(512), 0, ctx->stream, d_zb, ld,
                      (const int32_t *)ctx->aux, nt6, (int)bkc, (int)bkx, nsteps, lag, spin, np_,
-                     (unsigned long long *)d_gram, rounds, dyn);
+                     (unsigned long long *)d_gram, rounds, dyn, d_part, xoff);
   LAUNCHCHK();
+  if (d_part) {
+    hipLaunchKernelGGL(k_gram_part_reduce, dim3((unsigned)(BM3 * BN3 / 256), (unsigned)nt6), dim3(256), 0,
+                       ctx->stream, d_part, xoff, per, (int)bkc, (int)bkx, nsteps, nt6, (const int32_t *)ctx->aux,
+                       np_, d_gram);
+    LAUNCHCHK();
+  }
   return GRID_OK;
 }
 
