@@ -49,6 +49,9 @@ _SIGS = {
     "grid_norm_col_vars": [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
     "grid_sort_valid": [_vp, _vp, _i64, _vp, C.POINTER(_i64)],
     "grid_count_valid": [_vp, _vp, _i64, C.POINTER(_i64)],
+    "grid_norm_row_blocks_f64": [_vp, _vp, _i64, _i64, _i64, _vp, _vp],
+    "grid_norm_col_stats_f64": [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp],
+    "grid_norm_zquant_f64": [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _f64, _vp, _i64, C.POINTER(_i32)],
     "grid_select_kth": [_vp, _vp, _i64, _vp, _i32, _vp],
     "grid_select_gt": [_vp, _vp, _i64, _f64, _vp, C.POINTER(_i64)],
     "grid_round_decimals": [_vp, _vp, _i64, C.c_int, _vp],

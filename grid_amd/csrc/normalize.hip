@@ -184,9 +184,9 @@ __global__ __launch_bounds__(256) void k_row_blocks16(Q16 s16, int64_t ld, int64
 
 // ---- generic pairwise_sum (numpy) for a partial block, one thread ----
 // G: element accessor, get(k) -> int32 hundredths of element k.
-template <class G>
-__device__ double pairwise_leaf(const G &get, int lo, int n) {
-  auto a = [&](int i) { return qval(get(lo + i)); };
+template <class V>
+__device__ double pairwise_leaf_v(const V &val, int lo, int n) {
+  auto a = [&](int i) { return val(lo + i); };
   if (n < 8) {
     double res = 0.0;
     for (int i = 0; i < n; i++) res = res + a(i);
@@ -205,6 +205,10 @@ __device__ double pairwise_leaf(const G &get, int lo, int n) {
   double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
   for (; i < n; i++) res = res + a(i);
   return res;
+}
+template <class G>
+__device__ double pairwise_leaf(const G &get, int lo, int n) {
+  return pairwise_leaf_v([&](int k) { return qval(get(k)); }, lo, n);
 }
 
 // numpy's recursion over [0, n) with the leaves supplied by leaf(lo, len) in
@@ -1754,6 +1758,109 @@ int grid_norm_row_means(grid_ctx *ctx, const double *d_bsum, const int32_t *d_bc
 }
 
 // Scratch layout: [256 B flags][rinv: n doubles][bad: n + 64 bytes if wanted][extra] -> *rest
+// ---- fp64 depths: the drop-in step's route for depth text that is not exact
+// hundredths (the reference reads any decimal with float(); mosdepth itself
+// prints %.2f).  x = the parsed doubles, NaN = missing.  Same operation
+// orders as the integer kernels (NumPy pairwise row sums, sequential column
+// sums, the exact %.2f quantisation), none of their fast paths: a fallback.
+__device__ __forceinline__ bool yval_f64(double x, double rm, double ri, double &y) {
+  if (!(x == x) || rm == 0.0 || !(rm == rm)) return false;
+  y = div_exact(x, rm, ri);
+  return true;
+}
+
+// one wave per (row, 8192-block), the partial tail's scheme (pairwise_tree
+// leaves summed in parallel, combined in the recursion's order) for every block
+__global__ __launch_bounds__(64) void k_row_blocks_f64(const double *__restrict__ x, int64_t ld, int64_t m,
+                                                        int64_t nblk, double *__restrict__ bsum,
+                                                        int32_t *__restrict__ bcnt) {
+  __shared__ int s_lo[128], s_len[128];
+  __shared__ double s_val[128];
+  __shared__ int s_nl;
+  const int64_t row = blockIdx.y, b = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int len = (int)min((int64_t)BLK, m - b * BLK);
+  const double *p = x + row * ld + b * BLK;
+  auto val = [&](int k) { const double v = p[k]; return v == v ? v : 0.0; };
+  if (lane == 0) {
+    int nl = 0;
+    pairwise_tree(len, [&](int lo, int nn) { s_lo[nl] = lo; s_len[nl] = nn; nl++; return 0.0; });
+    s_nl = nl;
+  }
+  int c = 0;
+  for (int i = lane; i < len; i += 64) c += p[i] == p[i];
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
+  __syncthreads();
+  for (int l = lane; l < s_nl; l += 64) s_val[l] = pairwise_leaf_v(val, s_lo[l], s_len[l]);
+  __syncthreads();
+  if (lane == 0) {
+    int k = 0;
+    bsum[row * nblk + b] = pairwise_tree(len, [&](int, int) { return s_val[k++]; });
+    bcnt[row * nblk + b] = c;
+  }
+}
+
+// one thread per column, sequential over rows (NumPy's axis-0 order), as
+// k_col_means / k_col_vars' masked paths
+__global__ __launch_bounds__(256) void k_col_stats_f64(const double *__restrict__ x, int64_t n, int64_t m, int64_t ld,
+                                                       const double *__restrict__ rm, const double *__restrict__ rinv,
+                                                       int vars, double *__restrict__ mu, double *__restrict__ var,
+                                                       double *__restrict__ ratio) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  if (!vars) {
+    double acc = 0.0;
+    int64_t cnt = 0;
+    for (int64_t i = 0; i < n; i++) {
+      double y;
+      if (yval_f64(x[i * ld + j], rm[i], rinv[i], y)) { acc = acc + y; cnt++; }
+    }
+    mu[j] = acc / (double)cnt;                      // 0/0 -> NaN (numpy)
+    return;
+  }
+  const double mj = mu[j];
+  double acc = 0.0;
+  for (int64_t i = 0; i < n; i++) {
+    double y;
+    if (yval_f64(x[i * ld + j], rm[i], rinv[i], y)) {
+      const double d = y - mj, dd = d * d;
+      if (dd == dd) acc = acc + dd;                  // nansum: NaN (mu NaN) -> 0
+    }
+  }
+  const double vv = acc / (double)(n - 1);
+  var[j] = vv;
+  ratio[j] = (mj > 0.0) ? (100.0 * vv) / mj : __builtin_nan("");
+}
+
+// z hundredths of the selected columns, the exact fp64 chain per cell
+// (zquant's deferred path): GRID_ZQ_NAN for missing cells, GRID_ZQ_NEG0 for "-0.00"
+__global__ __launch_bounds__(256) void k_zquant_f64(const double *__restrict__ x, int64_t n, int64_t ld,
+                                                    const int32_t *__restrict__ sel, int64_t r,
+                                                    const double *__restrict__ rm, const double *__restrict__ rinv,
+                                                    const double *__restrict__ mus, const double *__restrict__ sq,
+                                                    const double *__restrict__ rsq, double scale,
+                                                    int32_t *__restrict__ zq, int64_t ld_zq,
+                                                    int32_t *__restrict__ overflow) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = blockIdx.y;
+  if (s >= r) return;
+  double y;
+  int32_t o = GRID_ZQ_NAN;
+  if (yval_f64(x[i * ld + sel[s]], rm[i], rinv[i], y)) {
+    const double z = div_exact(y - mus[s], sq[s], rsq[s]) * scale;
+    if (z == z) {
+      double kd = round_dec_k(z, 100.0);
+      if (fabs(kd) >= 2147483000.0) {
+        atomicOr(overflow, 1);
+        kd = 0.0;
+      }
+      o = (int32_t)kd;
+      if (o == 0 && signbit(z)) o = GRID_ZQ_NEG0;
+    }
+  }
+  zq[i * ld_zq + s] = o;
+}
+
 static int recip_rows(grid_ctx *ctx, const double *d_rm, int64_t n, size_t extra, double **rinv, char **rest,
                       uint8_t **bad = nullptr) {
   void *s = nullptr;
@@ -2030,6 +2137,62 @@ int grid_norm_zquant_kb_q16(grid_ctx *ctx, const grid_depth16 *q, int64_t n, int
   REQUIRE(np_zb >= n && np_zb % 64 == 0, "np_zb must be >= n and a multiple of 64");
   return zquant_impl(ctx, nullptr, to_q16(q), n, ld, d_sel, r, d_rm, d_mu, scale, d_zq, ld_zq, d_colmap, qmax, d_zb,
                      KBW, np_zb * KBW, h_overflow);
+}
+
+int grid_norm_row_blocks_f64(grid_ctx *ctx, const double *d_x, int64_t n, int64_t m, int64_t ld, double *d_bsum,
+                             int32_t *d_bcnt) {
+  REQUIRE(ctx && n >= 0 && m >= 0 && ld >= m && (n == 0 || m == 0 || d_x), "bad args");
+  if (n == 0 || m == 0) return GRID_OK;
+  REQUIRE(n <= 65535, "n > 65535 rows per launch");
+  const int64_t nblk = ceil_div(m, BLK);
+  hipLaunchKernelGGL(k_row_blocks_f64, dim3((unsigned)nblk, (unsigned)n), dim3(64), 0, ctx->stream, d_x, ld, m, nblk,
+                     d_bsum, d_bcnt);
+  LAUNCHCHK();
+  return GRID_OK;
+}
+
+int grid_norm_col_stats_f64(grid_ctx *ctx, const double *d_x, int64_t n, int64_t m, int64_t ld,
+                            const double *d_rowmean, double *d_mu, double *d_var, double *d_ratio) {
+  REQUIRE(ctx && n >= 0 && m >= 0 && ld >= m && d_mu && d_var && d_ratio, "bad args");
+  if (m == 0) return GRID_OK;
+  double *rinv;
+  char *rest;
+  int rc = recip_rows(ctx, d_rowmean, n, 0, &rinv, &rest);
+  if (rc) return rc;
+  const dim3 g((unsigned)ceil_div(m, 256));
+  hipLaunchKernelGGL(k_col_stats_f64, g, dim3(256), 0, ctx->stream, d_x, n, m, ld, d_rowmean, rinv, 0, d_mu, d_var,
+                     d_ratio);
+  hipLaunchKernelGGL(k_col_stats_f64, g, dim3(256), 0, ctx->stream, d_x, n, m, ld, d_rowmean, rinv, 1, d_mu, d_var,
+                     d_ratio);
+  LAUNCHCHK();
+  return GRID_OK;
+}
+
+int grid_norm_zquant_f64(grid_ctx *ctx, const double *d_x, int64_t n, int64_t ld, const int32_t *d_sel, int64_t r,
+                         const double *d_rm, const double *d_mu, double scale, int32_t *d_zq, int64_t ld_zq,
+                         int32_t *h_overflow) {
+  REQUIRE(ctx && n >= 0 && r >= 0 && h_overflow && (r == 0 || (d_x && d_sel && d_zq && ld_zq >= r)), "bad args");
+  *h_overflow = 0;
+  if (n == 0 || r == 0) return GRID_OK;
+  REQUIRE(n <= 65535, "n > 65535 rows per launch");
+  double *rinv;
+  char *rest;
+  const size_t rb = (((size_t)r * 8 + 255) & ~size_t(255));
+  int rc = recip_rows(ctx, d_rm, n, 4 * rb + 256, &rinv, &rest);
+  if (rc) return rc;
+  double *mus = (double *)rest, *sq = (double *)(rest + rb), *rsq = (double *)(rest + 2 * rb);
+  float2 *mc32 = (float2 *)(rest + 3 * rb);
+  int32_t *d_of = (int32_t *)(rest + 4 * rb);
+  HIPCHK(hipMemsetAsync(d_of, 0, 4, ctx->stream));
+  hipLaunchKernelGGL(k_zprep, dim3((unsigned)ceil_div(r, 256)), dim3(256), 0, ctx->stream, d_sel, r, d_mu, scale, mus,
+                     sq, rsq, mc32);
+  hipLaunchKernelGGL(k_zquant_f64, dim3((unsigned)ceil_div(r, 256), (unsigned)n), dim3(256), 0, ctx->stream, d_x, n,
+                     ld, d_sel, r, d_rm, rinv, mus, sq, rsq, scale, d_zq, ld_zq, d_of);
+  LAUNCHCHK();
+  HIPCHK(hipMemcpyAsync(ctx->pinned, d_of, 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  *h_overflow = *(int32_t *)ctx->pinned;
+  return GRID_OK;
 }
 
 }  // extern "C"

@@ -90,6 +90,24 @@ def normalize_stats(dev: Device, q: DevBuf, n: int, m: int, ld: int) -> NormStat
     return NormStats(n, m, rm, mu, var, ratio, nv.value, scale, srt)
 
 
+def normalize_stats_f64(dev: Device, x: DevBuf, n: int, m: int, ld: int) -> NormStats:
+    """normalize_stats on fp64 depths (NaN = missing): the route for depth text
+    that is not exact hundredths (the reference parses any decimal, :272,334)."""
+    nblk = -(-m // BLOCK)
+    bsum = dev.alloc((max(n, 1), max(nblk, 1)), F8)
+    bcnt = dev.alloc((max(n, 1), max(nblk, 1)), I4)
+    call("grid_norm_row_blocks_f64", dev.ctx, ptr(x), n, m, ld, bsum.ptr, bcnt.ptr)
+    rm = dev.alloc(max(n, 1), F8)
+    call("grid_norm_row_means", dev.ctx, bsum.ptr, bcnt.ptr, n, nblk, rm.ptr)
+    mu, var, ratio = dev.alloc(max(m, 1), F8), dev.alloc(max(m, 1), F8), dev.alloc(max(m, 1), F8)
+    call("grid_norm_col_stats_f64", dev.ctx, ptr(x), n, m, ld, rm.ptr, mu.ptr, var.ptr, ratio.ptr)
+    srt = dev.alloc(max(m, 1), F8)
+    nv = C.c_int64()
+    call("grid_sort_valid", dev.ctx, ratio.ptr, m, srt.ptr, C.byref(nv))
+    scale = median_scale(srt, nv.value)
+    return NormStats(n, m, rm, mu, var, ratio, nv.value, scale, srt)
+
+
 def select_regions(dev: Device, st: NormStats, top_frac: float):
     """select_high_variance_regions (normalize_mosdepth.py:492-499)."""
     if st.nvalid == 0:
@@ -107,6 +125,15 @@ def zquant(dev: Device, q, n, ld, sel: DevBuf, r: int, st: NormStats, zq: DevBuf
     of = C.c_int32()
     call("grid_norm_zquant", dev.ctx, ptr(q), n, ld, sel.ptr, r, st.rowmean.ptr, st.mu.ptr, st.scale,
          ptr(zq), r, ptr(colmap), qmax, ptr(zb), ld_zb, C.byref(of))
+    if of.value:
+        raise GridNativeError("normalised z-score exceeds the int32 hundredths range")
+
+
+def zquant_f64(dev: Device, x, n, ld, sel: DevBuf, r: int, st: NormStats, zq: DevBuf):
+    """zquant on fp64 depths (int32 z hundredths of the selected columns)."""
+    of = C.c_int32()
+    call("grid_norm_zquant_f64", dev.ctx, ptr(x), n, ld, sel.ptr, r, st.rowmean.ptr, st.mu.ptr, st.scale,
+         ptr(zq), r, C.byref(of))
     if of.value:
         raise GridNativeError("normalised z-score exceeds the int32 hundredths range")
 

@@ -341,14 +341,23 @@ def ingest_py(individuals, mosdepth_dir, chromosome, start, end, excluded, min_d
         try:
             q[i, js] = to_hundredths(d)
         except UnsupportedDepth as e:
-            # mosdepth prints "%.2f"; other text is not supported by the exact
-            # integer path: fail before any GPU work, naming file and value
-            nan = np.isnan(d)
-            bad = d[~nan & (np.rint(np.where(nan, 0.0, d) * 100.0) / 100.0 != np.where(nan, 0.0, d))]
+            # mosdepth prints "%.2f"; other depth text takes the fp64 route
+            # (the reference reads any decimal with float(), :272,334)
             where = find_bed_gz_for_individual(ind, mosdepth_dir)
-            raise UnsupportedDepth(f"{where}: {e}; first offending depth {bad[0]!r}" if len(bad) else
-                                   f"{where}: {e}") from None
+            msg = f"{where}: {e}; normalising the cohort from fp64 depths"
+            log(console, msg, style="warning") if console else print(msg)
+            return ids, regions, _depth_matrix_f64(per, ids, rows, col, len(regions))
     return ids, regions, q
+
+
+def _depth_matrix_f64(per, ids, rows, col, m):
+    """The sorted rows x sorted (start, end) float64 matrix, NaN missing (:379-416)."""
+    x = np.full((len(ids), m), np.nan, dtype=np.float64)
+    for i, ind in enumerate(ids):
+        rec = per[ind]
+        js = np.fromiter((col[r] for r in rows[ind]), dtype=np.int64, count=len(rows[ind]))
+        x[i, js] = np.fromiter((rec[r] for r in rows[ind]), dtype=np.float64, count=len(rows[ind]))
+    return x
 
 
 # ------------------------------------------------------------------ step --
@@ -396,11 +405,15 @@ def normalize_mosdepth(config, console):
     n, m = q.shape
     dev = get_device(config)
     qd = dev.upload(q)
-    st = engine.normalize_stats(dev, qd, n, m, m)
+    f64 = q.dtype == np.float64                      # depth text that is not exact hundredths
+    st = (engine.normalize_stats_f64 if f64 else engine.normalize_stats)(dev, qd, n, m, m)
     sel, r = engine.select_regions(dev, st, top_frac)
     zq = dev.alloc((n, max(r, 1)), np.int32)
     if r:
-        engine.zquant(dev, qd, n, m, sel, r, st, zq=zq)
+        if f64:
+            engine.zquant_f64(dev, qd, n, m, sel, r, st, zq)
+        else:
+            engine.zquant(dev, qd, n, m, sel, r, st, zq=zq)
     sel_h = sel.numpy()[:r]
     _write_normalized_q(output_path, ids, st.rowmean.numpy()[:n], st.mu.numpy()[:m][sel_h],
                         st.var.numpy()[:m][sel_h], zq.numpy()[:, :r])

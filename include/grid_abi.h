@@ -125,6 +125,20 @@ int grid_norm_col_vars(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t m, 
  * d_sorted must hold n doubles.  (np.median :462 / sorted() :495) */
 int grid_sort_valid(grid_ctx *ctx, const double *d_v, int64_t n, double *d_sorted,
                     int64_t *h_nvalid);
+/* fp64 depths (the route for depth text that is not exact hundredths; the
+ * reference reads any decimal with float(), :272,334): d_x [n][ld] doubles,
+ * NaN = missing.  The same results as the int32 hundredths entry points
+ * (NumPy pairwise row sums, sequential column sums, exact %.2f codes), without
+ * their fast paths. */
+int grid_norm_row_blocks_f64(grid_ctx *ctx, const double *d_x, int64_t n, int64_t m, int64_t ld,
+                             double *d_bsum, int32_t *d_bcnt);
+/* mu, var, ratio of every column (grid_norm_col_means + grid_norm_col_vars) */
+int grid_norm_col_stats_f64(grid_ctx *ctx, const double *d_x, int64_t n, int64_t m, int64_t ld,
+                            const double *d_rowmean, double *d_mu, double *d_var, double *d_ratio);
+/* int32 z hundredths of the selected columns (grid_norm_zquant's codes) */
+int grid_norm_zquant_f64(grid_ctx *ctx, const double *d_x, int64_t n, int64_t ld, const int32_t *d_sel,
+                         int64_t r, const double *d_rm, const double *d_mu, double scale, int32_t *d_zq,
+                         int64_t ld_zq, int32_t *h_overflow);
 /* Count of the non-NaN values of d_v (the length grid_sort_valid would report). */
 int grid_count_valid(grid_ctx *ctx, const double *d_v, int64_t n, int64_t *h_nvalid);
 /* h_vals[j] = the h_ks[j]-th smallest (0-based) non-NaN value of d_v, for

@@ -35,22 +35,25 @@ def to_q(mat):
     return np.ascontiguousarray(q)
 
 
-def run_normalize(dev, mat, top_frac=0.1):
+def run_normalize(dev, mat, top_frac=0.1, f64=False):
     from grid_amd import engine
-    q = to_q(mat)
+    q = np.ascontiguousarray(mat, dtype=np.float64) if f64 else to_q(mat)
     n, m = q.shape
     qd = dev.upload(q)
-    st = engine.normalize_stats(dev, qd, n, m, m)
+    st = (engine.normalize_stats_f64 if f64 else engine.normalize_stats)(dev, qd, n, m, m)
     sel, r = engine.select_regions(dev, st, top_frac)
     zq = dev.alloc((n, max(r, 1)), np.int32)
     if r:
-        engine.zquant(dev, qd, n, m, sel, r, st, zq=zq)
+        if f64:
+            engine.zquant_f64(dev, qd, n, m, sel, r, st, zq)
+        else:
+            engine.zquant(dev, qd, n, m, sel, r, st, zq=zq)
     return st, sel.numpy()[:r], zq.numpy()[:, :r]
 
 
-def check_normalize(dev, mat, top_frac=0.1):
+def check_normalize(dev, mat, top_frac=0.1, f64=False):
     from grid_amd import _abi
-    st, sel, zq = run_normalize(dev, mat, top_frac)
+    st, sel, zq = run_normalize(dev, mat, top_frac, f64)
     with np.errstate(all="ignore"):
         z, ratios, mu, var, scale = steps.normalize_matrix(mat)
         raw = nanmean_rows(mat)
@@ -363,3 +366,25 @@ def test_select_kth_equals_sorted(dev, n):
                 assert got == 0.0, (k, got, srt[k])
             else:
                 assert np.float64(got).view(np.uint64) == srt[k].view(np.uint64), (k, got, srt[k])
+
+
+@pytest.mark.gpu
+def test_normalize_f64_golden_g2(dev):
+    """The fp64-depth route reproduces the golden normalize_matrix outputs."""
+    d = np.load(os.path.join(G, "g2.npz"))
+    n_cases = len([k for k in d.files if k.endswith("_in")])
+    for ci in range(n_cases):
+        check_normalize(dev, d[f"c{ci}_in"], f64=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,m,seed", [(37, 20000, 11), (5, 8192 * 2 + 3, 12), (130, 1000, 13), (2, 7, 14)])
+def test_normalize_f64_random(dev, n, m, seed):
+    """Depths that are not hundredths (3+ decimals, as float() parses them), NaN
+    holes, a zero row: every statistic and z code equal to the oracle's."""
+    rng = np.random.default_rng(seed)
+    mat = rng.uniform(5.0, 80.0, size=(n, m)).round(rng.integers(3, 7))
+    mat[rng.random((n, m)) < 0.05] = np.nan
+    if n > 3:
+        mat[1] = 0.0
+    check_normalize(dev, mat, f64=True)

@@ -10,6 +10,7 @@ import pytest
 
 from grid_amd import _abi
 from grid_amd.utils import normalize_mosdepth as nm
+from oracle import ingest as oracle_ingest
 
 G = os.path.join(os.path.dirname(__file__), "golden")
 
@@ -146,9 +147,13 @@ def test_exotic_text_falls_back_identically(tmp_path, capsys):
         with pytest.raises(_abi.IngestUnsupported):
             nm.ingest_native(inds, d, None, None, None, {}, 20, 100, 2)
         if k == "decimals":
-            # the reference keeps 30.125 in the matrix -> the int32 path refuses it
-            with pytest.raises(nm.UnsupportedDepth, match=r"B\.regions\.bed\.gz.*30\.125"):
-                nm.ingest(inds, d, None, None, None, {}, 20, 100, 2)
+            # the reference keeps 30.125 in the matrix: the cohort takes the fp64
+            # route (NaN missing), equal to the oracle's float matrix
+            ids, regs, x = nm.ingest(inds, d, None, None, None, {}, 20, 100, 2)
+            o_ids, o_regs, o_mat = oracle_ingest.ingest(d, ["A", "B"], None, None, None, None, 20, 100)
+            assert x.dtype == np.float64 and ids == o_ids and regs == o_regs
+            assert np.array_equal(x, o_mat, equal_nan=True) and (x == 30.125).sum() == 1
+            assert "fp64" in capsys.readouterr().out
             continue
         got = nm.ingest(inds, d, None, None, None, {}, 20, 100, 2)
         _same(got, nm.ingest_py(inds, d, None, None, None, {}, 20, 100, 2))
