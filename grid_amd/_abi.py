@@ -373,7 +373,7 @@ def hi_levels(off: np.ndarray, nbr: np.ndarray):
 
 
 PACK_CAP = 16
-HI_UNIT_WEIGHTS, HI_LEGACY = 1, 2     # grid_hi_phase flags
+HI_UNIT_WEIGHTS, HI_LEGACY, HI_PAIRED = 1, 2, 4     # grid_hi_phase flags
 
 
 def hi_schedule(off: np.ndarray, nbr: np.ndarray, w: np.ndarray, packed_w: bool = True):

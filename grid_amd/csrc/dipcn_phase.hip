@@ -56,6 +56,23 @@ __device__ __forceinline__ void nbr_means(int64_t i, const double *hap, const in
   }
 }
 
+// nbr_means for one haplotype h of sample i
+__device__ __forceinline__ void nbr_mean_h(int64_t i, int h, const double *hap, const int64_t *off,
+                                           const int32_t *nbr, const double *w, double &ws, double &wv) {
+  double s = 1e-9, v = 0.0;
+  const int64_t e = off[2 * i + h + 1];
+  for (int64_t t = off[2 * i + h]; t < e; t++) {
+    double x = hap[nbr[t]];
+    if (x == x) {
+      double wt = w[t];
+      s = s + wt;
+      v = v + wt * x;
+    }
+  }
+  ws = s;
+  wv = v;
+}
+
 constexpr int PT = 256;
 constexpr int CAP = 16;   // neighbours per haplotype held in registers (longer lists: loop)
 
@@ -395,7 +412,42 @@ __device__ __forceinline__ void ph2_decode(PhReg<UNITW, CAPT> &it) {
   it.c1 = (it.c1 < 0 || it.c1 > CAPT) ? CAPT + 1 : it.c1;
 }
 
-template <bool UNITW, int CAPT, int PROBE = 0>
+// One haplotype's list (split-lane kernel): entry e, haplotype h.
+template <bool UNITW, int CAPT>
+struct PhReg1 {
+  int32_t i, c, ok;
+  int32_t nb[CAPT];
+  double wt[UNITW ? 1 : CAPT];
+};
+
+template <bool UNITW, int CAPT>
+__device__ __forceinline__ void ph3_fetch(int e, int e1, int h, const int32_t *__restrict__ order,
+                                          const int32_t *__restrict__ pk_nbr, const double *__restrict__ pk_w,
+                                          const int32_t *__restrict__ pk_cnt, PhReg1<UNITW, CAPT> &it) {
+  const bool ok = e < e1;
+  const int ee = ok ? e : 0;                       // loads stay unconditional (entry 0 exists)
+  const int64_t lh = (int64_t)ee * 2 + h;
+  it.i = order[ee];
+  it.c = pk_cnt[lh];
+  const int32_t *pn = pk_nbr + lh * CAP;
+#pragma unroll
+  for (int t = 0; t < CAPT; t += 4) {
+    const int4 a = *reinterpret_cast<const int4 *>(pn + t);
+    it.nb[t] = a.x; it.nb[t + 1] = a.y; it.nb[t + 2] = a.z; it.nb[t + 3] = a.w;
+  }
+  if (!UNITW) {
+    const double *pw = pk_w + lh * CAP;
+#pragma unroll
+    for (int t = 0; t < CAPT; t += 2) {
+      const double2 a = *reinterpret_cast<const double2 *>(pw + t);
+      it.wt[UNITW ? 0 : t] = a.x;
+      it.wt[UNITW ? 0 : t + 1] = a.y;
+    }
+  }
+  it.ok = ok;
+}
+
+template <bool UNITW, int CAPT, int PROBE = 0, int NT = PT, bool SPLIT = false>
 __device__ __forceinline__ void ph2_run(int64_t n, const double *__restrict__ irr,
                                         const int64_t *__restrict__ off, const int32_t *__restrict__ nbr,
                                         const double *__restrict__ w, int64_t min_nbr, int64_t iters,
@@ -419,10 +471,10 @@ __device__ __forceinline__ void ph2_run(int64_t n, const double *__restrict__ ir
   int32_t *lof = reinterpret_cast<int32_t *>(s_hap + 3 * n);
   uint8_t *okf = reinterpret_cast<uint8_t *>(lof + nlev + 1);
   const int tid = threadIdx.x;
-  for (int64_t i = tid; i < n; i += PT) irs[i] = irr[i];
-  for (int l = tid; l <= nlev; l += PT) lof[l] = loff[l];
+  for (int64_t i = tid; i < n; i += NT) irs[i] = irr[i];
+  for (int l = tid; l <= nlev; l += NT) lof[l] = loff[l];
   const double qnan = __builtin_nan("");
-  for (int64_t i = tid; i < n; i += PT) {
+  for (int64_t i = tid; i < n; i += NT) {
     bool ok = (off[2 * i + 1] - off[2 * i] >= min_nbr) && (off[2 * i + 2] - off[2 * i + 1] >= min_nbr);
     double v = ok ? irr[i] / 2 : qnan;
     hap[2 * i] = v;
@@ -441,19 +493,122 @@ __device__ __forceinline__ void ph2_run(int64_t n, const double *__restrict__ ir
     s_mean = m;
   }
   __syncthreads();
-  // chunk table: one sweep = nch chunks of <= PT entries, none crossing a level
+  // chunk table: one sweep = nch chunks of <= CHK entries, none crossing a level
   // (pointer arithmetic from s_hap, not via an integer, keeps it an LDS pointer)
   int2 *chk = reinterpret_cast<int2 *>(okf + ((n + 15) & ~15ll) + ((16 - (3 * n * 8 + (nlev + 1) * 4) % 16) % 16));
+  constexpr int CHK = SPLIT ? NT / 2 : NT;   // schedule entries per chunk
   __shared__ int s_nch;
   if (tid == 0) {
     int c = 0;
     for (int l = 0; l < nlev; l++)
-      for (int b = lof[l]; b < lof[l + 1]; b += PT) chk[c++] = make_int2(b, min(b + PT, lof[l + 1]));
+      for (int b = lof[l]; b < lof[l + 1]; b += CHK) chk[c++] = make_int2(b, min(b + CHK, lof[l + 1]));
     s_nch = c;
   }
   __syncthreads();
   const int nch = s_nch;
-  if (iters > 0 && nch > 0) {
+  if (SPLIT && iters > 0 && nch > 0) {
+    // lane pair (2j, 2j+1) owns schedule entry base + j, one haplotype each:
+    // half the gathers and add chains per lane; the pair's two means meet by a
+    // DPP swap for the shared denominator m0 + m1
+    const int h = tid & 1;
+    PhReg1<UNITW, CAPT> cur, nxt;
+    auto pin = [&](PhReg1<UNITW, CAPT> &it) {
+#pragma unroll
+      for (int t = 0; t < CAPT; t++) asm volatile("" : "+v"(it.nb[t]));
+      if (!UNITW) {
+#pragma unroll
+        for (int t = 0; t < CAPT; t++) asm volatile("" : "+v"(it.wt[UNITW ? 0 : t]));
+      }
+      asm volatile("" : "+v"(it.i), "+v"(it.c), "+v"(it.ok));
+      it.i = it.ok ? it.i : -1;
+      it.c = (it.c < 0 || it.c > CAPT) ? CAPT + 1 : it.c;
+    };
+    auto fetch = [&](int chunk, PhReg1<UNITW, CAPT> &it) {
+      const int2 cb = chk[chunk];
+      ph3_fetch<UNITW, CAPT>(cb.x + (tid >> 1), cb.y, h, order, pk_nbr, pk_w, pk_cnt, it);
+    };
+    auto work = [&](PhReg1<UNITW, CAPT> &cur) {
+      const int cmx = cur.i >= 0 ? min(cur.c, CAPT) : 0;
+      int nseg = 0;
+#pragma unroll
+      for (int sg = 0; sg < CAPT / 4; sg++) nseg += __ballot(cmx > 4 * sg) != 0;
+      const int me = cur.i >= 0 ? cur.i : 0;
+      const double hv = hap[2 * me];
+      double x[CAPT];
+#pragma unroll
+      for (int sg = 0; sg < CAPT / 4; sg++)
+        if (sg < nseg) {
+#pragma unroll
+          for (int j = 0; j < 4; j++) x[4 * sg + j] = hap[cur.nb[4 * sg + j]];
+        }
+#pragma unroll
+      for (int t = 0; t < CAPT; t++) asm volatile("" : "+v"(x[t]));
+      const bool act = cur.i >= 0 && hv == hv;     // the same for both lanes of a pair
+      double m = 0.0;
+      if (act) {
+        double ws, wv;
+        if (cur.c > CAPT) {
+          nbr_mean_h(cur.i, h, hap, off, nbr, w, ws, wv);
+        } else {
+          // the paired kernel's add chain for this lane's haplotype
+          double sw = 1e-9, sv = 0.0;
+          int k = 0;
+#pragma unroll
+          for (int sg = 0; sg < CAPT / 4; sg++)
+            if (sg < nseg) {
+#pragma unroll
+              for (int j = 0; j < 4; j++) {
+                const int t = 4 * sg + j;
+                const bool take = (t < cur.c) && (x[t] == x[t]);
+                if (UNITW) {
+                  sv = sv + (take ? x[t] : 0.0);
+                  k += take;
+                } else {
+                  const double wt = cur.wt[UNITW ? 0 : t];
+                  const double p = wt * x[t];
+                  sw = sw + (take ? wt : 0.0);
+                  sv = sv + (take ? p : 0.0);
+                }
+              }
+            }
+          ws = UNITW ? s_unit[k] : sw;
+          wv = sv;
+        }
+        m = wv / ws;
+      }
+      // all lanes are active here, so the partner's value is always readable
+      const uint64_t mb = (uint64_t)__double_as_longlong(m);
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)mb, 0xB1, 0xF, 0xF, false);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(mb >> 32), 0xB1, 0xF, 0xF, false);
+      const double mo = __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+      bool upd = false;
+      double nv = 0.0;
+      if (act) {
+        const double den = h ? mo + m : m + mo;   // m0 + m1
+        if (den > 0.0) {
+          nv = irs[cur.i] * m / den;
+          upd = true;
+        }
+      }
+      wg_barrier<true>();
+      if (upd) hap[2 * cur.i + h] = nv;
+      wg_barrier<true>();
+    };
+    const int64_t total = iters * (int64_t)nch;
+    fetch(0, cur);
+    pin(cur);
+    int c = 0;
+    for (int64_t g = 0; g < total; g++) {
+      const int cn = c + 1 == nch ? 0 : c + 1;
+      if (g + 1 < total) fetch(cn, nxt);
+      asm volatile("" ::: "memory");
+      work(cur);
+      c = cn;
+      pin(nxt);
+      cur = nxt;
+    }
+  } else if (iters > 0 && nch > 0) {
+
     // two register sets: the chunk in work and the next one (in flight)
     PhReg<UNITW, CAPT> cur, nxt;
     auto pin = [&](PhReg<UNITW, CAPT> &it) {
@@ -569,7 +724,7 @@ __device__ __forceinline__ void ph2_run(int64_t n, const double *__restrict__ ir
     }
   }
   const double mean = s_mean;
-  for (int64_t i = tid; i < n; i += PT) {
+  for (int64_t i = tid; i < n; i += NT) {
     double ws[2], wv[2];
     nbr_means(i, hap, off, nbr, w, ws, wv);
     double i0 = wv[0] / ws[0];
@@ -580,12 +735,12 @@ __device__ __forceinline__ void ph2_run(int64_t n, const double *__restrict__ ir
     imp[2 * i + 1] = i1;
   }
   __syncthreads();
-  for (int64_t e = tid; e < 2 * n; e += PT) hap_g[e] = hap[e];
+  for (int64_t e = tid; e < 2 * n; e += NT) hap_g[e] = hap[e];
   if (tid == 0) *mean_out = mean;
 }
 
-template <bool UNITW, int CAPT, int PROBE = 0>
-__global__ __launch_bounds__(PT) void k_phase2(int64_t n, const double *__restrict__ irr,
+template <bool UNITW, int CAPT, int PROBE = 0, int NT = PT, bool SPLIT = false>
+__global__ __launch_bounds__(NT) void k_phase2(int64_t n, const double *__restrict__ irr,
                                                const int64_t *__restrict__ off, const int32_t *__restrict__ nbr,
                                                const double *__restrict__ w, int64_t min_nbr, int64_t iters,
                                                const int32_t *__restrict__ order, const int32_t *__restrict__ loff,
@@ -594,16 +749,16 @@ __global__ __launch_bounds__(PT) void k_phase2(int64_t n, const double *__restri
                                                double *hap_g, double *__restrict__ imp,
                                                double *__restrict__ mean_out) {
   extern __shared__ __attribute__((aligned(16))) double s_hap[];
-  ph2_run<UNITW, CAPT, PROBE>(n, irr, off, nbr, w, min_nbr, iters, order, loff, nlev, pk_nbr, pk_w, pk_cnt, hap_g,
+  ph2_run<UNITW, CAPT, PROBE, NT, SPLIT>(n, irr, off, nbr, w, min_nbr, iters, order, loff, nlev, pk_nbr, pk_w, pk_cnt, hap_g,
                               imp, mean_out, s_hap);
 }
 
-template <bool UNITW, int CAPT>
-__global__ __launch_bounds__(PT) void k_phase2_batch(const grid_hi_locus *__restrict__ loci, int64_t min_nbr,
+template <bool UNITW, int CAPT, int NT = PT, bool SPLIT = false>
+__global__ __launch_bounds__(NT) void k_phase2_batch(const grid_hi_locus *__restrict__ loci, int64_t min_nbr,
                                                      int64_t iters) {
   extern __shared__ __attribute__((aligned(16))) double s_hap[];
   const grid_hi_locus &L = loci[blockIdx.x];
-  ph2_run<UNITW, CAPT, 0>(L.n, L.irr, L.off, L.nbr, L.w, min_nbr, iters, L.order, L.loff, L.nlev, L.pk_nbr,
+  ph2_run<UNITW, CAPT, 0, NT, SPLIT>(L.n, L.irr, L.off, L.nbr, L.w, min_nbr, iters, L.order, L.loff, L.nlev, L.pk_nbr,
                           L.pk_w, L.pk_cnt, L.hap, L.imp, L.mean, s_hap);
 }
 
@@ -668,8 +823,14 @@ int grid_hi_phase(grid_ctx *ctx, int64_t n, const double *d_irr, const int64_t *
   const bool unitw = flags & GRID_HI_UNIT_WEIGHTS;
   if (lds2 <= 120 * 1024 && !(flags & GRID_HI_LEGACY)) {
     // register-pipelined kernel; CAPT covers the longest list when it can
-    auto kern = unitw ? (max_list <= 8 ? k_phase2<true, 8> : k_phase2<true, 16>)
-                      : (max_list <= 8 ? k_phase2<false, 8> : k_phase2<false, 16>);
+    // default: 512 lanes, one haplotype per lane (256 entries per chunk);
+    // GRID_HI_PAIRED: 256 lanes, both haplotypes per lane
+    const bool split = !(flags & GRID_HI_PAIRED);
+    constexpr int NS = 2 * PT;
+    auto kern = split ? (unitw ? (max_list <= 8 ? k_phase2<true, 8, 0, NS, true> : k_phase2<true, 16, 0, NS, true>)
+                               : (max_list <= 8 ? k_phase2<false, 8, 0, NS, true> : k_phase2<false, 16, 0, NS, true>))
+                      : (unitw ? (max_list <= 8 ? k_phase2<true, 8> : k_phase2<true, 16>)
+                               : (max_list <= 8 ? k_phase2<false, 8> : k_phase2<false, 16>));
 #ifdef GRID_PROBES
     // tools build only -- GRID_PHASE_PROBE timing probes (wrong results):
     // 1 = no list prefetch, 2 = no arithmetic, 3 = neither
@@ -681,14 +842,14 @@ int grid_hi_phase(grid_ctx *ctx, int64_t n, const double *d_irr, const int64_t *
 #else
     const int probe = 0;
 #endif
-    static bool attr2[7] = {false, false, false, false, false, false, false};
-    const int slot = probe ? 3 + probe : (unitw ? 2 : 0) + (max_list <= 8 ? 0 : 1);
+    static bool attr2[11] = {};
+    const int slot = probe ? 3 + probe : (split ? 7 : 0) + (unitw ? 2 : 0) + (max_list <= 8 ? 0 : 1);
     if (!attr2[slot]) {
       HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024));
       attr2[slot] = true;
     }
-    hipLaunchKernelGGL(kern, dim3(1), dim3(PT), lds2, ctx->stream, n, d_irr, d_off, d_nbr, d_w, min_nbr, n_iters,
-                       d_order, d_loff, nlevels, d_pk_nbr, d_pk_w, d_pk_cnt, d_hap, d_imp, d_mean);
+    hipLaunchKernelGGL(kern, dim3(1), dim3(split && !probe ? NS : PT), lds2, ctx->stream, n, d_irr, d_off, d_nbr,
+                       d_w, min_nbr, n_iters, d_order, d_loff, nlevels, d_pk_nbr, d_pk_w, d_pk_cnt, d_hap, d_imp, d_mean);
   } else if (lds <= 120 * 1024) {
     static bool attr = false;
     if (!attr) {
@@ -716,15 +877,21 @@ int grid_hi_phase_batch(grid_ctx *ctx, int64_t n_loci, const grid_hi_locus *d_lo
   const size_t lds2 = lds + 32 + (size_t)(max_nlev + max_n / PT + 2) * 8;
   const bool unitw = flags & GRID_HI_UNIT_WEIGHTS;
   if (lds2 <= 120 * 1024 && !(flags & GRID_HI_LEGACY)) {
-    auto kern = unitw ? (max_list <= 8 ? k_phase2_batch<true, 8> : k_phase2_batch<true, 16>)
-                      : (max_list <= 8 ? k_phase2_batch<false, 8> : k_phase2_batch<false, 16>);
-    static bool attr[4] = {false, false, false, false};
-    const int slot = (unitw ? 2 : 0) + (max_list <= 8 ? 0 : 1);
+    const bool split = !(flags & GRID_HI_PAIRED);
+    constexpr int NS = 2 * PT;
+    auto kern = split ? (unitw ? (max_list <= 8 ? k_phase2_batch<true, 8, NS, true> : k_phase2_batch<true, 16, NS, true>)
+                               : (max_list <= 8 ? k_phase2_batch<false, 8, NS, true>
+                                                : k_phase2_batch<false, 16, NS, true>))
+                      : (unitw ? (max_list <= 8 ? k_phase2_batch<true, 8> : k_phase2_batch<true, 16>)
+                               : (max_list <= 8 ? k_phase2_batch<false, 8> : k_phase2_batch<false, 16>));
+    static bool attr[8] = {};
+    const int slot = (split ? 4 : 0) + (unitw ? 2 : 0) + (max_list <= 8 ? 0 : 1);
     if (!attr[slot]) {
       HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024));
       attr[slot] = true;
     }
-    hipLaunchKernelGGL(kern, dim3((unsigned)n_loci), dim3(PT), lds2, ctx->stream, d_loci, min_nbr, n_iters);
+    hipLaunchKernelGGL(kern, dim3((unsigned)n_loci), dim3(split ? NS : PT), lds2, ctx->stream, d_loci, min_nbr,
+                       n_iters);
   } else if (lds <= 120 * 1024) {
     static bool attr = false;
     if (!attr) {

@@ -310,9 +310,10 @@ def csr_from_lists(hap_nbrs):
 
 
 def phase(dev: Device, irr: np.ndarray, off: np.ndarray, nbr: np.ndarray, w: np.ndarray, min_nbr: int,
-          n_iters: int, legacy: bool = False):
+          n_iters: int, legacy: bool = False, paired: bool = False):
     """``legacy`` selects the per-neighbour LDS kernel (k_phase) that larger
-    loci run anyway (A/B tests; same results)."""
+    loci run anyway; ``paired`` the register-pipelined kernel with both
+    haplotypes of a sample on one lane (A/B tests; same results)."""
     n = len(irr)
     if n == 0:
         return np.zeros(0), np.zeros(0), 0.0
@@ -324,11 +325,11 @@ def phase(dev: Device, irr: np.ndarray, off: np.ndarray, nbr: np.ndarray, w: np.
     hap, imp, mean = dev.alloc(2 * n, F8), dev.alloc(2 * n, F8), dev.alloc(1, F8)
     call("grid_hi_phase", dev.ctx, n, bufs[0].ptr, bufs[1].ptr, bufs[2].ptr, bufs[3].ptr, min_nbr, n_iters,
          bufs[4].ptr, bufs[5].ptr, nl, bufs[6].ptr, bufs[7].ptr, bufs[8].ptr, hap.ptr, imp.ptr, mean.ptr,
-         flags | (_abi.HI_LEGACY if legacy else 0), max_list)
+         flags | (_abi.HI_LEGACY if legacy else 0) | (_abi.HI_PAIRED if paired else 0), max_list)
     return hap.numpy(), imp.numpy(), float(mean.numpy()[0])
 
 
-def phase_batch(dev: Device, loci, min_nbr: int, n_iters: int, legacy: bool = False):
+def phase_batch(dev: Device, loci, min_nbr: int, n_iters: int, legacy: bool = False, paired: bool = False):
     """Batched phasing + imputation of L independent loci in one launch (one
     workgroup per locus; BASELINE config 5).  ``loci``: sequence of
     (irr [n], off [2n+1], nbr, w) per locus (CSR as csr_from_lists).  Returns
@@ -368,7 +369,7 @@ def phase_batch(dev: Device, loci, min_nbr: int, n_iters: int, legacy: bool = Fa
     d_arr = dev.alloc(C.sizeof(arr), np.uint8)
     call("grid_h2d", dev.ctx, d_arr.ptr, C.addressof(arr), C.sizeof(arr))
     call("grid_hi_phase_batch", dev.ctx, len(descs), d_arr.ptr, max_n, max_nlev, min_nbr, n_iters,
-         flags_all | legacy, max_list)
+         flags_all | legacy | (_abi.HI_PAIRED if paired else 0), max_list)
     res = []
     for n, hap, imp, mean in outs:
         res.append((hap.numpy()[: 2 * n], imp.numpy()[: 2 * n], float(mean.numpy()[0]) if n else 0.0))

@@ -211,7 +211,7 @@ def _phase_device_csr(IRRs, off, nbr, w, MIN_NBR, N_ITERS, console=None, dev=Non
     return engine.phase(dev or get_device(), np.asarray(IRRs, dtype=np.float64), off, nbr, w, MIN_NBR, N_ITERS)
 
 
-def run_phasing_batch(IRRs_per_locus, hap_nbrs_per_locus, MIN_NBR, N_ITERS, dev=None):
+def run_phasing_batch(IRRs_per_locus, hap_nbrs_per_locus, MIN_NBR, N_ITERS, dev=None, paired=False):
     """_run_phasing + _compute_imp (:175-250) for many loci (VNTR regions) in
     one GPU launch, one workgroup per locus (BASELINE config 5).  Equal, locus
     by locus, to calling the reference per region.  Returns a list of
@@ -220,7 +220,7 @@ def run_phasing_batch(IRRs_per_locus, hap_nbrs_per_locus, MIN_NBR, N_ITERS, dev=
     for irrs, hap_nbrs in zip(IRRs_per_locus, hap_nbrs_per_locus):
         off, nbr, w = engine.csr_from_lists(hap_nbrs)
         loci.append((np.asarray(irrs, dtype=np.float64), off, nbr, w))
-    return engine.phase_batch(dev or get_device(), loci, MIN_NBR, N_ITERS)
+    return engine.phase_batch(dev or get_device(), loci, MIN_NBR, N_ITERS, paired=paired)
 
 
 def _compute_imp(i, hap_IRRs, hap_nbrs, mean_IRRs):

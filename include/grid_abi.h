@@ -330,6 +330,7 @@ int grid_hi_phase(grid_ctx *ctx, int64_t n, const double *d_irr, const int64_t *
                   double *d_hap, double *d_imp, double *d_mean, int32_t flags, int32_t max_list);
 #define GRID_HI_UNIT_WEIGHTS 1   /* every weight is 1.0 (IBS lists): weights are not read */
 #define GRID_HI_LEGACY 2         /* A/B: the previous (per-neighbour LDS round trip) kernel */
+#define GRID_HI_PAIRED 4         /* A/B: register-pipelined kernel with both haplotypes per lane */
 
 /* Haplotype-neighbour files -> CSR (host C++; Python text semantics for ASCII
  * input).  ids_nl: the dipCN file's sample IDs joined by '\n' (index = line

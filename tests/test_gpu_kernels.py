@@ -266,11 +266,15 @@ def test_phasing_random(dev, n, seed):
     assert np.array_equal(imp, np.array(ei).reshape(-1))
 
 
-@pytest.mark.parametrize("weighted,maxlen,legacy", [(False, 6, False), (True, 6, False), (True, 14, False),
-                                                    (False, 40, False), (True, 40, False), (True, 14, True)])
-def test_phasing_kernel_variants(dev, weighted, maxlen, legacy):
+@pytest.mark.parametrize("weighted,maxlen,legacy,paired", [
+    (False, 6, False, False), (True, 6, False, False), (True, 14, False, False), (False, 40, False, False),
+    (True, 40, False, False), (True, 14, True, False), (False, 6, False, True), (True, 14, False, True),
+    (True, 40, False, True)])
+def test_phasing_kernel_variants(dev, weighted, maxlen, legacy, paired):
     """Register capacities 8/16, unit and general weights, lists longer than
-    the packed capacity (CSR loop), and the legacy kernel, vs the oracle."""
+    the packed capacity (CSR loop), the legacy kernel and the paired-lane
+    register kernel (the default splits a sample's haplotypes over two
+    lanes), vs the oracle."""
     from grid_amd import engine
     rng = np.random.default_rng(maxlen * 2 + weighted)
     n = 700
@@ -286,7 +290,7 @@ def test_phasing_kernel_variants(dev, weighted, maxlen, legacy):
             lst.append((min(2 * j + int(rng.integers(0, 2)), 2 * n - 1), wt))
         hn.append(lst)
     off, nbr, w = engine.csr_from_lists(hn)
-    hap, imp, mean = engine.phase(dev, irr, off, nbr, w, 1, 15, legacy=legacy)
+    hap, imp, mean = engine.phase(dev, irr, off, nbr, w, 1, 15, legacy=legacy, paired=paired)
     eh, em = steps.run_phasing(list(irr), hn, 1, 15)
     assert np.array_equal(hap, np.array(eh), equal_nan=True)
     assert mean == em or (np.isnan(mean) and np.isnan(em))
@@ -307,9 +311,10 @@ def _random_locus(rng, n, weighted, maxlen):
     return list(irr), hn
 
 
-@pytest.mark.parametrize("big,weighted,min_nbr", [(False, False, 1), (False, True, 2), (True, False, 1),
-                                                  (True, True, 0)])
-def test_phasing_batch_equals_per_locus_oracle(dev, big, weighted, min_nbr):
+@pytest.mark.parametrize("big,weighted,min_nbr,paired", [(False, False, 1, False), (False, True, 2, False),
+                                                         (True, False, 1, False), (True, True, 0, False),
+                                                         (False, True, 2, True)])
+def test_phasing_batch_equals_per_locus_oracle(dev, big, weighted, min_nbr, paired):
     """grid_hi_phase_batch (one workgroup per locus, config 5) on loci of
     different sizes against the reference arithmetic run per locus; big=True
     puts a 5,000-sample locus in the batch, which moves every locus to the
@@ -319,7 +324,7 @@ def test_phasing_batch_equals_per_locus_oracle(dev, big, weighted, min_nbr):
     sizes = [1, 37, 256, 300, 1201] + ([5000] if big else [])
     loci = [_random_locus(rng, n, weighted and i % 2 == 0, 12 if i != 2 else 20) for i, n in enumerate(sizes)]
     iters = 9
-    got = run_phasing_batch([a for a, _ in loci], [b for _, b in loci], min_nbr, iters, dev=dev)
+    got = run_phasing_batch([a for a, _ in loci], [b for _, b in loci], min_nbr, iters, dev=dev, paired=paired)
     for (irr, hn), (hap, imp, mean) in zip(loci, got):
         eh, em = steps.run_phasing(irr, hn, min_nbr, iters)
         assert np.array_equal(hap, np.array(eh), equal_nan=True)

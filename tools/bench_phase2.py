@@ -1,5 +1,6 @@
-"""Phasing kernel cost vs neighbour-list length (same level structure), the
-register-pipelined kernel against the previous one (GRID_HI_LEGACY)."""
+"""Phasing kernel cost vs neighbour-list length (same level structure): the
+split-lane kernel (default) against the paired-lane one (GRID_HI_PAIRED) and
+the per-neighbour one (GRID_HI_LEGACY).  The probes run the paired kernel."""
 import os
 import sys
 
@@ -41,7 +42,8 @@ for keep in (10, 0):
     d = [A.upload(x) for x in (off, nb if nb.size else np.zeros(1, np.int32), ww if ww.size else np.zeros(1),
                                order, loff, pk_nbr, pk_w, pk_cnt)]
     hap, imp, mean = A.empty(2 * n, np.float64), A.empty(2 * n, np.float64), A.empty(1, np.float64)
-    for flags, name, probe in ((1, "k_phase2", "0"), (1 | 2, "legacy", "0"), (1, "probe-noprefetch", "1"),
+    for flags, name, probe in ((1, "k_phase2", "0"), (1 | 4, "paired", "0"), (1 | 2, "legacy", "0"),
+                               (1, "probe-noprefetch", "1"),
                                (1, "probe-noarith", "2"), (1, "probe-barriers-only", "3")):
         os.environ["GRID_PHASE_PROBE"] = probe
         ts = []
