@@ -30,6 +30,7 @@ ap.add_argument("--iters", type=int, default=100)
 ap.add_argument("--per-hap", type=int, default=10)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--cpu-samples", type=int, default=1000)
+ap.add_argument("--paired", action="store_true", help="A/B: the two-haplotypes-per-lane kernel")
 a = ap.parse_args()
 
 
@@ -56,7 +57,7 @@ res, times = None, []
 for rep in range(a.reps + 1):          # first call: schedules, uploads and warm-up
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    res = engine.phase_batch(dev, loci, 1, a.iters)
+    res = engine.phase_batch(dev, loci, 1, a.iters, paired=a.paired)
     torch.cuda.synchronize()
     times.append(time.perf_counter() - t1)
 prep_s = time.perf_counter() - t0
@@ -84,7 +85,8 @@ def device_ms():
     for _ in range(a.reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        _abi.call("grid_hi_phase_batch", dev.ctx, len(descs), d.ptr, a.samples, max_nl, 1, a.iters, 1, max_list)
+        _abi.call("grid_hi_phase_batch", dev.ctx, len(descs), d.ptr, a.samples, max_nl, 1, a.iters,
+                  1 | (_abi.HI_PAIRED if a.paired else 0), max_list)
         e1.record()
         torch.cuda.synchronize()
         ms.append(e0.elapsed_time(e1))
