@@ -447,7 +447,7 @@ __device__ __forceinline__ void ph3_fetch(int e, int e1, int h, const int32_t *_
   it.ok = ok;
 }
 
-template <bool UNITW, int CAPT, int PROBE = 0, int NT = PT, bool SPLIT = false>
+template <bool UNITW, int CAPT, int PROBE = 0, int NT = PT, bool SPLIT = false, bool GLB = false>
 __device__ __forceinline__ void ph2_run(int64_t n, const double *__restrict__ irr,
                                         const int64_t *__restrict__ off, const int32_t *__restrict__ nbr,
                                         const double *__restrict__ w, int64_t min_nbr, int64_t iters,
@@ -458,7 +458,9 @@ __device__ __forceinline__ void ph2_run(int64_t n, const double *__restrict__ ir
                                         double *__restrict__ mean_out, double *s_hap) {
   __shared__ double s_mean;
   __shared__ double s_unit[CAPT + 1];
-  double *hap = s_hap;
+  // GLB: hap too large for LDS -- it lives in the output buffer hap_g (the
+  // workgroup's own, so __syncthreads orders it); LDS holds the chunk table only
+  double *hap = GLB ? hap_g : s_hap;
   if (threadIdx.x == 0) {
     double u = 1e-9;
     for (int k = 0; k <= CAPT; k++) {
@@ -466,13 +468,17 @@ __device__ __forceinline__ void ph2_run(int64_t n, const double *__restrict__ ir
       u = u + 1.0;
     }
   }
-  // LDS: hap[2n] | irr[n] | level offsets[nlev+1] | phased flags[n]
-  double *irs = s_hap + 2 * n;
-  int32_t *lof = reinterpret_cast<int32_t *>(s_hap + 3 * n);
-  uint8_t *okf = reinterpret_cast<uint8_t *>(lof + nlev + 1);
+  // LDS: hap[2n] | irr[n] | level offsets[nlev+1] | phased flags[n] (GLB: none of them;
+  // the phased flags borrow imp, which is written only after the sweeps)
+  const double *irs = GLB ? irr : s_hap + 2 * n;
+  int32_t *lof = GLB ? nullptr : reinterpret_cast<int32_t *>(s_hap + 3 * n);
+  uint8_t *okf = GLB ? reinterpret_cast<uint8_t *>(imp) : reinterpret_cast<uint8_t *>(s_hap + 3 * n) + (nlev + 1) * 4;
+  const int32_t *lo = GLB ? loff : lof;
   const int tid = threadIdx.x;
-  for (int64_t i = tid; i < n; i += NT) irs[i] = irr[i];
-  for (int l = tid; l <= nlev; l += NT) lof[l] = loff[l];
+  if (!GLB) {
+    for (int64_t i = tid; i < n; i += NT) s_hap[2 * n + i] = irr[i];
+    for (int l = tid; l <= nlev; l += NT) lof[l] = loff[l];
+  }
   const double qnan = __builtin_nan("");
   for (int64_t i = tid; i < n; i += NT) {
     bool ok = (off[2 * i + 1] - off[2 * i] >= min_nbr) && (off[2 * i + 2] - off[2 * i + 1] >= min_nbr);
@@ -495,13 +501,15 @@ __device__ __forceinline__ void ph2_run(int64_t n, const double *__restrict__ ir
   __syncthreads();
   // chunk table: one sweep = nch chunks of <= CHK entries, none crossing a level
   // (pointer arithmetic from s_hap, not via an integer, keeps it an LDS pointer)
-  int2 *chk = reinterpret_cast<int2 *>(okf + ((n + 15) & ~15ll) + ((16 - (3 * n * 8 + (nlev + 1) * 4) % 16) % 16));
+  int2 *chk = GLB ? reinterpret_cast<int2 *>(s_hap)
+                  : reinterpret_cast<int2 *>(reinterpret_cast<uint8_t *>(s_hap + 3 * n) + (nlev + 1) * 4 +
+                                             ((n + 15) & ~15ll) + ((16 - (3 * n * 8 + (nlev + 1) * 4) % 16) % 16));
   constexpr int CHK = SPLIT ? NT / 2 : NT;   // schedule entries per chunk
   __shared__ int s_nch;
   if (tid == 0) {
     int c = 0;
     for (int l = 0; l < nlev; l++)
-      for (int b = lof[l]; b < lof[l + 1]; b += CHK) chk[c++] = make_int2(b, min(b + CHK, lof[l + 1]));
+      for (int b = lo[l]; b < lo[l + 1]; b += CHK) chk[c++] = make_int2(b, min(b + CHK, lo[l + 1]));
     s_nch = c;
   }
   __syncthreads();
@@ -590,9 +598,9 @@ __device__ __forceinline__ void ph2_run(int64_t n, const double *__restrict__ ir
           upd = true;
         }
       }
-      wg_barrier<true>();
+      wg_barrier<!GLB>();
       if (upd) hap[2 * cur.i + h] = nv;
-      wg_barrier<true>();
+      wg_barrier<!GLB>();
     };
     const int64_t total = iters * (int64_t)nch;
     fetch(0, cur);
@@ -700,12 +708,12 @@ __device__ __forceinline__ void ph2_run(int64_t n, const double *__restrict__ ir
             upd = true;
           }
         }
-        wg_barrier<true>();
+        wg_barrier<!GLB>();
         if (upd) {
           hap[2 * cur.i] = n0;
           hap[2 * cur.i + 1] = n1;
         }
-        wg_barrier<true>();
+        wg_barrier<!GLB>();
     };
     const int64_t total = iters * (int64_t)nch;
     fetch(0, cur);
@@ -735,11 +743,12 @@ __device__ __forceinline__ void ph2_run(int64_t n, const double *__restrict__ ir
     imp[2 * i + 1] = i1;
   }
   __syncthreads();
-  for (int64_t e = tid; e < 2 * n; e += NT) hap_g[e] = hap[e];
+  if (!GLB)
+    for (int64_t e = tid; e < 2 * n; e += NT) hap_g[e] = hap[e];
   if (tid == 0) *mean_out = mean;
 }
 
-template <bool UNITW, int CAPT, int PROBE = 0, int NT = PT, bool SPLIT = false>
+template <bool UNITW, int CAPT, int PROBE = 0, int NT = PT, bool SPLIT = false, bool GLB = false>
 __global__ __launch_bounds__(NT) void k_phase2(int64_t n, const double *__restrict__ irr,
                                                const int64_t *__restrict__ off, const int32_t *__restrict__ nbr,
                                                const double *__restrict__ w, int64_t min_nbr, int64_t iters,
@@ -749,16 +758,16 @@ __global__ __launch_bounds__(NT) void k_phase2(int64_t n, const double *__restri
                                                double *hap_g, double *__restrict__ imp,
                                                double *__restrict__ mean_out) {
   extern __shared__ __attribute__((aligned(16))) double s_hap[];
-  ph2_run<UNITW, CAPT, PROBE, NT, SPLIT>(n, irr, off, nbr, w, min_nbr, iters, order, loff, nlev, pk_nbr, pk_w, pk_cnt, hap_g,
+  ph2_run<UNITW, CAPT, PROBE, NT, SPLIT, GLB>(n, irr, off, nbr, w, min_nbr, iters, order, loff, nlev, pk_nbr, pk_w, pk_cnt, hap_g,
                               imp, mean_out, s_hap);
 }
 
-template <bool UNITW, int CAPT, int NT = PT, bool SPLIT = false>
+template <bool UNITW, int CAPT, int NT = PT, bool SPLIT = false, bool GLB = false>
 __global__ __launch_bounds__(NT) void k_phase2_batch(const grid_hi_locus *__restrict__ loci, int64_t min_nbr,
                                                      int64_t iters) {
   extern __shared__ __attribute__((aligned(16))) double s_hap[];
   const grid_hi_locus &L = loci[blockIdx.x];
-  ph2_run<UNITW, CAPT, 0, NT, SPLIT>(L.n, L.irr, L.off, L.nbr, L.w, min_nbr, iters, L.order, L.loff, L.nlev, L.pk_nbr,
+  ph2_run<UNITW, CAPT, 0, NT, SPLIT, GLB>(L.n, L.irr, L.off, L.nbr, L.w, min_nbr, iters, L.order, L.loff, L.nlev, L.pk_nbr,
                           L.pk_w, L.pk_cnt, L.hap, L.imp, L.mean, s_hap);
 }
 
@@ -820,6 +829,7 @@ int grid_hi_phase(grid_ctx *ctx, int64_t n, const double *d_irr, const int64_t *
   const size_t lds = (size_t)3 * n * sizeof(double) + (size_t)(nlevels + 1) * 4 + (size_t)n;
   // k_phase2 adds its chunk table (<= nlevels + n/PT + 1 entries, 16-B aligned)
   const size_t lds2 = lds + 32 + (size_t)(nlevels + n / PT + 2) * 8;
+  const size_t lds_g = 32 + (size_t)(nlevels + n / PT + 2) * 8;   // hap in global memory
   const bool unitw = flags & GRID_HI_UNIT_WEIGHTS;
   if (lds2 <= 120 * 1024 && !(flags & GRID_HI_LEGACY)) {
     // register-pipelined kernel; CAPT covers the longest list when it can
@@ -859,6 +869,20 @@ int grid_hi_phase(grid_ctx *ctx, int64_t n, const double *d_irr, const int64_t *
     }
     hipLaunchKernelGGL(k_phase<true>, dim3(1), dim3(PT), lds, ctx->stream, n, d_irr, d_off, d_nbr, d_w, min_nbr,
                        n_iters, d_order, d_loff, nlevels, d_pk_nbr, d_pk_w, d_pk_cnt, d_hap, d_imp, d_mean);
+  } else if (!(flags & (GRID_HI_LEGACY | GRID_HI_PAIRED)) && lds_g <= 120 * 1024) {
+    // hap in global memory, split-lane register kernel (LDS: the chunk table)
+    constexpr int NS = 2 * PT;
+    auto kern = unitw ? (max_list <= 8 ? k_phase2<true, 8, 0, NS, true, true> : k_phase2<true, 16, 0, NS, true, true>)
+                      : (max_list <= 8 ? k_phase2<false, 8, 0, NS, true, true>
+                                       : k_phase2<false, 16, 0, NS, true, true>);
+    static bool attrg[4] = {};
+    const int slot = (unitw ? 2 : 0) + (max_list <= 8 ? 0 : 1);
+    if (!attrg[slot]) {
+      HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024));
+      attrg[slot] = true;
+    }
+    hipLaunchKernelGGL(kern, dim3(1), dim3(NS), lds_g, ctx->stream, n, d_irr, d_off, d_nbr, d_w, min_nbr, n_iters,
+                       d_order, d_loff, nlevels, d_pk_nbr, d_pk_w, d_pk_cnt, d_hap, d_imp, d_mean);
   } else {
     hipLaunchKernelGGL(k_phase<false>, dim3(1), dim3(PT), 0, ctx->stream, n, d_irr, d_off, d_nbr, d_w, min_nbr,
                        n_iters, d_order, d_loff, nlevels, d_pk_nbr, d_pk_w, d_pk_cnt, d_hap, d_imp, d_mean);
@@ -875,6 +899,7 @@ int grid_hi_phase_batch(grid_ctx *ctx, int64_t n_loci, const grid_hi_locus *d_lo
   REQUIRE(d_loci, "d_loci is NULL");
   const size_t lds = (size_t)3 * max_n * sizeof(double) + (size_t)(max_nlev + 1) * 4 + (size_t)max_n;
   const size_t lds2 = lds + 32 + (size_t)(max_nlev + max_n / PT + 2) * 8;
+  const size_t lds_g = 32 + (size_t)(max_nlev + max_n / PT + 2) * 8;
   const bool unitw = flags & GRID_HI_UNIT_WEIGHTS;
   if (lds2 <= 120 * 1024 && !(flags & GRID_HI_LEGACY)) {
     const bool split = !(flags & GRID_HI_PAIRED);
@@ -901,8 +926,21 @@ int grid_hi_phase_batch(grid_ctx *ctx, int64_t n_loci, const grid_hi_locus *d_lo
     }
     hipLaunchKernelGGL(k_phase_batch<true>, dim3((unsigned)n_loci), dim3(PT), lds, ctx->stream, d_loci, min_nbr,
                        n_iters);
-  } else {
+  } else if (!(flags & (GRID_HI_LEGACY | GRID_HI_PAIRED)) && lds_g <= 120 * 1024) {
     // hap in each locus's global output buffer (L2-resident per workgroup)
+    constexpr int NS = 2 * PT;
+    auto kern = unitw ? (max_list <= 8 ? k_phase2_batch<true, 8, NS, true, true>
+                                       : k_phase2_batch<true, 16, NS, true, true>)
+                      : (max_list <= 8 ? k_phase2_batch<false, 8, NS, true, true>
+                                       : k_phase2_batch<false, 16, NS, true, true>);
+    static bool attrg[4] = {};
+    const int slot = (unitw ? 2 : 0) + (max_list <= 8 ? 0 : 1);
+    if (!attrg[slot]) {
+      HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024));
+      attrg[slot] = true;
+    }
+    hipLaunchKernelGGL(kern, dim3((unsigned)n_loci), dim3(NS), lds_g, ctx->stream, d_loci, min_nbr, n_iters);
+  } else {
     hipLaunchKernelGGL(k_phase_batch<false>, dim3((unsigned)n_loci), dim3(PT), 0, ctx->stream, d_loci, min_nbr,
                        n_iters);
   }

@@ -266,18 +266,19 @@ def test_phasing_random(dev, n, seed):
     assert np.array_equal(imp, np.array(ei).reshape(-1))
 
 
-@pytest.mark.parametrize("weighted,maxlen,legacy,paired", [
-    (False, 6, False, False), (True, 6, False, False), (True, 14, False, False), (False, 40, False, False),
-    (True, 40, False, False), (True, 14, True, False), (False, 6, False, True), (True, 14, False, True),
-    (True, 40, False, True)])
-def test_phasing_kernel_variants(dev, weighted, maxlen, legacy, paired):
+@pytest.mark.parametrize("weighted,maxlen,legacy,paired,n", [
+    (False, 6, False, False, 700), (True, 6, False, False, 700), (True, 14, False, False, 700),
+    (False, 40, False, False, 700), (True, 40, False, False, 700), (True, 14, True, False, 700),
+    (False, 6, False, True, 700), (True, 14, False, True, 700), (True, 40, False, True, 700),
+    (False, 6, False, False, 6000), (True, 40, False, False, 6000), (True, 14, False, True, 6000)])
+def test_phasing_kernel_variants(dev, weighted, maxlen, legacy, paired, n):
     """Register capacities 8/16, unit and general weights, lists longer than
     the packed capacity (CSR loop), the legacy kernel and the paired-lane
     register kernel (the default splits a sample's haplotypes over two
-    lanes), vs the oracle."""
+    lanes), vs the oracle.  n = 6000 does not fit LDS: the default runs the
+    split kernel with hap in global memory, paired the global k_phase."""
     from grid_amd import engine
-    rng = np.random.default_rng(maxlen * 2 + weighted)
-    n = 700
+    rng = np.random.default_rng(maxlen * 2 + weighted + n)
     irr = rng.uniform(0.1, 4.0, n)
     irr[3] = np.nan
     hn = []
