@@ -598,7 +598,10 @@ __device__ __forceinline__ void ph2_run(int64_t n, const double *__restrict__ ir
           upd = true;
         }
       }
-      wg_barrier<!GLB>();
+      // every gathered value has been waited for (the pins above), so the
+      // read barrier needs no vmcnt wait even with hap in global memory: the
+      // next chunk's prefetch stays in flight across it
+      wg_barrier<true>();
       if (upd) hap[2 * cur.i + h] = nv;
       wg_barrier<!GLB>();
     };

@@ -313,7 +313,10 @@ int grid_dipcn(grid_ctx *ctx, int64_t n, const double *d_reads, const uint8_t *d
  * as a level schedule (grid_hi_levels) that is bit-identical to the
  * sequential order.  Outputs hap[2n] (NaN = unphased), imp[2n], *h_mean.
  * grid_hi_phase flags: GRID_HI_UNIT_WEIGHTS when every weight is 1.0;
- * max_list = longest list (selects the register capacity of the kernel). */
+ * max_list = longest list (selects the register capacity of the kernel).
+ * Default kernel: one workgroup of 512 lanes, one haplotype per lane, with hap
+ * in LDS while 3n doubles fit (about 4,800 samples) and in d_hap otherwise.
+ * Every flag selects a kernel with the same results. */
 int grid_hi_levels(int64_t n, const int64_t *h_off, const int32_t *h_nbr, int32_t *h_order,
                    int32_t *h_level_off, int32_t *h_nlevels);
 /* Host: schedule-ordered packed neighbour lists for the kernel (cap = 16 per
