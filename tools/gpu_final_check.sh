@@ -1,0 +1,7 @@
+set -e
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out/final
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/final/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/final/pytest_gpu.log; exit 1; }
+tail -1 gpurun_out/final/pytest_gpu.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/final/smoke.log 2>&1
+echo smoke ok
