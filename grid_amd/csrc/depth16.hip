@@ -84,7 +84,7 @@ __global__ __launch_bounds__(ET) void k_q16_fill(S src, int64_t m, uint16_t *__r
         if (j0 + k < m) q16[i * ld16 + j0 + k] = cd[k];
     }
     // escapes of this chunk in column order: exclusive scan of per-thread counts
-    const int any = __syncthreads_or(ne);
+    const int any = __builtin_amdgcn_readfirstlane(__syncthreads_or(ne));   // scalar branch (uniform)
     if (!any) continue;
     s_pre[threadIdx.x] = ne;
     __syncthreads();

@@ -225,20 +225,24 @@ __device__ __forceinline__ void ph_run(int64_t n, const double *__restrict__ irr
   __syncthreads();
   if (iters > 0 && nlev > 0) {
     // chunk cursor (level l, base); two register sets A/B alternate so the
-    // next chunk's lists load while the current chunk computes (no copies)
-    int l = 0, base = lo[0];
-    while (base >= lo[l + 1] && l + 1 < nlev) { l++; base = lo[l]; }
+    // next chunk's lists load while the current chunk computes (no copies).
+    // The cursor decides the loop trips around the barriers of step(): its
+    // level offsets are read as scalars (the same address in every lane), so
+    // its branches compile to scalar branches (tools/isa_barriers.py)
+    auto lvl = [&](int k) { return __builtin_amdgcn_readfirstlane(lo[k]); };
+    int l = 0, base = lvl(0);
+    while (base >= lvl(l + 1) && l + 1 < nlev) { l++; base = lvl(l); }
     int64_t it = 0;
     PhItem ia, ib;
     ph_fetch(base + tid, lo[l + 1], order, pk_nbr, pk_w, pk_cnt, ia);
     auto advance = [&](int &cl, int &cb, int64_t &cit) {
       cb += PT;
-      if (cb >= lo[cl + 1]) {
+      if (cb >= lvl(cl + 1)) {
         do {
           cl++;
           if (cl == nlev) { cl = 0; cit++; }
-          cb = lo[cl];
-        } while (cb >= lo[cl + 1]);
+          cb = lvl(cl);
+        } while (cb >= lvl(cl + 1));
       }
     };
     auto step = [&](PhItem &cur) {
@@ -340,7 +344,12 @@ __global__ __launch_bounds__(PT) void k_phase_batch(const grid_hi_locus *__restr
                                                     int64_t iters) {
   extern __shared__ __attribute__((aligned(16))) double s_hap[];
   const grid_hi_locus &L = loci[blockIdx.x];
-  ph_run<USE_LDS>(L.n, L.irr, L.off, L.nbr, L.w, min_nbr, iters, L.order, L.loff, L.nlev, L.pk_nbr, L.pk_w,
+  // the locus sizes bound loops that hold barriers: read them as scalars so
+  // the loop branches are scalar (they are workgroup-uniform; a VGPR-held
+  // bound compiles to EXEC branches around the barriers, tools/isa_barriers.py)
+  const int64_t n = __builtin_amdgcn_readfirstlane((int)L.n);
+  const int32_t nlev = __builtin_amdgcn_readfirstlane(L.nlev);
+  ph_run<USE_LDS>(n, L.irr, L.off, L.nbr, L.w, min_nbr, iters, L.order, L.loff, nlev, L.pk_nbr, L.pk_w,
                   L.pk_cnt, L.hap, L.imp, L.mean, s_hap);
 }
 

@@ -49,36 +49,95 @@ inline const Api &api() {
   return a;
 }
 
+// Growable byte buffer that, unlike std::string::resize, never zero-fills:
+// capacity grows geometrically (realloc), so reserving room for a member
+// costs address space, not a memset of it.
+struct Buf {
+  char *p = nullptr;
+  size_t size = 0, cap = 0;
+  Buf() = default;
+  Buf(const Buf &) = delete;
+  Buf &operator=(const Buf &) = delete;
+  ~Buf() { free(p); }
+  bool reserve(size_t want) {
+    if (want <= cap) return true;
+    size_t c = cap ? cap : 1 << 16;
+    while (c < want) c *= 2;
+    char *q = (char *)realloc(p, c);
+    if (!q) return false;
+    p = q;
+    cap = c;
+    return true;
+  }
+  void release() {
+    free(p);
+    p = nullptr;
+    size = cap = 0;
+  }
+};
+
+// Inflated size of the gzip member at in[0, n) when its header says it (BGZF:
+// the "BC" extra subfield gives the member length, so ISIZE is the member's
+// last 4 bytes; mosdepth writes BGZF), or when the member is the whole rest of
+// the input (its ISIZE is in[n-4]); 0 = unknown.
+inline size_t member_isize(const unsigned char *in, size_t n, bool last_member_guess) {
+  if (n >= 18 && in[0] == 0x1f && in[1] == 0x8b && (in[3] & 4)) {      // FEXTRA
+    const size_t xlen = (size_t)in[10] | ((size_t)in[11] << 8);
+    size_t k = 12;
+    const size_t xe = 12 + xlen;
+    while (xe <= n && k + 4 <= xe) {
+      const size_t sl = (size_t)in[k + 2] | ((size_t)in[k + 3] << 8);
+      if (in[k] == 'B' && in[k + 1] == 'C' && sl == 2 && k + 6 <= xe) {
+        const size_t bsize = ((size_t)in[k + 4] | ((size_t)in[k + 5] << 8)) + 1;
+        if (bsize >= 18 + xlen && bsize <= n) {
+          uint32_t isz = 0;
+          memcpy(&isz, in + bsize - 4, 4);
+          return (size_t)isz;
+        }
+        break;
+      }
+      k += 4 + sl;
+    }
+  }
+  if (last_member_guess && n >= 18) {
+    uint32_t isz = 0;
+    memcpy(&isz, in + n - 4, 4);
+    return (size_t)isz;
+  }
+  return 0;
+}
+
 // Decode EVERY gzip member of in[0, n) into out (replaced).  true only when
 // all bytes form complete, CRC-checked members; anything else (corrupt,
 // truncated, trailing bytes, no library) returns false and the caller uses zlib.
-inline bool gunzip_all(const unsigned char *in, size_t n, std::string &out) {
+// Each member's output room comes from its own size (BGZF header, or the file
+// trailer for the first member), else 4x its compressed bytes, doubled on
+// LIBDEFLATE_INSUFFICIENT_SPACE; nothing is zero-filled, so a file of many
+// small members (BGZF: 64 KiB each) costs O(output) and not O(members x input).
+inline bool gunzip_all(const unsigned char *in, size_t n, Buf &out) {
   const Api &a = api();
   if (!a.ok || n < 18) return false;
   void *d = a.alloc_d();
   if (!d) return false;
-  out.clear();
+  out.size = 0;
   size_t pos = 0;
   bool good = true;
   while (pos < n) {
-    // ISIZE of a single-member file is its last 4 bytes; otherwise grow
-    uint32_t isz = 0;
-    memcpy(&isz, in + n - 4, 4);
-    size_t cap = pos == 0 ? (size_t)isz + 64 : (n - pos) * 4 + 65536;
-    if (cap < (n - pos) * 2) cap = (n - pos) * 4 + 65536;
+    const size_t rest = n - pos;
+    size_t room = member_isize(in + pos, rest, pos == 0);
+    if (room == 0) room = rest * 4 + 65536;
+    room += 64;
     for (;;) {
-      const size_t base = out.size();
-      out.resize(base + cap);
+      if (!out.reserve(out.size + room)) { good = false; break; }
       size_t used = 0, got = 0;
-      const int rc = a.gzip_dec_ex(d, in + pos, n - pos, &out[base], cap, &used, &got);
+      const int rc = a.gzip_dec_ex(d, in + pos, rest, out.p + out.size, room, &used, &got);
       if (rc == 0) {               // LIBDEFLATE_SUCCESS
-        out.resize(base + got);
+        out.size += got;
         pos += used;
         break;
       }
-      out.resize(base);
-      if (rc == 3 && cap < ((size_t)1 << 40)) {   // LIBDEFLATE_INSUFFICIENT_SPACE
-        cap *= 2;
+      if (rc == 3 && room < ((size_t)1 << 40)) {   // LIBDEFLATE_INSUFFICIENT_SPACE
+        room *= 2;
         continue;
       }
       good = false;

@@ -160,14 +160,36 @@ inline bool has_high_byte(const char *p, size_t n) {
   return (acc & 0x8080808080808080ull) != 0;
 }
 
-// Whole file into out when it is at most 1 GiB (the libdeflate path holds the
-// compressed and inflated bytes at once; bigger files stream through zlib).
-bool read_small_file(const char *path, std::string &out) {
+// Bytes the whole-file fast path may hold at once over all threads (each file:
+// its compressed bytes plus the inflated text).  A file that does not fit the
+// budget (or is over 1 GiB compressed) streams through zlib in 4 MiB pieces.
+constexpr int64_t kWholeFileBudget = (int64_t)8 << 30;
+std::atomic<int64_t> g_whole_inflight{0};
+
+// Reservation of the whole-file budget for one file (released on scope exit).
+struct WholeFileTicket {
+  int64_t bytes = 0;
+  bool take(int64_t b) {
+    if (g_whole_inflight.fetch_add(b) + b > kWholeFileBudget) {
+      g_whole_inflight.fetch_sub(b);
+      return false;
+    }
+    bytes = b;
+    return true;
+  }
+  ~WholeFileTicket() {
+    if (bytes) g_whole_inflight.fetch_sub(bytes);
+  }
+};
+
+// Whole file into out when it is at most 1 GiB and the budget above admits
+// it with `expand` x its size of inflated text.
+bool read_small_file(const char *path, std::string &out, WholeFileTicket &ticket, int64_t expand) {
   FILE *f = fopen(path, "rb");
   if (!f) return false;
   bool ok = fseek(f, 0, SEEK_END) == 0;
   const long n = ok ? ftell(f) : -1;
-  ok = ok && n > 0 && n <= (1L << 30) && fseek(f, 0, SEEK_SET) == 0;
+  ok = ok && n > 0 && n <= (1L << 30) && ticket.take((int64_t)n * (1 + expand)) && fseek(f, 0, SEEK_SET) == 0;
   if (ok) {
     out.resize((size_t)n);
     ok = fread(&out[0], 1, (size_t)n, f) == (size_t)n;
@@ -332,19 +354,20 @@ void parse_file(const char *path, const Opts &o, std::vector<Rec> &rec, FileRecs
   // hold) falls through to the streaming zlib reader, which decides the verdict.
   {
     std::string whole;
-    if (read_small_file(path, whole)) {
-      std::string text;
+    WholeFileTicket ticket;
+    if (read_small_file(path, whole, ticket, 4)) {
+      fastgz::Buf text;
       if (fastgz::gunzip_all((const unsigned char *)whole.data(), whole.size(), text)) {
         std::string().swap(whole);
         // Python decodes the whole file as UTF-8 text: a byte >= 0x80 anywhere
         // (even in a line the chromosome filter skips) leaves the fast path
-        if (has_high_byte(text.data(), text.size())) {
+        if (has_high_byte(text.p, text.size)) {
           fr.status = FS_EXOTIC;
           fr.why = "non-ASCII byte";
           return;
         }
-        char *p = text.empty() ? nullptr : &text[0];
-        lines(p, p + text.size(), true);
+        char *p = text.size ? text.p : nullptr;
+        lines(p, p + text.size, true);
         return;
       }
     }

@@ -1051,13 +1051,29 @@ __global__ __launch_bounds__(512, 1) void k_gram8(const uint16_t *__restrict__ z
       if constexpr (LAY == 2) g8h_run<MODE, BL, FL>(z, ld, I, tj, s0, s1, smem, acc, iacc);
       else if constexpr (LAY == 3) g8h_run<MODE, BL, FL, BL>(z, ld, I, tj, s0, s1, smem, acc, iacc);
       else g8_run<MODE, BL, FL, LAY == 1>(z, ld, I, tj, s0, s1, smem, acc, iacc);
-      if (part) g8_store_part<2>(iacc, part + (xoff.x[xcd] + u) * (int64_t)(BM3 * BN3));
-      else g6_atomics<2>(iacc, I, tj, np_, gram);
+      if constexpr (MODE == 9) {
+        // no-flush ISA probe (compile-only, tools/isa_barriers.py --probe): the
+        // tile's results are dropped, so every MFMA is dead code
+      } else if (part) {
+        g8_store_part<2>(iacc, part + (xoff.x[xcd] + u) * (int64_t)(BM3 * BN3));
+      } else {
+        g6_atomics<2>(iacc, I, tj, np_, gram);
+      }
     }
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_fetch_add(rounds + xcd * 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
+
+#ifdef GRID_ISA_PROBE
+// Compile-only (never linked into a library): the round-2 no-flush timing probe
+// of the half-split ring, rebuilt so its ISA can be compared with production
+// k_gram8<0, true, 1, 3> (tools/isa_barriers.py --probe).
+template __global__ void k_gram8<9, true, 1, 3>(const uint16_t *__restrict__, int64_t, const int32_t *__restrict__,
+                                                int, int, int, int64_t, int, int, int64_t,
+                                                unsigned long long *__restrict__, unsigned *__restrict__, int,
+                                                int32_t *__restrict__, GramXoff);
+#endif
 
 // ---- symmetric completion and row access ------------------------------------
 // The Gram kernels write the upper 128-tiles only.  k_mirror fills every 64x64

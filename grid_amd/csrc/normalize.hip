@@ -168,7 +168,10 @@ __global__ __launch_bounds__(256) void k_row_blocks16(Q16 s16, int64_t ld, int64
     }
     // blocks without a missing cell or an escape (the common case) read the
     // codes as plain hundredths
-    if (__builtin_expect(!__syncthreads_or(special), 1)) {
+    // __syncthreads_or is workgroup-uniform but returns a VGPR value;
+    // readfirstlane makes the branch scalar, so no wave can skip the
+    // barriers of either side (tools/isa_barriers.py)
+    if (__builtin_expect(!__builtin_amdgcn_readfirstlane(__syncthreads_or(special)), 1)) {
       rb_finish(s_q, [](uint16_t c, int) { return div100_exact((int32_t)c); }, s_leaf, s_cnt, cnt, row, b, nblk,
                 bsum, bcnt);
     } else {

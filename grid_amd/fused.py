@@ -590,6 +590,10 @@ class Steps47:
                 sel_c = (self.sel[s0:s1] - a).to(self.sel.dtype)
                 cmv = self.colmap[s0:s1]
                 cm_c = self.A.torch.where(cmv >= 0, cmv - kb[ci], cmv).to(self.colmap.dtype)
+            # what on_z_chunk may inspect: the chunk's depth buffer, its
+            # chunk-local selection / panel map, and the panel columns it fills
+            self.cur = {"ci": ci, "a": a, "b": b, "s0": s0, "s1": s1, "q": qc, "ld": ldc, "sel": sel_c,
+                        "colmap": cm_c, "k0": kb[ci], "used": used}
             self._zquant(q, qc, ldc, a, b, s0, s1, sel_c, cm_c)
             if used == 0 or n == 0:
                 continue
@@ -688,7 +692,11 @@ class Steps47:
         else:
             zcol, ld_zq = 0, rc
         if self.zq_is16 and (isinstance(q, Depth16) or ldc % 4 == 0):
-            e0 = self.nesc
+            # keep_z: the escapes of every chunk accumulate (flat indices into
+            # the whole output); streamed: each chunk's list is consumed by
+            # on_z_chunk before the next, so every chunk starts at 0 and the
+            # capacity (sized for one chunk's cells) applies per chunk
+            e0 = self.nesc if self.keep_z else 0
             cap = self.esc_idx.numel() - e0
             zt = self.zq16.view(-1)[zcol:]
             of, ne = o.zquant16(qc, n, ldc, sel_c, rc, self.rm, mu_c, self.scale, zt, ld_zq, cm_c, self.qmax, self.zb,
@@ -703,7 +711,7 @@ class Steps47:
                     self.on_z_chunk(self.zq16, ld_zq, s0, s1, self.esc_idx[e0:e0 + ne], self.esc_val[e0:e0 + ne])
                 return
             if self.nch > 1:
-                raise _abi.GridNativeError(f"more than {cap} int16 escapes (|z| > 327.65) in one chunk")
+                raise _abi.GridNativeError(f"more than {cap} int16 escapes (|z| > 327.65) in chunk [{s0}, {s1})")
         self.zq_is16 = False            # int32 output: no int16 codes (unaligned input, or too many escapes)
         if self.zq is None:
             self.zq = self.A.empty(tuple(self.zq16.shape), I4)

@@ -55,128 +55,7 @@ from grid.utils import hi_inference as ref_hi  # noqa: E402
 CONSOLE = Console(theme=grid.cli.grid_theme, quiet=True)
 
 
-# ------------------------------------------------------------ synthesis ----
-def synth_cohort(rng, n, m, n_clusters, bin_size=1000, start0=0):
-    """Depth hundredths (n x m) with per-bin base depth, cluster offsets,
-    per-sample scale, CNVs and gamma noise."""
-    base = rng.gamma(20.0, 1.5, size=m)
-    clus = rng.integers(0, n_clusters, size=n)
-    offs = 1.0 + rng.uniform(-0.08, 0.08, size=(n_clusters, m))
-    scale = rng.uniform(0.6, 1.4, size=n)
-    cnv = np.ones((n, m))
-    hit = rng.random((n, m)) < 0.02
-    cnv[hit] = rng.choice([0.5, 1.5], size=hit.sum())
-    lam = base[None, :] * offs[clus] * scale[:, None] * cnv
-    noise = rng.gamma(40.0, 1.0 / 40.0, size=(n, m))
-    q = np.maximum(0, np.rint(lam * noise * 100)).astype(np.int64)
-    starts = start0 + np.arange(m) * bin_size
-    return q, starts, clus
-
-
-def write_bed(path, chrom_rows):
-    with gzip.open(path, "wt") as f:
-        for chrom, s, e, q in chrom_rows:
-            f.write(f"{chrom}\t{s}\t{e}\t{q // 100}.{q % 100:02d}\n")
-
-
-def make_file_cohort(root: Path, rng, n, m, chrom, window=None, decoys=True,
-                     bin_size=1000, start0=0, n_clusters=4):
-    root.mkdir(parents=True, exist_ok=True)
-    md = root / "mosdepth"
-    md.mkdir(exist_ok=True)
-    q, starts, clus = synth_cohort(rng, n, m, n_clusters, bin_size, start0)
-    ids = [f"S{i:04d}" for i in range(n)]
-    for i, sid in enumerate(ids):
-        rows = []
-        if decoys:
-            # chr10 lines: start with "chr1" -> kept by the startswith filter
-            # (reference quirk Q2); first 30 collide with chr1 coordinates
-            # (last-wins, Q1), the rest are new coordinates.
-            for b in range(30):
-                rows.append(("chr10", int(starts[b]), int(starts[b] + bin_size), int(q[i, b] // 2 + 150)))
-            for b in range(3):
-                s = int(starts[-1] + (b + 5) * bin_size)
-                rows.append(("chr10", s, s + bin_size, int(3000 + 7 * i + b)))
-            rows.append(("chr2", 0, bin_size, 5000))
-        for b in range(m):
-            rows.append((chrom, int(starts[b]), int(starts[b] + bin_size), int(q[i, b])))
-        # a malformed line (skipped by the reference: < 4 fields)
-        rows_txt = rows
-        name = f"{sid}_LPA.regions.bed.gz" if i % 3 else f"{sid}.regions.bed.gz"
-        write_bed(md / name, rows_txt)
-    # a stray file for a sample not in the list
-    write_bed(md / "ZZ9999_LPA.regions.bed.gz", [(chrom, int(starts[0]), int(starts[0] + bin_size), 4000)])
-    # sample list: all + one with no file
-    (root / "samples.txt").write_text("\n".join(ids + ["S9998"]) + "\n")
-    # repeat mask: a handful of intervals, chrom without 'chr' prefix for one
-    lines = ["# repeat mask", ""]
-    for b in rng.choice(m, size=max(1, m // 40), replace=False):
-        s = int(starts[b]) + 200
-        lines.append(f"{chrom}\t{s}\t{s + 300}\tAluY")
-    lines.append(f"{chrom.replace('chr', '')}\t{int(starts[min(7, m-1)])}\t{int(starts[min(7, m-1)]) + 10}")
-    lines.append("chrX\t1")
-    (root / "mask.bed").write_text("\n".join(lines) + "\n")
-    # read counts (count_reads format, header replaced by pandas names=)
-    cnt = ["Sample\tchr6:1-2"]
-    for i, sid in enumerate(ids):
-        if i == 3:
-            cnt.append(f"{sid}\tError")
-            continue
-        if i == 5:
-            continue
-        cn = rng.choice([1.0, 1.5, 2.0, 2.5])
-        cnt.append(f"{sid}\t{int(rng.poisson(cn * 400 * (0.6 + (i % 7) * 0.1)))}")
-    (root / "counts.tsv").write_text("\n".join(cnt) + "\n")
-    # IBS (computeIBSpbwt) neighbours: header + ID hap nbrInd cMlen cMedge IDnbr hapNbr
-    ibs = ["ID\thap\tnbrInd\tcMlen\tcMedge\tIDnbr\thapNbr"]
-    for i, sid in enumerate(ids):
-        same = [j for j in range(n) if clus[j] == clus[i]]
-        for hap in (1, 2):
-            k = int(rng.integers(0, 14))
-            for t in range(k):
-                j = int(rng.choice(same))
-                ibs.append(f"{sid}\t{hap}\t{j}\t{rng.uniform(0.5, 9):.3f}\t0.1\t{ids[j]}\t{int(rng.integers(1, 3))}")
-        if i % 9 == 0:
-            ibs.append(f"{sid}\t3\t0\t1.0\t0.1\t{ids[0]}\t1")       # invalid hap
-            ibs.append(f"{sid}\t1\t0\t1.0\t0.1\tNOPE\t1")           # unknown id
-            ibs.append(f"{sid}\t1\t0\t1.0")                          # short line
-    with gzip.open(root / "ibs.tsv.gz", "wt") as f:
-        f.write("\n".join(ibs) + "\n")
-    # IBD (iLASH): FID1 HAP_ID1 FID2 HAP_ID2 CHR BP1 BP2 SNP_BP1 SNP_BP2 LENGTH MATCH
-    ibd = []
-    for t in range(n * 8):
-        i, j = int(rng.integers(0, n)), int(rng.integers(0, n))
-        h1, h2 = int(rng.integers(0, 2)), int(rng.integers(0, 2))
-        bp1 = int(rng.integers(0, 4_000_000))
-        bp2 = bp1 + int(rng.integers(1000, 3_000_000))
-        ibd.append(f"{ids[i]}\t{ids[i]}_{h1}\t{ids[j]}\t{ids[j]}_{h2}\t6\t{bp1}\t{bp2}\t{bp1}\t{bp2}"
-                   f"\t{rng.uniform(0.2, 12):.4f}\t{rng.uniform(0.5, 1.0):.3f}")
-    (root / "ibd.txt").write_text("\n".join(ibd) + "\n")
-    cfg = {
-        "samples_file": str(root / "samples.txt"),
-        "output_dir": str(root / "out"),
-        "threads": 1,
-        "chrom": chrom,
-        "output_file_type": "tsv",
-        "index": {"run": False},
-        "count_reads": {"run": False, "output_file_prefix": "counts"},
-        "mosdepth": {
-            "run": False,
-            "work_dir": str(md),
-            "remove_intermediate": False,
-            "normalize": {"run": True, "min_depth": 20, "max_depth": 100, "top_frac": 0.1,
-                          "output_file_prefix": "normalized", "repeat_mask_file": str(root / "mask.bed")},
-            "neighbors": {"run": True, "output_file_prefix": "neighbors", "num_neighbors": 5,
-                          "zmax": 2.0, "sigma2_max": 1000},
-        },
-        "compute_diploid_genotypes": {"run": True, "output_file_prefix": "dipcn", "n_nbr": 4},
-        "compute_haploid_genotypes": {"run": True, "output_file_prefix": "haploid", "method": "ibs",
-                                      "min_neighbors": 1, "max_neighbors": 10, "n_iters": 100,
-                                      "ibs_output": str(root / "ibs.tsv.gz")},
-    }
-    if window:
-        cfg["start_bp"], cfg["end_bp"] = window
-    return cfg
+from cohort_files import inputs_digest, make_file_cohort  # noqa: E402
 
 
 def run_reference(cfg, root: Path):
@@ -267,6 +146,49 @@ def file_cohort(name, seed, n, m, chrom, window=None, decoys=True, start0=0, bin
             print(f"{name}: ok (seed attempt {attempt})")
             return
         shutil.rmtree(tmp)
+    raise RuntimeError(f"{name}: could not make a tie-free cohort")
+
+
+def config1_cohort():
+    """BASELINE config 1: 100 samples x 30k bins (1 kb), k = 10, the reference's
+    CPU path.  The inputs (100 mosdepth files, ~3M lines) are regenerated by
+    the test from the recorded seed (tests/golden/cohort_files.py) and checked
+    against the recorded input digest; the small outputs are stored whole, the
+    normalised matrix as the sha256 + length of its decompressed text."""
+    import hashlib
+    name = "g_cfg1"
+    for attempt in range(20):
+        seed = 101 + 1000 * attempt
+        rng = np.random.default_rng(seed)
+        tmp = Path(tempfile.mkdtemp(prefix=f"golden_{name}_"))
+        cfg = make_file_cohort(tmp, rng, 100, 30_000, "chr1", decoys=True)
+        cfg["mosdepth"]["neighbors"]["num_neighbors"] = 10
+        cfg["compute_diploid_genotypes"]["n_nbr"] = 10
+        cfg_ibd = run_reference(cfg, tmp)
+        out = Path(cfg["output_dir"])
+        if not check_tie_free(out / "normalized.tsv.gz", 10, 2.0, 1000):
+            shutil.rmtree(tmp)
+            continue
+        dst = HERE / name
+        if dst.exists():
+            shutil.rmtree(dst)
+        (dst / "expected").mkdir(parents=True)
+        for f in out.iterdir():
+            if f.name != "normalized.tsv.gz":
+                shutil.copy(f, dst / "expected" / f.name)
+        text = gzip.decompress((out / "normalized.tsv.gz").read_bytes())
+        meta = {"seed": seed, "n": 100, "m": 30_000, "chrom": "chr1", "decoys": True, "k": 10,
+                "inputs_sha256": inputs_digest(tmp),
+                "normalized_sha256": hashlib.sha256(text).hexdigest(), "normalized_bytes": len(text),
+                "normalized_head": text[:2000].decode()}
+        (dst / "cohort.json").write_text(json.dumps(meta, indent=1))
+        # configs with paths relative to the regenerated cohort root
+        for fname, c in (("config.yaml", cfg), ("config_ibd.yaml", cfg_ibd)):
+            c = json.loads(json.dumps(c).replace(str(tmp) + "/", ""))
+            (dst / fname).write_text(yaml.safe_dump(c, sort_keys=False))
+        shutil.rmtree(tmp)
+        print(f"{name}: ok (seed {seed})")
+        return
     raise RuntimeError(f"{name}: could not make a tie-free cohort")
 
 
@@ -367,6 +289,9 @@ def main():
     import sklearn
     import pandas
     os.environ.setdefault("OMP_NUM_THREADS", "1")
+    if sys.argv[1:] == ["cfg1"]:
+        config1_cohort()
+        return
     file_cohort("g1", 11, 40, 2400, "chr1", decoys=True)
     file_cohort("g1b", 21, 10, 8600, "chr1", decoys=False)
     file_cohort("g1c", 31, 30, 60, "chr6", window=(160_605_062, 160_647_661), decoys=False,

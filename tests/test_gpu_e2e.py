@@ -94,3 +94,20 @@ def test_api_functions_match_oracle():
     hap, mean = hi._run_phasing(irr, hn, 1, 30)
     eh, em = steps.run_phasing(irr, hn, 1, 30)
     assert np.array_equal(np.array(hap), np.array(eh), equal_nan=True) and mean == em
+
+
+def test_config1_100x30k_matches_reference(tmp_path):
+    """BASELINE config 1 (100 samples x 30k bins, k = 10): the cohort is
+    regenerated from the golden's recorded seed (input digest checked) and
+    `grid wgs` steps 4-7 must give the reference's files (make_golden.py
+    cfg1): small outputs byte for byte after gunzip, the 13.7 MB normalised
+    matrix by its sha256."""
+    from grid_amd.pipeline import run_wgs_pipeline
+    from grid_amd.utils.hi_inference import hi_inference
+    from tests.golden import cohort_files
+    cfg, cfg_ibd, _ = cohort_files.regenerate("g_cfg1", tmp_path)
+    p = tmp_path / "config.yaml"
+    p.write_text(yaml.safe_dump(cfg))
+    run_wgs_pipeline(console=None, config=str(p))
+    hi_inference(cfg_ibd, None)                     # the golden's second step-7 run: IBD, weighted
+    cohort_files.check_outputs("g_cfg1", tmp_path / "out")

@@ -247,3 +247,47 @@ def test_libdeflate_and_zlib_paths_agree(tmp_path):
     subprocess.run([sys.executable, "-c", _ZLIB_ONLY, str(out), *paths], check=True, env=env,
                    cwd=os.path.dirname(os.path.dirname(__file__)))
     assert np.array_equal(fast, np.load(out))
+
+
+def _bgzf(data: bytes, block=65280):
+    """BGZF (what mosdepth writes, via htslib): gzip members of <= 64 KiB of
+    text, each with the "BC" extra subfield holding its length - 1, then the
+    28-byte empty EOF member."""
+    import struct
+    import zlib
+    out = bytearray()
+    for a in range(0, len(data), block):
+        chunk = data[a:a + block]
+        c = zlib.compressobj(6, zlib.DEFLATED, -15)
+        body = c.compress(chunk) + c.flush()
+        bsize = 12 + 6 + len(body) + 8
+        out += bytes([0x1F, 0x8B, 8, 4, 0, 0, 0, 0, 0, 0xFF]) + struct.pack("<H", 6)
+        out += b"BC" + struct.pack("<HH", 2, bsize - 1) + body
+        out += struct.pack("<II", zlib.crc32(chunk) & 0xFFFFFFFF, len(chunk))
+    out += bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+    return bytes(out)
+
+
+def test_bgzf_many_members_linear_time(tmp_path):
+    """A real mosdepth file is BGZF: thousands of 64 KiB members and an empty
+    EOF member last (ISIZE 0).  The whole-file inflate sizes each member from
+    its own BSIZE/ISIZE (fastgz.hpp member_isize), so the cost stays linear in
+    the text (the old sizing zero-filled 4x the rest of the file per
+    member, quadratic).  Same matrix as the line-by-line restatement."""
+    import time
+    rng = np.random.default_rng(11)
+    d = tmp_path / "md"
+    d.mkdir()
+    names = ["P1", "P2", "P3"]
+    for s in names:
+        (d / f"{s}.regions.bed.gz").write_bytes(_bgzf("".join(_rand_lines(rng, 120_000)).encode()))
+    assert (d / "P1.regions.bed.gz").stat().st_size > 600_000        # ~50 members per file
+    t0 = time.perf_counter()
+    a, b = _both(d, names, threads=3)
+    _same(a, b)
+    paths = [str(d / f"{s}.regions.bed.gz") for s in names]
+    t1 = time.perf_counter()
+    ing = _abi.Ingest(paths, None, None, {}, 20, 100, threads=1)
+    assert list(ing.status) == [0, 0, 0] and ing.m > 50_000
+    assert time.perf_counter() - t1 < 5.0, "BGZF inflate is not linear"
+    assert t1 - t0 < 120
