@@ -129,6 +129,53 @@ def cpu_baseline(q_host, n_total, m_total, k, n_iters, seed=SEED):
                        f"(extrapolated; host memory bounds the reference well below this shape)")}
 
 
+def cpu_baseline_from_files(n_target, m_target, k, n_iters):
+    """The reference's whole step cost, file to file: the oracle's steps 4-7
+    (oracle/pipeline.py: mosdepth gzip parse, normalize_matrix, "%.2f"/"%.3f"
+    text into gzip level 9, re-read and parse in step 5, exact k-NN, dipCN,
+    phasing), measured on BASELINE config 1 (100 samples x 30k bins, k=10;
+    the cohort regenerated from tests/golden/g_cfg1's seed) on this host's
+    cores, then each stage scaled by its complexity to n_target x m_target:
+    parse / normalise / text write / text read by cells (n m, selected
+    columns ~ m), k-NN by n^2 m, dipCN and the neighbour file by n, phasing by
+    n x n_iters / 100."""
+    import shutil
+    import tempfile
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from oracle import pipeline
+    from tests.golden import cohort_files
+    tmp = tempfile.mkdtemp(prefix="grid_cfg1_")
+    try:
+        t0 = time.perf_counter()
+        cfg, _, meta = cohort_files.regenerate("g_cfg1", tmp)
+        gen = time.perf_counter() - t0
+        t = pipeline.run(cfg)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    shape = t.pop("shape")
+    n1, m1 = meta["n"], meta["m"]
+    cells = (n_target * m_target) / (n1 * m1)
+    knn = (n_target / n1) ** 2 * (m_target / m1)
+    lin = n_target / n1
+    scale = {"ingest": cells, "normalize": cells, "write_normalized": cells, "read_normalized": cells,
+             "knn": knn, "write_neighbors": lin, "dipcn": lin, "load_hap_neighbors": lin,
+             "phasing": lin * n_iters / 100.0, "write_haploid": lin}
+    total1 = sum(t.values())
+    est = {kk: v * scale[kk] for kk, v in t.items()}
+    total = sum(est.values())
+    return {"config1_measured": {"samples": n1, "bins": m1, "k": meta["k"], "stages_s": {kk: round(v, 3) for kk, v
+            in t.items()}, "total_s": total1, "samples_per_s": n1 / total1, "shape": shape,
+            "cohort_generation_s": gen},
+            "extrapolated": {"samples": n_target, "bins": m_target, "total_s": total,
+                             "samples_per_s": n_target / total,
+                             "stages_s": {kk: round(v, 1) for kk, v in est.items()},
+                             "note": "config-1 stage times scaled by complexity; the reference's fp64 matrix "
+                                     "(8 B/cell) exceeds host memory well before this shape"},
+            "cores": 1, "kind": "port",
+            "sample": "oracle/pipeline.py steps 4-7 from mosdepth files to output files at BASELINE config 1 "
+                      "(single-threaded Python/NumPy, as the reference runs with threads=1)"}
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -176,6 +223,8 @@ def main():
     ap.add_argument("--cpu-samples", type=int, default=4096)
     ap.add_argument("--cpu-bins", type=int, default=16384)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-files-baseline", action="store_true",
+                    help="skip the from-files oracle run at config 1 (~1 min of host time)")
     ap.add_argument("--no-overlap", action="store_true", help="run step 7 inline on the main stream")
     ap.add_argument("--traffic-json", default=TRAFFIC_JSON,
                     help="rocprofv3 PMC summary (tools/pmc_traffic.py) of this same command, for roofline.traffic")
@@ -353,6 +402,9 @@ def main():
         qh = qs.cpu().numpy()
         del qs
         out["cpu_baseline"] = cpu_baseline(qh, n, m, args.k, args.n_iters)
+        if not args.no_files_baseline:
+            note("cpu baseline: the oracle from files at config 1")
+            out["cpu_baseline"]["from_files"] = cpu_baseline_from_files(n, m, args.k, args.n_iters)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

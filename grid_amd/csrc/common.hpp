@@ -1,5 +1,15 @@
 // Shared helpers for libgridhip.so (gfx950).  Not part of the ABI.
 #pragma once
+
+// A/B selectors that change a kernel, a layout or a schedule (timing
+// experiments): read only in the tools build (make probes, -DGRID_PROBES); the
+// product library sees them unset and carries no such name (tests/test_abi_cpu.py
+// enforces the list of the remaining, result-neutral knobs).
+#ifdef GRID_PROBES
+#define GRID_AB_KNOB(name) getenv(name)
+#else
+#define GRID_AB_KNOB(name) ((const char *)nullptr)
+#endif
 #include <hip/hip_runtime.h>
 
 #include <cmath>

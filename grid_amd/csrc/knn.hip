@@ -1447,7 +1447,7 @@ static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_
   // CU: ~25-50 us, i.e. tens of K-steps -- without it, short K ranges were cut
   // into hundreds of units and the flushes doubled the launch); the fewest
   // K-ranges within 1 % of the best cost, then the chunk count that wastes least
-  const char *ufe = getenv("GRID_GRAM_UF");
+  const char *ufe = GRID_AB_KNOB("GRID_GRAM_UF");
   const double UF = ufe ? atof(ufe) : 40.0;
   int64_t bkx = 8, bkc = 1;
   double bcost = -1.0;
@@ -1478,7 +1478,7 @@ static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_
   const char *le = getenv("GRID_GRAM_LAG"), *se = getenv("GRID_GRAM_SPIN"), *ke = getenv("GRID_GRAM_KC");
   const char *xe = getenv("GRID_GRAM_KX");
   const int lag = le ? atoi(le) : 1, spin = se ? atoi(se) : 20000;
-  const char *dye = getenv("GRID_GRAM_DYN");      // units from a per-XCD counter (1) or fixed per workgroup (0)
+  const char *dye = GRID_AB_KNOB("GRID_GRAM_DYN");      // units from a per-XCD counter (1) or fixed per workgroup (0)
   const int dyn = dye ? atoi(dye) != 0 : 1;
   if (xe && (atoi(xe) == 1 || atoi(xe) == 2 || atoi(xe) == 4 || atoi(xe) == 8)) {
     bkx = atoi(xe);
@@ -1502,7 +1502,7 @@ static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_
   // LDS image.  K-blocked panel ([kpad/KBW][np][KBW], KBW = 32): the half-split
   // ring (LAY 3).  Row-major panel (timing A/B, results identical): 1 quad-row
   // pieces (default), 2 half-split ring, 0 the earlier pair-row pieces (GRID_GRAM_QL)
-  const char *qe = getenv("GRID_GRAM_QL");
+  const char *qe = GRID_AB_KNOB("GRID_GRAM_QL");
   const int lay = qe ? atoi(qe) : 1;
   REQUIRE(lay >= 0 && lay <= 2, "GRID_GRAM_QL must be 0, 1 or 2");
   static_assert(KBW == BK / 2, "k_gram8's K-blocked path reads 32-wide K-blocks");
@@ -1512,7 +1512,7 @@ static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_
   // partial mode (GRID_GRAM_PART_MB > 0: while the slots fit that many MiB; off by default): plain
   // int32 stores of each unit's tile into its own slot, one reduction launch
   // after the Gram, in place of the int64 atomics (the atomics were not what bounds the Gram)
-  const char *pme = getenv("GRID_GRAM_PART_MB");
+  const char *pme = GRID_AB_KNOB("GRID_GRAM_PART_MB");
   const int64_t part_cap = (int64_t)(pme ? atof(pme) : 0.0) << 20;   // measured slower: 29.3 vs 28.3 ms at config 2
   int32_t *d_part = nullptr;
   GramXoff xoff{};

@@ -1715,7 +1715,7 @@ static int row_blocks_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, in
     const char *rn = getenv("GRID_ROWBLK_NT");
     const bool nt = rn ? atoi(rn) != 0 : ROWBLK_NT;
     if (c16) {
-      const char *pe = getenv("GRID_ROWBLK16_PB");
+      const char *pe = GRID_AB_KNOB("GRID_ROWBLK16_PB");
       const int pb = pe ? atoi(pe) : RB16_PB;
       REQUIRE(pb == 1 || pb == 2 || pb == 4, "GRID_ROWBLK16_PB must be 1, 2 or 4 (got %d)", pb);
       auto kern = pb == 1 ? (nt ? k_row_blocks16<1, true> : k_row_blocks16<1, false>)
@@ -1895,20 +1895,20 @@ static int col_stats_impl(grid_ctx *ctx, bool vars, const int32_t *d_q, const Q1
   // resident waves; 4 per thread left a 2.3-round tail: 14.5 vs 13.7 ms)
 #ifdef GRID_PROBES
   // tools build only: column-width / workgroup-shape alternatives (A/B)
-  const char *cv = getenv("GRID_COL_VW"), *cu = getenv("GRID_COL_CU");
+  const char *cv = GRID_AB_KNOB("GRID_COL_VW"), *cu = GRID_AB_KNOB("GRID_COL_CU");
   const int want = cv ? atoi(cv) : 1;
   const bool cu16 = cu && atoi(cu) == 16;
 #else
   const int want = 1;
-  const char *cu = getenv("GRID_COL16_CU");   // compact codes: 16 rows in flight (timing only)
+  const char *cu = GRID_AB_KNOB("GRID_COL16_CU");   // compact codes: 16 rows in flight (timing only)
   const bool cu16 = s16.q && cu && atoi(cu) == 16;
 #endif
-  const char *cpf = getenv("GRID_COL_PF");  // software-pipelined row groups, compact 2-column path (A/B)
+  const char *cpf = GRID_AB_KNOB("GRID_COL_PF");  // software-pipelined row groups, compact 2-column path (A/B)
   const bool pf = cpf ? atoi(cpf) != 0 : COL_PF;
   const char *cn = getenv("GRID_COL_NT");   // streaming (nontemporal) loads, 1-column path (A/B)
   const bool nt = cn ? atoi(cn) != 0 : COL_NT;
   // compact codes: GRID_COL16_VW columns per thread (1: 2-B loads, 2: 4-B loads, the default; timing only)
-  const char *c16v = getenv("GRID_COL16_VW");
+  const char *c16v = GRID_AB_KNOB("GRID_COL16_VW");
   const int vw16 = c16v ? atoi(c16v) : COL16_VW;
   REQUIRE(vw16 == 1 || vw16 == 2 || vw16 == 4 || vw16 == 8, "GRID_COL16_VW must be 1, 2, 4 or 8 (got %d)", vw16);
   // 16-B rows (VW 8) need 16-B aligned rows of the compact matrix
@@ -2012,25 +2012,25 @@ static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, int64_
     const dim3 g6((unsigned)ceil_div(n, rpw), (unsigned)ceil_div(ceil_div(ld, 4), 256));
 #define Z6_PICK(ZT, CS) (nt ? (rpw > ZR ? k_zquant6<true, ZT, 1, CS> : k_zquant6<false, ZT, 1, CS>)                    \
                             : (rpw > ZR ? k_zquant6<true, ZT, 0, CS> : k_zquant6<false, ZT, 0, CS>))
-    const char *z7e = getenv("GRID_ZQUANT7");        // compact source, int16 output: 1 (default) = k_zquant7
+    const char *z7e = GRID_AB_KNOB("GRID_ZQUANT7");        // compact source, int16 output: 1 (default) = k_zquant7
     const bool z7 = c16 && d_zq16 && (!z7e || atoi(z7e) != 0);
     if (z7) {
       // k_zquant7 reads overlapping 24-B windows: plain loads (the rows' lines
       // serve neighbouring lanes from L2) unless GRID_ZQUANT_NT=1 (15.7 vs 17.8 ms)
       const bool nt7 = ntv && atoi(ntv) == 1;
       // 16-B loads (GRID_Z7_W16, timing A/B; results identical); needs 16-B aligned operands
-      const char *w16e = getenv("GRID_Z7_W16");
+      const char *w16e = GRID_AB_KNOB("GRID_Z7_W16");
       const bool w16 = (w16e ? atoi(w16e) != 0 : Z7W16) && (ld % 8) == 0 && ((uintptr_t)s16.q % 16) == 0 &&
                        ((uintptr_t)d_sel % 16) == 0 && (!d_colmap || ((uintptr_t)d_colmap % 16) == 0) &&
                        ((uintptr_t)mc32 % 16) == 0;
       // paired 16-B stores (GRID_Z7_PAIR, timing A/B; results identical; with the 16-B loads)
-      const char *pre = getenv("GRID_Z7_PAIR");
+      const char *pre = GRID_AB_KNOB("GRID_Z7_PAIR");
       const int pr7v = pre ? atoi(pre) : (Z7PAIR ? 1 : 0);   // 2: the pair variant at 3 waves/SIMD
       const bool pr7 = pr7v != 0 && w16;
       REQUIRE(ceil_div(ceil_div(r, 4), 256) <= 65535, "r too large for one launch");
       // super-tiles of rgs row groups x cbw column blocks (GRID_Z7_RGS / GRID_Z7_CBW; RGS=0: the 2-D grid,
       // row groups fastest)
-      const char *rge = getenv("GRID_Z7_RGS"), *cbe = getenv("GRID_Z7_CBW");
+      const char *rge = GRID_AB_KNOB("GRID_Z7_RGS"), *cbe = GRID_AB_KNOB("GRID_Z7_CBW");
       const int rgs = rge ? atoi(rge) : Z7RGS, cbw = cbe ? atoi(cbe) : Z7CBW;
       REQUIRE(rgs >= 0 && cbw > 0, "GRID_Z7_RGS must be >= 0 and GRID_Z7_CBW > 0");
       const int64_t nrg7 = ceil_div(n, ZR), ncb7 = ceil_div(ceil_div(r, 4), 256);

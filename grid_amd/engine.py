@@ -203,7 +203,10 @@ def _knn_zq(dev: Device, zq: np.ndarray, cols: np.ndarray, k: int, zmax: float, 
       * otherwise (clips are not hundredths): fixed-order fp64 distances.
     Returns (idx, d2, cnt); d2 is float64 in value^2 units when ``values``,
     else int64 hundredths^2 (integer paths only)."""
-    zq = np.ascontiguousarray(zq, dtype=np.int32)
+    if isinstance(zq, DevBuf):                  # already on the device (step-4 hand-off)
+        assert zq.dtype == np.int32 and len(zq.shape) == 2
+    else:
+        zq = np.ascontiguousarray(zq, dtype=np.int32)
     n, ld = zq.shape
     r = len(cols)
     kk = max(k, 1)
@@ -211,7 +214,7 @@ def _knn_zq(dev: Device, zq: np.ndarray, cols: np.ndarray, k: int, zmax: float, 
         return np.zeros((0, kk), I4), np.zeros((0, kk), F8 if values else I8), np.zeros(0, I4)
     q = int(round(zmax * 100))
     hundredths = q / 100.0 == zmax and 0 <= q < 2 ** 30
-    dz = dev.upload(zq)
+    dz = zq if isinstance(zq, DevBuf) else dev.upload(zq)
     dcols = dev.upload(np.ascontiguousarray(cols if r else np.zeros(1), dtype=I4))
     np_ = pad_to(n, 256)
     if hundredths and q <= 256:
@@ -279,6 +282,16 @@ def knn_values(dev: Device, data: np.ndarray, k: int):
     idx, d2, cnt = dev.alloc((n, kk), I4), dev.alloc((n, kk), F8), dev.alloc(n, I4)
     call("grid_knn_topk_d2", dev.ctx, d2m.ptr, np_, scale, n, k, 0, n, idx.ptr, d2.ptr, cnt.ptr)
     return idx.numpy(), d2.numpy(), cnt.numpy()
+
+
+def round_decimals(dev: Device, v: np.ndarray, decimals: int) -> np.ndarray:
+    """float("%.{decimals}f" % x) for every x (grid_round_decimals; NaN stays NaN)."""
+    v = np.ascontiguousarray(v, dtype=F8)
+    if v.size == 0:
+        return v.copy()
+    d = dev.upload(v)
+    call("grid_round_decimals", dev.ctx, d.ptr, v.size, decimals, d.ptr)
+    return d.numpy()
 
 
 # ------------------------------------------------------------------ step 6 --

@@ -46,6 +46,8 @@ def run_wgs_pipeline(console=False, config=None, **args):
             find_neighbors(cfg, console)
         except Exception as e:
             log(console, f"Failed to find neighbors: {e}", style="danger")
+    from .utils import handoff
+    handoff.clear()                 # step 4's device matrix, if step 5 did not run
 
     if cfg["compute_diploid_genotypes"].get("run") == True:  # noqa: E712
         try:

@@ -22,6 +22,7 @@ import numpy as np
 
 from .. import _abi, engine
 from ..device import get_device
+from . import handoff
 from .utils import log, progress_bar
 
 
@@ -141,14 +142,19 @@ def find_neighbors(config, console):
         return
     output_file.parent.mkdir(parents=True, exist_ok=True)
 
-    ids, scales, zq, ratios = _read_normalized_q(input_file)
+    got = handoff.take(input_file)              # step 4 ran in this process: its matrix, no re-parse
+    if got is not None:
+        ids, sc, ratios, zq, _shape = got
+        scales = {i: float(v) for i, v in zip(ids, sc)}
+    else:
+        ids, scales, zq, ratios = _read_normalized_q(input_file)
     N = len(ids)
     valid, R_use = filter_regions_by_variance(ratios, frac_r=frac_r, sigma2_max=sigma2_max, console=console)
 
     # clip (:57), NaN -> 0 (:58) and the column filter (:171) run on the device
     # over the int32 hundredths (no host copies of the matrix)
     with progress_bar(console, total=N, description="Finding neighbors...") as (progress, task):
-        idx, d2, cnt = engine.knn_from_zq(get_device(config), zq.reshape(N, -1) if N else zq,
+        idx, d2, cnt = engine.knn_from_zq(get_device(config), zq.reshape(N, -1) if N and got is None else zq,
                                           np.asarray(valid, dtype=np.int32), int(n_neighbors), float(zmax))
         progress.advance(task, N)
 

@@ -19,6 +19,7 @@ import numpy as np
 
 from .. import _abi, engine
 from ..device import get_device
+from . import handoff
 from .mosdepth import remove_intermediate_files
 from .utils import get_samples, log, progress_bar, setup_output_file
 
@@ -415,8 +416,15 @@ def normalize_mosdepth(config, console):
         else:
             engine.zquant(dev, qd, n, m, sel, r, st, zq=zq)
     sel_h = sel.numpy()[:r]
-    _write_normalized_q(output_path, ids, st.rowmean.numpy()[:n], st.mu.numpy()[:m][sel_h],
-                        st.var.numpy()[:m][sel_h], zq.numpy()[:, :r])
+    raw = st.rowmean.numpy()[:n]
+    sel_means, sel_vars = st.mu.numpy()[:m][sel_h], st.var.numpy()[:m][sel_h]
+    _write_normalized_q(output_path, ids, raw, sel_means, sel_vars, zq.numpy()[:, :r])
+    # step 5 in this process takes the matrix from here instead of re-parsing
+    # the file (values exactly as the text prints them; handoff.py)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        ratios = np.where(sel_means > 0, 100.0 * sel_vars / sel_means, np.nan)
+    handoff.publish(output_path, ids, engine.round_decimals(dev, raw, 2), engine.round_decimals(dev, ratios, 3),
+                    zq, (n, r))
     log(console, f"Mosdepth normalization complete. Results written to {output_path}", style="success")
     if remove_intermediate:
         remove_intermediate_files(mosdepth_dir, console, include_region_bed_gz=True)

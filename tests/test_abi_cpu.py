@@ -109,3 +109,9 @@ def test_product_library_has_no_probe_selectors():
     # every GRID_* string in the binary is either an allowed knob or a message token, never a probe selector
     assert not (env_like & set(PROBE_SELECTORS))
     assert allowed & env_like                     # the knobs are present (sanity of the scan)
+    # the getenv names themselves (NUL-terminated strings): exactly the tested,
+    # result-neutral knobs (tests/test_gpu_streamed.py::test_performance_knobs_do_not_change_results,
+    # GRID_NO_LIBDEFLATE: tests/test_ingest_cpu.py); every A/B selector reads
+    # through GRID_AB_KNOB, which the product build compiles to "unset"
+    names = set(re.findall(rb"\x00(GRID_[A-Z0-9_]+)\x00", blob))
+    assert names <= allowed | {b"GRID_NO_LIBDEFLATE"}, sorted(names - allowed)

@@ -111,3 +111,29 @@ def test_config1_100x30k_matches_reference(tmp_path):
     run_wgs_pipeline(console=None, config=str(p))
     hi_inference(cfg_ibd, None)                     # the golden's second step-7 run: IBD, weighted
     cohort_files.check_outputs("g_cfg1", tmp_path / "out")
+
+
+def test_step5_handoff_and_reparse_agree(tmp_path):
+    """Steps 4 and 5 in one process: step 5 takes step 4's matrix from the
+    hand-off (grid_amd/utils/handoff.py) instead of re-parsing the file; a
+    step 5 whose file changed since (here: only its mtime) parses the file.
+    Both give the reference's neighbour file."""
+    import time
+    from grid_amd.utils import handoff
+    from grid_amd.utils.find_neighbors import find_neighbors
+    from grid_amd.utils.normalize_mosdepth import normalize_mosdepth
+    c, _ = _stage("g1b", tmp_path)
+    out, exp = c["output_dir"], os.path.join(G, "g1b", "expected")
+    normalize_mosdepth(c, None)
+    norm = os.path.join(out, "normalized.tsv.gz")
+    assert handoff._entries, "step 4 published its matrix"
+    find_neighbors(c, None)                                   # hand-off path
+    assert not handoff._entries
+    nb = "neighbors.zMax2.0.tsv.gz"
+    assert _content(os.path.join(out, nb)) == _content(os.path.join(exp, nb))
+    os.remove(os.path.join(out, nb))
+    normalize_mosdepth(c, None)
+    st = os.stat(norm)
+    os.utime(norm, ns=(st.st_atime_ns, st.st_mtime_ns + 1_000_000_000))
+    find_neighbors(c, None)                                   # stale entry: parse the file
+    assert _content(os.path.join(out, nb)) == _content(os.path.join(exp, nb))

@@ -142,7 +142,8 @@ def HostSource_(q):
 
 @pytest.mark.parametrize("knobs", [{"GRID_ROWBLK_NT": "0"}, {"GRID_COL_NT": "0"}, {"GRID_ZQUANT_NT": "0"},
                                    {"GRID_ZQUANT_GROUPS": "3"},
-                                   {"GRID_GRAM_KX": "1", "GRID_GRAM_LAG": "0", "GRID_GRAM_SPIN": "0"}])
+                                   {"GRID_GRAM_KX": "1", "GRID_GRAM_LAG": "0", "GRID_GRAM_SPIN": "0"},
+                                   {"GRID_GRAM_KC": "5", "GRID_GRAM_LAG": "3"}])
 def test_performance_knobs_do_not_change_results(resident, knobs, monkeypatch):
     """The product library's getenv knobs are performance-only: every
     alternative they select gives the default chain's results bit for bit."""

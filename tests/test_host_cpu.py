@@ -164,3 +164,26 @@ def test_cli(tmp_path):
         res = r.invoke(cli, ["wgs", write_config(tmp_path)])
     assert res.exit_code == 0, res.output
     m.assert_called_once()
+
+
+def test_handoff_only_for_the_unchanged_file(tmp_path):
+    """grid_amd/utils/handoff.py: an entry is taken once, and only while the
+    file is byte-for-byte the one published (size and mtime)."""
+    import os
+    from grid_amd.utils import handoff
+    p = tmp_path / "normalized.tsv.gz"
+    p.write_bytes(b"x" * 10)
+    handoff.publish(p, ["A"], [1.0], [2.0], "dev", (1, 1))
+    got = handoff.take(str(p))
+    assert got is not None and got[0] == ["A"] and got[3] == "dev"
+    assert handoff.take(p) is None                          # consumed
+    handoff.publish(p, ["A"], [1.0], [2.0], "dev", (1, 1))
+    p.write_bytes(b"y" * 11)                                 # replaced
+    assert handoff.take(p) is None
+    handoff.publish(p, ["A"], [1.0], [2.0], "dev", (1, 1))
+    st = os.stat(p)
+    os.utime(p, ns=(st.st_atime_ns, st.st_mtime_ns + 10**9))
+    assert handoff.take(p) is None
+    handoff.publish(p, ["A"], [1.0], [2.0], "dev", (1, 1))
+    handoff.clear()
+    assert handoff.take(p) is None
