@@ -112,6 +112,16 @@ _SIGS = {
     "grid_ingest_population_means": [_vp, _vp, _vp, _vp, _i64, C.POINTER(_i64)],
     "grid_ingest_fill": [_vp, _vp, _vp, _i64, _i64],
     "grid_ingest_free": [_vp],
+    "grid_gunzip_batch": [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp],
+    "grid_gz_text_size": [_vp, _i64, C.POINTER(_i64), C.POINTER(_i32)],
+    "grid_md_count": [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp],
+    "grid_md_parse_ref": [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp,
+                          C.POINTER(_i64), C.POINTER(_i32)],
+    "grid_md_parse_map": [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp,
+                          _vp],
+    "grid_fill_i32": [_vp, _vp, _i64, _i32],
+    "grid_md_finish": [_vp, _vp, _i64, _i64, _i64, _vp, _i32, _f64, _f64, _vp, _vp, _vp, _vp, _vp, C.POINTER(_i64)],
+    "grid_md_gather": [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp],
 }
 EXPORTS = tuple(_SIGS) + ("grid_last_error",)
 
@@ -399,6 +409,61 @@ def hi_schedule(off: np.ndarray, nbr: np.ndarray, w: np.ndarray, packed_w: bool 
             pk_w[:] = 0
     lens = np.diff(off) if len(off) > 1 else np.zeros(1, np.int64)
     return order, loff, nl, pk_nbr, pk_w, pk_cnt, flags, int(lens.max()) if lens.size else 0
+
+
+GZ_MEMBER_BYTES = 24                 # include/grid_abi.h grid_gz_member
+GZ_OK, GZ_EDATA, GZ_ETRUNC, GZ_ESPACE, GZ_EHEADER, GZ_ECRC = range(6)
+
+
+def gunzip_batch(dev, blobs, caps, mcap=None):
+    """Inflate gzip files on the device (grid_gunzip_batch, one wave per file).
+    blobs: compressed bytes per file; caps: output capacity per file.  Returns
+    (status [n], lengths [n], members [n], out DevBuf, out offsets [n]) -- the
+    text of file f is out[off[f] : off[f] + lengths[f]] when status[f] == 0."""
+    n = len(blobs)
+    in_off = np.zeros(max(n, 1), np.int64)
+    out_off = np.zeros(max(n, 1), np.int64)
+    pos = opos = 0
+    for f, b in enumerate(blobs):
+        in_off[f], out_off[f] = pos, opos
+        pos += -(-max(len(b), 1) // 256) * 256
+        opos += -(-max(int(caps[f]), 1) // 256) * 256
+    src = np.zeros(pos + 256, np.uint8)
+    for f, b in enumerate(blobs):
+        src[in_off[f]:in_off[f] + len(b)] = np.frombuffer(b, np.uint8)
+    mcap = mcap or max(1, max((len(b) // 4096 + 16 for b in blobs), default=1))
+    d_src = dev.upload(src)
+    d_in_off, d_out_off = dev.upload(in_off), dev.upload(out_off)
+    d_in_len = dev.upload(np.array([len(b) for b in blobs] or [0], np.int64))
+    d_cap = dev.upload(np.asarray(list(caps) or [0], np.int64))
+    out = dev.alloc(opos + 256, np.uint8)
+    mem = dev.alloc(max(n, 1) * mcap * GZ_MEMBER_BYTES, np.uint8)
+    st, ln, nm = dev.alloc(max(n, 1), np.int32), dev.alloc(max(n, 1), np.int64), dev.alloc(max(n, 1), np.int32)
+    call("grid_gunzip_batch", dev.ctx, d_src.ptr, d_in_off.ptr, d_in_len.ptr, n, out.ptr, d_out_off.ptr, d_cap.ptr,
+         mem.ptr, mcap, st.ptr, ln.ptr, nm.ptr)
+    return st.numpy()[:n], ln.numpy()[:n], nm.numpy()[:n], out, out_off[:n]
+
+
+class MdOpts(C.Structure):
+    """include/grid_abi.h grid_md_opts (device pointers)."""
+    _fields_ = [("d_prefix", C.c_void_p), ("npre", C.c_int32), ("has_window", C.c_int32), ("start", C.c_int64),
+                ("end", C.c_int64), ("nmask", C.c_int32), ("reserved", C.c_int32), ("d_mask_names", C.c_void_p),
+                ("d_mask_name_off", C.c_void_p), ("d_mask_kb_off", C.c_void_p), ("d_mask_kb", C.c_void_p)]
+
+
+MD_EXOTIC, MD_NOTINK = 1, 2
+
+
+def gz_text_size(buf) -> tuple[int, int] | None:
+    """(inflated size, members) of a gzip file held in ``buf`` (bytes/ndarray),
+    None if it is not gzip (host C++)."""
+    a = np.frombuffer(buf, np.uint8) if not isinstance(buf, np.ndarray) else buf
+    size, m = _i64(), _i32()
+    rc = load().grid_gz_text_size(a.ctypes.data if a.size else None, a.size, C.byref(size), C.byref(m))
+    if rc == GRID_EUNSUPPORTED:
+        return None
+    check(rc, "grid_gz_text_size")
+    return size.value, m.value
 
 
 class Depth16Desc(C.Structure):

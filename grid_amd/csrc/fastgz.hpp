@@ -134,6 +134,9 @@ inline bool gunzip_all(const unsigned char *in, size_t n, Buf &out) {
       if (rc == 0) {               // LIBDEFLATE_SUCCESS
         out.size += got;
         pos += used;
+        // zero padding after a member is skipped, as CPython's gzip reader
+        // (the reference's gzip.open) does in _GzipReader._read_eof
+        while (pos < n && in[pos] == 0) pos++;
         break;
       }
       if (rc == 3 && room < ((size_t)1 << 40)) {   // LIBDEFLATE_INSUFFICIENT_SPACE

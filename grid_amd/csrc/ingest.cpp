@@ -848,6 +848,52 @@ int grid_ingest_fill(grid_ingest *h, const int32_t *row_of_file, int32_t *q, int
   return GRID_OK;
 }
 
+int grid_gz_text_size(const uint8_t *buf, int64_t n, int64_t *size, int32_t *members) {
+  if (!buf || !size || !members || n < 0) {
+    grid_set_error("grid_gz_text_size: bad args");
+    return GRID_EINVAL;
+  }
+  *size = 0;
+  *members = 0;
+  if (n < 18 || buf[0] != 0x1f || buf[1] != 0x8b) return GRID_EUNSUPPORTED;
+  // BGZF (what mosdepth writes): every member says its length ("BC" extra
+  // subfield), its ISIZE is its last 4 bytes; zero padding may follow
+  int64_t pos = 0, tot = 0;
+  int32_t m = 0;
+  bool bgzf = true;
+  while (pos < n) {
+    const unsigned char *h = buf + pos;
+    const int64_t rest = n - pos;
+    if (rest < 18 || h[0] != 0x1f || h[1] != 0x8b || !(h[3] & 4)) { bgzf = false; break; }
+    const int64_t xlen = (int64_t)h[10] | ((int64_t)h[11] << 8);
+    int64_t k = 12, bsize = -1;
+    while (k + 4 <= 12 + xlen && 12 + xlen <= rest) {
+      const int64_t sl = (int64_t)h[k + 2] | ((int64_t)h[k + 3] << 8);
+      if (h[k] == 'B' && h[k + 1] == 'C' && sl == 2) bsize = ((int64_t)h[k + 4] | ((int64_t)h[k + 5] << 8)) + 1;
+      k += 4 + sl;
+    }
+    if (bsize < 18 + xlen || bsize > rest) { bgzf = false; break; }
+    uint32_t isz;
+    memcpy(&isz, h + bsize - 4, 4);
+    tot += isz;
+    m++;
+    pos += bsize;
+    while (pos < n && buf[pos] == 0) pos++;
+  }
+  if (bgzf) {
+    *size = tot;
+    *members = m;
+    return GRID_OK;
+  }
+  // otherwise: one member (the trailer's ISIZE = its length mod 2^32); a file
+  // of several plain members shows up as "no space" when it is inflated
+  uint32_t isz;
+  memcpy(&isz, buf + n - 4, 4);
+  *size = isz;
+  *members = 1;
+  return GRID_OK;
+}
+
 int grid_ingest_free(grid_ingest *h) {
   delete h;
   return GRID_OK;

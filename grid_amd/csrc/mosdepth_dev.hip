@@ -1,0 +1,523 @@
+// Step-4 ingest on the device: mosdepth regions text (inflated in HBM by
+// inflate.hip) -> the int32 hundredths matrix, with the reference's filters
+// and orders (normalize_mosdepth.py:218-416 as restated by ingest.cpp):
+//   * a line is read only if it starts with the chromosome prefix (the raw
+//     startswith test, :272-276 / :334-338), then CHROM\tSTART\tEND\tDEPTH in
+//     the canonical mosdepth grammar (anything else -> the host parser takes
+//     the whole cohort: GRID_MD_EXOTIC), depth > 0, the window test and the
+//     repeat-mask test (1 kb keys of the normalised chromosome name);
+//   * records are keyed by (start, end) only (reference quirk Q1); the key
+//     list K is the reference file's kept keys (strictly increasing, else the
+//     host path), every other file's records are placed by K index: the
+//     reference file's line -> K-index map is tried first (same bins on the
+//     same lines: one compare), a binary search otherwise; a key outside K or
+//     a repeated key -> the host path;
+//   * population means: per column, the files in FILE ORDER (the reference's
+//     threads=1 order, as ingest.cpp), q / 100.0 exactly (div100_exact).
+//
+// Kernels per batch of files: k_md_count (newlines per 64 KiB chunk, any
+// byte >= 0x80), k_md_scan (per-file prefix of the chunk counts), k_md_parse
+// (one workgroup per chunk: the chunk in LDS, one thread per 256-byte
+// segment, each line parsed by the thread whose segment holds its first
+// byte, its index from a block scan of the newline counts).
+#include "common.hpp"
+
+#include <hipcub/hipcub.hpp>
+
+namespace {
+
+constexpr int CH = 65536, SEG = 256, PTH = CH / SEG, MAXLINE = 256;
+
+struct MdOpts {
+  const char *prefix;       // device bytes (npre of them)
+  int npre;
+  int has_window;
+  int64_t wstart, wend;
+  int nmask;                // mask chromosomes (normalised names, "chr..." )
+  const char *mnames;       // concatenated names
+  const int32_t *mname_off; // [nmask + 1]
+  const int64_t *mkb_off;   // [nmask + 1] into mkb
+  const int64_t *mkb;       // sorted unique 1 kb keys per chromosome
+};
+
+__device__ __forceinline__ bool md_masked(const MdOpts &o, const uint8_t *c, int clen, int64_t s, int64_t e) {
+  if (o.nmask == 0) return false;
+  // the normalised chromosome name: the field itself if it starts with "chr",
+  // else "chr" + field (norm_chrom, normalize_mosdepth.py:210-215)
+  const bool has = clen >= 3 && c[0] == 'c' && c[1] == 'h' && c[2] == 'r';
+  const int nlen = has ? clen : clen + 3;
+  for (int k = 0; k < o.nmask; k++) {
+    const int a = o.mname_off[k], b = o.mname_off[k + 1];
+    if (b - a != nlen) continue;
+    bool eq = true;
+    for (int t = 0; t < nlen && eq; t++) {
+      const char want = o.mnames[a + t];
+      const char got = has ? (char)c[t] : (t < 3 ? "chr"[t] : (char)c[t - 3]);
+      eq = want == got;
+    }
+    if (!eq) continue;
+    // any 1 kb key in [floor(s / 1000), floor(e / 1000)] in the mask
+    const int64_t lo = s >= 0 ? s / 1000 : -((-s + 999) / 1000);
+    const int64_t hi = e >= 0 ? e / 1000 : -((-e + 999) / 1000);
+    if (hi < lo) return false;
+    int64_t l = o.mkb_off[k], r = o.mkb_off[k + 1];
+    while (l < r) {                    // lower_bound(lo)
+      const int64_t m = (l + r) >> 1;
+      if (o.mkb[m] < lo) l = m + 1;
+      else r = m;
+    }
+    return l < o.mkb_off[k + 1] && o.mkb[l] <= hi;
+  }
+  return false;
+}
+
+// newlines per chunk; any byte >= 0x80 in a file -> flags |= GRID_MD_EXOTIC
+__global__ __launch_bounds__(256) void k_md_count(const uint8_t *__restrict__ text, const int64_t *__restrict__ toff,
+                                                  const int64_t *__restrict__ tlen, const int32_t *__restrict__ cfile,
+                                                  const int64_t *__restrict__ cstart, int32_t *__restrict__ cnl,
+                                                  int32_t *__restrict__ flags) {
+  const int c = blockIdx.x, f = cfile[c];
+  const int64_t a = cstart[c], b = min(tlen[f], a + CH);
+  const uint8_t *t = text + toff[f];
+  int n = 0, hi = 0;
+  for (int64_t i = a + threadIdx.x * 16; i < b; i += 256 * 16) {
+    if (i + 16 <= b) {
+      const uint4 v = *reinterpret_cast<const uint4 *>(t + i);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t x = w[k] ^ 0x0A0A0A0Au;            // bytes equal to '\n' become 0
+        n += __builtin_popcount(((x - 0x01010101u) & ~x & 0x80808080u));
+        hi |= (w[k] & 0x80808080u) != 0;
+      }
+    } else {
+      for (int64_t j = i; j < b; j++) {
+        n += t[j] == '\n';
+        hi |= t[j] >= 0x80;
+      }
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    n += __shfl_xor(n, o, 64);
+    hi |= __shfl_xor(hi, o, 64);
+  }
+  __shared__ int s_n[4], s_hi[4];
+  if ((threadIdx.x & 63) == 0) {
+    s_n[threadIdx.x >> 6] = n;
+    s_hi[threadIdx.x >> 6] = hi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    cnl[c] = s_n[0] + s_n[1] + s_n[2] + s_n[3];
+    if (s_hi[0] | s_hi[1] | s_hi[2] | s_hi[3]) atomicOr(flags + f, GRID_MD_EXOTIC);
+  }
+}
+
+// per file: newlines before each chunk (exclusive prefix over its chunks)
+__global__ void k_md_scan(const int32_t *__restrict__ cfirst, const int32_t *__restrict__ cnl,
+                          int64_t *__restrict__ cline0, int nfiles) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= nfiles) return;
+  int64_t s = 0;
+  for (int c = cfirst[f]; c < cfirst[f + 1]; c++) {
+    cline0[c] = s;
+    s += cnl[c];
+  }
+}
+
+// canonical "CHROM\tSTART\tEND\tDEPTH" (ingest.cpp canonical_line)
+__device__ __forceinline__ bool md_line(const uint8_t *p, int len, int &clen, int64_t &s, int64_t &e, int64_t &q) {
+  int i = 0;
+  while (i < len && (unsigned)(p[i] - 0x21) < 0x5e) i++;
+  if (i == 0 || i == len || p[i] != '\t') return false;
+  clen = i++;
+  int64_t v[2];
+  for (int k = 0; k < 2; k++) {
+    const int d = i;
+    int64_t x = 0;
+    while (i < len && (unsigned)(p[i] - '0') < 10) x = x * 10 + (p[i++] - '0');
+    if (i == d || i - d > 18 || i == len || p[i] != '\t') return false;
+    v[k] = x;
+    i++;
+  }
+  const int d = i;
+  int64_t ip = 0;
+  while (i < len && (unsigned)(p[i] - '0') < 10) ip = ip * 10 + (p[i++] - '0');
+  if (i == d || i - d > 15) return false;
+  int64_t fp = 0;
+  if (i < len) {
+    if (p[i] != '.') return false;
+    i++;
+    const int f0 = i;
+    while (i < len && (unsigned)(p[i] - '0') < 10) fp = fp * 10 + (p[i++] - '0');
+    if (i != len || i - f0 > 2) return false;
+    if (i - f0 == 1) fp *= 10;
+  }
+  q = ip * 100 + fp;
+  if (q > 2147483647LL) return false;
+  s = v[0];
+  e = v[1];
+  return true;
+}
+
+struct Key2 {
+  int64_t s, e;
+};
+
+__device__ __forceinline__ bool key_lt(int64_t as, int64_t ae, const Key2 &b) {
+  return as < b.s || (as == b.s && ae < b.e);
+}
+
+// MODE 0 (reference file): kept[i] = 1 and keys[i] = (s, e) for every kept
+// line i.  MODE 1 (map): Q[row(f)][K index] = q, kept[f] += 1.
+template <int MODE>
+__global__ __launch_bounds__(PTH) void k_md_parse(const uint8_t *__restrict__ text, const int64_t *__restrict__ toff,
+                                                  const int64_t *__restrict__ tlen,
+                                                  const int32_t *__restrict__ cfile,
+                                                  const int64_t *__restrict__ cstart,
+                                                  const int64_t *__restrict__ cline0, MdOpts o,
+                                                  int32_t *__restrict__ flags,
+                                                  // MODE 0
+                                                  uint8_t *__restrict__ ref_kept, Key2 *__restrict__ ref_keys,
+                                                  int64_t ref_cap,
+                                                  // MODE 1
+                                                  const Key2 *__restrict__ K, int64_t nK,
+                                                  const int32_t *__restrict__ ref_kidx, int64_t ref_nlines,
+                                                  int32_t *__restrict__ Q, int64_t ldq,
+                                                  const int32_t *__restrict__ qrow,
+                                                  unsigned long long *__restrict__ kept) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_t[CH + MAXLINE + 32];
+  __shared__ int s_scan[PTH];
+  const int c = blockIdx.x, f = cfile[c], tid = threadIdx.x;
+  const int64_t L = tlen[f], a = cstart[c], b = min(L, a + CH);
+  const uint8_t *t = text + toff[f];
+  // s_t[16 + k] = byte a + k, for k in [-16, CH + MAXLINE) within the file
+  const int64_t lo = a - 16, hi = min(L, b + MAXLINE);
+  for (int64_t i = lo + tid; i < hi; i += PTH)
+    if (i >= 0) s_t[i - lo] = t[i];
+  // newlines in my segment [a + tid*SEG, ...) -> line index of my first start
+  const int64_t s0 = a + (int64_t)tid * SEG, s1 = min(b, s0 + SEG);
+  __syncthreads();
+  int nl = 0;
+  for (int64_t i = s0; i < s1; i++) nl += s_t[i - lo] == '\n';
+  s_scan[tid] = nl;
+  __syncthreads();
+  for (int d = 1; d < PTH; d <<= 1) {               // inclusive scan (Hillis-Steele)
+    const int v = tid >= d ? s_scan[tid - d] : 0;
+    __syncthreads();
+    s_scan[tid] += v;
+    __syncthreads();
+  }
+  int64_t idx = cline0[c] + (s_scan[tid] - nl);      // newlines in [0, s0)
+  int bad = 0;
+  unsigned long long nkept = 0;
+  for (int64_t x = s0; x < s1; x++) {
+    const bool start = x == 0 || s_t[x - 1 - lo] == '\n';
+    if (start) {
+      // the line [x, end): up to the next '\n' or the file end
+      const uint8_t *p = s_t + (x - lo);
+      const int64_t lim = min(L, x + MAXLINE + 1) - x;
+      int len = 0;
+      while (len < lim && p[len] != '\n') len++;
+      if (len == lim && x + len < L) {
+        bad |= GRID_MD_EXOTIC;                      // a line longer than MAXLINE
+      } else if (o.npre == 0 || (len >= o.npre && [&] {
+                   for (int k = 0; k < o.npre; k++)
+                     if (p[k] != (uint8_t)o.prefix[k]) return false;
+                   return true;
+                 }())) {
+        int clen;
+        int64_t s, e, q;
+        if (!md_line(p, len, clen, s, e, q)) {
+          bad |= GRID_MD_EXOTIC;
+        } else if (q > 0 && (!o.has_window || (e >= o.wstart && s <= o.wend)) && !md_masked(o, p, clen, s, e)) {
+          if (MODE == 0) {
+            if (idx < ref_cap) {
+              ref_kept[idx] = 1;
+              ref_keys[idx] = Key2{s, e};
+            } else {
+              bad |= GRID_MD_NOTINK;
+            }
+          } else {
+            int64_t j = idx < ref_nlines ? ref_kidx[idx] : -1;
+            if (j < 0 || K[j].s != s || K[j].e != e) {
+              int64_t l = 0, r = nK;                 // lower_bound of (s, e) in K
+              while (l < r) {
+                const int64_t m = (l + r) >> 1;
+                if (K[m].s < s || (K[m].s == s && K[m].e < e)) l = m + 1;
+                else r = m;
+              }
+              j = (l < nK && K[l].s == s && K[l].e == e) ? l : -1;
+            }
+            if (j < 0) {
+              bad |= GRID_MD_NOTINK;
+            } else {
+              Q[(int64_t)qrow[f] * ldq + j] = (int32_t)q;
+              nkept++;
+            }
+          }
+        }
+      }
+    }
+    if (s_t[x - lo] == '\n') idx++;
+  }
+  if (bad) atomicOr(flags + f, bad);
+  if (MODE == 1) {
+    for (int k = 32; k > 0; k >>= 1) nkept += __shfl_xor(nkept, k, 64);
+    if ((tid & 63) == 0 && nkept) atomicAdd(kept + f, nkept);
+  }
+}
+
+// K from the reference file: kept keys in line order, their K index per line
+__global__ void k_md_ref_index(const uint8_t *__restrict__ kept, const int64_t *__restrict__ pos, int64_t n,
+                               const Key2 *__restrict__ keys, Key2 *__restrict__ K, int32_t *__restrict__ kidx) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (kept[i]) {
+    K[pos[i]] = keys[i];
+    kidx[i] = (int32_t)pos[i];
+  } else {
+    kidx[i] = -1;
+  }
+}
+
+__global__ void k_md_sorted(const Key2 *__restrict__ K, int64_t nK, int32_t *__restrict__ bad) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j + 1 >= nK) return;
+  if (!key_lt(K[j].s, K[j].e, K[j + 1])) atomicOr(bad, 1);
+}
+
+__global__ void k_fill_i32(int32_t *__restrict__ p, int64_t n, int32_t v) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+
+// per column: population sum in file order over the rows listed (ok files),
+// count, mean, valid flag; per row: present entries (duplicate check)
+__global__ __launch_bounds__(256) void k_md_popmeans(const int32_t *__restrict__ Q, int64_t ldq, int64_t nK,
+                                                     const int32_t *__restrict__ rows, int nrows, double min_d,
+                                                     double max_d, double *__restrict__ mean,
+                                                     int32_t *__restrict__ valid) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nK) return;
+  double s = 0.0;
+  int64_t c = 0;
+  for (int r = 0; r < nrows; r++) {
+    const int32_t q = Q[(int64_t)rows[r] * ldq + j];
+    if (q != GRID_MISSING) {
+      s = s + div100_exact(q);
+      c++;
+    }
+  }
+  const double m = c > 0 ? s / (double)c : 0.0;
+  mean[j] = m;
+  valid[j] = c > 0 && min_d <= m && m <= max_d;
+}
+
+// per row: entries present (all K) and present in valid columns
+__global__ __launch_bounds__(256) void k_md_rowcount(const int32_t *__restrict__ Q, int64_t ldq, int64_t nK,
+                                                     const int32_t *__restrict__ valid,
+                                                     unsigned long long *__restrict__ present,
+                                                     unsigned long long *__restrict__ nvalid) {
+  const int r = blockIdx.y;
+  unsigned long long a = 0, v = 0;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nK; j += (int64_t)gridDim.x * blockDim.x) {
+    const bool p = Q[(int64_t)r * ldq + j] != GRID_MISSING;
+    a += p;
+    v += p && valid[j];
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    v += __shfl_xor(v, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (a) atomicAdd(present + r, a);
+    if (v) atomicAdd(nvalid + r, v);
+  }
+}
+
+// out[dst_row[r]][cpos[j]] = Q[r][j] for valid j (rows with dst_row < 0 skipped)
+__global__ __launch_bounds__(256) void k_md_gather(const int32_t *__restrict__ Q, int64_t ldq, int64_t nK,
+                                                   const int32_t *__restrict__ valid,
+                                                   const int64_t *__restrict__ cpos,
+                                                   const int32_t *__restrict__ dst_row, int32_t *__restrict__ out,
+                                                   int64_t ldo) {
+  const int r = blockIdx.y;
+  const int32_t d = dst_row[r];
+  if (d < 0) return;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nK; j += (int64_t)gridDim.x * blockDim.x)
+    if (valid[j]) out[(int64_t)d * ldo + cpos[j]] = Q[(int64_t)r * ldq + j];
+}
+
+__global__ void k_md_cols(const Key2 *__restrict__ K, int64_t nK, const int32_t *__restrict__ valid,
+                          const int64_t *__restrict__ cpos, int64_t *__restrict__ starts, int64_t *__restrict__ ends) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < nK && valid[j]) {
+    starts[cpos[j]] = K[j].s;
+    ends[cpos[j]] = K[j].e;
+  }
+}
+
+template <class T>
+struct ToI64 {
+  __host__ __device__ __forceinline__ int64_t operator()(const T &v) const { return (int64_t)v; }
+};
+
+// exclusive prefix sum in int64 of n small counts
+template <class TI>
+int excl_scan(grid_ctx *ctx, const TI *in, int64_t *out, int64_t n) {
+  REQUIRE(n < (1ll << 31), "scan too long");
+  hipcub::TransformInputIterator<int64_t, ToI64<TI>, const TI *> it(in, ToI64<TI>());
+  size_t tmp = 0;
+  HIPCHK(hipcub::DeviceScan::ExclusiveScan(nullptr, tmp, it, out, hipcub::Sum(), (int64_t)0, (int)n, ctx->stream));
+  void *s = nullptr;
+  int rc = grid_scratch(ctx, tmp + 256, &s);
+  if (rc) return rc;
+  HIPCHK(hipcub::DeviceScan::ExclusiveScan(s, tmp, it, out, hipcub::Sum(), (int64_t)0, (int)n, ctx->stream));
+  return GRID_OK;
+}
+
+MdOpts to_opts(const grid_md_opts *h) {
+  MdOpts o;
+  o.prefix = h->d_prefix;
+  o.npre = h->npre;
+  o.has_window = h->has_window;
+  o.wstart = h->start;
+  o.wend = h->end;
+  o.nmask = h->nmask;
+  o.mnames = h->d_mask_names;
+  o.mname_off = h->d_mask_name_off;
+  o.mkb_off = h->d_mask_kb_off;
+  o.mkb = h->d_mask_kb;
+  return o;
+}
+
+}  // namespace
+
+extern "C" {
+
+int grid_md_count(grid_ctx *ctx, const uint8_t *d_text, const int64_t *d_toff, const int64_t *d_tlen,
+                  int64_t nchunks, const int32_t *d_cfile, const int64_t *d_cstart, const int32_t *d_cfirst,
+                  int64_t nfiles, int32_t *d_cnl, int64_t *d_cline0, int32_t *d_flags) {
+  REQUIRE(ctx && nchunks >= 0 && nchunks <= 0x7fffffff && nfiles >= 0, "bad args");
+  if (nchunks == 0) return GRID_OK;
+  hipLaunchKernelGGL(k_md_count, dim3((unsigned)nchunks), dim3(256), 0, ctx->stream, d_text, d_toff, d_tlen, d_cfile,
+                     d_cstart, d_cnl, d_flags);
+  LAUNCHCHK();
+  hipLaunchKernelGGL(k_md_scan, dim3((unsigned)((nfiles + 63) / 64)), dim3(64), 0, ctx->stream, d_cfirst, d_cnl,
+                     d_cline0, (int)nfiles);
+  LAUNCHCHK();
+  return GRID_OK;
+}
+
+int grid_md_parse_ref(grid_ctx *ctx, const uint8_t *d_text, const int64_t *d_toff, const int64_t *d_tlen,
+                      int64_t nchunks, const int32_t *d_cfile, const int64_t *d_cstart, const int64_t *d_cline0,
+                      const grid_md_opts *opts, int32_t *d_flags, int64_t nlines, uint8_t *d_kept_line,
+                      void *d_keys_line, void *d_K, int32_t *d_kidx, int64_t *h_nK, int32_t *h_unsorted) {
+  REQUIRE(ctx && opts && h_nK && h_unsorted && nlines >= 0 && nchunks >= 0, "bad args");
+  *h_nK = 0;
+  *h_unsorted = 0;
+  if (nlines == 0 || nchunks == 0) return GRID_OK;
+  HIPCHK(hipMemsetAsync(d_kept_line, 0, (size_t)nlines, ctx->stream));
+  hipLaunchKernelGGL(k_md_parse<0>, dim3((unsigned)nchunks), dim3(PTH), 0, ctx->stream, d_text, d_toff, d_tlen,
+                     d_cfile, d_cstart, d_cline0, to_opts(opts), d_flags, d_kept_line, (Key2 *)d_keys_line, nlines,
+                     nullptr, (int64_t)0, nullptr, (int64_t)0, nullptr, (int64_t)0, nullptr, nullptr);
+  LAUNCHCHK();
+  // positions of the kept lines: exclusive scan of the flags (int64 output)
+  void *s = nullptr;
+  const size_t need = (size_t)nlines * 8 + 1024;
+  int64_t *pos = nullptr;
+  HIPCHK(hipMallocAsync((void **)&pos, need, ctx->stream));
+  int rc = excl_scan(ctx, d_kept_line, pos, nlines);
+  if (rc) { (void)hipFreeAsync(pos, ctx->stream); return rc; }
+  int64_t last_pos = 0;
+  uint8_t last_kept = 0;
+  HIPCHK(hipMemcpyAsync(&last_pos, pos + nlines - 1, 8, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipMemcpyAsync(&last_kept, d_kept_line + nlines - 1, 1, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  const int64_t nK = last_pos + last_kept;
+  hipLaunchKernelGGL(k_md_ref_index, dim3((unsigned)((nlines + 255) / 256)), dim3(256), 0, ctx->stream, d_kept_line,
+                     pos, nlines, (const Key2 *)d_keys_line, (Key2 *)d_K, d_kidx);
+  LAUNCHCHK();
+  rc = grid_scratch(ctx, 256, &s);
+  if (rc) { (void)hipFreeAsync(pos, ctx->stream); return rc; }
+  HIPCHK(hipMemsetAsync(s, 0, 4, ctx->stream));
+  if (nK > 1) {
+    hipLaunchKernelGGL(k_md_sorted, dim3((unsigned)((nK + 255) / 256)), dim3(256), 0, ctx->stream, (const Key2 *)d_K,
+                       nK, (int32_t *)s);
+    LAUNCHCHK();
+  }
+  HIPCHK(hipMemcpyAsync(h_unsorted, s, 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipFreeAsync(pos, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  *h_nK = nK;
+  return GRID_OK;
+}
+
+int grid_md_parse_map(grid_ctx *ctx, const uint8_t *d_text, const int64_t *d_toff, const int64_t *d_tlen,
+                      int64_t nchunks, const int32_t *d_cfile, const int64_t *d_cstart, const int64_t *d_cline0,
+                      const grid_md_opts *opts, int32_t *d_flags, const void *d_K, int64_t nK,
+                      const int32_t *d_kidx, int64_t ref_nlines, int32_t *d_Q, int64_t ldq, const int32_t *d_qrow,
+                      uint64_t *d_kept) {
+  REQUIRE(ctx && opts && nchunks >= 0 && nK >= 0 && ldq >= nK, "bad args");
+  if (nchunks == 0) return GRID_OK;
+  hipLaunchKernelGGL(k_md_parse<1>, dim3((unsigned)nchunks), dim3(PTH), 0, ctx->stream, d_text, d_toff, d_tlen,
+                     d_cfile, d_cstart, d_cline0, to_opts(opts), d_flags, nullptr, nullptr, (int64_t)0,
+                     (const Key2 *)d_K, nK, d_kidx, ref_nlines, d_Q, ldq, d_qrow, (unsigned long long *)d_kept);
+  LAUNCHCHK();
+  return GRID_OK;
+}
+
+int grid_fill_i32(grid_ctx *ctx, int32_t *d_p, int64_t n, int32_t v) {
+  REQUIRE(ctx && n >= 0, "bad args");
+  if (n == 0) return GRID_OK;
+  hipLaunchKernelGGL(k_fill_i32, dim3(4096), dim3(256), 0, ctx->stream, d_p, n, v);
+  LAUNCHCHK();
+  return GRID_OK;
+}
+
+int grid_md_finish(grid_ctx *ctx, const int32_t *d_Q, int64_t ldq, int64_t nK, int64_t nfiles,
+                   const int32_t *d_rows, int32_t nrows, double min_depth, double max_depth, double *d_mean,
+                   int32_t *d_valid, int64_t *d_cpos, uint64_t *d_present, uint64_t *d_nvalid, int64_t *h_m) {
+  REQUIRE(ctx && h_m && nK >= 0 && nfiles >= 0 && nrows >= 0, "bad args");
+  *h_m = 0;
+  if (nK == 0) return GRID_OK;
+  hipLaunchKernelGGL(k_md_popmeans, dim3((unsigned)((nK + 255) / 256)), dim3(256), 0, ctx->stream, d_Q, ldq, nK,
+                     d_rows, nrows, min_depth, max_depth, d_mean, d_valid);
+  LAUNCHCHK();
+  int rc = excl_scan(ctx, d_valid, d_cpos, nK);
+  if (rc) return rc;
+  HIPCHK(hipMemsetAsync(d_present, 0, (size_t)(nfiles > 0 ? nfiles : 1) * 8, ctx->stream));
+  HIPCHK(hipMemsetAsync(d_nvalid, 0, (size_t)(nfiles > 0 ? nfiles : 1) * 8, ctx->stream));
+  if (nfiles > 0) {
+    REQUIRE(nfiles <= 65535, "too many files for one launch (%lld)", (long long)nfiles);
+    hipLaunchKernelGGL(k_md_rowcount, dim3(64, (unsigned)nfiles), dim3(256), 0, ctx->stream, d_Q, ldq, nK, d_valid,
+                       (unsigned long long *)d_present, (unsigned long long *)d_nvalid);
+    LAUNCHCHK();
+  }
+  int64_t lp = 0;
+  int32_t lv = 0;
+  HIPCHK(hipMemcpyAsync(&lp, d_cpos + nK - 1, 8, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipMemcpyAsync(&lv, d_valid + nK - 1, 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  *h_m = lp + lv;
+  return GRID_OK;
+}
+
+int grid_md_gather(grid_ctx *ctx, const int32_t *d_Q, int64_t ldq, int64_t nK, int64_t nfiles,
+                   const int32_t *d_valid, const int64_t *d_cpos, const int32_t *d_dst_row, int32_t *d_out,
+                   int64_t ldo, const void *d_K, int64_t *d_starts, int64_t *d_ends) {
+  REQUIRE(ctx && nK >= 0 && nfiles >= 0 && nfiles <= 65535, "bad args");
+  if (nK == 0) return GRID_OK;
+  if (nfiles > 0) {
+    hipLaunchKernelGGL(k_md_gather, dim3(256, (unsigned)nfiles), dim3(256), 0, ctx->stream, d_Q, ldq, nK, d_valid,
+                       d_cpos, d_dst_row, d_out, ldo);
+    LAUNCHCHK();
+  }
+  hipLaunchKernelGGL(k_md_cols, dim3((unsigned)((nK + 255) / 256)), dim3(256), 0, ctx->stream, (const Key2 *)d_K, nK,
+                     d_valid, d_cpos, d_starts, d_ends);
+  LAUNCHCHK();
+  return GRID_OK;
+}
+
+}  // extern "C"

@@ -19,7 +19,7 @@ import numpy as np
 
 from .. import _abi, engine
 from ..device import get_device
-from . import handoff
+from . import handoff, ingest_device
 from .mosdepth import remove_intermediate_files
 from .utils import get_samples, log, progress_bar, setup_output_file
 
@@ -253,13 +253,22 @@ def _read_all(individuals, mosdepth_dir, chromosome, start, end, excluded, threa
 
 
 def ingest(individuals, mosdepth_dir, chromosome, start, end, excluded, min_depth, max_depth, threads,
-           console=None):
+           console=None, dev=None):
     """R1-R4 (:218-416): mosdepth files -> (ids, regions, int32 hundredths).
-    The host C++ parser (``grid_ingest_*``, grid_amd/csrc/ingest.cpp) does
-    it with one multithreaded parse per file; a cohort whose text leaves the
-    strict mosdepth grammar (or a non-integer window) goes through the
-    line-by-line restatement ``ingest_py`` instead."""
+    With a device (``dev``): inflated and parsed in HBM (ingest_device.py;
+    the matrix is returned as a device buffer); the host C++ parser
+    (``grid_ingest_*``, grid_amd/csrc/ingest.cpp) takes any cohort outside
+    that path's common case, with one multithreaded parse per file; text that
+    leaves the strict mosdepth grammar (or a non-integer window) goes through
+    the line-by-line restatement ``ingest_py``."""
     ints = all(v is None or (isinstance(v, int) and not isinstance(v, bool)) for v in (start, end))
+    if ints and dev is not None:
+        try:
+            return _ingest_dev(dev, individuals, mosdepth_dir, chromosome, start, end, excluded, min_depth,
+                               max_depth, threads, console)
+        except ingest_device.DeviceIngestUnsupported as e:
+            msg = f"device mosdepth parser: {e}; using the host parser"
+            log(console, msg, style="warning") if console else print(msg)
     if ints:
         try:
             return ingest_native(individuals, mosdepth_dir, chromosome, start, end, excluded, min_depth,
@@ -269,6 +278,31 @@ def ingest(individuals, mosdepth_dir, chromosome, start, end, excluded, min_dept
             log(console, msg, style="warning") if console else print(msg)
     return ingest_py(individuals, mosdepth_dir, chromosome, start, end, excluded, min_depth, max_depth,
                      threads, console)
+
+
+def _ingest_dev(dev, individuals, mosdepth_dir, chromosome, start, end, excluded, min_depth, max_depth, threads,
+                console=None):
+    """R1-R4 on the device (ingest_device.py); same (ids, regions, matrix) as
+    ``ingest_native``, the matrix a device buffer."""
+    inds = list(individuals)
+    paths = []
+    for ind in inds:
+        p = find_bed_gz_for_individual(ind, mosdepth_dir)
+        paths.append(str(p) if p.exists() else None)
+    window = (start, end) if start is not None and end is not None else None
+    rows, state, nval, status = ingest_device.ingest_device(
+        dev, paths, norm_chrom(chromosome) if chromosome else None, window, excluded or {}, min_depth, max_depth,
+        threads=max(1, int(threads or 1)))
+    keep = {ind: i for i, ind in enumerate(inds) if status[i] == 0 and state is not None and nval[i] > 0}
+    removed = len(inds) - len(keep)
+    if removed > 0:                           # filter_empty_samples (:576-600)
+        msg = f"Removed {removed} samples with 0 regions"
+        log(console, msg, style="warning") if console else print(msg)
+    ids = sorted(keep)
+    if not ids:
+        return [], [], np.zeros((0, 0), dtype=np.int32)
+    q, regions = ingest_device.gather(dev, state, [keep[i] for i in ids], len(inds))
+    return ids, regions, q
 
 
 def ingest_native(individuals, mosdepth_dir, chromosome, start, end, excluded, min_depth, max_depth, threads,
@@ -395,17 +429,21 @@ def normalize_mosdepth(config, console):
         sys.exit(1)
     excluded = load_repeat_mask(repeat_mask)
 
+    dev = get_device(config)
+    # mosdepth.normalize.device_ingest: inflate and parse the files in HBM
+    # (ingest_device.py); off by default: the threaded host parser is faster on
+    # single-member gzip files
+    dev_ingest = bool(config["mosdepth"]["normalize"].get("device_ingest", False))
     with progress_bar(console, total=len(individuals), description="Extracting per-sample regions...") as (p, t):
         ids, regions, q = ingest(individuals, mosdepth_dir, chrom, start, end, excluded, min_depth, max_depth,
-                                 threads, console)
+                                 threads, console, dev=dev if dev_ingest else None)
         p.update(t, completed=len(individuals))
     if not ids:
         log(console, "No valid samples with regions found.", style="danger")
         sys.exit(1)
 
     n, m = q.shape
-    dev = get_device(config)
-    qd = dev.upload(q)
+    qd = q if isinstance(q, _abi.DevBuf) else dev.upload(q)     # the device ingest leaves it in HBM
     f64 = q.dtype == np.float64                      # depth text that is not exact hundredths
     st = (engine.normalize_stats_f64 if f64 else engine.normalize_stats)(dev, qd, n, m, m)
     sel, r = engine.select_regions(dev, st, top_frac)

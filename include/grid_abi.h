@@ -447,6 +447,77 @@ int grid_ingest_fill(grid_ingest *h, const int32_t *h_row_of_file, int32_t *h_q,
                      int64_t ld);
 int grid_ingest_free(grid_ingest *h);
 
+/* ---- gzip on the device (step-4 ingest: normalize_mosdepth.py:96-112 reads
+ * every regions.bed.gz with gzip.open; grid_amd/csrc/inflate.hip) ---- */
+/* one gzip member of an inflated file: output bytes [start, end), trailer */
+typedef struct grid_gz_member {
+  int64_t start, end;
+  uint32_t crc, isize;
+} grid_gz_member;
+#define GRID_GZ_EDATA 1     /* invalid deflate / gzip data */
+#define GRID_GZ_ETRUNC 2    /* input ended inside a member */
+#define GRID_GZ_ESPACE 3    /* output or member capacity exceeded */
+#define GRID_GZ_EHEADER 4   /* not a gzip file (or empty) */
+#define GRID_GZ_ECRC 5      /* a member's CRC-32 does not match its bytes */
+/* Inflate n_files gzip files (each: every member back to back) in one launch,
+ * one wave per file.  d_src + d_in_off[f] (256-B aligned) holds d_in_len[f]
+ * bytes; the text goes to d_out + d_out_off[f] (16-B aligned), at most
+ * d_out_cap[f] bytes; d_mem[f * mcap ...] receives the members.  Per file:
+ * d_status (0 or GRID_GZ_E*), d_out_len, d_nmem.  Asynchronous on the stream. */
+/* ---- mosdepth text -> depth matrix on the device (grid_amd/csrc/mosdepth_dev.hip;
+ * normalize_mosdepth.py:218-416 as ingest.cpp restates it).  Driven per batch of
+ * inflated files by grid_amd/utils/ingest_device.py; every file is cut in
+ * 64 KiB chunks (chunk c: file d_cfile[c], byte offset d_cstart[c]; a file's
+ * chunks are d_cfirst[f] .. d_cfirst[f+1]-1). ---- */
+typedef struct grid_md_opts {
+  const char *d_prefix;            /* chromosome prefix (raw startswith), npre bytes */
+  int32_t npre;
+  int32_t has_window;
+  int64_t start, end;              /* window: keep e >= start && s <= end */
+  int32_t nmask;                   /* repeat mask: normalised chromosome names ... */
+  int32_t reserved;
+  const char *d_mask_names;
+  const int32_t *d_mask_name_off;  /* [nmask + 1] */
+  const int64_t *d_mask_kb_off;    /* [nmask + 1] */
+  const int64_t *d_mask_kb;        /* ... and their sorted 1 kb keys */
+} grid_md_opts;
+#define GRID_MD_EXOTIC 1   /* a line outside the canonical grammar, or a byte >= 0x80 */
+#define GRID_MD_NOTINK 2   /* a kept (start, end) outside the reference key list */
+/* newlines per chunk and their per-file prefix; flags |= GRID_MD_EXOTIC for bytes >= 0x80 */
+int grid_md_count(grid_ctx *ctx, const uint8_t *d_text, const int64_t *d_toff, const int64_t *d_tlen,
+                  int64_t nchunks, const int32_t *d_cfile, const int64_t *d_cstart, const int32_t *d_cfirst,
+                  int64_t nfiles, int32_t *d_cnl, int64_t *d_cline0, int32_t *d_flags);
+/* the reference file (one file, nlines lines): its kept keys in line order -> the key list
+ * d_K ((start, end) int64 pairs, *h_nK of them), d_kidx[line] = K index or -1; *h_unsorted = 1
+ * when the keys are not strictly increasing (the caller then uses the host parser) */
+int grid_md_parse_ref(grid_ctx *ctx, const uint8_t *d_text, const int64_t *d_toff, const int64_t *d_tlen,
+                      int64_t nchunks, const int32_t *d_cfile, const int64_t *d_cstart, const int64_t *d_cline0,
+                      const grid_md_opts *opts, int32_t *d_flags, int64_t nlines, uint8_t *d_kept_line,
+                      void *d_keys_line, void *d_K, int32_t *d_kidx, int64_t *h_nK, int32_t *h_unsorted);
+/* every file of the batch: d_Q[d_qrow[f] * ldq + K index] = depth hundredths, d_kept[f] += records */
+int grid_md_parse_map(grid_ctx *ctx, const uint8_t *d_text, const int64_t *d_toff, const int64_t *d_tlen,
+                      int64_t nchunks, const int32_t *d_cfile, const int64_t *d_cstart, const int64_t *d_cline0,
+                      const grid_md_opts *opts, int32_t *d_flags, const void *d_K, int64_t nK,
+                      const int32_t *d_kidx, int64_t ref_nlines, int32_t *d_Q, int64_t ldq, const int32_t *d_qrow,
+                      uint64_t *d_kept);
+int grid_fill_i32(grid_ctx *ctx, int32_t *d_p, int64_t n, int32_t v);
+/* population means over the rows d_rows (file order), valid columns, their positions
+ * (*h_m valid), per row: entries present and entries present in valid columns */
+int grid_md_finish(grid_ctx *ctx, const int32_t *d_Q, int64_t ldq, int64_t nK, int64_t nfiles,
+                   const int32_t *d_rows, int32_t nrows, double min_depth, double max_depth, double *d_mean,
+                   int32_t *d_valid, int64_t *d_cpos, uint64_t *d_present, uint64_t *d_nvalid, int64_t *h_m);
+/* the matrix: d_out[d_dst_row[f] * ldo + column] for the valid columns; their (start, end) */
+int grid_md_gather(grid_ctx *ctx, const int32_t *d_Q, int64_t ldq, int64_t nK, int64_t nfiles,
+                   const int32_t *d_valid, const int64_t *d_cpos, const int32_t *d_dst_row, int32_t *d_out,
+                   int64_t ldo, const void *d_K, int64_t *d_starts, int64_t *d_ends);
+/* host: the inflated size of a gzip file in memory (BGZF: the members' sizes; else the
+ * trailer's ISIZE of a single member); GRID_EUNSUPPORTED if it is not gzip */
+int grid_gz_text_size(const uint8_t *h_buf, int64_t n, int64_t *size, int32_t *members);
+int grid_gunzip_batch(grid_ctx *ctx, const uint8_t *d_src, const int64_t *d_in_off, const int64_t *d_in_len,
+                      int64_t n_files, uint8_t *d_out, const int64_t *d_out_off, const int64_t *d_out_cap,
+                      grid_gz_member *d_mem, int32_t mcap, int32_t *d_status, int64_t *d_out_len,
+                      int32_t *d_nmem);
+
 #ifdef __cplusplus
 }
 #endif

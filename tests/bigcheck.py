@@ -152,13 +152,15 @@ def check_row_means(dev, st, seed, n, m, ncl, blocks):
         q = torch.empty((n, w), dtype=torch.int32, device="cuda")
         _abi.call("grid_synth_depth", dev.ctx, seed, n, w, w, c0, ncl, q.data_ptr())
         # nanmean's operand np.where(isnan(a), 0, a) with a = q / 100.0, built
-        # column-major (the transposed copy is made on the device, so the
-        # oracle's column walks read contiguous memory): same IEEE values
-        qt = q.t().contiguous()
+        # column-major: the int32 transpose is made on the device (so the
+        # oracle's column walks read contiguous memory), the division by NumPy
+        # (torch divides by a scalar as a multiply by its reciprocal: not IEEE /)
+        qt = q.t().contiguous().cpu().numpy()
+        del q
         miss = qt == _abi.MISSING
-        z0 = torch.where(miss, 0.0, qt.to(torch.float64) / 100.0).cpu().numpy().T
-        cnt = (~miss).sum(0).cpu().numpy()
-        del q, qt, miss
+        z0 = np.where(miss, 0.0, qt / 100.0).T
+        cnt = (~miss).sum(axis=0)
+        del qt, miss
         exp = npsum.pairwise_cols(z0, 0, w)
         assert np.array_equal(bsum[:, b], exp), f"row block sums, block {b}"
         assert np.array_equal(bcnt[:, b], cnt), f"row block counts, block {b}"

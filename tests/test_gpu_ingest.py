@@ -1,0 +1,124 @@
+"""Step-4 ingest on the device (grid_amd/utils/ingest_device.py: gzip inflate,
+mosdepth parse, population means, valid columns, row order -- all in HBM)
+against the host parser ingest_native (itself pinned to the reference's
+golden cohorts and the line-by-line restatement in test_ingest_cpu.py and
+test_host_cpu.py): the same ids, regions and matrix, bit for bit, or the
+documented hand-over to the host parser for cohorts outside the device path's
+common case."""
+import gzip
+import os
+import shutil
+
+import numpy as np
+import pytest
+import yaml
+
+from grid_amd import _abi
+from grid_amd.utils import ingest_device
+from grid_amd.utils import normalize_mosdepth as nm
+from tests.test_ingest_cpu import _bgzf, _cohort, _rand_lines
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import torch
+    d = _abi.Device(0)
+    d.set_stream(torch.cuda.current_stream())
+    return d
+
+
+def _dev_vs_host(dev, d, samples, chrom=None, start=None, end=None, excluded=None, lo=20, hi=100):
+    inds = nm.map_mosdepth_files_to_samples(d, samples)
+    ex = excluded or {}
+    a = nm._ingest_dev(dev, inds, d, chrom, start, end, ex, lo, hi, 4)
+    b = nm.ingest_native(inds, d, chrom, start, end, ex, lo, hi, 4)
+    assert a[0] == b[0], (a[0], b[0])
+    assert a[1] == b[1]
+    qa = a[2].numpy() if isinstance(a[2], _abi.DevBuf) else a[2]
+    assert qa.shape == b[2].shape and np.array_equal(qa, b[2])
+    return a
+
+
+def test_random_cohorts(dev, tmp_path):
+    rng = np.random.default_rng(1)
+    files = {f"S{i:03d}": _rand_lines(rng, 3000) for i in range(12)}
+    d = _cohort(tmp_path, files, members=1)
+    a = _dev_vs_host(dev, d, sorted(files) + ["MISSING1"])
+    assert len(a[0]) == 12 and a[2].shape[1] > 100
+    # window, mask, chromosome prefix
+    _dev_vs_host(dev, d, sorted(files), chrom="1", start=500_000, end=2_000_000, excluded={"chr1": {7, 8, 900}})
+
+
+def test_golden_cohorts(dev, tmp_path):
+    """g1b / g1c on the device path; g1's chr10 decoy lines repeat chr1's
+    (start, end) keys (reference quirk Q1, last line wins) -- outside the
+    device path, handed over to the host parser, same result."""
+    for name in ("g1", "g1b", "g1c"):
+        c = yaml.safe_load(open(os.path.join(G, name, "config.yaml")))
+        src = os.path.join(G, name, "inputs")
+        samples = [s.strip() for s in open(os.path.join(src, "samples.txt")) if s.strip()]
+        ex = nm.load_repeat_mask(os.path.join(src, "mask.bed"))
+        kw = dict(chrom=c.get("chrom"), start=c.get("start_bp"), end=c.get("end_bp"), excluded=ex,
+                  lo=c["mosdepth"]["normalize"]["min_depth"], hi=c["mosdepth"]["normalize"]["max_depth"])
+        d = os.path.join(src, "mosdepth")
+        if name == "g1":
+            inds = nm.map_mosdepth_files_to_samples(d, samples)
+            with pytest.raises(ingest_device.DeviceIngestUnsupported):
+                nm._ingest_dev(dev, inds, d, kw["chrom"], kw["start"], kw["end"], ex, kw["lo"], kw["hi"], 2)
+            continue
+        _dev_vs_host(dev, d, samples, **kw)
+
+
+def test_subsets_bgzf_empty_corrupt_and_zero_depth(dev, tmp_path):
+    rng = np.random.default_rng(2)
+    base = _rand_lines(rng, 5000)
+    files = {}
+    for i in range(8):
+        lines = list(base)
+        for j in rng.choice(len(lines), 40, replace=False):            # zero-depth bins: keys missing per file
+            lines[j] = lines[j].rsplit("\t", 1)[0] + "\t0.00\n"
+        if i == 3:
+            lines = lines[:4000]                                        # a shorter file (a subset of the keys)
+        files[f"S{i:03d}"] = lines
+    d = tmp_path / "md"
+    d.mkdir()
+    for k, (name, lines) in enumerate(files.items()):
+        data = "".join(lines).encode()
+        blob = _bgzf(data) if k % 2 else gzip.compress(data, 6)
+        (d / f"{name}.regions.bed.gz").write_bytes(blob)
+    (d / "E000.regions.bed.gz").write_bytes(b"")                       # empty file: no lines
+    good = (d / "S001.regions.bed.gz").read_bytes()
+    (d / "C000.regions.bed.gz").write_bytes(good[: len(good) // 2])    # truncated: dropped
+    (d / "N000.regions.bed.gz").write_bytes(b"not a gzip file at all")  # dropped
+    samples = sorted(files) + ["E000", "C000", "N000"]
+    a = _dev_vs_host(dev, d, samples)
+    assert len(a[0]) == 8
+
+
+def test_outside_the_common_case_hands_over(dev, tmp_path):
+    """Unsorted reference keys, duplicate keys, keys outside the reference,
+    non-canonical text: DeviceIngestUnsupported, and ingest() gives the host
+    parser's result."""
+    rng = np.random.default_rng(3)
+    base = _rand_lines(rng, 800)
+    cases = {
+        "unsorted": ([base[5]] + base[:5] + base[6:], base),
+        "dup": (base, base[:100] + [base[50]] + base[100:]),
+        "extra_key": (base[:-1], base),
+        "exotic": (base, base[:10] + ["chr1\t9999000\t9999100\t3e1\n"] + base[10:]),
+    }
+    for name, (la, lb) in cases.items():
+        root = tmp_path / name
+        root.mkdir()
+        d = _cohort(root, {"A": la, "B": lb})
+        inds = nm.map_mosdepth_files_to_samples(d, ["A", "B"])
+        with pytest.raises(ingest_device.DeviceIngestUnsupported):
+            nm._ingest_dev(dev, inds, d, None, None, None, {}, 20, 100, 2)
+        got = nm.ingest(inds, d, None, None, None, {}, 20, 100, 2, dev=dev)
+        exp = nm.ingest_native(inds, d, None, None, None, {}, 20, 100, 2) if name != "exotic" else \
+            nm.ingest_py(inds, d, None, None, None, {}, 20, 100, 2)
+        assert got[0] == exp[0] and got[1] == exp[1]
+        assert np.array_equal(np.asarray(got[2]), np.asarray(exp[2]))

@@ -291,3 +291,18 @@ def test_bgzf_many_members_linear_time(tmp_path):
     assert list(ing.status) == [0, 0, 0] and ing.m > 50_000
     assert time.perf_counter() - t1 < 5.0, "BGZF inflate is not linear"
     assert t1 - t0 < 120
+
+
+def test_zero_padding_after_members(tmp_path):
+    """CPython's gzip reader (the reference's gzip.open) skips zero bytes after
+    a member; the native ingest does too."""
+    rng = np.random.default_rng(3)
+    d = tmp_path / "md"
+    d.mkdir()
+    lines = "".join(_rand_lines(rng, 3000)).encode()
+    blob = gzip.compress(lines[:40000]) + b"\x00" * 9 + gzip.compress(lines[40000:]) + b"\x00" * 3
+    (d / "Z1.regions.bed.gz").write_bytes(blob)
+    assert gzip.decompress(blob) == lines
+    a, b = _both(d, ["Z1"], threads=1)
+    _same(a, b)
+    assert a[2].shape[1] > 1000
