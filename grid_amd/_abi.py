@@ -114,6 +114,8 @@ _SIGS = {
     "grid_ingest_free": [_vp],
     "grid_gunzip_batch": [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp],
     "grid_gz_text_size": [_vp, _i64, C.POINTER(_i64), C.POINTER(_i32)],
+    "grid_gz_members": [_vp, _i64, _vp, _vp, _vp, _i32, C.POINTER(_i32)],
+    "grid_gunzip_host": [_vp, _i64, _vp, _i64, C.POINTER(_i64), C.POINTER(_i32)],
     "grid_md_count": [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp],
     "grid_md_parse_ref": [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp,
                           C.POINTER(_i64), C.POINTER(_i32)],
@@ -464,6 +466,36 @@ def gz_text_size(buf) -> tuple[int, int] | None:
         return None
     check(rc, "grid_gz_text_size")
     return size.value, m.value
+
+
+def gz_members(buf):
+    """BGZF members of a gzip file held in ``buf``: (offsets, lengths, isizes)
+    int64/int64/uint32 arrays, or None if the file is not BGZF throughout."""
+    a = np.frombuffer(buf, np.uint8) if not isinstance(buf, np.ndarray) else buf
+    cap = max(16, a.size // 8192 + 16)
+    for _ in range(2):
+        st, ln, isz = np.empty(cap, np.int64), np.empty(cap, np.int64), np.empty(cap, np.uint32)
+        cnt = _i32()
+        rc = load().grid_gz_members(a.ctypes.data if a.size else None, a.size, st.ctypes.data, ln.ctypes.data,
+                                    isz.ctypes.data, cap, C.byref(cnt))
+        if rc == GRID_EUNSUPPORTED:
+            return None
+        check(rc, "grid_gz_members")
+        if cnt.value <= cap:
+            k = cnt.value
+            return st[:k], ln[:k], isz[:k]
+        cap = cnt.value
+    raise GridNativeError("grid_gz_members: member count changed")
+
+
+def gunzip_host(src, out) -> tuple[int, int]:
+    """Inflate the gzip file in ``src`` into the uint8 array ``out`` (host,
+    libdeflate or zlib; releases the GIL).  Returns (status GZ_*, bytes)."""
+    a = np.frombuffer(src, np.uint8) if not isinstance(src, np.ndarray) else src
+    n, st = _i64(), _i32()
+    call("grid_gunzip_host", a.ctypes.data if a.size else None, a.size, out.ctypes.data if out.size else None,
+         out.size, C.byref(n), C.byref(st))
+    return st.value, n.value
 
 
 class Depth16Desc(C.Structure):

@@ -9,9 +9,14 @@
 // output.  Per wave: a 32 KiB ring in LDS holds the DEFLATE window (every
 // distance is <= 32768 back, and the region a copy overwrites is never read
 // by a later copy of the same window), output leaves the ring in 4 KiB
-// pieces of 16-B stores; the compressed bytes are read through a 256-B
-// window in one VGPR (lane k holds bytes 4k..4k+3).  The bit-level decoder
-// is inflate_core.hpp, the same code the host model runs against zlib.
+// pieces of 16-B stores; the compressed bytes are read through 256-B
+// windows held in one VGPR each (lane k holds bytes 4k..4k+3).  The bit-level
+// decoder is inflate_core.hpp (headers, tables, stored blocks, the last
+// symbols of a stream); a block's codes run in fast_codes below: 64-bit bit
+// buffer refilled 8 bytes at a time from two windows (the next one loaded
+// ahead), one u32 table entry per literal/length or distance code that
+// carries the base and extra-bit count, literals written to the ring 8 at a
+// time, copies without a division.
 //
 // k_gz_crc: one workgroup per file checks every member's CRC-32 and size
 // (gzip's trailer): lanes compute the raw CRC register of 256 byte ranges
@@ -27,32 +32,64 @@ constexpr int RING = 32768, RMASK = RING - 1, FLUSH = 4096;
 
 __constant__ uint32_t c_crc_pow[48][32];   // columns of M^(2^k), M = one zero byte
 
+// Fast-table entries (u32, LDS), 0 = no entry (a longer code: decode slowly).
+// literal/length table (2^LFAST):
+//   [31:16] literal byte | length base | symbol (kind 0), [15:11] length
+//   symbol - 257, [10:8] extra bits, [7:4] kind, [3:0] code length
+// distance table (2^DFAST; the code-length code while a header is read):
+//   [31:17] distance base, [16:12] symbol, [11:8] extra bits, [7:4] kind,
+//   [3:0] code length
+// kind 0 = a symbol the fast loop does not take (286, 287, distance 30, 31)
+constexpr uint32_t K_LIT = 1, K_LEN = 2, K_EOB = 3, K_DIST = 1;
+constexpr int F_LEN = 1 << icore::LFAST, F_DIST = 1 << icore::DFAST;
+
+__device__ __forceinline__ uint32_t fast_entry(int ft, uint32_t sym, uint32_t l) {
+  if (ft == icore::FT_LEN) {
+    if (sym < 256) return (sym << 16) | (K_LIT << 4) | l;
+    if (sym == 256) return (K_EOB << 4) | l;
+    if (sym < 286)
+      return ((uint32_t)icore::kLenBase[sym - 257] << 16) | ((sym - 257) << 11) |
+             ((uint32_t)icore::kLenExtra[sym - 257] << 8) | (K_LEN << 4) | l;
+    return (sym << 16) | l;
+  }
+  if (sym < 30)
+    return ((uint32_t)icore::kDistBase[sym] << 17) | (sym << 12) | ((uint32_t)icore::kDistExtra[sym] << 8) |
+           (K_DIST << 4) | l;
+  return (sym << 12) | l;
+}
+
 struct DevP {
   const uint8_t *src;
   int64_t n_in;
-  uint16_t *tab;                 // LDS
+  uint16_t *tab;                 // LDS: the core's u16 slots
+  uint32_t *ftab;                // LDS: F_LEN literal/length entries, then F_DIST distance entries
   uint8_t *ring;                 // LDS
   uint8_t *out;                  // global
   int64_t cap;
   int64_t pos, flushed, mstart;
   grid_gz_member *mem;
   int nmem, mcap, lane;
-  uint32_t win;                  // input window: lane k = bytes wbase + 4k .. + 3
+  uint32_t win;                  // core input window: lane k = bytes wbase + 4k .. + 3
   int64_t wbase;
+  uint32_t fcur, fnxt;           // fast_codes' windows: bytes fbase .. +256, +256 .. +512
+  int64_t fbase;
 
+  __device__ __forceinline__ uint32_t load_word(int64_t b) const {
+    const int64_t o = b + 4 * lane;
+    uint32_t w = 0;
+    if (o + 4 <= n_in) {
+      w = *reinterpret_cast<const uint32_t *>(src + o);
+    } else {
+      for (int k = 0; k < 4; k++)
+        if (o + k < n_in) w |= (uint32_t)src[o + k] << (8 * k);
+    }
+    return w;
+  }
   __device__ __forceinline__ uint8_t in(int64_t i) {
     const int64_t b = i & ~(int64_t)255;
     if (b != wbase) {
       wbase = b;
-      const int64_t o = b + 4 * lane;
-      uint32_t w = 0;
-      if (o + 4 <= n_in) {
-        w = *reinterpret_cast<const uint32_t *>(src + o);
-      } else {
-        for (int k = 0; k < 4; k++)
-          if (o + k < n_in) w |= (uint32_t)src[o + k] << (8 * k);
-      }
-      win = w;
+      win = load_word(b);
     }
     const int r = (int)(i - wbase);
     const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)win, r >> 2);
@@ -69,16 +106,42 @@ struct DevP {
     for (int k = lane; k < n; k += 64) tab[i + k] = v;
     __builtin_amdgcn_wave_barrier();
   }
-  __device__ __forceinline__ void stride_fill(int i, int st, int n, uint16_t v) {
-    for (int k = lane; k < n; k += 64) tab[i + k * st] = v;
+  __device__ __forceinline__ void fclear(int ft, int n) {
+    uint32_t *t = ftab + (ft == icore::FT_LEN ? 0 : F_LEN);
+    for (int k = lane; k < n; k += 64) t[k] = 0;
     __builtin_amdgcn_wave_barrier();
+  }
+  __device__ __forceinline__ void fput(int ft, int i, int st, int n, uint32_t sym, uint32_t l) {
+    const uint32_t v = fast_entry(ft, sym, l);
+    uint32_t *t = ftab + (ft == icore::FT_LEN ? 0 : F_LEN);
+    for (int k = lane; k < n; k += 64) t[i + k * st] = v;
+    __builtin_amdgcn_wave_barrier();
+  }
+  __device__ __forceinline__ uint32_t ftab_rd(int i) const {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)ftab[i]);
+  }
+  __device__ __forceinline__ uint32_t frd(int ft, int i) const {   // sym << 4 | len, 0 = none
+    if (ft == icore::FT_LEN) {
+      const uint32_t e = ftab_rd(i), kind = (e >> 4) & 15;
+      if (!e) return 0;
+      const uint32_t sym = kind == K_LEN ? 257 + ((e >> 11) & 31) : kind == K_EOB ? 256 : e >> 16;
+      return (sym << 4) | (e & 15);
+    }
+    const uint32_t e = ftab_rd(F_LEN + i);
+    return e ? ((((e >> 12) & 31) << 4) | (e & 15)) : 0;
   }
   __device__ __forceinline__ void flush_full() {
     while (pos - flushed >= FLUSH) {
-      const uint4 *s = reinterpret_cast<const uint4 *>(ring + (flushed & RMASK));
-      uint4 *d = reinterpret_cast<uint4 *>(out + flushed);
+      if (((uintptr_t)(out + flushed) & 15) == 0) {
+        const uint4 *s = reinterpret_cast<const uint4 *>(ring + (flushed & RMASK));
+        uint4 *d = reinterpret_cast<uint4 *>(out + flushed);
 #pragma unroll
-      for (int k = 0; k < FLUSH / 1024; k++) d[k * 64 + lane] = s[k * 64 + lane];
+        for (int k = 0; k < FLUSH / 1024; k++) d[k * 64 + lane] = s[k * 64 + lane];
+      } else {                          // a stream whose output does not start 16-B aligned
+        const uint8_t *s = ring + (flushed & RMASK);
+        uint8_t *d = out + flushed;
+        for (int k = lane; k < FLUSH; k += 64) d[k] = s[k];
+      }
       flushed += FLUSH;
     }
   }
@@ -94,24 +157,182 @@ struct DevP {
     if (pos - flushed >= FLUSH) flush_full();
     return true;
   }
+  // lane k moves byte k of the match; an overlapping match (dist < len)
+  // repeats its first dist bytes, so byte k comes from k mod dist, which
+  // precedes pos: (k + 0.5) / dist is >= 0.5 / 258 from any integer, far
+  // more than the reciprocal's error, so the quotient below is exact
+  __device__ __forceinline__ void copy_bytes(uint32_t dist, uint32_t len) {
+    const int64_t s0 = pos - dist;
+    const float rdist = __builtin_amdgcn_rcpf((float)dist);
+    for (uint32_t k0 = 0; k0 < len; k0 += 64) {
+      const uint32_t k = k0 + lane;
+      if (k < len) {
+        const uint32_t j = dist >= len ? k : k - dist * (uint32_t)(((float)k + 0.5f) * rdist);
+        ring[(pos + k) & RMASK] = ring[(s0 + j) & RMASK];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    pos += len;
+  }
   __device__ __forceinline__ int copy(uint32_t dist, int len) {
     if ((int64_t)dist > pos - mstart) return icore::E_DATA;
     if (pos + len > cap) return icore::E_SPACE;
-    for (int k0 = 0; k0 < len; k0 += 64) {
-      const int k = k0 + lane;
-      uint8_t v = 0;
-      if (k < len) {
-        const int j = k < (int)dist ? k : k % (int)dist;
-        v = ring[(pos - dist + j) & RMASK];
-      }
-      __builtin_amdgcn_wave_barrier();
-      if (k < len) ring[(pos + k) & RMASK] = v;
-      __builtin_amdgcn_wave_barrier();
-    }
-    pos += len;
+    copy_bytes(dist, (uint32_t)len);
     if (pos - flushed >= FLUSH) flush_full();
     return 0;
   }
+  __device__ __forceinline__ void put_lits(uint64_t lit, int n) {   // n bytes at pos
+    if (lane < n) ring[(pos + lane) & RMASK] = (uint8_t)(lit >> (8 * lane));
+    __builtin_amdgcn_wave_barrier();
+    pos += n;
+  }
+  __device__ __forceinline__ uint32_t fword(int i) const {   // word i of fcur|fnxt, i < 128
+    return (uint32_t)(i < 64 ? __builtin_amdgcn_readlane((int)fcur, i) : __builtin_amdgcn_readlane((int)fnxt, i - 64));
+  }
+
+  // everything but a fast literal, for fast_codes: false = leave the loop
+  // (ret: 1 end of block, -1 error, 0 out of room)
+  template <class I>
+  __device__ __forceinline__ bool nonlit(I &inf, uint32_t e, uint64_t &bb, int &bc, uint64_t &lit, int &nl,
+                                         int &ret) {
+    auto slow = [&](int co, int so) -> int {   // puff's canonical walk (-1: no such code)
+      int code = 0, first = 0, index = 0;
+      for (int l = 1; l < 16; l++) {
+        code |= (int)(bb & 1);
+        bb >>= 1;
+        bc--;
+        const int count = rd(co + l);
+        if (code - count < first) return rd(so + index + (code - first));
+        index += count;
+        first += count;
+        first <<= 1;
+        code <<= 1;
+      }
+      return -1;
+    };
+    const uint32_t kind = (e >> 4) & 15;
+    uint32_t len;
+    if (kind == K_LEN) {
+      const int l = e & 15, x = (e >> 8) & 7;
+      len = (e >> 16) + (uint32_t)((bb >> l) & ((1u << x) - 1));
+      bb >>= l + x;
+      bc -= l + x;
+    } else if (kind == K_EOB) {
+      const int l = e & 15;
+      bb >>= l;
+      bc -= l;
+      ret = 1;
+      return false;
+    } else {                            // a code longer than LFAST bits, or 286/287
+      const int sym = slow(icore::T_LCNT, icore::T_LSYM);
+      if (sym < 0 || sym > 285) { inf.err = icore::E_DATA; ret = -1; return false; }
+      if (sym == 256) { ret = 1; return false; }
+      if (sym < 256) {
+        lit |= (uint64_t)sym << (8 * nl);
+        if (++nl == 8) {
+          put_lits(lit, 8);
+          lit = 0;
+          nl = 0;
+          if (pos - flushed >= FLUSH) flush_full();
+          return pos + 296 <= cap;
+        }
+        return true;
+      }
+      const int x = icore::kLenExtra[sym - 257];
+      len = icore::kLenBase[sym - 257] + (uint32_t)(bb & ((1u << x) - 1));
+      bb >>= x;
+      bc -= x;
+    }
+    const uint32_t d = ftab_rd(F_LEN + (int)(bb & (F_DIST - 1)));
+    uint32_t dist;
+    if (((d >> 4) & 15) == K_DIST) {
+      const int l = d & 15, x = (d >> 8) & 15;
+      dist = (d >> 17) + (uint32_t)((bb >> l) & ((1u << x) - 1));
+      bb >>= l + x;
+      bc -= l + x;
+    } else {
+      const int ds = slow(icore::T_DCNT, icore::T_DSYM);
+      if (ds < 0 || ds >= 30) { inf.err = icore::E_DATA; ret = -1; return false; }
+      const int x = icore::kDistExtra[ds];
+      dist = icore::kDistBase[ds] + (uint32_t)(bb & ((1u << x) - 1));
+      bb >>= x;
+      bc -= x;
+    }
+    if (nl) {
+      put_lits(lit, nl);
+      lit = 0;
+      nl = 0;
+    }
+    if ((int64_t)dist > pos - mstart) { inf.err = icore::E_DATA; ret = -1; return false; }
+    copy_bytes(dist, len);
+    if (pos - flushed >= FLUSH) flush_full();
+    return pos + 296 <= cap;
+  }
+
+  // A block's codes while >= 16 input bytes and >= 296 bytes of output room
+  // remain.  Returns 1 after the end-of-block code, -1 on an error (err set),
+  // 0 when the core's per-symbol loop must finish the block.  Literals wait
+  // in `lit` (8 at most) and reach the ring together; pos excludes them.
+  // Self-contained (no call into the core: its state would crowd the scalar
+  // registers of this loop): every iteration starts with >= 48 bits in bb,
+  // enough for the longest symbol (15 + 5 length bits, 15 + 13 distance).
+  template <class I>
+  __device__ int fast_codes(I &inf) {
+    if (pos + 296 > cap) return 0;
+    if (inf.ip - fbase < 0 || inf.ip - fbase >= 256) {
+      fbase = inf.ip & ~(int64_t)255;
+      fcur = load_word(fbase);
+      fnxt = load_word(fbase + 256);
+    }
+    uint64_t bb = inf.bb, lit = 0;
+    int bc = inf.bc, nl = 0, ret = 0;
+    int64_t ip = inf.ip;
+    // one loop, one exit (`go`): the literal path goes straight back to the
+    // top, everything else is rarer
+    bool go = true;
+    while (go) {
+      if (bc < 48) {                    // 8 more bytes, of which (63 - bc) / 8 are kept
+        if (ip + 16 > n_in) {
+          go = false;
+          continue;
+        }
+        if (ip - fbase >= 256) {         // ip moved < 256 since the last refill
+          fbase += 256;
+          fcur = fnxt;
+          fnxt = load_word(fbase + 256);
+        }
+        const int r = (int)(ip - fbase), i = r >> 2, sh = (r & 3) * 8;
+        const uint64_t lo = (uint64_t)fword(i) | ((uint64_t)fword(i + 1) << 32);
+        const uint64_t v = sh ? (lo >> sh) | ((uint64_t)fword(i + 2) << (64 - sh)) : lo;
+        bb |= v << bc;
+        const int take = (63 - bc) >> 3;
+        ip += take;
+        bc += take * 8;
+      }
+      const uint32_t e = ftab_rd((int)(bb & (F_LEN - 1)));
+      if (((e >> 4) & 15) == K_LIT) {
+        const int l = e & 15;
+        bb >>= l;
+        bc -= l;
+        lit |= (uint64_t)(e >> 16) << (8 * nl);
+        if (++nl == 8) {
+          put_lits(lit, 8);
+          lit = 0;
+          nl = 0;
+          if (pos - flushed >= FLUSH) flush_full();
+          go = pos + 296 <= cap;
+        }
+        continue;
+      }
+      go = nonlit(inf, e, bb, bc, lit, nl, ret);
+    }
+    if (nl) put_lits(lit, nl);
+    inf.bb = bb;
+    inf.bc = bc;
+    inf.ip = ip;
+    return ret;
+  }
+
   __device__ __forceinline__ bool member(uint32_t crc, uint32_t isz) {
     if ((uint32_t)(pos - mstart) != isz) return false;   // ISIZE = length mod 2^32
     if (nmem >= mcap) return false;
@@ -138,11 +359,19 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ src,
                                                 int32_t *__restrict__ nmem) {
   __shared__ __attribute__((aligned(16))) uint8_t s_ring[RING];
   __shared__ uint16_t s_tab[icore::T_SIZE];
+  __shared__ uint32_t s_ftab[F_LEN + F_DIST];   // 38.9 KiB in all: 4 waves per CU
   const int f = blockIdx.x;
   DevP p;
-  p.src = src + in_off[f];
-  p.n_in = in_len[f];
+  // the stream starts `skew` bytes into a 4-B aligned word (a BGZF member
+  // anywhere in its file): the decoder reads from the aligned word and
+  // starts at byte skew
+  const int64_t io = in_off[f];
+  const int skew = (int)(io & 3);
+  p.src = src + (io - skew);
+  p.n_in = in_len[f] + skew;
   p.tab = s_tab;
+  p.ftab = s_ftab;
+  p.fbase = -((int64_t)1 << 40);
   p.ring = s_ring;
   p.out = out + out_off[f];
   p.cap = out_cap[f];
@@ -154,7 +383,8 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ src,
   p.win = 0;
   p.wbase = -1;
   icore::Inflater<DevP> inf(p);
-  const int rc = p.n_in > 0 ? inf.gunzip() : (int)icore::E_HEADER;
+  inf.ip = skew;
+  const int rc = in_len[f] > 0 ? inf.gunzip() : (int)icore::E_HEADER;
   p.flush_full();
   p.flush_tail();
   if (threadIdx.x == 0) {

@@ -5,9 +5,16 @@
 //   P::in(i)            compressed byte i (0 <= i < P::n_in)
 //   P::put(b)           append one output byte
 //   P::copy(dist, len)  append len bytes starting dist back (may overlap)
-//   P::rd(i) / wr(i, v) the decode tables (u16 slots the policy owns; the
-//                       device keeps them in LDS, written by one lane)
+//   P::rd(i) / wr(i, v) the u16 table slots below (the device keeps them in
+//                       LDS, written by one lane)
+//   P::fclear(ft, n) / fput(ft, i, stride, n, sym, len) / frd(ft, i)
+//                       the FAST tables ft = FT_LEN (literal/length) and
+//                       FT_DIST (distance, and the code-length code while the
+//                       dynamic header is read): frd returns sym << 4 | len,
+//                       0 = no entry; the policy stores them as it likes
 //   P::member(crc, isz) a gzip member's trailer, after its deflate stream
+//   P::fast_codes(inflater)  an optional faster loop over a block's codes
+//                       (see codes()); returning 0 = none
 // The decoder never reads output it did not write and never writes past the
 // caller's output capacity (P::put / copy report overflow).
 //
@@ -27,10 +34,10 @@
 namespace icore {
 
 constexpr int LFAST = 10, DFAST = 8;
-// u16 slots of the table area: litlen fast, dist fast, litlen count/symbols,
-// dist count/symbols, code-length code count/symbols, lengths scratch
-constexpr int T_LFAST = 0, T_DFAST = T_LFAST + (1 << LFAST), T_LCNT = T_DFAST + (1 << DFAST),
-              T_LSYM = T_LCNT + 16, T_DCNT = T_LSYM + 288, T_DSYM = T_DCNT + 16, T_CCNT = T_DSYM + 32,
+constexpr int FT_LEN = 0, FT_DIST = 1;   // the fast tables (policy-owned)
+// u16 slots of the table area: litlen count/symbols, dist count/symbols,
+// code-length code count/symbols, lengths scratch, offsets scratch
+constexpr int T_LCNT = 0, T_LSYM = T_LCNT + 16, T_DCNT = T_LSYM + 288, T_DSYM = T_DCNT + 16, T_CCNT = T_DSYM + 32,
               T_CSYM = T_CCNT + 16, T_LENS = T_CSYM + 19, T_OFFS = T_LENS + 320, T_SIZE = T_OFFS + 16;
 
 enum Status : int { OK = 0, E_DATA = 1, E_TRUNC = 2, E_SPACE = 3, E_HEADER = 4 };
@@ -89,9 +96,9 @@ struct Inflater {
   }
   IC_HD bool past_end() const { return byte_pos() > p.n_in; }
 
-  // canonical table build from lengths[0..n) (0 = unused): fast table of
-  // 2^fast entries at tab[fo], count[16] at tab[co], symbols sorted at tab[so]
-  IC_HD bool build(const int lo, int n, int fast, int fo, int co, int so) {
+  // canonical table build from lengths[0..n) (0 = unused): fast table ft of
+  // 2^fast entries, count[16] at tab[co], symbols sorted at tab[so]
+  IC_HD bool build(const int lo, int n, int fast, int ft, int co, int so) {
     // lengths are the table slots [lo, lo + n)
     for (int l = 0; l < 16; l++) p.wr(co + l, 0);
     for (int s = 0; s < n; s++) {
@@ -115,7 +122,7 @@ struct Inflater {
         p.wr(T_OFFS + l, (uint16_t)(o + 1));
       }
     }
-    p.fill(fo, 1 << fast, 0);
+    p.fclear(ft, 1 << fast);
     // walk the canonical codes in order, reversed into LSB-first indices
     int code = 0, idx = 0;
     for (int l = 1; l <= fast; l++) {
@@ -123,7 +130,7 @@ struct Inflater {
       for (int k = 0; k < cnt; k++, idx++) {
         int rev = 0;
         for (int b = 0; b < l; b++) rev |= ((code >> b) & 1) << (l - 1 - b);
-        p.stride_fill(fo + rev, 1 << l, 1 << (fast - l), (uint16_t)((p.rd(so + idx) << 4) | l));
+        p.fput(ft, rev, 1 << l, 1 << (fast - l), p.rd(so + idx), l);
         code++;
       }
       code <<= 1;
@@ -146,10 +153,10 @@ struct Inflater {
     err = E_DATA;
     return -1;
   }
-  IC_HD int decode(int fo, int fast, int co, int so) {
+  IC_HD int decode(int ft, int fast, int co, int so) {
     if (bc < 16) refill();
     if (err) return -1;
-    const uint16_t e = p.rd(fo + (int)(bb & ((1u << fast) - 1)));
+    const uint32_t e = p.frd(ft, (int)(bb & ((1u << fast) - 1)));
     if (e) {
       const int l = e & 15;
       bb >>= l;
@@ -164,20 +171,20 @@ struct Inflater {
     p.fill(T_LENS + 144, 112, 9);
     p.fill(T_LENS + 256, 24, 7);
     p.fill(T_LENS + 280, 8, 8);
-    if (!build(T_LENS, 288, LFAST, T_LFAST, T_LCNT, T_LSYM)) return false;
+    if (!build(T_LENS, 288, LFAST, FT_LEN, T_LCNT, T_LSYM)) return false;
     p.fill(T_LENS, 30, 5);
-    return build(T_LENS, 30, DFAST, T_DFAST, T_DCNT, T_DSYM);
+    return build(T_LENS, 30, DFAST, FT_DIST, T_DCNT, T_DSYM);
   }
 
   IC_HD bool dynamic_tables() {
     const int nlen = (int)bits(5) + 257, ndist = (int)bits(5) + 1, ncode = (int)bits(4) + 4;
     if (nlen > 286 || ndist > 30) return false;
     for (int i = 0; i < 19; i++) p.wr(T_LENS + kClOrder[i], i < ncode ? (uint16_t)bits(3) : 0);
-    // code-length code: its fast table shares the dist fast slots (DFAST >= 7)
-    if (!build(T_LENS, 19, 7, T_DFAST, T_CCNT, T_CSYM)) return false;
+    // code-length code: its fast table is the distance one (DFAST >= 7)
+    if (!build(T_LENS, 19, 7, FT_DIST, T_CCNT, T_CSYM)) return false;
     int idx = 0;
     while (idx < nlen + ndist) {
-      const int sym = decode(T_DFAST, 7, T_CCNT, T_CSYM);
+      const int sym = decode(FT_DIST, 7, T_CCNT, T_CSYM);
       if (sym < 0 || err) return false;
       if (sym < 16) {
         p.wr(T_LENS + idx++, (uint16_t)sym);
@@ -199,14 +206,20 @@ struct Inflater {
       idx += rep;
     }
     if (p.rd(T_LENS + 256) == 0) return false;   // no end-of-block code
-    if (!build(T_LENS, nlen, LFAST, T_LFAST, T_LCNT, T_LSYM)) return false;
+    if (!build(T_LENS, nlen, LFAST, FT_LEN, T_LCNT, T_LSYM)) return false;
     // the distance lengths follow the literal/length ones in the same slots
-    return build(T_LENS + nlen, ndist, DFAST, T_DFAST, T_DCNT, T_DSYM);
+    return build(T_LENS + nlen, ndist, DFAST, FT_DIST, T_DCNT, T_DSYM);
   }
 
   IC_HD bool codes() {
+    // the policy's own loop first (the device's: inflate.hip fast_codes); it
+    // hands back at the end of the block (1), on an error (-1, err set), or
+    // near the end of the input or the output room (0: this loop finishes)
+    const int f = p.fast_codes(*this);
+    if (f > 0) return true;
+    if (f < 0) return false;
     for (;;) {
-      int sym = decode(T_LFAST, LFAST, T_LCNT, T_LSYM);
+      int sym = decode(FT_LEN, LFAST, T_LCNT, T_LSYM);
       if (sym < 0 || err) return false;
       if (sym < 256) {
         if (!p.put((uint8_t)sym)) { err = E_SPACE; return false; }
@@ -216,7 +229,7 @@ struct Inflater {
       sym -= 257;
       if (sym >= 29) return false;
       const int len = kLenBase[sym] + (int)bits(kLenExtra[sym]);
-      const int ds = decode(T_DFAST, DFAST, T_DCNT, T_DSYM);
+      const int ds = decode(FT_DIST, DFAST, T_DCNT, T_DSYM);
       if (ds < 0 || ds >= 30 || err) return false;
       const uint32_t dist = kDistBase[ds] + bits(kDistExtra[ds]);
       if (past_end()) { err = E_TRUNC; return false; }
@@ -287,9 +300,8 @@ struct Inflater {
       const uint32_t last = bits(1), type = bits(2);
       bool ok;
       if (type == 0) ok = stored();
-      else if (type == 1) ok = fixed_tables() && codes();
-      else if (type == 2) ok = dynamic_tables() && codes();
-      else ok = false;
+      else if (type == 3) ok = false;
+      else ok = (type == 1 ? fixed_tables() : dynamic_tables()) && codes();   // one codes() site
       if (!ok) return err ? err : E_DATA;
       if (past_end()) return E_TRUNC;
       if (last) return OK;

@@ -848,6 +848,102 @@ int grid_ingest_fill(grid_ingest *h, const int32_t *row_of_file, int32_t *q, int
   return GRID_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// BGZF member walk: fn(start, bsize, isize) per member; false if some member
+// is not BGZF (then nothing is known about the rest)
+template <class F>
+bool bgzf_walk(const uint8_t *buf, int64_t n, F fn) {
+  int64_t pos = 0;
+  while (pos < n) {
+    const unsigned char *h = buf + pos;
+    const int64_t rest = n - pos;
+    if (rest < 18 || h[0] != 0x1f || h[1] != 0x8b || !(h[3] & 4)) return false;
+    const int64_t xlen = (int64_t)h[10] | ((int64_t)h[11] << 8);
+    int64_t k = 12, bsize = -1;
+    while (k + 4 <= 12 + xlen && 12 + xlen <= rest) {
+      const int64_t sl = (int64_t)h[k + 2] | ((int64_t)h[k + 3] << 8);
+      if (h[k] == 'B' && h[k + 1] == 'C' && sl == 2) bsize = ((int64_t)h[k + 4] | ((int64_t)h[k + 5] << 8)) + 1;
+      k += 4 + sl;
+    }
+    if (bsize < 18 + xlen || bsize > rest) return false;
+    uint32_t isz;
+    memcpy(&isz, h + bsize - 4, 4);
+    fn(pos, bsize, isz);
+    pos += bsize;
+    while (pos < n && buf[pos] == 0) pos++;
+  }
+  return true;
+}
+
+// every member of in[0, n) through zlib into out[0, cap)
+int gunzip_zlib(const uint8_t *in, int64_t n, uint8_t *out, int64_t cap, int64_t *out_len) {
+  z_stream z{};
+  if (inflateInit2(&z, 16 + 15) != Z_OK) return GRID_GZ_EDATA;
+  int64_t pos = 0, got = 0;
+  int rc = GRID_OK;
+  while (pos < n) {
+    z.next_in = const_cast<Bytef *>(in + pos);
+    z.next_out = out + got;
+    int zr = Z_OK;
+    int64_t in0 = pos, out0 = got;
+    for (;;) {
+      const int64_t ain = std::min<int64_t>(n - in0, 1 << 30), aout = std::min<int64_t>(cap - out0, 1 << 30);
+      z.avail_in = (uInt)ain;
+      z.avail_out = (uInt)aout;
+      zr = inflate(&z, Z_NO_FLUSH);
+      in0 += ain - z.avail_in;
+      out0 += aout - z.avail_out;
+      if (zr == Z_STREAM_END) break;
+      if (zr != Z_OK && zr != Z_BUF_ERROR) break;
+      if (out0 >= cap && z.avail_out == 0) { zr = Z_MEM_ERROR; break; }   // no room left
+      if (ain - z.avail_in == 0 && aout - z.avail_out == 0) break;           // no progress: truncated
+    }
+    if (zr != Z_STREAM_END) {
+      rc = zr == Z_MEM_ERROR ? GRID_GZ_ESPACE : GRID_GZ_EDATA;
+      break;
+    }
+    pos = in0;
+    got = out0;
+    while (pos < n && in[pos] == 0) pos++;
+    inflateReset(&z);
+  }
+  inflateEnd(&z);
+  *out_len = got;
+  return rc;
+}
+// every member of in[0, n) into out[0, cap): libdeflate, else zlib; a GRID_GZ_* status
+int gunzip_any(const uint8_t *in, int64_t n, uint8_t *out, int64_t cap, int64_t *out_len) {
+  if (n < 18 || in[0] != 0x1f || in[1] != 0x8b) return GRID_GZ_EHEADER;
+  const fastgz::Api &a = fastgz::api();
+  if (a.ok) {
+    void *d = a.alloc_d();
+    if (d) {
+      int64_t pos = 0, got = 0;
+      int rc = GRID_OK;
+      while (pos < n) {
+        size_t used = 0, g = 0;
+        const int r = a.gzip_dec_ex(d, in + pos, (size_t)(n - pos), out + got, (size_t)(cap - got), &used, &g);
+        if (r != 0) {           // 3 = LIBDEFLATE_INSUFFICIENT_SPACE
+          rc = r == 3 ? GRID_GZ_ESPACE : GRID_GZ_EDATA;
+          break;
+        }
+        got += (int64_t)g;
+        pos += (int64_t)used;
+        while (pos < n && in[pos] == 0) pos++;
+      }
+      a.free_d(d);
+      *out_len = got;
+      return rc;
+    }
+  }
+  return gunzip_zlib(in, n, out, cap, out_len);
+}
+}  // namespace
+
+extern "C" {
+
 int grid_gz_text_size(const uint8_t *buf, int64_t n, int64_t *size, int32_t *members) {
   if (!buf || !size || !members || n < 0) {
     grid_set_error("grid_gz_text_size: bad args");
@@ -858,29 +954,9 @@ int grid_gz_text_size(const uint8_t *buf, int64_t n, int64_t *size, int32_t *mem
   if (n < 18 || buf[0] != 0x1f || buf[1] != 0x8b) return GRID_EUNSUPPORTED;
   // BGZF (what mosdepth writes): every member says its length ("BC" extra
   // subfield), its ISIZE is its last 4 bytes; zero padding may follow
-  int64_t pos = 0, tot = 0;
+  int64_t tot = 0;
   int32_t m = 0;
-  bool bgzf = true;
-  while (pos < n) {
-    const unsigned char *h = buf + pos;
-    const int64_t rest = n - pos;
-    if (rest < 18 || h[0] != 0x1f || h[1] != 0x8b || !(h[3] & 4)) { bgzf = false; break; }
-    const int64_t xlen = (int64_t)h[10] | ((int64_t)h[11] << 8);
-    int64_t k = 12, bsize = -1;
-    while (k + 4 <= 12 + xlen && 12 + xlen <= rest) {
-      const int64_t sl = (int64_t)h[k + 2] | ((int64_t)h[k + 3] << 8);
-      if (h[k] == 'B' && h[k + 1] == 'C' && sl == 2) bsize = ((int64_t)h[k + 4] | ((int64_t)h[k + 5] << 8)) + 1;
-      k += 4 + sl;
-    }
-    if (bsize < 18 + xlen || bsize > rest) { bgzf = false; break; }
-    uint32_t isz;
-    memcpy(&isz, h + bsize - 4, 4);
-    tot += isz;
-    m++;
-    pos += bsize;
-    while (pos < n && buf[pos] == 0) pos++;
-  }
-  if (bgzf) {
+  if (bgzf_walk(buf, n, [&](int64_t, int64_t, uint32_t isz) { tot += isz; m++; })) {
     *size = tot;
     *members = m;
     return GRID_OK;
@@ -891,6 +967,35 @@ int grid_gz_text_size(const uint8_t *buf, int64_t n, int64_t *size, int32_t *mem
   memcpy(&isz, buf + n - 4, 4);
   *size = isz;
   *members = 1;
+  return GRID_OK;
+}
+
+int grid_gz_members(const uint8_t *buf, int64_t n, int64_t *start, int64_t *len, uint32_t *isize, int32_t cap,
+                    int32_t *count) {
+  if (!buf || !count || n < 0 || cap < 0 || (cap > 0 && (!start || !len || !isize))) {
+    grid_set_error("grid_gz_members: bad args");
+    return GRID_EINVAL;
+  }
+  int32_t m = 0;
+  const bool ok = n >= 18 && bgzf_walk(buf, n, [&](int64_t s, int64_t l, uint32_t isz) {
+    if (m < cap) {
+      start[m] = s;
+      len[m] = l;
+      isize[m] = isz;
+    }
+    m++;
+  });
+  *count = ok ? m : 0;
+  return ok ? GRID_OK : GRID_EUNSUPPORTED;
+}
+
+int grid_gunzip_host(const uint8_t *in, int64_t n, uint8_t *out, int64_t cap, int64_t *out_len, int32_t *status) {
+  if (!out_len || !status || n < 0 || cap < 0 || (n > 0 && !in) || (cap > 0 && !out)) {
+    grid_set_error("grid_gunzip_host: bad args");
+    return GRID_EINVAL;
+  }
+  *out_len = 0;
+  *status = gunzip_any(in, n, out, cap, out_len);
   return GRID_OK;
 }
 

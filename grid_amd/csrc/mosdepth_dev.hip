@@ -7,7 +7,7 @@
 //     the whole cohort: GRID_MD_EXOTIC), depth > 0, the window test and the
 //     repeat-mask test (1 kb keys of the normalised chromosome name);
 //   * records are keyed by (start, end) only (reference quirk Q1); the key
-//     list K is the reference file's kept keys (strictly increasing, else the
+//     list K is the reference file's keys, zero depths included (strictly increasing, else the
 //     host path), every other file's records are placed by K index: the
 //     reference file's line -> K-index map is tried first (same bins on the
 //     same lines: one compare), a binary search otherwise; a key outside K or
@@ -168,8 +168,30 @@ __device__ __forceinline__ bool key_lt(int64_t as, int64_t ae, const Key2 &b) {
   return as < b.s || (as == b.s && ae < b.e);
 }
 
-// MODE 0 (reference file): kept[i] = 1 and keys[i] = (s, e) for every kept
-// line i.  MODE 1 (map): Q[row(f)][K index] = q, kept[f] += 1.
+// 16-bit mask of the '\n' bytes of a 16-byte word (exact per byte)
+__device__ __forceinline__ uint32_t nl_mask16(const uint4 v) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t m = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t x = w[k] ^ 0x0A0A0A0Au;                          // '\n' -> 0
+    const uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);   // bit 7 of each zero byte
+    m |= (((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u)) << (4 * k);
+  }
+  return m;
+}
+
+// MODE 0 (reference file): kept[i] = 1 and keys[i] = (s, e) for every line i
+// that passes the prefix, window and mask tests, whatever its depth (a bin
+// the reference sample did not cover can be covered by another sample; a key
+// no file keeps gets count 0 and is never valid).  MODE 1 (map): every line
+// that also has depth > 0: Q[row(f)][K index] = q, kept[f] += 1.
+//
+// One workgroup per 64 KiB chunk: the chunk (and 16 bytes before it, up to
+// MAXLINE after it) is loaded into LDS with 16-byte loads all in flight; each
+// thread owns a 256-byte segment and parses the lines that START in it, found
+// from the newline bit masks of its 16 words; line numbers come from a block
+// scan of the per-segment newline counts.
 template <int MODE>
 __global__ __launch_bounds__(PTH) void k_md_parse(const uint8_t *__restrict__ text, const int64_t *__restrict__ toff,
                                                   const int64_t *__restrict__ tlen,
@@ -186,80 +208,138 @@ __global__ __launch_bounds__(PTH) void k_md_parse(const uint8_t *__restrict__ te
                                                   int32_t *__restrict__ Q, int64_t ldq,
                                                   const int32_t *__restrict__ qrow,
                                                   unsigned long long *__restrict__ kept) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_t[CH + MAXLINE + 32];
-  __shared__ int s_scan[PTH];
+  constexpr int HALO = 16, SPAN = HALO + CH + MAXLINE + 16;   // bytes a-16 .. a+CH+MAXLINE (+16 slack)
+  __shared__ __attribute__((aligned(16))) uint8_t s_t[SPAN];
+  __shared__ int s_wsum[PTH / 64];
   const int c = blockIdx.x, f = cfile[c], tid = threadIdx.x;
   const int64_t L = tlen[f], a = cstart[c], b = min(L, a + CH);
   const uint8_t *t = text + toff[f];
-  // s_t[16 + k] = byte a + k, for k in [-16, CH + MAXLINE) within the file
-  const int64_t lo = a - 16, hi = min(L, b + MAXLINE);
-  for (int64_t i = lo + tid; i < hi; i += PTH)
-    if (i >= 0) s_t[i - lo] = t[i];
-  // newlines in my segment [a + tid*SEG, ...) -> line index of my first start
-  const int64_t s0 = a + (int64_t)tid * SEG, s1 = min(b, s0 + SEG);
-  __syncthreads();
-  int nl = 0;
-  for (int64_t i = s0; i < s1; i++) nl += s_t[i - lo] == '\n';
-  s_scan[tid] = nl;
-  __syncthreads();
-  for (int d = 1; d < PTH; d <<= 1) {               // inclusive scan (Hillis-Steele)
-    const int v = tid >= d ? s_scan[tid - d] : 0;
-    __syncthreads();
-    s_scan[tid] += v;
-    __syncthreads();
-  }
-  int64_t idx = cline0[c] + (s_scan[tid] - nl);      // newlines in [0, s0)
-  int bad = 0;
-  unsigned long long nkept = 0;
-  for (int64_t x = s0; x < s1; x++) {
-    const bool start = x == 0 || s_t[x - 1 - lo] == '\n';
-    if (start) {
-      // the line [x, end): up to the next '\n' or the file end
-      const uint8_t *p = s_t + (x - lo);
-      const int64_t lim = min(L, x + MAXLINE + 1) - x;
-      int len = 0;
-      while (len < lim && p[len] != '\n') len++;
-      if (len == lim && x + len < L) {
-        bad |= GRID_MD_EXOTIC;                      // a line longer than MAXLINE
-      } else if (o.npre == 0 || (len >= o.npre && [&] {
-                   for (int k = 0; k < o.npre; k++)
-                     if (p[k] != (uint8_t)o.prefix[k]) return false;
-                   return true;
-                 }())) {
-        int clen;
-        int64_t s, e, q;
-        if (!md_line(p, len, clen, s, e, q)) {
-          bad |= GRID_MD_EXOTIC;
-        } else if (q > 0 && (!o.has_window || (e >= o.wstart && s <= o.wend)) && !md_masked(o, p, clen, s, e)) {
-          if (MODE == 0) {
-            if (idx < ref_cap) {
-              ref_kept[idx] = 1;
-              ref_keys[idx] = Key2{s, e};
-            } else {
-              bad |= GRID_MD_NOTINK;
-            }
-          } else {
-            int64_t j = idx < ref_nlines ? ref_kidx[idx] : -1;
-            if (j < 0 || K[j].s != s || K[j].e != e) {
-              int64_t l = 0, r = nK;                 // lower_bound of (s, e) in K
-              while (l < r) {
-                const int64_t m = (l + r) >> 1;
-                if (K[m].s < s || (K[m].s == s && K[m].e < e)) l = m + 1;
-                else r = m;
-              }
-              j = (l < nK && K[l].s == s && K[l].e == e) ? l : -1;
-            }
-            if (j < 0) {
-              bad |= GRID_MD_NOTINK;
-            } else {
-              Q[(int64_t)qrow[f] * ldq + j] = (int32_t)q;
-              nkept++;
-            }
-          }
+  // load [a - 16, min(L, b + MAXLINE)): whole 16-byte words inside the file
+  // (text offsets are 256-B aligned, chunk starts multiples of CH), the
+  // file's last partial word byte by byte, zeros past the file end
+  {
+    const int64_t lo = a - HALO, hi = min(L, b + MAXLINE);
+    constexpr int NW = SPAN / 16, G = 6;            // words; loads in flight per thread
+    for (int k0 = 0; k0 * PTH < NW; k0 += G) {
+      uint4 v[G];
+#pragma unroll
+      for (int k = 0; k < G; k++) {
+        const int w = tid + (k0 + k) * PTH;
+        const int64_t p = lo + 16 * (int64_t)w;
+        v[k] = make_uint4(0, 0, 0, 0);
+        if (w < NW && p >= 0 && p + 16 <= hi) v[k] = *reinterpret_cast<const uint4 *>(t + p);
+      }
+#pragma unroll
+      for (int k = 0; k < G; k++) {
+        const int w = tid + (k0 + k) * PTH;
+        const int64_t p = lo + 16 * (int64_t)w;
+        if (w >= NW) continue;
+        if (p >= 0 && p + 16 > hi && p < hi) {
+          uint8_t q[16];
+          for (int j = 0; j < 16; j++) q[j] = p + j < hi ? t[p + j] : 0;
+          v[k] = *reinterpret_cast<const uint4 *>(q);
         }
+        reinterpret_cast<uint4 *>(s_t)[w] = v[k];
       }
     }
-    if (s_t[x - lo] == '\n') idx++;
+  }
+  __syncthreads();
+  // my segment [s0, s1): its newline masks and count
+  const int64_t s0 = a + (int64_t)tid * SEG, s1 = min(b, s0 + SEG);
+  const int nw = s1 > s0 ? (int)((s1 - s0 + 15) / 16) : 0;
+  const uint4 *seg = reinterpret_cast<const uint4 *>(s_t + HALO + tid * SEG);
+  auto mask = [&](int k) {              // newlines of word k, inside the segment only
+    uint32_t mk = nl_mask16(seg[k]);
+    const int64_t rest = s1 - (s0 + 16 * k);
+    if (rest < 16) mk &= (1u << rest) - 1u;
+    return mk;
+  };
+  int nl = 0;
+  for (int k = 0; k < nw; k++) nl += __builtin_popcount(mask(k));
+  // newlines before my segment within the chunk: wave scan + wave sums
+  int incl = nl;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(incl, d, 64);
+    if ((tid & 63) >= d) incl += y;
+  }
+  if ((tid & 63) == 63) s_wsum[tid >> 6] = incl;
+  __syncthreads();
+  int before = incl - nl;
+  for (int w = 0; w < (tid >> 6); w++) before += s_wsum[w];
+  const int64_t idx0 = cline0[c] + before;               // line number of a line starting at s0
+  int bad = 0;
+  unsigned long long nkept = 0;
+  // one line: [x, x + len), its line number idx
+  auto line = [&](int64_t x, int len, int64_t idx) {
+    const uint8_t *p = s_t + HALO + (x - a);
+    if (o.npre != 0) {
+      if (len < o.npre) return;
+      for (int k = 0; k < o.npre; k++)
+        if (p[k] != (uint8_t)o.prefix[k]) return;
+    }
+    int clen;
+    int64_t s, e, q;
+    if (!md_line(p, len, clen, s, e, q)) {
+      bad |= GRID_MD_EXOTIC;
+      return;
+    }
+    if (!((MODE == 0 || q > 0) && (!o.has_window || (e >= o.wstart && s <= o.wend)) &&
+          !md_masked(o, p, clen, s, e)))
+      return;
+    if (MODE == 0) {
+      if (idx < ref_cap) {
+        ref_kept[idx] = 1;
+        ref_keys[idx] = Key2{s, e};
+      } else {
+        bad |= GRID_MD_NOTINK;
+      }
+    } else {
+      int64_t j = idx < ref_nlines ? ref_kidx[idx] : -1;
+      if (j < 0 || K[j].s != s || K[j].e != e) {
+        int64_t l = 0, r = nK;                 // lower_bound of (s, e) in K
+        while (l < r) {
+          const int64_t mid = (l + r) >> 1;
+          if (K[mid].s < s || (K[mid].s == s && K[mid].e < e)) l = mid + 1;
+          else r = mid;
+        }
+        j = (l < nK && K[l].s == s && K[l].e == e) ? l : -1;
+      }
+      if (j < 0) {
+        bad |= GRID_MD_NOTINK;
+      } else {
+        Q[(int64_t)qrow[f] * ldq + j] = (int32_t)q;
+        nkept++;
+      }
+    }
+  };
+  if (s1 > s0) {
+    // lines starting in [s0, s1): at s0 if it follows a newline (or starts
+    // the file), then after every newline of the segment but its last byte
+    int64_t cur = (s0 == 0 || s_t[HALO + (s0 - a) - 1] == '\n') ? s0 : -1;
+    int64_t idx = idx0;
+    for (int k = 0; k < nw; k++) {
+      uint32_t mk = mask(k);
+      while (mk) {
+        const int64_t y = s0 + 16 * k + __builtin_ctz(mk);   // a newline
+        mk &= mk - 1;
+        if (cur >= 0) {
+          const int64_t len = y - cur;
+          if (len > MAXLINE) bad |= GRID_MD_EXOTIC;
+          else line(cur, (int)len, idx);
+        }
+        idx++;
+        cur = y + 1 < s1 ? y + 1 : -1;
+      }
+    }
+    if (cur >= 0) {                     // the last line started here ends in a later segment
+      const uint8_t *p = s_t + HALO + (cur - a);
+      const int64_t lim = min(L, cur + MAXLINE + 1) - cur;
+      int len = 0;
+      while (len < lim && p[len] != '\n') len++;
+      if (len == lim && cur + len < L) bad |= GRID_MD_EXOTIC;    // longer than MAXLINE
+      else line(cur, len, idx);
+    }
   }
   if (bad) atomicOr(flags + f, bad);
   if (MODE == 1) {

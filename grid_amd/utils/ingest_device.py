@@ -3,13 +3,23 @@ hundredths depth matrix in HBM (R1-R4, normalize_mosdepth.py:96-112 and
 :218-416), for the cohorts the host parser would read the common way.
 
 Per batch of files (bounded compressed and text bytes): host threads read the
-compressed bytes into pinned memory, one copy to the device, the files are
-inflated there (grid_gunzip_batch: one wave per file, CRC-checked), cut in
-64 KiB chunks and parsed (grid_md_count / grid_md_parse_map: the reference's
-line filters, each record placed by its (start, end) in the key list K of the
-reference file).  Then the population means in file order, the valid
-columns, the empty-sample filter and the rows in sorted-ID order
-(grid_md_finish / grid_md_gather) -- the matrix never exists on the host.
+compressed bytes into pinned memory and find each file's BGZF members (what
+mosdepth writes: independent gzip members of <= 64 KiB text).  The batch's
+files are then inflated by the GPU and the host CPUs AT ONCE, split by a cost
+model whose rates are re-measured every batch (``_Split``):
+  * GPU (grid_gunzip_batch, CRC-checked): one wave per BGZF member -- a
+    member-granular work list that fills every CU -- or one wave per file for
+    a single-member gzip file (serial by nature: the model gives the GPU such
+    a file only when a wave's rate makes it worth it);
+  * CPU (grid_gunzip_host: libdeflate, zlib without it): threads inflate
+    whole files into pinned staging, copied to HBM on a second stream while
+    the GPU works.
+The text then is cut in 64 KiB chunks and parsed on the GPU (grid_md_count /
+grid_md_parse_map: the reference's line filters, each record placed by its
+(start, end) in the key list K of the reference file).  Then the population
+means in file order, the valid columns, the empty-sample filter and the rows
+in sorted-ID order (grid_md_finish / grid_md_gather) -- the matrix never
+exists on the host.
 
 Anything outside the common shape -- a line outside the canonical mosdepth
 grammar or a non-ASCII byte, reference keys that are not strictly
@@ -23,6 +33,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import time
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -33,6 +44,8 @@ from .._abi import MdOpts, call
 CH = 65536                      # parse chunk (mosdepth_dev.hip CH)
 BATCH_IN = 4 << 30              # compressed bytes per batch
 BATCH_TEXT = 24 << 30           # inflated bytes per batch
+STAGE = 1 << 30                 # pinned staging per CPU sub-batch (two of them)
+TRACE = bool(os.environ.get("GRID_INGEST_TRACE"))   # per-batch phase times on stderr
 
 
 class DeviceIngestUnsupported(Exception):
@@ -75,6 +88,63 @@ def _opts(dev, prefix, window, excluded, keep):
                   d_koff.ptr, d_kb.ptr)
 
 
+class _Split:
+    """Which files of a batch the GPU inflates and which the CPU threads do,
+    from rates measured on the previous batches (initial values: MI355X with
+    16 host threads, tools/bench_inflate.py): the GPU's aggregate text rate
+    over BGZF members, one wave's rate on a whole single-member file, and one
+    CPU thread's rate.  Greedy, largest file first, to the side that would
+    finish sooner."""
+
+    def __init__(self, threads):
+        self.threads = max(1, int(threads))
+        self.gpu = 10.0e9         # B/s, member-parallel
+        self.wave = 9.0e6         # B/s, one wave on one whole file
+        self.cpu = 0.6e9          # B/s per thread
+
+    def plan(self, files, text, bgzf):
+        g_mem = g_whole = c = 0.0
+        gpu, cpu = [], []
+        for k in sorted(files, key=lambda k: -int(text[k])):
+            s = float(text[k])
+            tg = max((g_mem + s) / self.gpu, g_whole) if bgzf[k] else max(g_mem / self.gpu, g_whole, s / self.wave)
+            tc = (c + s) / (self.cpu * self.threads)
+            cur_g = max(g_mem / self.gpu, g_whole)
+            cur_c = c / (self.cpu * self.threads)
+            if max(tg, cur_c) <= max(cur_g, tc):
+                gpu.append(k)
+                if bgzf[k]:
+                    g_mem += s
+                else:
+                    g_whole = max(g_whole, s / self.wave)
+            else:
+                cpu.append(k)
+                c += s
+        return sorted(gpu), sorted(cpu)
+
+    def learn(self, g_mem_bytes, g_whole_max, t_gpu, c_bytes, t_cpu):
+        a = 0.5                   # moving average over batches
+        if t_gpu > 0.05:
+            if g_mem_bytes and not g_whole_max:
+                self.gpu = (1 - a) * self.gpu + a * g_mem_bytes / t_gpu
+            elif g_whole_max and not g_mem_bytes:
+                self.wave = (1 - a) * self.wave + a * g_whole_max / t_gpu
+        if t_cpu > 0.05 and c_bytes:
+            self.cpu = (1 - a) * self.cpu + a * c_bytes / (t_cpu * self.threads)
+
+
+def _gpu_inflate(dev, d_in, d_text, units, mcap):
+    """Launch grid_gunzip_batch over units (in_off, in_len, out_off, cap);
+    returns the device buffers to read after the stream syncs."""
+    n = len(units[0])
+    d = [dev.upload(np.asarray(u, np.int64)) for u in units]
+    mem = dev.alloc(n * mcap * _abi.GZ_MEMBER_BYTES, np.uint8)
+    st, ln, nm = dev.alloc(n, np.int32), dev.alloc(n, np.int64), dev.alloc(n, np.int32)
+    call("grid_gunzip_batch", dev.ctx, d_in.ptr, d[0].ptr, d[1].ptr, n, d_text.ptr, d[2].ptr, d[3].ptr, mem.ptr,
+         mcap, st.ptr, ln.ptr, nm.ptr)
+    return d, mem, st, ln, nm
+
+
 def _chunks(files, tlen):
     """Chunk table of the files (batch-local indices) with text."""
     cfile, cstart, cfirst = [], [], [0]
@@ -110,7 +180,16 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
     if cur:
         batches.append(cur)
     pins = [_Pinned(), _Pinned()]
-    pool = ThreadPoolExecutor(max(1, min(int(threads or 1), 32)))
+    stages = [_Pinned(), _Pinned()]
+    nthreads = max(1, min(int(threads or 1), 32))
+    pool = ThreadPoolExecutor(nthreads)
+    rpool = ThreadPoolExecutor(1)         # the next batch's read (its files on `pool`)
+    copier = ThreadPoolExecutor(1)        # H2D of CPU-inflated text, on its own stream
+    waiter = ThreadPoolExecutor(1)        # notes when the GPU's inflate ends
+    import torch
+    cstream = torch.cuda.Stream(device=dev.index)
+    cdev = _abi.Device(dev.index, cstream)
+    split = _Split(nthreads)
 
     def read_batch(bi):
         fs = batches[bi]
@@ -124,18 +203,123 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
                 n = fh.readinto(memoryview(buf)[off[k]:off[k] + sizes[f]])
             if n != sizes[f]:
                 raise DeviceIngestUnsupported(f"{paths[f]} changed while reading")
-            return _abi.gz_text_size(buf[off[k]:off[k] + sizes[f]]) if sizes[f] else (0, 0)
-        caps = list(pool.map(one, range(len(fs))))
-        return buf, off, caps
+            if not sizes[f]:
+                return (0, 0), None
+            v = buf[off[k]:off[k] + sizes[f]]
+            return _abi.gz_text_size(v), _abi.gz_members(v)
+        info = list(pool.map(one, range(len(fs))))
+        return buf, off, [i[0] for i in info], [i[1] for i in info]
+
+    def inflate(buf, off, fs, caps_, gz, members, toff, d_in, d_text):
+        """Inflate the batch's files into d_text + toff[k]; (status, length) per file."""
+        nb = len(fs)
+        gst = np.zeros(nb, np.int32)
+        tlen = np.zeros(nb, np.int64)
+        todo = [k for k in range(nb) if gz[k] and sizes[fs[k]] > 0]
+        for k in range(nb):
+            if not sizes[fs[k]]:
+                gst[k] = 0                             # an empty file: no lines (gzip.open reads nothing)
+            elif not gz[k]:
+                gst[k] = _abi.GZ_EHEADER
+        bgzf = {k: members[k] is not None for k in todo}
+        on_gpu, on_cpu = split.plan(todo, caps_, bgzf)
+        t0 = time.perf_counter()
+        launched = []
+        if on_gpu:
+            call("grid_h2d", dev.ctx, d_in.ptr, buf.ctypes.data, int(off[-1]))
+            mu = [k for k in on_gpu if bgzf[k]]
+            wu = [k for k in on_gpu if not bgzf[k]]
+            if wu:                                     # whole files: one wave each, started first
+                mcap = max(1, int(max(sizes[fs[k]] // 4096 + 16 for k in wu)))
+                units = ([off[k] for k in wu], [sizes[fs[k]] for k in wu], [toff[k] for k in wu],
+                         [caps_[k] for k in wu])
+                launched.append(("whole", wu, None, _gpu_inflate(dev, d_in, d_text, units, mcap)))
+            if mu:                                     # BGZF: one wave per member
+                uo, ul, to, tc, owner = [], [], [], [], []
+                for k in mu:
+                    ms, ml, mi = members[k]
+                    uo.append(off[k] + ms)
+                    ul.append(ml)
+                    cum = np.zeros(len(mi), np.int64)
+                    np.cumsum(mi[:-1], out=cum[1:])
+                    to.append(toff[k] + cum)
+                    tc.append(mi.astype(np.int64))
+                    owner.append(np.full(len(mi), k, np.int64))
+                units = [np.concatenate(x) for x in (uo, ul, to, tc)]
+                launched.append(("members", mu, np.concatenate(owner), _gpu_inflate(dev, d_in, d_text, units, 1)))
+            gpu_done = waiter.submit(lambda: (dev.sync(), time.perf_counter())[1])
+        # CPU files meanwhile: sub-batches through two pinned stages, each
+        # copied to HBM on the copy stream while the next one inflates
+        c_bytes = 0
+        pend = [None, None]
+        i = sb = 0
+        while i < len(on_cpu):
+            grp, room = [], 0
+            while i < len(on_cpu) and (not grp or room + _align(caps_[on_cpu[i]]) <= STAGE):
+                grp.append(on_cpu[i])
+                room += _align(caps_[on_cpu[i]])
+                i += 1
+            j = sb % 2
+            sb += 1
+            if pend[j] is not None:
+                pend[j].result()
+            stage = stages[j].get(room + 256)
+            soff = np.zeros(len(grp) + 1, np.int64)
+            soff[1:] = np.cumsum([_align(caps_[k]) for k in grp])
+
+            def one(t, grp=grp, stage=stage, soff=soff):
+                k = grp[t]
+                v = buf[off[k]:off[k] + sizes[fs[k]]]
+                return _abi.gunzip_host(v, stage[soff[t]:soff[t] + caps_[k]])
+            res = list(pool.map(one, range(len(grp))))
+            for t, k in enumerate(grp):
+                gst[k], tlen[k] = res[t]
+                c_bytes += int(tlen[k])
+
+            def h2d(grp=grp, stage=stage, soff=soff, res=res):
+                for t, k in enumerate(grp):
+                    if res[t][0] == 0 and res[t][1]:
+                        call("grid_h2d", cdev.ctx, d_text.ptr + int(toff[k]), stage.ctypes.data + int(soff[t]),
+                             int(res[t][1]))
+            pend[j] = copier.submit(h2d)
+        t_cpu = time.perf_counter() - t0
+        for p_ in pend:
+            if p_ is not None:
+                p_.result()
+        g_mem = g_whole = 0
+        t_gpu = 0.0
+        if launched:
+            t_gpu = gpu_done.result() - t0
+            for kind, ks, owner, (_d, _mem, st, ln, _nm) in launched:
+                ust, uln = st.numpy(), ln.numpy()
+                if kind == "whole":
+                    gst[ks], tlen[ks] = ust, uln
+                    g_whole = max(g_whole, int(uln.max()))
+                else:
+                    bad = np.zeros(nb, np.int32)
+                    # a member past its BGZF size is corrupt (dropped), not several members
+                    np.maximum.at(bad, owner, np.where(ust == _abi.GZ_ESPACE, _abi.GZ_EDATA, ust))
+                    tot = np.zeros(nb, np.int64)
+                    np.add.at(tot, owner, uln)
+                    gst[ks], tlen[ks] = bad[ks], tot[ks]
+                    g_mem += int(uln.sum())
+        split.learn(g_mem, g_whole, t_gpu, c_bytes, t_cpu)
+        if TRACE:
+            import sys
+            print(f"[ingest] batch files gpu {len(on_gpu)} cpu {len(on_cpu)} text gpu {g_mem + g_whole:.3e} "
+                  f"cpu {c_bytes:.3e} B  t_gpu {t_gpu:.3f} t_cpu {t_cpu:.3f} s  rates gpu {split.gpu:.3e} "
+                  f"cpu/thread {split.cpu:.3e} B/s", file=sys.stderr, flush=True)
+        return gst, tlen
 
     K = kidx = Q = None
     nK = ref_nlines = 0
     d_in = d_text = None
-    pending = pool.submit(read_batch, 0) if batches else None
+    pending = rpool.submit(read_batch, 0) if batches else None
     try:
         for bi, fs in enumerate(batches):
-            buf, off, caps = pending.result()
-            pending = pool.submit(read_batch, bi + 1) if bi + 1 < len(batches) else None
+            t_w = time.perf_counter()
+            buf, off, caps, members = pending.result()
+            pending = rpool.submit(read_batch, bi + 1) if bi + 1 < len(batches) else None
             nb = len(fs)
             caps_ = np.array([c[0] if c else 0 for c in caps], np.int64)
             gz = np.array([c is not None for c in caps])
@@ -148,21 +332,10 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
                 d_in = dev.alloc(int(max(off[-1] + 256, BATCH_IN + 256)), np.uint8)
             if d_text is None or d_text.nbytes < toff[-1] + 256:
                 d_text = dev.alloc(int(max(toff[-1] + 256, min(BATCH_TEXT, 1 << 34))), np.uint8)
-            call("grid_h2d", dev.ctx, d_in.ptr, buf.ctypes.data, int(off[-1]))
-            lens = np.array([sizes[f] if gz[k] else 0 for k, f in enumerate(fs)], np.int64)
-            mcap = max(1, int(max((s // 4096 + 16 for s in lens), default=1)))
-            d_off, d_len = dev.upload(off[:nb]), dev.upload(lens)
-            d_toff, d_tcap = dev.upload(toff[:nb]), dev.upload(caps_)
-            mem = dev.alloc(nb * mcap * _abi.GZ_MEMBER_BYTES, np.uint8)
-            st, ln, nm = dev.alloc(nb, np.int32), dev.alloc(nb, np.int64), dev.alloc(nb, np.int32)
-            call("grid_gunzip_batch", dev.ctx, d_in.ptr, d_off.ptr, d_len.ptr, nb, d_text.ptr, d_toff.ptr,
-                 d_tcap.ptr, mem.ptr, mcap, st.ptr, ln.ptr, nm.ptr)
-            gst, tlen = st.numpy(), ln.numpy()
+            t_b = time.perf_counter()
+            gst, tlen = inflate(buf, off, fs, caps_, gz, members, toff, d_in, d_text)
+            t_i = time.perf_counter()
             for k, f in enumerate(fs):
-                if sizes[f] == 0:
-                    gst[k], tlen[k] = 0, 0                 # an empty file: no lines (gzip.open reads nothing)
-                elif not gz[k]:
-                    gst[k] = _abi.GZ_EHEADER
                 if gst[k] == _abi.GZ_ESPACE:
                     raise DeviceIngestUnsupported(f"{paths[f]}: several gzip members (text size unknown)")
                 status[f] = 0 if gst[k] == 0 else 1        # 1: failed (the reference drops the sample)
@@ -170,7 +343,7 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
             cfile, cstart, cfirst, nch = _chunks(okb, tlen)
             if nch == 0:
                 continue
-            d_tl = dev.upload(tlen)
+            d_tl, d_toff = dev.upload(tlen), dev.upload(toff[:nb])
             d_cfile, d_cstart, d_cfirst = dev.upload(cfile), dev.upload(cstart), dev.upload(cfirst)
             cnl, cline0 = dev.alloc(nch, np.int32), dev.alloc(nch, np.int64)
             # flags per batch file, folded into the cohort's afterwards
@@ -216,13 +389,21 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
             kept_h = kept.numpy()
             kept_h[np.asarray(fs)] += bkv
             kept.copy_from(kept_h)
+            if TRACE:
+                import sys
+                print(f"[ingest] batch {bi}: {nb} files, wait read {t_b - t_w:.3f} inflate {t_i - t_b:.3f} "
+                      f"parse {time.perf_counter() - t_i:.3f} s", file=sys.stderr, flush=True)
     finally:
         if pending is not None:
             try:
                 pending.result()
             except Exception:
                 pass
+        rpool.shutdown(wait=True)
         pool.shutdown(wait=True)
+        copier.shutdown(wait=True)
+        waiter.shutdown(wait=True)
+        cdev.close()
     if K is None:
         return [], [], None, status
     rows = np.array([f for f in range(nfiles) if status[f] == 0], np.int32)

@@ -459,11 +459,6 @@ typedef struct grid_gz_member {
 #define GRID_GZ_ESPACE 3    /* output or member capacity exceeded */
 #define GRID_GZ_EHEADER 4   /* not a gzip file (or empty) */
 #define GRID_GZ_ECRC 5      /* a member's CRC-32 does not match its bytes */
-/* Inflate n_files gzip files (each: every member back to back) in one launch,
- * one wave per file.  d_src + d_in_off[f] (256-B aligned) holds d_in_len[f]
- * bytes; the text goes to d_out + d_out_off[f] (16-B aligned), at most
- * d_out_cap[f] bytes; d_mem[f * mcap ...] receives the members.  Per file:
- * d_status (0 or GRID_GZ_E*), d_out_len, d_nmem.  Asynchronous on the stream. */
 /* ---- mosdepth text -> depth matrix on the device (grid_amd/csrc/mosdepth_dev.hip;
  * normalize_mosdepth.py:218-416 as ingest.cpp restates it).  Driven per batch of
  * inflated files by grid_amd/utils/ingest_device.py; every file is cut in
@@ -513,6 +508,23 @@ int grid_md_gather(grid_ctx *ctx, const int32_t *d_Q, int64_t ldq, int64_t nK, i
 /* host: the inflated size of a gzip file in memory (BGZF: the members' sizes; else the
  * trailer's ISIZE of a single member); GRID_EUNSUPPORTED if it is not gzip */
 int grid_gz_text_size(const uint8_t *h_buf, int64_t n, int64_t *size, int32_t *members);
+/* host: the BGZF members of a gzip file in memory -- byte offset, length and ISIZE of each
+ * (zero padding between members skipped) -- *count of them, at most cap written (a larger
+ * *count: call again with more room); GRID_EUNSUPPORTED if the file is not BGZF throughout */
+int grid_gz_members(const uint8_t *h_buf, int64_t n, int64_t *h_start, int64_t *h_len, uint32_t *h_isize,
+                    int32_t cap, int32_t *count);
+/* host: inflate a gzip file in memory (every member, zero padding after a member skipped, as
+ * CPython's gzip reader) into h_out[0, cap): libdeflate when the system library loads, else
+ * zlib; *out_len bytes; *status 0, or GRID_GZ_ESPACE (cap too small), GRID_GZ_EHEADER (not
+ * gzip), GRID_GZ_EDATA (anything else: corrupt, truncated, CRC) */
+int grid_gunzip_host(const uint8_t *h_in, int64_t n, uint8_t *h_out, int64_t cap, int64_t *out_len,
+                     int32_t *status);
+/* Inflate n_files gzip streams (each: every member back to back) in one launch,
+ * one wave per stream (a whole file, or one BGZF member of one).  d_src +
+ * d_in_off[f] (4-B aligned) holds d_in_len[f] bytes; the text goes to d_out +
+ * d_out_off[f], at most d_out_cap[f] bytes; d_mem[f * mcap ...] receives the
+ * members.  Per stream: d_status (0 or GRID_GZ_E*), d_out_len, d_nmem.
+ * Asynchronous on the stream. */
 int grid_gunzip_batch(grid_ctx *ctx, const uint8_t *d_src, const int64_t *d_in_off, const int64_t *d_in_len,
                       int64_t n_files, uint8_t *d_out, const int64_t *d_out_off, const int64_t *d_out_cap,
                       grid_gz_member *d_mem, int32_t mcap, int32_t *d_status, int64_t *d_out_len,

@@ -118,3 +118,47 @@ def test_inflate_rejects_exactly_what_zlib_rejects(dev):
             assert st[f] != 0, f
         else:
             assert st[f] == 0 and got[f] == r, (f, st[f])
+
+
+def test_streams_at_any_offset(dev):
+    """The ingest's member-granular launch: every BGZF member is its own
+    stream, packed at any byte offset, its text at any byte offset (the
+    members of a file back to back) -- and the reject cases with them."""
+    rng = random.Random(11)
+    texts = [b"".join(b"chr1\t%d\t%d\t%.2f\n" % (i * 1000, i * 1000 + 1000, rng.uniform(0, 90))
+                      for i in range(n)) for n in (1, 700, 9000)]
+    streams, refs = [], []
+    for t in texts:
+        bg = _bgzf(t, block=rng.choice([4093, 65280]))
+        ms, ml, mi = _abi.gz_members(bg)
+        for s_, l_, i_ in zip(ms, ml, mi):
+            streams.append(bg[s_:s_ + l_])
+            refs.append(zlib.decompress(bg[s_:s_ + l_], 31))
+            assert len(refs[-1]) == i_
+    streams.append(gzip.compress(texts[1], 1)[:-9])        # truncated
+    refs.append(None)
+    src = bytearray(b"\x00" * 3)
+    in_off, out_off, caps = [], [], []
+    opos = 5
+    for b, r in zip(streams, refs):
+        src += b"\x00" * rng.randrange(0, 4)
+        in_off.append(len(src))
+        src += b
+        out_off.append(opos)
+        caps.append(len(r) if r is not None else 1 << 16)
+        opos += caps[-1] + rng.randrange(0, 3)
+    n = len(streams)
+    d_src = dev.upload(np.frombuffer(bytes(src) + b"\x00" * 256, np.uint8))
+    d_io, d_il = dev.upload(np.array(in_off, np.int64)), dev.upload(np.array([len(b) for b in streams], np.int64))
+    d_oo, d_cap = dev.upload(np.array(out_off, np.int64)), dev.upload(np.array(caps, np.int64))
+    out = dev.alloc(opos + 256, np.uint8)
+    mem = dev.alloc(n * 4 * _abi.GZ_MEMBER_BYTES, np.uint8)
+    st, ln, nm = dev.alloc(n, np.int32), dev.alloc(n, np.int64), dev.alloc(n, np.int32)
+    _abi.call("grid_gunzip_batch", dev.ctx, d_src.ptr, d_io.ptr, d_il.ptr, n, out.ptr, d_oo.ptr, d_cap.ptr, mem.ptr,
+              4, st.ptr, ln.ptr, nm.ptr)
+    st, ln, host = st.numpy(), ln.numpy(), out.numpy()
+    for f, r in enumerate(refs):
+        if r is None:
+            assert st[f] != 0
+        else:
+            assert st[f] == 0 and bytes(host[out_off[f]:out_off[f] + ln[f]]) == r, f

@@ -30,6 +30,21 @@ def dev():
     return d
 
 
+SPLITS = {
+    "gpu": lambda self, files, text, bgzf: (sorted(files), []),
+    "cpu": lambda self, files, text, bgzf: ([], sorted(files)),
+    "alternate": lambda self, files, text, bgzf: (sorted(files)[0::2], sorted(files)[1::2]),
+}
+
+
+@pytest.fixture(params=["model", "gpu", "cpu", "alternate"])
+def split(request, monkeypatch):
+    """Which side inflates: the cost model, or forced GPU / CPU / every other file."""
+    if request.param != "model":
+        monkeypatch.setattr(ingest_device._Split, "plan", SPLITS[request.param])
+    return request.param
+
+
 def _dev_vs_host(dev, d, samples, chrom=None, start=None, end=None, excluded=None, lo=20, hi=100):
     inds = nm.map_mosdepth_files_to_samples(d, samples)
     ex = excluded or {}
@@ -42,7 +57,7 @@ def _dev_vs_host(dev, d, samples, chrom=None, start=None, end=None, excluded=Non
     return a
 
 
-def test_random_cohorts(dev, tmp_path):
+def test_random_cohorts(dev, tmp_path, split):
     rng = np.random.default_rng(1)
     files = {f"S{i:03d}": _rand_lines(rng, 3000) for i in range(12)}
     d = _cohort(tmp_path, files, members=1)
@@ -72,7 +87,10 @@ def test_golden_cohorts(dev, tmp_path):
         _dev_vs_host(dev, d, samples, **kw)
 
 
-def test_subsets_bgzf_empty_corrupt_and_zero_depth(dev, tmp_path):
+def test_subsets_bgzf_empty_corrupt_and_zero_depth(dev, tmp_path, split, monkeypatch):
+    # small batches and staging: several batches, both staging buffers reused
+    monkeypatch.setattr(ingest_device, "BATCH_IN", 48 << 10)
+    monkeypatch.setattr(ingest_device, "STAGE", 64 << 10)
     rng = np.random.default_rng(2)
     base = _rand_lines(rng, 5000)
     files = {}
@@ -93,7 +111,10 @@ def test_subsets_bgzf_empty_corrupt_and_zero_depth(dev, tmp_path):
     good = (d / "S001.regions.bed.gz").read_bytes()
     (d / "C000.regions.bed.gz").write_bytes(good[: len(good) // 2])    # truncated: dropped
     (d / "N000.regions.bed.gz").write_bytes(b"not a gzip file at all")  # dropped
-    samples = sorted(files) + ["E000", "C000", "N000"]
+    bg = bytearray(_bgzf("".join(files["S001"]).encode()))
+    bg[len(bg) // 2] ^= 0x55                                            # a corrupt BGZF member: dropped
+    (d / "B000.regions.bed.gz").write_bytes(bytes(bg))
+    samples = sorted(files) + ["E000", "C000", "N000", "B000"]
     a = _dev_vs_host(dev, d, samples)
     assert len(a[0]) == 8
 
@@ -114,7 +135,8 @@ def test_outside_the_common_case_hands_over(dev, tmp_path):
         root = tmp_path / name
         root.mkdir()
         d = _cohort(root, {"A": la, "B": lb})
-        inds = nm.map_mosdepth_files_to_samples(d, ["A", "B"])
+        m = nm.map_mosdepth_files_to_samples(d, ["A", "B"])
+        inds = {k: m[k] for k in ("A", "B")}          # A first: A's keys are the key list K
         with pytest.raises(ingest_device.DeviceIngestUnsupported):
             nm._ingest_dev(dev, inds, d, None, None, None, {}, 20, 100, 2)
         got = nm.ingest(inds, d, None, None, None, {}, 20, 100, 2, dev=dev)

@@ -306,3 +306,32 @@ def test_zero_padding_after_members(tmp_path):
     a, b = _both(d, ["Z1"], threads=1)
     _same(a, b)
     assert a[2].shape[1] > 1000
+
+
+def test_host_gunzip_and_bgzf_members():
+    """grid_gunzip_host (the CPU side of the device ingest) and
+    grid_gz_members against zlib / CPython gzip: BGZF, multi-member, zero
+    padding, too little room, corrupt and truncated input, not gzip."""
+    import gzip
+    rng = np.random.default_rng(5)
+    t = "".join(_rand_lines(rng, 20000)).encode()
+    bg = _bgzf(t)
+    ms, ml, mi = _abi.gz_members(bg)
+    assert len(ms) == -(-len(t) // 65280) + 1 and int(mi.sum()) == len(t) and mi[-1] == 0
+    assert ms[0] == 0 and int(ms[-1] + ml[-1]) == len(bg)
+    assert _abi.gz_members(gzip.compress(t)) is None
+    cases = [bg, gzip.compress(t, 1), gzip.compress(t[:999]) + b"\0\0" + gzip.compress(t[999:]),
+             bg + b"\0" * 7]
+    for b in cases:
+        out = np.empty(len(t) + 3, np.uint8)
+        st, n = _abi.gunzip_host(b, out)
+        assert st == 0 and out[:n].tobytes() == t
+    small = np.empty(100, np.uint8)
+    assert _abi.gunzip_host(bg, small)[0] == _abi.GZ_ESPACE
+    assert _abi.gunzip_host(b"plain text, not gzip", small)[0] == _abi.GZ_EHEADER
+    big = np.empty(len(t), np.uint8)
+    assert _abi.gunzip_host(bg[: len(bg) // 2], big)[0] == _abi.GZ_EDATA
+    x = bytearray(gzip.compress(t, 6))
+    x[len(x) // 2] ^= 0x10
+    assert _abi.gunzip_host(bytes(x), big)[0] == _abi.GZ_EDATA
+    assert _abi.gunzip_host(bg + b"junk after the members", big)[0] == _abi.GZ_EDATA

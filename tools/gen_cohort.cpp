@@ -3,12 +3,16 @@
 // "chr1\tSTART\tEND\tDEPTH\n" with 1 kb bins and DEPTH printed "%.2f" like
 // mosdepth.  The depth model is the bench cohort's (grid_amd/csrc/
 // synth_model.hpp, restated for the host: per-bin base and cluster offset,
-// one 64-bit hash per cell).  Samples are written in parallel, gzip level 1.
+// one 64-bit hash per cell).  Samples are written in parallel, gzip level 1:
+// one gzip member per file, or with "bgzf" BGZF (what mosdepth writes through
+// htslib: 65280-byte blocks, each its own member with the "BC" length field,
+// then the 28-byte end-of-file member).
 //   g++ -O3 -std=c++17 -pthread -o tools/gen_cohort tools/gen_cohort.cpp -lz
-//   tools/gen_cohort DIR N_SAMPLES N_BINS SEED THREADS [FIRST_SAMPLE]
+//   tools/gen_cohort DIR N_SAMPLES N_BINS SEED THREADS [FIRST_SAMPLE [bgzf]]
 // (samples FIRST_SAMPLE .. FIRST_SAMPLE + N_SAMPLES - 1: batches of one cohort)
 #include <zlib.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cmath>
 #include <cstdint>
@@ -26,6 +30,57 @@ static inline uint64_t mix(uint64_t z) {
   return z ^ (z >> 31);
 }
 static inline float unif(uint64_t h) { return (float)(h >> 40) * (1.0f / 16777216.0f); }
+// BGZF writer: text in, 65280-byte blocks out as gzip members
+struct Bgzf {
+  FILE *f = nullptr;
+  std::vector<char> blk;
+  std::vector<unsigned char> z;
+  bool ok = true;
+  explicit Bgzf(FILE *ff) : f(ff), z(70000) { blk.reserve(65280); }
+  void block(const char *p, size_t n, int level) {
+    z_stream s{};
+    deflateInit2(&s, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY);
+    s.next_in = (Bytef *)p;
+    s.avail_in = (uInt)n;
+    s.next_out = z.data() + 18;
+    s.avail_out = (uInt)(z.size() - 26);
+    const int rc = deflate(&s, Z_FINISH);
+    const size_t c = z.size() - 26 - s.avail_out;
+    deflateEnd(&s);
+    if (rc != Z_STREAM_END || c + 26 > 65536) {
+      if (level) block(p, n, 0);   // incompressible: stored
+      else ok = false;
+      return;
+    }
+    const unsigned char h[18] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 'B', 'C', 2, 0,
+                                 (unsigned char)((c + 25) & 255), (unsigned char)((c + 25) >> 8)};
+    memcpy(z.data(), h, 18);
+    const uint32_t crc = (uint32_t)crc32(0, (const Bytef *)p, (uInt)n), isz = (uint32_t)n;
+    memcpy(z.data() + 18 + c, &crc, 4);
+    memcpy(z.data() + 22 + c, &isz, 4);
+    ok = ok && fwrite(z.data(), 1, c + 26, f) == c + 26;
+  }
+  void write(const char *p, size_t n) {
+    while (n) {
+      const size_t k = std::min(n, (size_t)65280 - blk.size());
+      blk.insert(blk.end(), p, p + k);
+      p += k;
+      n -= k;
+      if (blk.size() == 65280) {
+        block(blk.data(), blk.size(), 1);
+        blk.clear();
+      }
+    }
+  }
+  bool close() {
+    if (!blk.empty()) block(blk.data(), blk.size(), 1);
+    static const unsigned char eof[28] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 0x42, 0x43,
+                                          2,    0,    0x1b, 0, 3, 0, 0, 0, 0, 0, 0,    0, 0, 0};
+    ok = ok && fwrite(eof, 1, 28, f) == 28;
+    return fclose(f) == 0 && ok;
+  }
+};
+
 static inline char *put_u(char *o, uint64_t v) {
   char t[24];
   int k = 0;
@@ -44,6 +99,7 @@ int main(int argc, char **argv) {
   const uint64_t seed = strtoull(argv[4], nullptr, 10);
   const int nt = atoi(argv[5]);
   const int64_t first = argc > 6 ? atoll(argv[6]) : 0;
+  const bool bgzf = argc > 7 && !strcmp(argv[7], "bgzf");
   const int ncl = 26;
   // per-bin parts, shared by every sample
   std::vector<float> base(m), off((size_t)m * ncl);
@@ -63,9 +119,21 @@ int main(int argc, char **argv) {
       const float scale = 0.6f + 0.8f * unif(hs);
       char path[4096];
       snprintf(path, sizeof path, "%s/S%05lld.regions.bed.gz", dir.c_str(), (long long)i);
-      gzFile f = gzopen(path, "wb1");
-      if (!f) { failed++; continue; }
-      gzbuffer(f, 1 << 20);
+      gzFile f = nullptr;
+      Bgzf *bw = nullptr;
+      if (bgzf) {
+        FILE *ff = fopen(path, "wb");
+        if (!ff) { failed++; continue; }
+        bw = new Bgzf(ff);
+      } else {
+        f = gzopen(path, "wb1");
+        if (!f) { failed++; continue; }
+        gzbuffer(f, 1 << 20);
+      }
+      auto emit = [&](const char *p, size_t k) {
+        if (bw) bw->write(p, k);
+        else gzwrite(f, p, (unsigned)k);
+      };
       size_t pos = 0;
       for (int64_t b = 0; b < m; b++) {
         const uint64_t h = mix(seed ^ ((uint64_t)i << 40) ^ (uint64_t)b);
@@ -78,7 +146,7 @@ int main(int argc, char **argv) {
         const float noise = 1.0f + 0.2f * (u1 + u2 - 1.0f);
         const float d = base[b] * (1.0f + off[(size_t)b * ncl + c]) * scale * cnv * noise * spike;
         const int32_t q = (int32_t)rintf(d * 100.0f);
-        if (pos + 64 > buf.size()) { gzwrite(f, buf.data(), (unsigned)pos); pos = 0; }
+        if (pos + 64 > buf.size()) { emit(buf.data(), pos); pos = 0; }
         char *o = buf.data() + pos;
         memcpy(o, "chr1\t", 5);
         o += 5;
@@ -93,8 +161,13 @@ int main(int argc, char **argv) {
         *o++ = '\n';
         pos = (size_t)(o - buf.data());
       }
-      if (pos) gzwrite(f, buf.data(), (unsigned)pos);
-      if (gzclose(f) != Z_OK) failed++;
+      if (pos) emit(buf.data(), pos);
+      if (bw) {
+        if (!bw->close()) failed++;
+        delete bw;
+      } else if (gzclose(f) != Z_OK) {
+        failed++;
+      }
     }
   };
   std::vector<std::thread> th;
