@@ -250,7 +250,9 @@ def main():
     torch.cuda.set_device(local)
     dist = None
     comm = None
-    if world > 1:
+    # GRID_BENCH_FORCE_DIST=1: the torch.distributed path (RCCL collectives,
+    # TorchComm) even at world 1 -- a one-GPU check of the multi-GPU code path
+    if world > 1 or os.environ.get("GRID_BENCH_FORCE_DIST") == "1":
         import torch.distributed as dist
         backend = os.environ.get("GRID_DIST_BACKEND", "nccl")     # "nccl" = RCCL on ROCm
         if backend == "nccl":

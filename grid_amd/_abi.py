@@ -83,6 +83,7 @@ _SIGS = {
     "grid_hi_phase": [_vp, _i64, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
                       _i32, _i32],
     "grid_hi_phase_batch": [_vp, _i64, _vp, _i64, _i32, _i64, _i64, _i32, _i32],
+    "grid_hi_pack_batch": [_vp, _i64, _vp, _i64],
     "grid_write_normalized_gz": [C.c_char_p, _i64, _i64, C.c_char_p, _vp, _vp, _vp, _vp, _i64, _i32, _i32],
     "grid_read_normalized_gz": [C.c_char_p, _i32, C.POINTER(_vp), C.POINTER(_i64), C.POINTER(_i64)],
     "grid_ntext_ids_len": [_vp, C.POINTER(_i64)],

@@ -903,6 +903,43 @@ int grid_hi_phase(grid_ctx *ctx, int64_t n, const double *d_irr, const int64_t *
   return GRID_OK;
 }
 
+// grid_hi_pack for every locus of a batch, on the device: thread = (schedule
+// entry e, haplotype h) of locus blockIdx.y; its CAP packed neighbours are
+// 64 contiguous bytes (4 int4 stores), so a wave writes 4 KiB contiguously.
+__global__ void k_hi_pack_batch(const grid_hi_locus *__restrict__ loci) {
+  const grid_hi_locus L = loci[blockIdx.y];
+  const int64_t eh = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (eh >= 2 * L.n) return;
+  const int64_t e = eh >> 1;
+  const int h = (int)(eh & 1);
+  const int64_t i = L.order[e];
+  const int64_t o = L.off[2 * i + h], c = L.off[2 * i + h + 1] - o;
+  int32_t v[CAP];
+#pragma unroll
+  for (int t = 0; t < CAP; t++) v[t] = t < c ? L.nbr[o + t] : 0;
+  int4 *pn = (int4 *)(const_cast<int32_t *>(L.pk_nbr) + eh * CAP);
+#pragma unroll
+  for (int t = 0; t < CAP; t += 4) pn[t / 4] = make_int4(v[t], v[t + 1], v[t + 2], v[t + 3]);
+  if (L.pk_w) {
+    double *pw = const_cast<double *>(L.pk_w) + eh * CAP;
+#pragma unroll
+    for (int t = 0; t < CAP; t++) pw[t] = t < c ? L.w[o + t] : 0.0;
+  }
+  const_cast<int32_t *>(L.pk_cnt)[eh] = c <= CAP ? (int32_t)c : -1;
+}
+
+int grid_hi_pack_batch(grid_ctx *ctx, int64_t n_loci, const grid_hi_locus *d_loci, int64_t max_n) {
+  REQUIRE(ctx && n_loci >= 0 && max_n >= 0, "bad args");
+  REQUIRE(n_loci <= 65535, "at most 65535 loci per pack launch");
+  if (n_loci == 0 || max_n == 0) return GRID_OK;
+  REQUIRE(d_loci, "d_loci is NULL");
+  const int64_t nb = (2 * max_n + 255) / 256;
+  REQUIRE(nb <= 0x7fffffff, "locus too large");
+  hipLaunchKernelGGL(k_hi_pack_batch, dim3((unsigned)nb, (unsigned)n_loci), dim3(256), 0, ctx->stream, d_loci);
+  HIPCHK(hipGetLastError());
+  return GRID_OK;
+}
+
 int grid_hi_phase_batch(grid_ctx *ctx, int64_t n_loci, const grid_hi_locus *d_loci, int64_t max_n,
                         int32_t max_nlev, int64_t min_nbr, int64_t n_iters, int32_t flags, int32_t max_list) {
   REQUIRE(ctx && n_loci >= 0 && max_n >= 0 && max_nlev >= 0 && n_iters >= 0 && max_list >= 0, "bad args");

@@ -1322,6 +1322,8 @@ __global__ __launch_bounds__(256) void k_topk_radix(const T *__restrict__ rows, 
 // ---- general-value k-NN (values that are not bf16-exact) -----------------
 // Panel of the MFMA path from int32 hundredths: K-blocked bf16 of
 // clip(zq[i][cols[c]], -qmax, qmax), GRID_MISSING -> 0 (find_neighbors.py:57-58).
+// The step-4 output handed over in one process (utils/handoff.py) carries the
+// "-0.00" sentinel GRID_ZQ_NEG0: float("-0.00") is -0.0, a zero here.
 __global__ void k_panel_i32(const int32_t *__restrict__ zq, int64_t n, int64_t ld, const int32_t *__restrict__ cols,
                             int64_t r, int32_t qmax, uint16_t *__restrict__ zb, int64_t np_, int64_t kpad) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1330,7 +1332,7 @@ __global__ void k_panel_i32(const int32_t *__restrict__ zq, int64_t n, int64_t l
   int32_t v = 0;
   if (i < n && c < r) {
     v = zq[i * ld + cols[c]];
-    v = v == GRID_MISSING ? 0 : min(max(v, -qmax), qmax);        // np.clip order: max, then min
+    v = (v == GRID_MISSING || v == GRID_ZQ_NEG0) ? 0 : min(max(v, -qmax), qmax);   // np.clip: max, then min
   }
   zb[(c / KBW) * np_ * KBW + i * KBW + (c % KBW)] = (uint16_t)(__float_as_uint((float)v) >> 16);
 }
@@ -1343,7 +1345,7 @@ __global__ void k_gather_i32(const int32_t *__restrict__ zq, int64_t n, int64_t 
   const int64_t i = blockIdx.y;
   if (c >= r) return;
   const int32_t v = zq[i * ld + cols[c]];
-  out[i * r + c] = v == GRID_MISSING ? 0 : min(max(v, -qmax), qmax);
+  out[i * r + c] = (v == GRID_MISSING || v == GRID_ZQ_NEG0) ? 0 : min(max(v, -qmax), qmax);
 }
 __global__ void k_gather_f64(const int32_t *__restrict__ zq, int64_t n, int64_t ld, const int32_t *__restrict__ cols,
                              int64_t r, double zmax, double *__restrict__ out) {
@@ -1351,7 +1353,7 @@ __global__ void k_gather_f64(const int32_t *__restrict__ zq, int64_t n, int64_t 
   const int64_t i = blockIdx.y;
   if (c >= r) return;
   const int32_t v = zq[i * ld + cols[c]];
-  const double x = (double)v / 100.0;                           // float("%.2f" text)
+  const double x = v == GRID_ZQ_NEG0 ? -0.0 : (double)v / 100.0; // float("%.2f" text)
   const double lo = -zmax, y = x < lo ? lo : x;                  // np.clip: maximum(x, -zmax) ...
   out[i * r + c] = v == GRID_MISSING ? 0.0 : (y > zmax ? zmax : y);   // ... then minimum(., zmax)
 }

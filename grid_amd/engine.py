@@ -196,7 +196,8 @@ def _dist_key_scale(bound: float, integer: bool) -> float:
 
 
 def _knn_zq(dev: Device, zq: np.ndarray, cols: np.ndarray, k: int, zmax: float, values: bool):
-    """Step 5 on integer hundredths zq [n][ld] (GRID_MISSING = NaN) restricted
+    """Step 5 on integer hundredths zq [n][ld] (GRID_MISSING = NaN; GRID_ZQ_NEG0,
+    the step-4 "-0.00" code in a hand-off, = 0) restricted
     to columns ``cols``, clipped to +-zmax (find_neighbors.py:57-58).  Path:
       * zmax = q/100, q <= 256: bf16-exact MFMA Gram (k_gram8) + row top-k;
       * zmax = q/100, q > 256: exact int64 direct-difference distances;
@@ -346,44 +347,100 @@ def phase_batch(dev: Device, loci, min_nbr: int, n_iters: int, legacy: bool = Fa
     """Batched phasing + imputation of L independent loci in one launch (one
     workgroup per locus; BASELINE config 5).  ``loci``: sequence of
     (irr [n], off [2n+1], nbr, w) per locus (CSR as csr_from_lists).  Returns
-    a list of (hap [2n], imp [2n], mean) equal to phase() per locus."""
-    import ctypes as C
+    a list of (hap [2n], imp [2n], mean) equal to phase() per locus.
+
+    Host work is the level schedules (grid_hi_levels, host C++ on a thread
+    pool: the calls release the GIL) and one arena of every locus's inputs,
+    copied to HBM in ONE transfer; the packed neighbour lists are built on the
+    device (grid_hi_pack_batch) and the outputs come back in one transfer.
+    Unit-weight loci share one device vector of ones as their weights."""
     import os
     from concurrent.futures import ThreadPoolExecutor
-    descs, keep, outs = [], [], []
-    flags_all, max_list, max_n, max_nlev = _abi.HI_UNIT_WEIGHTS, 0, 0, 0
-    legacy = _abi.HI_LEGACY if legacy else 0
-    # per-locus schedules in parallel (the C++ schedule / pack calls release the GIL)
-    with ThreadPoolExecutor(max(1, min(16, os.cpu_count() or 1))) as ex:
-        full = list(ex.map(lambda l: _abi.hi_schedule(l[1], l[2], l[3], packed_w=bool(legacy)), loci))
-    sched = []
-    for (irr, off, nbr, w), (order, loff, nl, pk_nbr, pk_w, pk_cnt, flags, ml) in zip(loci, full):
-        flags_all &= flags
-        max_list, max_n, max_nlev = max(max_list, ml), max(max_n, len(irr)), max(max_nlev, nl)
-        sched.append((order, loff, nl, pk_nbr, pk_w, pk_cnt))
-    if not flags_all and not legacy:   # some locus has weights: every locus needs its packed weights
-        sched = [(o, lf, nl, pn, pw if pw is not None else _abi.hi_schedule(l[1], l[2], l[3])[4], pc)
-                 for l, (o, lf, nl, pn, pw, pc) in zip(loci, sched)]
-    for (irr, off, nbr, w), (order, loff, nl, pk_nbr, pk_w, pk_cnt) in zip(loci, sched):
-        n = len(irr)
-        # pk_w None: unit weights, not packed -> NULL in the descriptor (read as 1.0)
-        b = [None if a is None else dev.upload(np.ascontiguousarray(a)) for a in
-             (np.asarray(irr if n else np.zeros(1), F8), np.asarray(off, I8),
-              np.asarray(nbr if len(nbr) else np.zeros(1), I4), np.asarray(w if len(w) else np.zeros(1), F8),
-              np.asarray(order if n else np.zeros(1), I4), np.asarray(loff, I4), pk_nbr, pk_w, pk_cnt)]
-        hap, imp, mean = dev.alloc(max(2 * n, 1), F8), dev.alloc(max(2 * n, 1), F8), dev.alloc(1, F8)
-        keep += b
-        outs.append((n, hap, imp, mean))
-        descs.append(_abi.HiLocus(n, b[0].ptr, b[1].ptr, b[2].ptr, b[3].ptr, b[4].ptr, b[5].ptr, nl, 0, b[6].ptr,
-                                  None if b[7] is None else b[7].ptr, b[8].ptr, hap.ptr, imp.ptr, mean.ptr))
-    if not descs:
+    if not len(loci):
         return []
+    pool = ThreadPoolExecutor(max(1, min(16, os.cpu_count() or 1)))
+
+    def prep(l):
+        irr, off, nbr, w = l
+        off = np.ascontiguousarray(off, dtype=I8)
+        nbr = np.ascontiguousarray(nbr if len(nbr) else np.zeros(1), dtype=I4)
+        order, loff, nl = _abi.hi_levels(off, nbr)
+        unit = len(w) == 0 or bool(np.all(np.asarray(w) == 1.0))
+        lens = np.diff(off) if len(off) > 1 else np.zeros(1, I8)
+        return off, nbr, order, loff, nl, unit, int(lens.max()) if lens.size else 0
+
+    try:
+        pre = list(pool.map(prep, loci))
+        flags_all = _abi.HI_UNIT_WEIGHTS if all(p[5] for p in pre) else 0
+        legacy_f = _abi.HI_LEGACY if legacy else 0
+        need_pkw = bool(legacy_f) or not flags_all
+        max_n = max(len(l[0]) for l in loci)
+        max_nlev = max(p[4] for p in pre)
+        max_list = max(p[6] for p in pre)
+        max_nnz = max(len(p[1]) for p in pre)
+
+        def al(x):
+            return -(-int(x) // 256) * 256
+        # input arena: irr, off, nbr, w (weighted loci only), order, loff per locus
+        arrs, offs, pos = [], [], 0
+        for (irr, _, _, w), (off, nbr, order, loff, nl, unit, _) in zip(loci, pre):
+            n = len(irr)
+            la = [np.ascontiguousarray(irr if n else np.zeros(1), dtype=F8), off, nbr,
+                  None if unit else np.ascontiguousarray(w if len(w) else np.zeros(1), dtype=F8),
+                  np.ascontiguousarray(order if n else np.zeros(1), dtype=I4), np.ascontiguousarray(loff, dtype=I4)]
+            lo = []
+            for x in la:
+                lo.append(None if x is None else pos)
+                pos += 0 if x is None else al(x.nbytes)
+            arrs.append(la)
+            offs.append(lo)
+        host = np.empty(max(pos, 1), dtype=U1)
+
+        def fill(k):
+            for x, o in zip(arrs[k], offs[k]):
+                if x is not None:
+                    host[o:o + x.nbytes] = x.view(U1).reshape(-1)
+        list(pool.map(fill, range(len(loci))))
+    finally:
+        pool.shutdown(wait=True)
+    d_in = dev.upload(host)
+    ones = dev.upload(np.ones(max(max_nnz, 1), dtype=F8)) if any(p[5] for p in pre) else None
+    # device arenas: packed lists (built on the device) and outputs
+    sizes = [len(l[0]) for l in loci]
+    pk_pos, ppos = [], 0
+    for n in sizes:
+        n1 = max(n, 1)
+        pk_pos.append((ppos, ppos + al(n1 * 2 * _abi.PACK_CAP * 4), ppos + al(n1 * 2 * _abi.PACK_CAP * 4) + al(n1 * 8)))
+        ppos = pk_pos[-1][2] + (al(n1 * 2 * _abi.PACK_CAP * 8) if need_pkw else 0)
+    d_pk = dev.alloc(max(ppos, 1), U1)
+    o_hap = np.zeros(len(sizes) + 1, dtype=np.int64)
+    np.cumsum([2 * max(n, 1) for n in sizes], out=o_hap[1:])
+    tot = int(o_hap[-1])
+    d_out = dev.alloc(2 * tot + len(sizes), F8)
+    descs = []
+    for k, n in enumerate(sizes):
+        io = [None if o is None else d_in.ptr + o for o in offs[k]]
+        p0, p1, p2 = (d_pk.ptr + x for x in pk_pos[k])
+        hap = d_out.ptr + 8 * int(o_hap[k])
+        imp = d_out.ptr + 8 * (tot + int(o_hap[k]))
+        mean = d_out.ptr + 8 * (2 * tot + k)
+        w_ptr = io[3] if io[3] is not None else ones.ptr
+        descs.append(_abi.HiLocus(n, io[0], io[1], io[2], w_ptr, io[4], io[5], pre[k][4], 0, p0,
+                                  p2 if need_pkw else None, p1, hap, imp, mean))
     arr = (_abi.HiLocus * len(descs))(*descs)
-    d_arr = dev.alloc(C.sizeof(arr), np.uint8)
+    d_arr = dev.alloc(C.sizeof(arr), U1)
     call("grid_h2d", dev.ctx, d_arr.ptr, C.addressof(arr), C.sizeof(arr))
+    step = 65535
+    for l0 in range(0, len(descs), step):          # grid.y of the pack launch
+        call("grid_hi_pack_batch", dev.ctx, min(step, len(descs) - l0), d_arr.ptr + l0 * C.sizeof(_abi.HiLocus),
+             max_n)
     call("grid_hi_phase_batch", dev.ctx, len(descs), d_arr.ptr, max_n, max_nlev, min_nbr, n_iters,
-         flags_all | legacy | (_abi.HI_PAIRED if paired else 0), max_list)
+         flags_all | legacy_f | (_abi.HI_PAIRED if paired else 0), max_list)
+    out = d_out.numpy()
     res = []
-    for n, hap, imp, mean in outs:
-        res.append((hap.numpy()[: 2 * n], imp.numpy()[: 2 * n], float(mean.numpy()[0]) if n else 0.0))
+    for k, n in enumerate(sizes):
+        h0 = int(o_hap[k])
+        res.append((out[h0:h0 + 2 * n].copy(), out[tot + h0:tot + h0 + 2 * n].copy(),
+                    float(out[2 * tot + k]) if n else 0.0))
+    del d_in, d_pk, d_arr, ones
     return res

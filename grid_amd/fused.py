@@ -361,7 +361,7 @@ class Steps47:
         self.ldc = pad_to(max(cw, 1), 4)
         self.qc = None
         self.qc_holds = None                                  # chunk index the buffer holds
-        if self.world > 1:
+        if comm is not None:                                  # (world 1 too: the collective path itself)
             self.bsum_pad = a.empty((n1, max(self.nblk_max, 1)), F8)
             self.bcnt_pad = a.empty((n1, max(self.nblk_max, 1)), I4)
         self.rm = a.empty(n1, F8)
@@ -394,7 +394,7 @@ class Steps47:
         self.norms.zero_()
         kk = max(k, 1)
         self.rows_per = self.np_rs // self.world
-        if self.world > 1:
+        if comm is not None:
             self.grow = a.empty((self.rows_per, self.np_), I8)
         self.idx_l = a.empty((self.rows_per, kk), I4)
         self.d2_l = a.empty((self.rows_per, kk), I8)

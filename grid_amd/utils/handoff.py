@@ -26,7 +26,8 @@ def _stamp(path):
 def publish(path, ids, scales, ratios, zq_dev, shape):
     """Record step 4's output for ``path`` (call after the file is closed).
     scales / ratios: the values the text holds ("%.2f" / "%.3f" read back),
-    zq_dev: device int32 hundredths [n][r] (GRID_MISSING = "NA")."""
+    zq_dev: device int32 hundredths [n][r] (GRID_ZQ_NAN = "NA", GRID_ZQ_NEG0 =
+    "-0.00": the k-NN gathers read both as zero, find_neighbors.py:57-58)."""
     _entries.clear()                       # one matrix at a time: it holds device memory
     _entries[os.path.realpath(path)] = (_stamp(path), list(ids), scales, ratios, zq_dev, shape)
 

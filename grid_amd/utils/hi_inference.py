@@ -331,9 +331,14 @@ def hi_inference_loci(config, console, comm=None):
       * ``dip_cn_file`` (default ``{output_dir}/{dip_prefix}.{locus}.{type}``,
         {locus} = ``{chrom}_{start}_{end}_{gene}``: gene names repeat in the
         734-region table, regions do not),
-      * ``ibs_output`` / ``ibd_output`` (a template, or one shared file: the
-        IBD loader filters and weights segments by each locus' region, as
-        the reference does with start_bp/end_bp),
+      * ``ibs_output`` / ``ibd_output`` (a template, or one shared file).  The
+        reference's IBD loader (hi_inference.py:86-172) does not filter
+        segments by region or chromosome: every locus reads every segment of
+        its file, and only ``weighted`` uses the locus' start/end (the
+        Lorentzian weight of the segment's distance to the region).  One
+        shared IBD file across loci on several chromosomes is therefore read
+        genome-wide for each locus, as the reference would; a warning says so
+        (use a {chrom} template for per-chromosome files),
       * ``loci_output`` (default ``{output_dir}/{prefix}.{locus}.{type}``).
     Each output file is what the reference's hi_inference writes for a
     config with that locus' chrom/start_bp/end_bp.  ``comm``: a
@@ -369,6 +374,10 @@ def hi_inference_loci(config, console, comm=None):
         log(console, "Config error: loci_output names collide (add {index} or {start} to the template)",
             style="danger")
         return None
+    if method == "ibd" and "{" not in str(nbr_t) and len({lc["chrom"] for lc in loci}) > 1:
+        log(console, f"ibd_output {nbr_t} is one file for loci on {len({lc['chrom'] for lc in loci})} "
+            "chromosomes: every locus reads all of its segments (no region filter, as the reference)",
+            style="warning")
     rank, world = _rank_world(comm)
     mine = [lc for lc in loci if lc["index"] % world == rank]
     log(console, f"Phasing {len(mine)} of {len(loci)} loci on rank {rank}/{world} ({method})")

@@ -369,6 +369,11 @@ typedef struct grid_hi_locus {
   double *imp;                     /* [2n] out */
   double *mean;                    /* [1] out */
 } grid_hi_locus;
+/* grid_hi_pack of every locus on the device: fills each descriptor's pk_nbr
+ * [n][2][16], pk_cnt [n][2] and (when non-NULL) pk_w from its off / nbr / w /
+ * order -- the same arrays as the host grid_hi_pack, without their host build
+ * and upload (config 5: 6.8 MB per 50k-sample locus).  max_n: the largest n. */
+int grid_hi_pack_batch(grid_ctx *ctx, int64_t n_loci, const grid_hi_locus *d_loci, int64_t max_n);
 /* max_n / max_nlev: the largest n / nlev in the batch (LDS sizing); flags and
  * max_list as grid_hi_phase, over the whole batch. */
 int grid_hi_phase_batch(grid_ctx *ctx, int64_t n_loci, const grid_hi_locus *d_loci, int64_t max_n,
