@@ -197,7 +197,10 @@ def plan_memory(n, ml, world, budget):
     """Resident (one chunk) when the whole shard fits the HBM budget, else the
     widest 8192-multiple chunk that does.  Returns (chunk or None, bytes)."""
     np_ = -(-max(n, 1) // 256) * 256
-    fixed = np_ * np_ * 8 * (1 + (1.0 / world if world > 1 else 0.0)) + n * (-(-ml // 8192)) * 24 + ml * 64
+    # Gram + (multi-GPU) the segment send / receive buffers: (2W+1)/(4W) and
+    # 1/W of that of np^2 int64 (fused.Steps47._step5_segments)
+    seg = (2 * world + 1) / (4.0 * world) * (1 + 1.0 / world) if world > 1 else 0.0
+    fixed = np_ * np_ * 8 * (1 + seg) + n * (-(-ml // 8192)) * 24 + ml * 64
     per_col_resident = n * 4 + n * 2 + np_ * 2            # q int32 + z int16 + bf16 panel
     if fixed + per_col_resident * ml <= budget:
         return None, fixed + per_col_resident * ml
@@ -293,9 +296,10 @@ def main():
         _abi.call("grid_synth_depth", dev.ctx, SEED, n, ml, ml, c0, NCL, q.data_ptr())
         ldq = ml
     reads, off, nbr, w = synth_reads_and_ibs(n)
-    # step 7 on its own stream: it overlaps the next pass's steps 4-5 (every
-    # pass is still complete inside the timed region: the final synchronize
-    # waits for both streams)
+    # step 7 on its own stream, deferred behind the next pass's Gram (fused.py
+    # Steps47): it overlaps that pass's top-k/dipCN and the next statistics;
+    # every pass's phasing still completes inside the timed region (finish()
+    # before the final synchronize)
     lane = None
     if not args.no_overlap:
         pdev = _abi.Device(local)
@@ -315,6 +319,7 @@ def main():
     note(f"{n} x {m}, shard {ml} bins, {st.nch} chunk(s); warmup {args.warmup}, steps {args.steps}")
     for w_ in range(args.warmup):
         st.run(q, ldq)
+        st.finish()
         torch.cuda.synchronize()
         note(f"warmup {w_} done")
     torch.cuda.synchronize()
@@ -329,6 +334,7 @@ def main():
         gram_pairs += st.gram_evs
         if st.nch > 1:                          # long streamed steps: progress for the watchdog
             note(f"step {s} queued")
+    st.finish()                                 # the last step's (deferred) phasing, inside the clock
     torch.cuda.synchronize()
     note("timed steps done")
     if dist:

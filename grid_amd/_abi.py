@@ -23,6 +23,7 @@ ZQ_NEG0 = -(2 ** 31) + 1
 ZQ16_NAN, ZQ16_NEG0, ZQ16_ESC = -32768, -32767, -32766   # GRID_ZQ16_* (grid_norm_zquant_kb16)
 BLOCK = 8192
 KBW = 32                       # K-block width of the k-NN panel (common.hpp KBW)
+SEG_K1 = 16                    # GRID_SEG_K1: candidate keys per row / column (multi-GPU step 5)
 
 _i64, _i32, _f64, _vp = C.c_int64, C.c_int32, C.c_double, C.c_void_p
 
@@ -72,6 +73,8 @@ _SIGS = {
     "grid_knn_diag": [_vp, _vp, _i64, _i64, _vp],
     "grid_knn_topk_rows": [_vp, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp],
     "grid_knn_topk_d2": [_vp, _vp, _i64, _f64, _i64, _i64, _i64, _i64, _vp, _vp, _vp],
+    "grid_knn_seg_topk": [_vp, _vp, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _i64, _vp, _vp],
+    "grid_knn_seg_merge": [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp],
     "grid_knn_dist_i32": [_vp, _vp, _i64, _i64, _i64, _vp, _i64],
     "grid_knn_dist_f64": [_vp, _vp, _i64, _i64, _i64, _vp, _i64],
     "grid_knn_panel_i32": [_vp, _vp, _i64, _i64, _vp, _i64, _i32, _vp, _i64, _i64],

@@ -1180,11 +1180,16 @@ __device__ __forceinline__ void topk_emit(const Src &src, const unsigned long lo
 // (branch-free insertion, taken only when a key beats the lane's largest);
 // each wave then extracts its ktake smallest by wave-wide minimum rounds, and
 // one lane merges the four waves' sorted lists.
+// j0 / raw (the multi-GPU segment path, grid_knn_seg_topk): only columns
+// [j0, n) are scanned (rows points j0 elements before the segment row), and
+// the ktake smallest packed keys are written to raw[orow][K1] (ascending,
+// ~0 padded) instead of the neighbour lists.
 template <int K1, class T>
 __global__ __launch_bounds__(256) void k_topk_small(const T *__restrict__ rows, int64_t ld,
                                                     const int64_t *__restrict__ nrm, double scale, int64_t n,
                                                     int64_t k, int64_t row0, int32_t *__restrict__ idx,
-                                                    void *__restrict__ d2o, int32_t *__restrict__ cnto) {
+                                                    void *__restrict__ d2o, int32_t *__restrict__ cnto,
+                                                    int64_t j0 = 0, unsigned long long *__restrict__ raw = nullptr) {
   __shared__ unsigned long long s_w[4][K1];
   __shared__ unsigned long long s_m[4 * K1];
   const int64_t orow = blockIdx.x, i = row0 + orow;
@@ -1204,7 +1209,7 @@ __global__ __launch_bounds__(256) void k_topk_small(const T *__restrict__ rows, 
       }
     }
   };
-  int64_t j = tid;
+  int64_t j = j0 + tid;
   for (; j + 3 * 256 < n; j += 4 * 256) {       // four loads of each kind in flight
     unsigned long long kk[4];
     src.load4(j, 256, kk);
@@ -1240,8 +1245,112 @@ __global__ __launch_bounds__(256) void k_topk_small(const T *__restrict__ rows, 
       p[bw]++;
       s_m[e] = bv;
     }
-    topk_emit(src, s_m, ktake, i, k, orow, idx, (typename decltype(src)::out_t *)d2o, cnto);
+    if (raw) {
+      for (int e = 0; e < K1; e++) raw[orow * K1 + e] = e < ktake ? s_m[e] : ~0ull;
+    } else {
+      topk_emit(src, s_m, ktake, i, k, orow, idx, (typename decltype(src)::out_t *)d2o, cnto);
+    }
   }
+}
+
+// ---- multi-GPU: neighbour candidates from upper-triangle row SEGMENTS -------
+// A sharded run reduce-scatters only segment b = Gram rows [b*B, (b+1)*B) x
+// columns [b*B, np) of the 2W row blocks (rank r: blocks r and 2W-1-r, equal
+// volumes), about half of the full rows.  Every pair (i, j) lies in some
+// segment: in block(i)'s segment when j >= block(i)*B, else in block(j)'s at
+// (row j, column i).  So the true k+1 nearest of row i are among (a) the
+// k+1 smallest of row i in its own segment (k_topk_small in raw mode) and
+// (b) for every block b <= block(i), the k+1 smallest of COLUMN i in segment
+// b (k_seg_cols); k_seg_merge picks them exactly by the packed (d2, j) key.
+//
+// Column candidates: one thread per segment column t (j = c0 + t < n), rows
+// i = r0 + u (u < B, i < n) in order; keys (d2 << 20 | i), K1 smallest kept
+// sorted in registers; raw[t][K1] ascending, ~0 padded.
+template <int K1>
+__global__ __launch_bounds__(256) void k_seg_cols(const int64_t *__restrict__ seg, int64_t ld, int64_t nrows,
+                                                  int64_t ncols, const int64_t *__restrict__ nrm, int64_t n,
+                                                  int64_t r0, int64_t c0, unsigned long long *__restrict__ raw) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ncols) return;
+  const int64_t j = c0 + t;
+  unsigned long long L[K1];
+#pragma unroll
+  for (int e = 0; e < K1; e++) L[e] = ~0ull;
+  if (j < n) {
+    const int64_t gjj = nrm[j];
+    const int64_t ue = n - r0 < nrows ? n - r0 : nrows;
+    for (int64_t u = 0; u < ue; u++) {
+      const int64_t i = r0 + u;
+      unsigned long long key = ((unsigned long long)(nrm[i] + gjj - 2 * seg[u * ld + t]) << 20) |
+                               (unsigned long long)i;
+      if (key < L[K1 - 1]) {
+#pragma unroll
+        for (int e = 0; e < K1; e++) {
+          const unsigned long long lo = key < L[e] ? key : L[e];
+          key = key < L[e] ? L[e] : key;
+          L[e] = lo;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < K1; e++) raw[t * K1 + e] = L[e];
+}
+
+// Row i (one thread): the union of its row list (rowc[block(i)][i - block*B])
+// and the column lists colc[b][i - b*B] of every block b <= block(i), equal
+// keys once (a pair of the diagonal block is in both), the ktake smallest,
+// then topk_emit (self dropped, first k kept) -- the rows' top-k exactly as
+// k_topk_small on full rows.
+template <int K1>
+__global__ __launch_bounds__(256) void k_seg_merge(const unsigned long long *__restrict__ rowc,
+                                                   const unsigned long long *__restrict__ colc, int64_t ldc,
+                                                   int64_t B, int64_t n, int64_t k, int32_t *__restrict__ idx,
+                                                   int64_t *__restrict__ d2o, int32_t *__restrict__ cnto) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t ktake = (k + 1 < n) ? k + 1 : n;
+  const int64_t bi = i / B;
+  unsigned long long L[K1];
+#pragma unroll
+  for (int e = 0; e < K1; e++) L[e] = ~0ull;
+  auto insert = [&](unsigned long long key) {
+    if (key < L[K1 - 1]) {
+      bool dup = false;
+#pragma unroll
+      for (int e = 0; e < K1; e++) dup |= L[e] == key;
+      if (dup) return;
+#pragma unroll
+      for (int e = 0; e < K1; e++) {
+        const unsigned long long lo = key < L[e] ? key : L[e];
+        key = key < L[e] ? L[e] : key;
+        L[e] = lo;
+      }
+    }
+  };
+  const unsigned long long *rl = rowc + i * K1;        // block-major rows = global row order
+  for (int e = 0; e < K1; e++) insert(rl[e]);
+  for (int64_t b = 0; b <= bi; b++) {
+    const unsigned long long *cl = colc + (b * ldc + (i - b * B)) * K1;
+    for (int e = 0; e < K1; e++) insert(cl[e]);
+  }
+  int64_t w = 0;
+  bool self = false;
+  for (int64_t e = 0; e < ktake; e++) {
+    const unsigned long long key = L[e];
+    const int64_t j = (int64_t)(key & 0xFFFFFull);
+    if (j == i && !self) { self = true; continue; }
+    if (w < k) {
+      idx[i * k + w] = (int32_t)j;
+      d2o[i * k + w] = (int64_t)(key >> 20);
+      w++;
+    }
+  }
+  for (int64_t e = w; e < k; e++) {
+    idx[i * k + e] = -1;
+    d2o[i * k + e] = 0;
+  }
+  cnto[i] = (int32_t)w;
 }
 
 // Row top-(k+1) for larger k: 8-pass radix select on the packed keys over the
@@ -1252,7 +1361,8 @@ template <class T>
 __global__ __launch_bounds__(256) void k_topk_radix(const T *__restrict__ rows, int64_t ld,
                                                     const int64_t *__restrict__ nrm, double scale, int64_t n,
                                                     int64_t k, int64_t row0, int32_t *__restrict__ idx,
-                                                    void *__restrict__ d2o, int32_t *__restrict__ cnto) {
+                                                    void *__restrict__ d2o, int32_t *__restrict__ cnto,
+                                                    int64_t = 0, unsigned long long *__restrict__ = nullptr) {
   __shared__ unsigned hist[256];
   __shared__ unsigned long long s_prefix;
   __shared__ long long s_rank;
@@ -1678,7 +1788,7 @@ int grid_knn_topk_rows(grid_ctx *ctx, const int64_t *d_rows, int64_t ld, const i
   auto kern = ktake <= 16 ? k_topk_small<16, int64_t> : ktake <= 32 ? k_topk_small<32, int64_t>
                                                                       : k_topk_radix<int64_t>;
   hipLaunchKernelGGL(kern, dim3((unsigned)nrows), dim3(256), 0, ctx->stream, d_rows, ld, d_norms, 1.0, n, k, row0,
-                     d_idx, (void *)d_d2, d_cnt);
+                     d_idx, (void *)d_d2, d_cnt, (int64_t)0, (unsigned long long *)nullptr);
   LAUNCHCHK();
   return GRID_OK;
 }
@@ -1696,7 +1806,8 @@ int grid_knn_topk_d2(grid_ctx *ctx, const double *d_d2rows, int64_t ld, double k
   auto kern = ktake <= 16 ? k_topk_small<16, double> : ktake <= 32 ? k_topk_small<32, double>
                                                                      : k_topk_radix<double>;
   hipLaunchKernelGGL(kern, dim3((unsigned)nrows), dim3(256), 0, ctx->stream, d_d2rows, ld,
-                     (const int64_t *)nullptr, key_scale, n, k, row0, d_idx, (void *)d_d2, d_cnt);
+                     (const int64_t *)nullptr, key_scale, n, k, row0, d_idx, (void *)d_d2, d_cnt, (int64_t)0,
+                     (unsigned long long *)nullptr);
   LAUNCHCHK();
   return GRID_OK;
 }
@@ -1771,6 +1882,46 @@ int grid_knn_topk(grid_ctx *ctx, int64_t *d_gram, int64_t n, int64_t np_, int64_
   rc = grid_knn_diag(ctx, d_gram, np_, n, nrm);
   if (rc) return rc;
   return grid_knn_topk_rows(ctx, d_gram + row0 * np_, np_, nrm, n, k, row0, nrows, d_idx, d_d2, d_cnt);
+}
+
+int grid_knn_seg_topk(grid_ctx *ctx, const int64_t *d_seg, int64_t ld, int64_t nrows, int64_t ncols,
+                      const int64_t *d_norms, int64_t n, int64_t k, int64_t r0, int64_t c0,
+                      unsigned long long *d_rowc, unsigned long long *d_colc) {
+  REQUIRE(ctx && d_seg && d_norms && d_rowc && d_colc, "bad args");
+  REQUIRE(n > 0 && n <= (1 << 20) && k >= 0 && k + 1 <= GRID_SEG_K1, "bad n / k (k + 1 <= %d)", GRID_SEG_K1);
+  REQUIRE(nrows >= 0 && ncols >= 0 && ld >= ncols && r0 >= 0 && c0 >= 0, "bad segment");
+  // rows of the segment that are samples: row lists (raw mode, columns [c0, n))
+  const int64_t rr = r0 < n ? (n - r0 < nrows ? n - r0 : nrows) : 0;
+  if (rr > 0) {
+    hipLaunchKernelGGL((k_topk_small<GRID_SEG_K1, int64_t>), dim3((unsigned)rr), dim3(256), 0, ctx->stream,
+                       d_seg - c0, ld, d_norms, 1.0, n, k, r0, (int32_t *)nullptr, (void *)nullptr,
+                       (int32_t *)nullptr, c0, d_rowc);
+    LAUNCHCHK();
+  }
+  if (nrows > rr) {          // padding rows: no candidates
+    HIPCHK(hipMemsetAsync(d_rowc + rr * GRID_SEG_K1, 0xFF, (nrows - rr) * GRID_SEG_K1 * 8, ctx->stream));
+  }
+  if (ncols > 0) {
+    hipLaunchKernelGGL(k_seg_cols<GRID_SEG_K1>, dim3((unsigned)((ncols + 255) / 256)), dim3(256), 0, ctx->stream,
+                       d_seg, ld, nrows, ncols, d_norms, n, r0, c0, d_colc);
+    LAUNCHCHK();
+  }
+  return GRID_OK;
+}
+
+int grid_knn_seg_merge(grid_ctx *ctx, const unsigned long long *d_rowc, const unsigned long long *d_colc,
+                       int64_t ldc, int64_t B, int64_t n, int64_t k, int32_t *d_idx, int64_t *d_d2,
+                       int32_t *d_cnt) {
+  REQUIRE(ctx && d_rowc && d_colc && d_idx && d_d2 && d_cnt, "bad args");
+  REQUIRE(n > 0 && n <= (1 << 20) && k >= 0 && k + 1 <= GRID_SEG_K1 && B > 0 && ldc >= B, "bad args");
+  if (k == 0) {
+    HIPCHK(hipMemsetAsync(d_cnt, 0, n * 4, ctx->stream));
+    return GRID_OK;
+  }
+  hipLaunchKernelGGL(k_seg_merge<GRID_SEG_K1>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, d_rowc,
+                     d_colc, ldc, B, n, k, d_idx, d_d2, d_cnt);
+  LAUNCHCHK();
+  return GRID_OK;
 }
 
 }  // extern "C"

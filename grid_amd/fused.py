@@ -25,11 +25,15 @@ Multi-GPU: the bin (column) axis is sharded in 8192-aligned ranges
   * column statistics need no communication (sequential over all rows,
     locally); the median and the selection threshold come from all-gathered
     ratio vectors, sorted identically on every rank;
-  * the Gram matrix is an integer sum over bins: each rank mirrors its
-    partial Gram to full rows and ONE reduce-scatter (int64 sum: order-free,
-    exact) leaves rank r the complete rows [r*np/W, (r+1)*np/W); the norms
-    G_jj come from an all-reduce of the partial diagonals (n int64);
-  * top-k on the rank's rows, then an all-gather of the neighbour lists;
+  * the Gram matrix is an integer sum over bins (int64 sums: order-free,
+    exact).  Its rows are cut into 2W blocks of B; ONE reduce-scatter of the
+    upper-triangle SEGMENTS (block b's rows x columns >= b*B) leaves rank r
+    the complete segments of blocks r and 2W-1-r -- equal shares, about half
+    the bytes of whole rows; the norms G_jj come from an all-reduce of the
+    partial diagonals (n int64);
+  * every pair lies in one segment (as a row or as a column entry), so the
+    per-segment row and column candidates (k+1 each), all-gathered, give
+    every rank the exact neighbour lists of all rows (grid_knn_seg_merge);
     dipCN and phasing are replicated (tiny / sequential per locus).
 
 The chain is written against an ``ops`` object.  The product always uses
@@ -250,6 +254,13 @@ class HipOps:
     def diag(self, gram, np_, n, norms):
         call("grid_knn_diag", self.ctx, ptr(gram), np_, n, ptr(norms))
 
+    def seg_topk(self, seg, ld, nrows, ncols, norms, n, k, r0, c0, rowc, colc):
+        call("grid_knn_seg_topk", self.ctx, ptr(seg), ld, nrows, ncols, ptr(norms), n, k, r0, c0, ptr(rowc),
+             ptr(colc))
+
+    def seg_merge(self, rowc, colc, ldc, B, n, k, idx, d2, cnt):
+        call("grid_knn_seg_merge", self.ctx, ptr(rowc), ptr(colc), ldc, B, n, k, ptr(idx), ptr(d2), ptr(cnt))
+
     def topk_rows(self, rows, ld, norms, n, k, row0, nrows, idx, d2, cnt):
         call("grid_knn_topk_rows", self.ctx, ptr(rows), ld, ptr(norms), n, k, row0, nrows, ptr(idx), ptr(d2),
              ptr(cnt))
@@ -327,10 +338,16 @@ class Steps47:
                  sigma2_max=1000.0, frac_r=1.0, min_nbr=1, n_iters=100, comm=None, phase_lane=None, zq16=True,
                  chunk=None, keep_z=True, on_z_chunk=None):
         """``phase_lane``: optional (ops, torch.cuda.Stream) pair on which step
-        7 runs, ordered after this pass's dipCN by an event; the next pass's
-        dipCN waits for it.  Phasing is one workgroup for ~6 ms, so on its own
-        stream it overlaps the next pass's steps 4-5 instead of idling the
-        other 255 CUs (and, multi-GPU, it no longer adds to every rank's step)."""
+        7 runs.  Phasing is one workgroup for ~4 ms, so on its own stream it
+        overlaps other work instead of idling the other 255 CUs.  It is
+        DEFERRED: pass i's phasing is issued during pass i+1, ordered after
+        that pass's last Gram launch (an event), so its workgroup never holds
+        a CU while the persistent Gram (one workgroup per CU) is resident -- a
+        Gram workgroup queued behind it held the whole launch open (the short
+        per-rank steps of the multi-GPU runs).  It then overlaps pass i+1's
+        top-k / dipCN and pass i+2's statistics and quantisation.  dipCN
+        writes alternate buffers; ``finish()`` issues the last pass's phasing
+        (call it before reading ``hap`` / ``imp`` or stopping a clock)."""
         self.ops, self.A, self.comm = ops, alloc, comm
         self.phase_lane = phase_lane
         self.ev_phase = None
@@ -383,7 +400,12 @@ class Steps47:
             cap = min(n1 * zw, max(1 << 20, (n1 * zw) >> 10))
             self.esc_idx, self.esc_val = a.empty(cap, I8), a.empty(cap, I4)
         self.np_ = pad_to(n1, 256)
-        self.np_rs = pad_to(self.np_, self.world)         # Gram rows: equal blocks for the reduce-scatter
+        # multi-GPU step 5 (comm given): the Gram's 2W row blocks of B rows; rank
+        # r reduces only the upper-triangle segments of blocks r and 2W-1-r
+        # (grid_knn_seg_topk), about half of the full rows, equal per rank
+        self.B = -(-self.np_ // (2 * self.world))
+        self.npw = 2 * self.world * self.B
+        self.np_rs = self.npw if comm is not None else self.np_
         self.kpad = pad_to(cw, 64)
         # step-5 input panel (bf16), K-blocked [kpad/32][np][32]: one K-step of a
         # row panel is contiguous for the Gram kernel's DMA
@@ -393,15 +415,35 @@ class Steps47:
         self.norms = a.empty(self.np_, I8)
         self.norms.zero_()
         kk = max(k, 1)
-        self.rows_per = self.np_rs // self.world
         if comm is not None:
-            self.grow = a.empty((self.rows_per, self.np_), I8)
-        self.idx_l = a.empty((self.rows_per, kk), I4)
-        self.d2_l = a.empty((self.rows_per, kk), I8)
-        self.cnt_l = a.empty(self.rows_per, I4)
+            if kk + 1 > _abi.SEG_K1:
+                raise _abi.GridNativeError(f"the sharded chain needs k + 1 <= {_abi.SEG_K1}")
+            W, B = self.world, self.B
+            self.my_blocks = (self.rank, 2 * W - 1 - self.rank)
+            self.seg_len = B * (2 * W + 1) * B                 # int64 cells of one rank's two segments
+            self.seg_send = a.empty(W * self.seg_len, I8)
+            self.seg_recv = a.empty(self.seg_len, I8)
+            K1 = _abi.SEG_K1
+            self.rowc_l = a.empty((2, B, K1), I8)               # packed keys (uint64 bits)
+            self.colc_l = a.empty((2, self.npw, K1), I8)
+            # gathered lists -> global block order: block b is rank b (slot 0)
+            # for b < W, else rank 2W-1-b (slot 1)
+            self.blk_src = [(b, 0) if b < W else (2 * W - 1 - b, 1) for b in range(2 * W)]
+            self.idx_l = a.empty((n1, kk), I4)
+            self.d2_l = a.empty((n1, kk), I8)
+            self.cnt_l = a.empty(n1, I4)
+        else:
+            self.idx_l = a.empty((n1, kk), I4)
+            self.d2_l = a.empty((n1, kk), I8)
+            self.cnt_l = a.empty(n1, I4)
         self.scale2 = a.empty(n1, F8)
         self.nscale = a.empty((n1, kk), F8)
-        self.dip = a.empty(n1, F8)
+        # dipCN output, double-buffered: the deferred phasing of pass i reads
+        # one buffer while pass i+1's dipCN writes the other
+        self._dips = [a.empty(n1, F8), a.empty(n1, F8)]
+        self._cur = 0
+        self._ev_free = [None, None]        # event: the phasing that read _dips[b] is done
+        self._pending = None                 # dipCN buffer whose phasing is not issued yet
         self.valid = a.empty(n1, U1)
         self.hap = a.empty(2 * n1, F8)
         self.imp = a.empty(2 * n1, F8)
@@ -422,6 +464,11 @@ class Steps47:
         self.nlev = nl
         self.sched = (up(np.asarray(order, I4)), up(np.asarray(loff, I4)), nl, up(pk_nbr), up(pk_w), up(pk_cnt),
                       flags, max_list)
+
+    @property
+    def dip(self):
+        """dipCN values of the last pass."""
+        return self._dips[self._cur]
 
     def set_reads(self, reads):
         self.reads = self.A.upload(np.asarray(reads, F8))
@@ -614,55 +661,110 @@ class Steps47:
                 ev[1].record()
                 self.gram_evs.append(ev)
         self._mark("zquant_gram")
+        # the previous pass's deferred phasing starts once this pass's Gram is done
+        if not profile:
+            self._issue_pending()
         # ---- step 5: full rows (mirror), reduce-scatter by row blocks, top-k ----
         o.mirror(self.gram, self.np_)
         o.diag(self.gram, self.np_, n, self.norms)
         if self.comm is not None:
             self.comm.all_reduce_sum(self.norms)
-            self.comm.reduce_scatter_sum(self.grow, self.gram)
-            rows = self.grow
-            self._mark("reduce_scatter")
+            self._step5_segments()
         else:
-            rows = self.gram
-        r0 = min(self.rank * self.rows_per, n)
-        nr = max(min(n - r0, self.rows_per), 0)
-        o.topk_rows(rows, self.np_, self.norms, n, self.k, r0, nr, self.idx_l, self.d2_l, self.cnt_l)
-        if self.comm is not None:
-            kk = max(self.k, 1)
-            idx = self.comm.all_gather(self.idx_l).view(-1, kk)[:n].contiguous()
-            self.d2 = self.comm.all_gather(self.d2_l).view(-1, kk)[:n].contiguous()
-            cnt = self.comm.all_gather(self.cnt_l).view(-1)[:n].contiguous()
-        else:
-            idx, self.d2, cnt = self.idx_l, self.d2_l, self.cnt_l
+            o.topk_rows(self.gram, self.np_, self.norms, n, self.k, 0, n, self.idx_l, self.d2_l, self.cnt_l)
+        idx, self.d2, cnt = self.idx_l, self.d2_l, self.cnt_l
         self._mark("topk")
         # ---- step 6: dipCN (scales as printed "%.2f", neighbour gather) ----
         lane = None if profile else self.phase_lane
-        if self.ev_phase is not None:
+        if lane is None:
+            self.finish()                     # a deferred phasing of an earlier pass first
+        b = self._cur ^ 1 if lane is not None else self._cur
+        if self._ev_free[b] is not None:
             import torch
-            torch.cuda.current_stream().wait_event(self.ev_phase)   # previous pass's phasing read dip
-            self.ev_phase = None
+            torch.cuda.current_stream().wait_event(self._ev_free[b])   # the phasing that read it is done
+            self._ev_free[b] = None
         o.round_decimals(self.rm, n, 2, self.scale2)
         o.gather(self.scale2, idx, n * max(self.k, 1), self.nscale)
         if o.dipcn(n, self.reads, self.has, self.scale2, idx, self.nscale, cnt, max(self.k, 1), self.n_nbr,
-                   self.dip, self.valid):
+                   self._dips[b], self.valid):
             raise ZeroDivisionError("float division by zero")
+        self._cur = b
         self._mark("dipcn")
         # ---- step 7: level-scheduled Gauss-Seidel phasing + imputation ----
         if lane is not None:
-            import torch
-            pops, pstream = lane
-            ev = torch.cuda.Event()
-            ev.record()
-            pstream.wait_event(ev)
-            pops.phase(n, self.dip, self.off, self.nbr, self.w, self.min_nbr, self.n_iters, self.sched, self.hap,
-                       self.imp, self.mean)
-            self.ev_phase = torch.cuda.Event()
-            self.ev_phase.record(pstream)
+            self._pending = b                 # issued by the next pass after its Gram, or by finish()
         else:
-            o.phase(n, self.dip, self.off, self.nbr, self.w, self.min_nbr, self.n_iters, self.sched, self.hap,
-                    self.imp, self.mean)
+            o.phase(n, self._dips[b], self.off, self.nbr, self.w, self.min_nbr, self.n_iters, self.sched,
+                    self.hap, self.imp, self.mean)
         self._mark("phase")
         self.idx_out, self.cnt_out = idx, cnt
+
+    def _step5_segments(self):
+        """Sharded step 5: reduce-scatter the upper-triangle segments (each
+        rank sends W segment pairs, receives its own two, summed over ranks),
+        row and column candidates per segment, an all-gather of the candidate
+        lists, and the exact merge into every row's neighbours on every rank
+        (grid_knn_seg_topk / grid_knn_seg_merge)."""
+        o, n, W, B, npw, np_ = self.ops, self.n, self.world, self.B, self.npw, self.np_
+        torch = self.A.torch
+        send = self.seg_send.view(W, self.seg_len)
+        for q in range(W):                       # rank q's slot: its blocks q and 2W-1-q
+            off = 0
+            for b in (q, 2 * W - 1 - q):
+                nc = (2 * W - b) * B
+                dst = send[q, off:off + B * nc].view(B, nc)
+                r0, r1 = b * B, min((b + 1) * B, np_)
+                cv = max(min(np_, npw) - b * B, 0)
+                if r1 > r0 and cv > 0:
+                    dst[: r1 - r0, :cv].copy_(self.gram[r0:r1, b * B:b * B + cv])
+                    if cv < nc:
+                        dst[: r1 - r0, cv:].zero_()
+                if r1 - r0 < B:
+                    dst[max(r1 - r0, 0):].zero_()
+                off += B * nc
+        self.comm.reduce_scatter_sum(self.seg_recv, self.seg_send)
+        self._mark("reduce_scatter")
+        off = 0
+        for slot, b in enumerate(self.my_blocks):
+            nc = (2 * W - b) * B
+            o.seg_topk(self.seg_recv[off:off + B * nc], nc, B, nc, self.norms, n, self.k, b * B, b * B,
+                       self.rowc_l[slot], self.colc_l[slot])
+            off += B * nc
+        rg = self.comm.all_gather(self.rowc_l)              # [W][2][B][K1]
+        cg = self.comm.all_gather(self.colc_l)              # [W][2][npw][K1]
+        sel_q = torch.tensor([q for q, _ in self.blk_src], device=rg.device)
+        sel_s = torch.tensor([s_ for _, s_ in self.blk_src], device=rg.device)
+        rowc = rg[sel_q, sel_s].contiguous()                # [2W][B][K1] = global row order
+        colc = cg[sel_q, sel_s].contiguous()                # [2W][npw][K1]
+        o.seg_merge(rowc, colc, npw, B, n, self.k, self.idx_l, self.d2_l, self.cnt_l)
+
+    def _issue_pending(self):
+        """Issue the deferred phasing of _dips[_pending] on the phase lane,
+        after everything issued so far on the main stream."""
+        if self._pending is None:
+            return
+        import torch
+        b, self._pending = self._pending, None
+        pops, pstream = self.phase_lane
+        ev = torch.cuda.Event()
+        ev.record()
+        pstream.wait_event(ev)
+        pops.phase(self.n, self._dips[b], self.off, self.nbr, self.w, self.min_nbr, self.n_iters, self.sched,
+                   self.hap, self.imp, self.mean)
+        done = torch.cuda.Event()
+        done.record(pstream)
+        self._ev_free[b] = done
+        self.ev_phase = done
+
+    def finish(self):
+        """Issue the last pass's deferred phasing and order the main stream
+        after it (hap / imp / mean are then the last pass's once the stream
+        syncs)."""
+        self._issue_pending()
+        if self.ev_phase is not None:
+            import torch
+            torch.cuda.current_stream().wait_event(self.ev_phase)
+            self.ev_phase = None
 
     def _chunk_bounds(self, r_loc):
         """Per chunk: the range [sb[c], sb[c+1]) of selected indices whose

@@ -293,6 +293,27 @@ int grid_knn_gather_f64(grid_ctx *ctx, const int32_t *d_zq, int64_t n, int64_t l
  * is filled in place). */
 int grid_knn_topk(grid_ctx *ctx, int64_t *d_gram, int64_t n, int64_t np_, int64_t k,
                   int64_t row0, int64_t nrows, int32_t *d_idx, int64_t *d_d2, int32_t *d_cnt);
+/* Multi-GPU (the sharded chain's step 5; find_neighbors.py:207-225 on a Gram
+ * summed over bin shards): ranks reduce only upper-triangle SEGMENTS of the
+ * Gram -- block b = rows [r0, r0 + nrows) x columns [c0, c0 + ncols), r0 = c0
+ * = b*B -- and take the neighbours from candidates.  grid_knn_seg_topk on one
+ * segment (d_seg[u*ld + t] = G(r0 + u, c0 + t), norms as grid_knn_topk_rows):
+ *   d_rowc [nrows][GRID_SEG_K1]: per segment row i < n, the k+1 smallest
+ *     packed keys (d2 << 20 | j) over its columns j in [c0, n), ascending;
+ *   d_colc [ncols][GRID_SEG_K1]: per column j < n, the k+1 smallest keys
+ *     (d2 << 20 | i) over the segment's rows i < n;
+ * unused entries ~0.  grid_knn_seg_merge: rows' candidates d_rowc [n'][K1]
+ * in global row order and every block's column lists d_colc [2W][ldc][K1]
+ * (block b's column t = sample b*B + t) -> the neighbour lists of all n rows,
+ * as grid_knn_topk_rows would give them on complete rows (exact: every pair
+ * is in the segment of the lower block index, as row or as column). */
+#define GRID_SEG_K1 16
+int grid_knn_seg_topk(grid_ctx *ctx, const int64_t *d_seg, int64_t ld, int64_t nrows, int64_t ncols,
+                      const int64_t *d_norms, int64_t n, int64_t k, int64_t r0, int64_t c0,
+                      unsigned long long *d_rowc, unsigned long long *d_colc);
+int grid_knn_seg_merge(grid_ctx *ctx, const unsigned long long *d_rowc, const unsigned long long *d_colc,
+                       int64_t ldc, int64_t B, int64_t n, int64_t k, int32_t *d_idx, int64_t *d_d2,
+                       int32_t *d_cnt);
 
 /* ---------------------------------------------------- step 6: diploid CN
  * Replaces grid/utils/compute_dipcn.py :62-88.

@@ -163,6 +163,54 @@ class NumpyOps:
     def diag(self, gram, np_, n, norms):
         _np(norms)[:n] = np.diag(_np(gram)[:n, :n])
 
+    # multi-GPU step 5 (grid_knn_seg_topk / grid_knn_seg_merge): packed keys
+    # (d2 << 20 | index) as uint64 bits in int64 buffers, K1 = 16 per list
+    K1 = 16
+
+    def seg_topk(self, seg, ld, nrows, ncols, norms, n, k, r0, c0, rowc, colc):
+        s = _np(seg).reshape(-1)[: nrows * ld].reshape(nrows, ld)[:, :ncols]
+        dg = _np(norms)[:n].astype(np.int64)
+        rc = _np(rowc).reshape(nrows, self.K1).view(np.uint64)
+        cc = _np(colc).reshape(-1, self.K1)[:ncols].view(np.uint64)
+        rc[:] = np.uint64(2 ** 64 - 1)
+        cc[:] = np.uint64(2 ** 64 - 1)
+        ktake = min(k + 1, n)
+        for u in range(nrows):
+            i = r0 + u
+            if i >= n:
+                break
+            js = np.arange(c0, n)
+            d = dg[i] + dg[js] - 2 * s[u, : n - c0]
+            keys = np.sort((d.astype(np.uint64) << np.uint64(20)) | js.astype(np.uint64))[:ktake]
+            rc[u, : len(keys)] = keys
+        for t in range(ncols):
+            j = c0 + t
+            if j >= n:
+                break
+            iu = np.arange(min(nrows, max(n - r0, 0)))
+            d = dg[r0 + iu] + dg[j] - 2 * s[iu, t]
+            keys = np.sort((d.astype(np.uint64) << np.uint64(20)) | (r0 + iu).astype(np.uint64))[: self.K1]
+            cc[t, : len(keys)] = keys
+
+    def seg_merge(self, rowc, colc, ldc, B, n, k, idx, d2, cnt):
+        rc = _np(rowc).reshape(-1, self.K1).view(np.uint64)
+        cc = _np(colc).reshape(-1, ldc, self.K1).view(np.uint64)
+        ktake = min(k + 1, n)
+        for i in range(n):
+            bi = i // B
+            cand = set(rc[i].tolist())
+            for b in range(bi + 1):
+                cand.update(cc[b, i - b * B].tolist())
+            keys = sorted(c for c in cand if c != 2 ** 64 - 1)[:ktake]
+            lst = [(key & 0xFFFFF, key >> 20) for key in keys]
+            lst = [(j, dd) for j, dd in lst if j != i][:k] if any(j == i for j, _ in lst) else lst[:k]
+            _np(idx)[i, :] = -1
+            _np(d2)[i, :] = 0
+            for t, (j, dd) in enumerate(lst):
+                _np(idx)[i, t] = j
+                _np(d2)[i, t] = dd
+            _np(cnt)[i] = len(lst)
+
     def topk_rows(self, rows, ld, norms, n, k, row0, nrows, idx, d2, cnt):
         g = _np(rows).reshape(-1)
         dg = _np(norms)[:n]

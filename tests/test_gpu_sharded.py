@@ -56,6 +56,7 @@ def run_chain(rank, world, comm, lane):
     st.set_phasing_graph(off, nbr, w)
     st.run(qs, c1 - c0)
     st.run(qs, c1 - c0)                  # second pass: the lane's cross-pass ordering
+    st.finish()                          # the second pass's deferred phasing
     torch.cuda.synchronize()
     ml = c1 - c0
     return {
