@@ -1263,23 +1263,26 @@ __global__ __launch_bounds__(256) void k_topk_small(const T *__restrict__ rows, 
 // (b) for every block b <= block(i), the k+1 smallest of COLUMN i in segment
 // b (k_seg_cols); k_seg_merge picks them exactly by the packed (d2, j) key.
 //
-// Column candidates: one thread per segment column t (j = c0 + t < n), rows
-// i = r0 + u (u < B, i < n) in order; keys (d2 << 20 | i), K1 smallest kept
-// sorted in registers; raw[t][K1] ascending, ~0 padded.
+// Column candidates: 32 columns x 8 row groups per workgroup; thread (g, c)
+// scans the rows u = g, g + 8, ... (i = r0 + u < n) of column t (j = c0 + t
+// < n) keeping the K1 smallest keys (d2 << 20 | i) sorted in registers, and
+// one thread per column merges the 8 sorted lists (keys are unique: distinct
+// i).  raw[t][K1] ascending, ~0 padded.
 template <int K1>
 __global__ __launch_bounds__(256) void k_seg_cols(const int64_t *__restrict__ seg, int64_t ld, int64_t nrows,
                                                   int64_t ncols, const int64_t *__restrict__ nrm, int64_t n,
                                                   int64_t r0, int64_t c0, unsigned long long *__restrict__ raw) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= ncols) return;
+  __shared__ unsigned long long s_l[8][32][K1];
+  const int c = threadIdx.x & 31, g = threadIdx.x >> 5;
+  const int64_t t = (int64_t)blockIdx.x * 32 + c;
   const int64_t j = c0 + t;
   unsigned long long L[K1];
 #pragma unroll
   for (int e = 0; e < K1; e++) L[e] = ~0ull;
-  if (j < n) {
+  if (t < ncols && j < n) {
     const int64_t gjj = nrm[j];
     const int64_t ue = n - r0 < nrows ? n - r0 : nrows;
-    for (int64_t u = 0; u < ue; u++) {
+    for (int64_t u = g; u < ue; u += 8) {
       const int64_t i = r0 + u;
       unsigned long long key = ((unsigned long long)(nrm[i] + gjj - 2 * seg[u * ld + t]) << 20) |
                                (unsigned long long)i;
@@ -1294,7 +1297,22 @@ __global__ __launch_bounds__(256) void k_seg_cols(const int64_t *__restrict__ se
     }
   }
 #pragma unroll
-  for (int e = 0; e < K1; e++) raw[t * K1 + e] = L[e];
+  for (int e = 0; e < K1; e++) s_l[g][c][e] = L[e];
+  __syncthreads();
+  if (g == 0 && t < ncols) {
+    int p[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int e = 0; e < K1; e++) {
+      int bw = 0;
+      unsigned long long bv = ~0ull;
+#pragma unroll
+      for (int w = 0; w < 8; w++) {
+        const unsigned long long v = p[w] < K1 ? s_l[w][c][p[w]] : ~0ull;
+        if (v < bv) { bv = v; bw = w; }
+      }
+      p[bw]++;
+      raw[t * K1 + e] = bv;
+    }
+  }
 }
 
 // Row i (one thread): the union of its row list (rowc[block(i)][i - block*B])
@@ -1902,7 +1920,7 @@ int grid_knn_seg_topk(grid_ctx *ctx, const int64_t *d_seg, int64_t ld, int64_t n
     HIPCHK(hipMemsetAsync(d_rowc + rr * GRID_SEG_K1, 0xFF, (nrows - rr) * GRID_SEG_K1 * 8, ctx->stream));
   }
   if (ncols > 0) {
-    hipLaunchKernelGGL(k_seg_cols<GRID_SEG_K1>, dim3((unsigned)((ncols + 255) / 256)), dim3(256), 0, ctx->stream,
+    hipLaunchKernelGGL(k_seg_cols<GRID_SEG_K1>, dim3((unsigned)((ncols + 31) / 32)), dim3(256), 0, ctx->stream,
                        d_seg, ld, nrows, ncols, d_norms, n, r0, c0, d_colc);
     LAUNCHCHK();
   }

@@ -31,6 +31,9 @@ ap.add_argument("--out", default="/tmp/grid_e2e_out")
 ap.add_argument("--threads", type=int, default=16)
 ap.add_argument("--json", default=os.path.join(ROOT, "gpurun_out", "e2e_files.json"))
 ap.add_argument("--keep", action="store_true", help="keep the generated cohort")
+ap.add_argument("--bgzf", action="store_true", help="BGZF files (what mosdepth writes) instead of one gzip member")
+ap.add_argument("--device-ingest", action="store_true", help="mosdepth.normalize.device_ingest: inflate + parse in HBM")
+ap.add_argument("--reuse", action="store_true", help="keep the cohort in --data for a later run (implies --keep)")
 a = ap.parse_args()
 
 
@@ -42,7 +45,8 @@ def rss_gb():
     return resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6
 
 
-res = {"config": {"samples": a.samples, "bins": a.bins, "data": a.data, "out": a.out}, "phases_s": {},
+res = {"config": {"samples": a.samples, "bins": a.bins, "data": a.data, "out": a.out, "bgzf": a.bgzf,
+                  "device_ingest": a.device_ingest, "threads": a.threads}, "phases_s": {},
        "peak_rss_gb_after": {}}
 mos = os.path.join(a.data, "mosdepth")
 os.makedirs(mos, exist_ok=True)
@@ -60,7 +64,8 @@ if have != a.samples:
     step = 200
     for i0 in range(0, a.samples, step):        # batches: progress lines for the watchdog
         n_b = min(step, a.samples - i0)
-        subprocess.run([gen, mos, str(n_b), str(a.bins), "20260821", str(a.threads), str(i0)], check=True)
+        subprocess.run([gen, mos, str(n_b), str(a.bins), "20260821", str(a.threads), str(i0)]
+                       + (["bgzf"] if a.bgzf else []), check=True)
         note(f"  {i0 + n_b} files")
 res["phases_s"]["generate_cohort"] = time.perf_counter() - t0
 res["cohort_bytes"] = sum(os.path.getsize(os.path.join(mos, f)) for f in os.listdir(mos))
@@ -85,6 +90,7 @@ cfg = {
     "count_reads": {"run": False, "output_file_prefix": "counts"},
     "mosdepth": {"run": False, "work_dir": mos, "remove_intermediate": False,
                  "normalize": {"run": True, "min_depth": 20, "max_depth": 100, "top_frac": 0.1,
+                               "device_ingest": a.device_ingest,
                                "output_file_prefix": "normalized",
                                "repeat_mask_file": os.path.join(a.data, "mask.bed")},
                  "neighbors": {"run": True, "output_file_prefix": "neighbors", "num_neighbors": 10, "zmax": 2.0,
@@ -141,5 +147,7 @@ res["samples_per_s_from_files"] = a.samples / res["steps_4_7_s"]
 os.makedirs(os.path.dirname(a.json), exist_ok=True)
 json.dump(res, open(a.json, "w"), indent=1)
 print(json.dumps(res), flush=True)
-if not a.keep:
+if not (a.keep or a.reuse):
     subprocess.run(["rm", "-rf", a.data, a.out])
+elif a.reuse:
+    subprocess.run(["rm", "-rf", a.out])
