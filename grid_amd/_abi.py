@@ -89,6 +89,9 @@ _SIGS = {
     "grid_hi_pack_batch": [_vp, _i64, _vp, _i64],
     "grid_write_normalized_gz": [C.c_char_p, _i64, _i64, C.c_char_p, _vp, _vp, _vp, _vp, _i64, _i32, _i32],
     "grid_read_normalized_gz": [C.c_char_p, _i32, C.POINTER(_vp), C.POINTER(_i64), C.POINTER(_i64)],
+    "grid_write_normalized_gz_dev": [_vp, C.c_char_p, _i64, _i64, C.c_char_p, _vp, _vp, _vp, _vp, _i64, _i32, _i32,
+                                     _i64],
+    "grid_gz_huffman_member": [_vp, _i64, _vp, _i64, C.POINTER(_i64)],
     "grid_ntext_ids_len": [_vp, C.POINTER(_i64)],
     "grid_ntext_fetch": [_vp, _vp, _i64, _vp, _vp, _vp, _vp],
     "grid_ntext_free": [_vp],
@@ -320,6 +323,22 @@ def write_normalized_gz(path, ids, raw, sel_means, sel_ratios, zq, level=6, thre
     thr = threads or min(16, os.cpu_count() or 1)
     call("grid_write_normalized_gz", str(path).encode(), n, r, ids_b, raw.ctypes.data, mu.ctypes.data,
          rt.ctypes.data, zq.ctypes.data if zq.size else None, max(r, 0), level, thr)
+
+
+def write_normalized_gz_dev(dev, path, ids, raw, sel_means, sel_ratios, d_zq, n, r, ld, level=1, threads=None,
+                           batch_bytes=0):
+    """Step-4 output file from the int32 hundredths in HBM (d_zq: DevBuf or
+    device pointer, [n][ld]): row members formatted and Huffman-coded on the
+    device (grid_write_normalized_gz_dev), same decompressed text as
+    write_normalized_gz."""
+    raw = np.ascontiguousarray(raw, dtype=np.float64)
+    mu = np.ascontiguousarray(sel_means, dtype=np.float64)
+    rt = np.ascontiguousarray(sel_ratios, dtype=np.float64)
+    ids_b = "\n".join(ids).encode()
+    thr = threads or min(16, os.cpu_count() or 1)
+    call("grid_write_normalized_gz_dev", dev.ctx, str(path).encode(), n, r, ids_b, raw.ctypes.data if n else None,
+         mu.ctypes.data if r else None, rt.ctypes.data if r else None, ptr(d_zq) if (n and r) else None, max(ld, r),
+         level, thr, int(batch_bytes))
 
 
 def read_normalized_gz(path, threads=None):

@@ -1,0 +1,928 @@
+// Normalised-matrix writer on the device (the text that
+// normalize_mosdepth.py:502-554 writes and find_neighbors.py:81-124 reads).
+//
+// Same file as grid_write_normalized_gz (textio.cpp): a multi-member gzip,
+// member 0 the two header lines, then one member per chunk of whole rows, each
+// member carrying the 'GR' {member size, first row} FEXTRA index; the
+// decompressed text is byte-identical to the reference's.  What moves to the
+// GPU is the row members -- 99.9 % of the bytes (43 GB of text at BASELINE
+// config 2):
+//   1. k_fmt_len / k_fmt_rows: the "%.2f" cells of the int32 hundredths that
+//      step 4 left in HBM, laid out row after row (prefix "ID \t scale \t" and
+//      the newline come from the host), staged per 2048-cell block in LDS;
+//   2. one length-limited canonical Huffman code per file (package-merge on
+//      the histogram of the first batch, every byte value encodable), written
+//      as ONE dynamic-Huffman deflate block per member: literals only (on
+//      this text an LZ77 match of 3-4 bytes costs as many bits as the
+//      literals it replaces), ~13 % larger than libdeflate level 1;
+//   3. k_seg_bits: code bits per 4 KiB text segment (host scan -> each
+//      segment's absolute output bit); k_encode: each segment packs its codes
+//      into an LDS word image and stores it, atomically only on the two edge
+//      words it may share with a neighbour;
+//   4. k_member_crc: CRC-32 per member, one wave per member, lanes on equal
+//      slices (slicing-by-4 tables in LDS) folded with the GF(2) shift
+//      x^(8 len) mod P (zlib's crc32_combine algorithm, restated);
+//   5. k_frame: gzip header, block header bits, end-of-block code, CRC and
+//      ISIZE of every member.
+// The compressed batch is copied to pinned host memory and written by a host
+// thread while the GPU works on the next batch.  No text, and no int32
+// matrix, crosses PCIe: only the compressed bytes (~18 GB at config 2
+// instead of the 34.6 GB matrix the host writer formats).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "common.hpp"
+
+// textio.cpp: member 0 (the two header lines, host libdeflate) and the
+// row-prefix formatter, shared with the host writer
+bool grid_textio_header_member(int64_t n, int64_t r, const double *sel_means, const double *sel_ratios, int level,
+                               std::string &out);
+void grid_textio_row_prefix(const char *id_b, const char *id_e, double raw, std::string &out);
+
+namespace {
+
+constexpr uint32_t POLY = 0xedb88320u;   // CRC-32 (gzip), reflected
+constexpr int CPB = 2048;                // cells per format block (256 threads x 8 cells)
+constexpr int CELL_MAX = 14;             // '\t' + '-' + 8 digits + '.' + 2 digits
+constexpr int SEG = 4096;                // text bytes per encode segment (256 threads x 16 B)
+constexpr int GR_XLEN = 20;
+constexpr int GR_HDR = 10 + 2 + GR_XLEN; // = textio.cpp's member header
+
+// ---- Huffman code construction (host) ----------------------------------------
+// Optimal code lengths limited to maxbits (package-merge); symbols with freq 0
+// get length 0.  With >= 2 used symbols the code is complete (Kraft sum 1).
+void limited_lengths(const uint64_t *freq, int n, int maxbits, uint8_t *len) {
+  std::fill(len, len + n, 0);
+  struct Node {
+    uint64_t w;
+    int a, b, leaf;
+  };
+  std::vector<Node> nodes;
+  std::vector<int> leaves;
+  for (int i = 0; i < n; i++)
+    if (freq[i]) {
+      nodes.push_back({freq[i], -1, -1, i});
+      leaves.push_back((int)nodes.size() - 1);
+    }
+  if (leaves.empty()) return;
+  if (leaves.size() == 1) {
+    len[nodes[leaves[0]].leaf] = 1;
+    return;
+  }
+  std::stable_sort(leaves.begin(), leaves.end(), [&](int x, int y) { return nodes[x].w < nodes[y].w; });
+  std::vector<int> cur = leaves;
+  for (int lvl = 1; lvl < maxbits; lvl++) {
+    std::vector<int> pk;
+    for (size_t i = 0; i + 1 < cur.size(); i += 2) {
+      nodes.push_back({nodes[cur[i]].w + nodes[cur[i + 1]].w, cur[i], cur[i + 1], -1});
+      pk.push_back((int)nodes.size() - 1);
+    }
+    std::vector<int> nxt;
+    nxt.reserve(leaves.size() + pk.size());
+    size_t a = 0, b = 0;
+    while (a < leaves.size() || b < pk.size()) {
+      if (b >= pk.size() || (a < leaves.size() && nodes[leaves[a]].w <= nodes[pk[b]].w)) nxt.push_back(leaves[a++]);
+      else nxt.push_back(pk[b++]);
+    }
+    cur.swap(nxt);
+  }
+  std::vector<int> st(cur.begin(), cur.begin() + (2 * leaves.size() - 2));
+  while (!st.empty()) {
+    const int x = st.back();
+    st.pop_back();
+    if (nodes[x].leaf >= 0) {
+      len[nodes[x].leaf]++;
+    } else {
+      st.push_back(nodes[x].a);
+      st.push_back(nodes[x].b);
+    }
+  }
+}
+
+// Canonical codes (RFC 1951 3.2.2), bit-reversed for LSB-first packing.
+void canonical_codes(const uint8_t *len, int n, uint16_t *rcode) {
+  int bl[16] = {0}, next[16] = {0};
+  for (int i = 0; i < n; i++) bl[len[i]]++;
+  bl[0] = 0;
+  int code = 0;
+  for (int b = 1; b < 16; b++) {
+    code = (code + bl[b - 1]) << 1;
+    next[b] = code;
+  }
+  for (int i = 0; i < n; i++) {
+    rcode[i] = 0;
+    if (!len[i]) continue;
+    const int c = next[len[i]]++;
+    int r = 0;
+    for (int k = 0; k < len[i]; k++) r |= ((c >> k) & 1) << (len[i] - 1 - k);
+    rcode[i] = (uint16_t)r;
+  }
+}
+
+struct BitW {
+  std::vector<uint8_t> buf;
+  uint64_t acc = 0;
+  int nb = 0;
+  void put(uint32_t v, int n) {
+    acc |= (uint64_t)v << nb;
+    nb += n;
+    while (nb >= 8) {
+      buf.push_back((uint8_t)acc);
+      acc >>= 8;
+      nb -= 8;
+    }
+  }
+  int64_t bits() const { return (int64_t)buf.size() * 8 + nb; }
+  void flush() {
+    if (nb) buf.push_back((uint8_t)acc);
+    acc = 0;
+    nb = 0;
+  }
+};
+
+// The literal-only code of a file: 257 lit/len lengths (EOB = 256), the block
+// header (BFINAL 1, BTYPE dynamic, HLIT 257 codes, HDIST 2 codes of length 1
+// -- complete, as zlib's own deflate emits for match-free blocks -- HCLEN and
+// the code-length code) as a bit string.
+struct Code {
+  uint8_t len[257];
+  uint16_t rcode[257];
+  std::vector<uint32_t> hdr;   // header bits, LSB-first in 32-bit words
+  int hdr_bits = 0;
+};
+
+void build_code(const uint64_t *hist256, Code &c) {
+  uint64_t f[257];
+  for (int i = 0; i < 256; i++) f[i] = hist256[i] + 1;     // every byte encodable (IDs, anything)
+  f[256] = 1;
+  limited_lengths(f, 257, 15, c.len);
+  canonical_codes(c.len, 257, c.rcode);
+  std::vector<uint8_t> seq(c.len, c.len + 257);
+  seq.push_back(1);
+  seq.push_back(1);                                         // two distance codes of length 1
+  uint64_t cf[19] = {0};
+  for (uint8_t v : seq) cf[v]++;
+  uint8_t cl[19];
+  uint16_t cc[19];
+  limited_lengths(cf, 19, 7, cl);
+  canonical_codes(cl, 19, cc);
+  static const int ord[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+  int hclen = 19;
+  while (hclen > 4 && cl[ord[hclen - 1]] == 0) hclen--;
+  BitW w;
+  w.put(1, 1);              // BFINAL
+  w.put(2, 2);              // BTYPE = 10: dynamic Huffman
+  w.put(0, 5);              // HLIT: 257 codes
+  w.put(1, 5);              // HDIST: 2 codes
+  w.put((uint32_t)(hclen - 4), 4);
+  for (int i = 0; i < hclen; i++) w.put(cl[ord[i]], 3);
+  for (uint8_t v : seq) w.put(cc[v], cl[v]);
+  c.hdr_bits = (int)w.bits();
+  w.flush();
+  c.hdr.assign((w.buf.size() + 3) / 4 + 1, 0u);
+  for (size_t i = 0; i < w.buf.size(); i++) c.hdr[i / 4] |= (uint32_t)w.buf[i] << (8 * (i % 4));
+}
+
+// ---- CRC-32 helpers (host + device) -------------------------------------------
+__host__ __device__ inline uint32_t multmodp(uint32_t a, uint32_t b) {
+  uint32_t m = 1u << 31, p = 0;
+  for (;;) {
+    if (a & m) {
+      p ^= b;
+      if ((a & (m - 1)) == 0) break;
+    }
+    m >>= 1;
+    b = (b & 1) ? (b >> 1) ^ POLY : b >> 1;
+  }
+  return p;
+}
+struct X2N {
+  uint32_t t[32];
+};
+X2N make_x2n() {
+  X2N x;
+  uint32_t p = 1u << 30;    // x^1
+  x.t[0] = p;
+  for (int k = 1; k < 32; k++) x.t[k] = p = multmodp(p, p);
+  return x;
+}
+// x^(8 n) mod P
+__host__ __device__ inline uint32_t x8n(uint64_t n, const X2N &x) {
+  uint32_t p = 1u << 31;    // x^0
+  unsigned k = 3;
+  while (n) {
+    if (n & 1) p = multmodp(x.t[k & 31], p);
+    n >>= 1;
+    k++;
+  }
+  return p;
+}
+// crc(A || B) from crc(A), crc(B), |B|
+__host__ __device__ inline uint32_t crc_combine(uint32_t ca, uint32_t cb, uint64_t lb, const X2N &x) {
+  return multmodp(x8n(lb, x), ca) ^ cb;
+}
+void crc_tables(uint32_t *t /* [4][256] */) {
+  for (uint32_t i = 0; i < 256; i++) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ POLY : c >> 1;
+    t[i] = c;
+  }
+  for (int s = 1; s < 4; s++)
+    for (int i = 0; i < 256; i++) t[s * 256 + i] = (t[(s - 1) * 256 + i] >> 8) ^ t[t[(s - 1) * 256 + i] & 0xff];
+}
+
+// ---- device: text formatting -----------------------------------------------------
+__device__ __forceinline__ int cell_len(int32_t v) {
+  if (v == GRID_ZQ_NAN) return 2;
+  if (v == GRID_ZQ_NEG0) return 5;
+  const uint32_t a = v < 0 ? 0u - (uint32_t)v : (uint32_t)v;
+  const uint32_t ip = a / 100;
+  const int d = ip < 10 ? 1 : ip < 100 ? 2 : ip < 1000 ? 3 : ip < 10000 ? 4 : ip < 100000 ? 5 : ip < 1000000 ? 6
+              : ip < 10000000 ? 7 : 8;
+  return (v < 0) + d + 3;
+}
+// "%.2f" of hundredths v at p (textio.cpp put_hundredths, same bytes)
+__device__ __forceinline__ int put_cell(char *p, int32_t v) {
+  if (v == GRID_ZQ_NAN) { p[0] = 'N'; p[1] = 'A'; return 2; }
+  if (v == GRID_ZQ_NEG0) { p[0] = '-'; p[1] = '0'; p[2] = '.'; p[3] = '0'; p[4] = '0'; return 5; }
+  int o = 0;
+  uint32_t a = (uint32_t)v;
+  if (v < 0) { p[o++] = '-'; a = 0u - a; }
+  uint32_t ip = a / 100;
+  const uint32_t fp = a - ip * 100;
+  char tmp[8];
+  int t = 0;
+  do { tmp[t++] = (char)('0' + ip % 10); ip /= 10; } while (ip);
+  while (t) p[o++] = tmp[--t];
+  p[o++] = '.';
+  p[o++] = (char)('0' + fp / 10);
+  p[o++] = (char)('0' + fp % 10);
+  return o;
+}
+
+// Block text length of cells [b*CPB, (b+1)*CPB) of row i (each cell but the
+// row's first carries its leading tab): blen[row][b].
+__global__ __launch_bounds__(256) void k_fmt_len(const int32_t *__restrict__ zq, int64_t ld, int64_t r, int64_t row0,
+                                                 int64_t nblk, int64_t y0, int64_t *__restrict__ blen) {
+  __shared__ int64_t s_sum[4];
+  const int64_t b = blockIdx.x, row = y0 + blockIdx.y, i = row0 + row;
+  const int tid = threadIdx.x;
+  const int64_t c0 = b * CPB + (int64_t)tid * 8;
+  int64_t sum = 0;
+  const int32_t *z = zq + i * ld;
+#pragma unroll
+  for (int u = 0; u < 8; u++) {
+    const int64_t c = c0 + u;
+    if (c < r) sum += cell_len(z[c]) + (c > 0);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+  if ((tid & 63) == 0) s_sum[tid >> 6] = sum;
+  __syncthreads();
+  if (tid == 0) blen[row * nblk + b] = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
+}
+
+// boff[row][b] (absolute text offsets): row start + prefix + exclusive scan
+// of the row's block lengths.  One workgroup per row.
+__global__ __launch_bounds__(256) void k_fmt_scan(const int64_t *__restrict__ blen, int64_t nblk,
+                                                  const int64_t *__restrict__ rowoff,
+                                                  const int64_t *__restrict__ prelen, int64_t *__restrict__ boff) {
+  __shared__ int64_t s_w[4];
+  __shared__ int64_t s_carry;
+  const int64_t row = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) s_carry = rowoff[row] + prelen[row];
+  __syncthreads();
+  for (int64_t base = 0; base < nblk; base += 256) {
+    const int64_t b = base + tid;
+    const int64_t v = b < nblk ? blen[row * nblk + b] : 0;
+    int64_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) s_w[wv] = x;
+    __syncthreads();
+    int64_t pre = s_carry;
+    for (int w = 0; w < wv; w++) pre += s_w[w];
+    if (b < nblk) boff[row * nblk + b] = pre + x - v;
+    __syncthreads();
+    if (tid == 0) s_carry += s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    __syncthreads();
+  }
+}
+
+// The text of block b of row i: cells through an LDS image, then byte stores
+// (a wave stores 64 consecutive bytes).  Block 0 also copies the row prefix,
+// the row's last block appends the newline.
+__global__ __launch_bounds__(256) void k_fmt_rows(const int32_t *__restrict__ zq, int64_t ld, int64_t r, int64_t row0,
+                                                  int64_t nblk, int64_t y0, const int64_t *__restrict__ boff,
+                                                  const char *__restrict__ pre, const int64_t *__restrict__ preoff,
+                                                  const int64_t *__restrict__ rowoff, char *__restrict__ text) {
+  __shared__ char s_txt[CPB * CELL_MAX];
+  __shared__ int s_w[4];
+  const int64_t b = blockIdx.x, row = y0 + blockIdx.y, i = row0 + row;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t c0 = b * CPB + (int64_t)tid * 8;
+  const int32_t *z = zq + i * ld;
+  int32_t v[8];
+  int len = 0;
+#pragma unroll
+  for (int u = 0; u < 8; u++) {
+    const int64_t c = c0 + u;
+    v[u] = c < r ? z[c] : 0;
+    if (c < r) len += cell_len(v[u]) + (c > 0);
+  }
+  int x = len;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_w[wv] = x;
+  __syncthreads();
+  int pos = x - len;
+  for (int w = 0; w < wv; w++) pos += s_w[w];
+  const int total = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+#pragma unroll
+  for (int u = 0; u < 8; u++) {
+    const int64_t c = c0 + u;
+    if (c < r) {
+      if (c > 0) s_txt[pos++] = '\t';
+      pos += put_cell(s_txt + pos, v[u]);
+    }
+  }
+  __syncthreads();
+  char *dst = text + boff[row * nblk + b];
+  for (int e = tid; e < total; e += 256) dst[e] = s_txt[e];
+  if (b == 0) {
+    const int64_t p0 = preoff[row], p1 = preoff[row + 1];
+    char *rd = text + rowoff[row];
+    for (int64_t e = tid; e < p1 - p0; e += 256) rd[e] = pre[p0 + e];
+  }
+  if (b == nblk - 1 && tid == 0) dst[total] = '\n';
+}
+
+// Byte histogram of text[0, n) (the code of the file).
+__global__ __launch_bounds__(256) void k_hist(const uint8_t *__restrict__ text, int64_t n,
+                                              unsigned long long *__restrict__ hist) {
+  __shared__ unsigned int s_h[256];
+  const int tid = threadIdx.x;
+  s_h[tid] = 0;
+  __syncthreads();
+  for (int64_t e = (int64_t)blockIdx.x * 256 + tid; e < n; e += (int64_t)gridDim.x * 256) atomicAdd(&s_h[text[e]], 1u);
+  __syncthreads();
+  if (s_h[tid]) atomicAdd(&hist[tid], (unsigned long long)s_h[tid]);
+}
+
+// ---- device: entropy coding ------------------------------------------------------
+struct CodeDev {
+  uint8_t len[256];
+  uint16_t rcode[256];
+};
+
+// Code bits of each 4 KiB segment s = [sstart[s], sstart[s] + slen[s]).
+__global__ __launch_bounds__(256) void k_seg_bits(const uint8_t *__restrict__ text, const int64_t *__restrict__ sstart,
+                                                  const int32_t *__restrict__ slen, const CodeDev *__restrict__ cd,
+                                                  uint32_t *__restrict__ sbits) {
+  __shared__ uint8_t s_len[256];
+  __shared__ uint32_t s_w[4];
+  const int tid = threadIdx.x;
+  s_len[tid] = cd->len[tid];
+  __syncthreads();
+  const int64_t s = blockIdx.x;
+  const uint8_t *p = text + sstart[s];
+  const int L = slen[s];
+  uint32_t bits = 0;
+  const int o = tid * 16;
+#pragma unroll
+  for (int u = 0; u < 16; u++)
+    if (o + u < L) bits += s_len[p[o + u]];
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) bits += __shfl_xor(bits, d, 64);
+  if ((tid & 63) == 0) s_w[tid >> 6] = bits;
+  __syncthreads();
+  if (tid == 0) sbits[s] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+
+constexpr int SEG_WORDS = (SEG * 15) / 32 + 3;
+
+__device__ __forceinline__ void lds_put(uint32_t *w, uint32_t bitpos, uint32_t v32, int nbits) {
+  // nbits <= 32 bits of v32 at bit position bitpos of the LDS word image
+  const uint32_t wi = bitpos >> 5, sh = bitpos & 31;
+  atomicOr(&w[wi], v32 << sh);
+  if (sh && sh + nbits > 32) atomicOr(&w[wi + 1], v32 >> (32 - sh));
+}
+
+// Segment s: its codes packed at absolute output bit sbase[s] (LSB-first
+// deflate order in little-endian words).  Interior words are stored, the two
+// edge words (shared with the neighbouring segment or the member's header /
+// end-of-block bits) OR-ed atomically into the zeroed output.
+__global__ __launch_bounds__(256) void k_encode(const uint8_t *__restrict__ text, const int64_t *__restrict__ sstart,
+                                                const int32_t *__restrict__ slen, const int64_t *__restrict__ sbase,
+                                                const uint32_t *__restrict__ sbits, const CodeDev *__restrict__ cd,
+                                                uint32_t *__restrict__ out) {
+  __shared__ uint8_t s_len[256];
+  __shared__ uint16_t s_code[256];
+  __shared__ uint32_t s_img[SEG_WORDS];
+  __shared__ uint32_t s_wsum[4];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  s_len[tid] = cd->len[tid];
+  s_code[tid] = cd->rcode[tid];
+  for (int e = tid; e < SEG_WORDS; e += 256) s_img[e] = 0;
+  __syncthreads();
+  const int64_t s = blockIdx.x;
+  const uint8_t *p = text + sstart[s];
+  const int L = slen[s];
+  const int o = tid * 16;
+  uint8_t c[16];
+  uint32_t bits = 0;
+#pragma unroll
+  for (int u = 0; u < 16; u++) {
+    c[u] = o + u < L ? p[o + u] : 0;
+    if (o + u < L) bits += s_len[c[u]];
+  }
+  uint32_t x = bits;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) s_wsum[wv] = x;
+  __syncthreads();
+  uint32_t pre = x - bits;
+  for (int w = 0; w < wv; w++) pre += s_wsum[w];
+  const uint64_t abs0 = (uint64_t)sbase[s];
+  uint32_t pos = (uint32_t)(abs0 & 31) + pre;       // bit position in the LDS image
+  uint64_t acc = 0;
+  int na = 0;
+#pragma unroll
+  for (int u = 0; u < 16; u++) {
+    if (o + u < L) {
+      acc |= (uint64_t)s_code[c[u]] << na;
+      na += s_len[c[u]];
+      if (na >= 32) {
+        lds_put(s_img, pos, (uint32_t)acc, 32);
+        pos += 32;
+        acc >>= 32;
+        na -= 32;
+      }
+    }
+  }
+  if (na) lds_put(s_img, pos, (uint32_t)acc, na);
+  __syncthreads();
+  const uint32_t total = sbits[s];
+  if (total == 0) return;
+  const uint64_t w0 = abs0 >> 5, w1 = (abs0 + total - 1) >> 5;
+  for (uint64_t w = w0 + tid; w <= w1; w += 256) {
+    const uint32_t val = s_img[w - w0];
+    if (w == w0 || w == w1) atomicOr(&out[w], val);
+    else out[w] = val;
+  }
+}
+
+__device__ __forceinline__ void glb_put(uint32_t *out, uint64_t bitpos, uint32_t v32, int nbits) {
+  const uint64_t wi = bitpos >> 5;
+  const uint32_t sh = (uint32_t)(bitpos & 31);
+  if (nbits < 32) v32 &= (1u << nbits) - 1;
+  atomicOr(&out[wi], v32 << sh);
+  if (sh && sh + nbits > 32) atomicOr(&out[wi + 1], v32 >> (32 - sh));
+}
+__device__ __forceinline__ void glb_byte(uint32_t *out, uint64_t byte, uint32_t v) {
+  atomicOr(&out[byte >> 2], (v & 0xffu) << (8 * (byte & 3)));
+}
+
+// CRC-32 of every member text [mstart, mstart + mlen): one wave per member,
+// lane l on its 1/64 slice (slicing-by-4), folded in order by crc_combine.
+__global__ __launch_bounds__(64) void k_member_crc(const uint8_t *__restrict__ text, const int64_t *__restrict__ mstart,
+                                                   const int64_t *__restrict__ mlen, const uint32_t *__restrict__ tab,
+                                                   X2N x2n, uint32_t *__restrict__ crc) {
+  __shared__ uint32_t t[4][256];
+  __shared__ uint32_t s_c[64];
+  __shared__ int64_t s_l[64];
+  const int lane = threadIdx.x;
+  for (int e = lane; e < 1024; e += 64) t[e >> 8][e & 255] = tab[e];
+  __syncthreads();
+  const int64_t m = blockIdx.x, L = mlen[m];
+  const uint8_t *base = text + mstart[m];
+  const int64_t per = (L + 63) / 64;
+  const int64_t a = min(L, per * lane), b = min(L, per * (lane + 1));
+  uint32_t c = 0xffffffffu;
+  int64_t e = a;
+  for (; e < b && ((uintptr_t)(base + e) & 3); e++) c = t[0][(c ^ base[e]) & 0xff] ^ (c >> 8);
+  for (; e + 4 <= b; e += 4) {
+    c ^= *(const uint32_t *)(base + e);
+    c = t[3][c & 0xff] ^ t[2][(c >> 8) & 0xff] ^ t[1][(c >> 16) & 0xff] ^ t[0][c >> 24];
+  }
+  for (; e < b; e++) c = t[0][(c ^ base[e]) & 0xff] ^ (c >> 8);
+  s_c[lane] = c ^ 0xffffffffu;
+  s_l[lane] = b - a;
+  __syncthreads();
+  if (lane == 0) {
+    uint32_t acc = 0;                 // crc of the empty string
+    for (int l = 0; l < 64; l++) acc = crc_combine(acc, s_c[l], (uint64_t)s_l[l], x2n);
+    crc[m] = acc;
+  }
+}
+
+// gzip framing of member m at byte moff[m]: header with the GR index, the
+// block header bits, the end-of-block code after mbits[m] data bits, CRC and
+// ISIZE.  The output is zeroed; everything is OR-ed in.
+__global__ __launch_bounds__(64) void k_frame(uint32_t *__restrict__ out, const int64_t *__restrict__ moff,
+                                              const int64_t *__restrict__ msize, const int64_t *__restrict__ mrow,
+                                              const int64_t *__restrict__ mlen, const int64_t *__restrict__ mbits,
+                                              const uint32_t *__restrict__ crc, const uint32_t *__restrict__ hdr,
+                                              int hdr_bits, uint32_t eob_code, int eob_len, int64_t nmem) {
+  const int64_t m = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (m >= nmem) return;
+  const uint64_t o = (uint64_t)moff[m];
+  const uint64_t total = (uint64_t)msize[m];
+  uint8_t h[GR_HDR];
+  h[0] = 0x1f; h[1] = 0x8b; h[2] = 8; h[3] = 4;
+  h[4] = h[5] = h[6] = h[7] = 0;
+  h[8] = 0; h[9] = 255;
+  h[10] = GR_XLEN; h[11] = 0;
+  h[12] = 'G'; h[13] = 'R';
+  h[14] = 16; h[15] = 0;
+  for (int k = 0; k < 8; k++) h[16 + k] = (uint8_t)(total >> (8 * k));
+  for (int k = 0; k < 8; k++) h[24 + k] = (uint8_t)((uint64_t)mrow[m] >> (8 * k));
+  for (int k = 0; k < GR_HDR; k++) glb_byte(out, o + k, h[k]);
+  const uint64_t b0 = 8 * (o + GR_HDR);
+  for (int k = 0; k < hdr_bits; k += 32) glb_put(out, b0 + k, hdr[k >> 5], min(32, hdr_bits - k));
+  const uint64_t eb = b0 + hdr_bits + (uint64_t)mbits[m];
+  glb_put(out, eb, eob_code, eob_len);
+  const uint64_t tb = (eb + eob_len + 7) / 8;
+  const uint32_t c = crc[m], isz = (uint32_t)mlen[m];
+  for (int k = 0; k < 4; k++) glb_byte(out, tb + k, c >> (8 * k));
+  for (int k = 0; k < 4; k++) glb_byte(out, tb + 4 + k, isz >> (8 * k));
+}
+
+template <class T>
+struct DBuf {
+  T *p = nullptr;
+  size_t n = 0;
+  ~DBuf() {
+    if (p) (void)hipFree(p);
+  }
+  hipError_t need(size_t k) {
+    if (k <= n) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    hipError_t e = hipMalloc((void **)&p, std::max<size_t>(k, 1) * sizeof(T));
+    if (e == hipSuccess) n = std::max<size_t>(k, 1);
+    return e;
+  }
+};
+struct HBuf {
+  void *p = nullptr;
+  size_t n = 0;
+  ~HBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+  hipError_t need(size_t k) {
+    if (k <= n) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    n = 0;
+    hipError_t e = hipHostMalloc(&p, std::max<size_t>(k, 1), 0);
+    if (e == hipSuccess) n = std::max<size_t>(k, 1);
+    return e;
+  }
+};
+
+#define HIPCHK_E(x)                                                                   \
+  do {                                                                                \
+    hipError_t e_ = (x);                                                              \
+    if (e_ != hipSuccess) {                                                           \
+      grid_set_error("%s:%d %s: %s", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      return GRID_EHIP;                                                               \
+    }                                                                                 \
+  } while (0)
+
+}  // namespace
+
+extern "C" {
+
+int grid_gz_huffman_member(const uint8_t *text, int64_t n, uint8_t *out, int64_t cap, int64_t *out_len) {
+  REQUIRE(n >= 0 && (text || !n) && out && out_len && cap >= 0, "grid_gz_huffman_member: bad args");
+  uint64_t hist[256] = {0};
+  for (int64_t e = 0; e < n; e++) hist[text[e]]++;
+  Code c;
+  build_code(hist, c);
+  BitW w;
+  for (int k = 0; k < c.hdr_bits; k++) w.put((c.hdr[k >> 5] >> (k & 31)) & 1, 1);
+  for (int64_t e = 0; e < n; e++) w.put(c.rcode[text[e]], c.len[text[e]]);
+  w.put(c.rcode[256], c.len[256]);
+  w.flush();
+  uint32_t t[1024];
+  crc_tables(t);
+  uint32_t crc = 0xffffffffu;
+  for (int64_t e = 0; e < n; e++) crc = t[(crc ^ text[e]) & 0xff] ^ (crc >> 8);
+  crc ^= 0xffffffffu;
+  const int64_t total = 10 + (int64_t)w.buf.size() + 8;
+  *out_len = total;
+  REQUIRE(total <= cap, "grid_gz_huffman_member: output capacity %lld < %lld", (long long)cap, (long long)total);
+  const uint8_t h[10] = {0x1f, 0x8b, 8, 0, 0, 0, 0, 0, 0, 255};
+  memcpy(out, h, 10);
+  memcpy(out + 10, w.buf.data(), w.buf.size());
+  for (int k = 0; k < 4; k++) out[10 + w.buf.size() + k] = (uint8_t)(crc >> (8 * k));
+  for (int k = 0; k < 4; k++) out[14 + w.buf.size() + k] = (uint8_t)((uint64_t)n >> (8 * k));
+  return GRID_OK;
+}
+
+int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int64_t r, const char *ids_nl,
+                                 const double *raw, const double *sel_means, const double *sel_ratios,
+                                 const int32_t *d_zq, int64_t ld_zq, int32_t level, int32_t threads,
+                                 int64_t batch_bytes) {
+  REQUIRE(ctx && path && n >= 0 && r >= 0 && ld_zq >= r && level >= 0 && level <= 9, "bad args");
+  REQUIRE(!n || (ids_nl && raw && (!r || d_zq)), "bad args");
+  REQUIRE(!r || (sel_means && sel_ratios), "bad args");
+  if (batch_bytes <= 0) batch_bytes = 2ll << 30;
+  // row prefixes "ID \t scale \t" (host: n strings)
+  std::vector<int64_t> preoff((size_t)n + 1, 0);
+  std::string pre;
+  {
+    const char *p = ids_nl;
+    std::string tmp;
+    for (int64_t i = 0; i < n; i++) {
+      const char *q = strchr(p, '\n');
+      const char *e = q ? q : p + strlen(p);
+      tmp.clear();
+      grid_textio_row_prefix(p, e, raw[i], tmp);
+      pre += tmp;
+      preoff[i + 1] = (int64_t)pre.size();
+      p = q ? q + 1 : e;
+    }
+  }
+  // member 0 (header lines) on a host thread meanwhile
+  std::string hdr_member;
+  bool hdr_ok = false;
+  std::thread hdr_thr([&] { hdr_ok = grid_textio_header_member(n, r, sel_means, sel_ratios, level, hdr_member); });
+  FILE *f = fopen(path, "wb");
+  if (!f) {
+    hdr_thr.join();
+    grid_set_error("cannot open %s for writing", path);
+    return GRID_EINVAL;
+  }
+  hipStream_t st = ctx->stream;
+  const int64_t nblk = std::max<int64_t>(1, (r + CPB - 1) / CPB);
+  // rows per member (the host writer's rule: ~8 MB of text per member)
+  const int64_t row_bytes = 24 + 6 * r;
+  const int64_t rpc = std::max<int64_t>(1, (8ll << 20) / std::max<int64_t>(row_bytes, 1));
+  std::vector<uint32_t> crctab(1024);
+  crc_tables(crctab.data());
+  const X2N x2n = make_x2n();
+  DBuf<int64_t> d_blen, d_boff, d_rowoff, d_prelen, d_preoff, d_sstart, d_sbase, d_moff, d_msize, d_mrow, d_mlen,
+      d_mbits, d_mstart;
+  DBuf<int32_t> d_slen;
+  DBuf<uint32_t> d_sbits, d_crc, d_hdr, d_tab, d_out;
+  DBuf<char> d_pre, d_text;
+  DBuf<CodeDev> d_code;
+  DBuf<unsigned long long> d_hist;
+  HBuf hb[2];
+  int rc = GRID_OK;
+  bool io_ok = true;
+  // writer thread: member 0 first, then the batches in order
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::pair<int, size_t>> q;      // (pinned buffer, bytes); -1 = end
+  int busy[2] = {0, 0};
+  std::thread wr([&] {
+    hdr_thr.join();
+    if (!hdr_ok || fwrite(hdr_member.data(), 1, hdr_member.size(), f) != hdr_member.size()) io_ok = false;
+    for (;;) {
+      std::pair<int, size_t> job;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return !q.empty(); });
+        job = q.front();
+        q.pop_front();
+      }
+      if (job.first < 0) return;
+      if (io_ok && fwrite(hb[job.first].p, 1, job.second, f) != job.second) io_ok = false;
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        busy[job.first] = 0;
+      }
+      cv.notify_all();
+    }
+  });
+  auto finish = [&](int code) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      q.push_back({-1, 0});
+    }
+    cv.notify_all();
+    wr.join();
+    if (fclose(f) != 0) io_ok = false;
+    if (code == GRID_OK && !io_ok) {
+      grid_set_error("grid_write_normalized_gz_dev: %s failed", hdr_ok ? "write" : "header deflate");
+      return (int)GRID_EINVAL;
+    }
+    return code;
+  };
+#define STEP(x)                                                                       \
+  do {                                                                                \
+    hipError_t e_ = (x);                                                              \
+    if (e_ != hipSuccess) {                                                           \
+      grid_set_error("%s:%d %s: %s", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      return finish(GRID_EHIP);                                                       \
+    }                                                                                 \
+  } while (0)
+  if (n > 0) {
+    STEP(d_pre.need(pre.size() + 1));
+    STEP(hipMemcpyAsync(d_pre.p, pre.data(), pre.size() + 1, hipMemcpyHostToDevice, st));
+    STEP(d_tab.need(1024));
+    STEP(hipMemcpyAsync(d_tab.p, crctab.data(), 4096, hipMemcpyHostToDevice, st));
+  }
+  Code code;
+  bool have_code = false;
+  std::vector<int64_t> h_blen, h_rowoff, h_prelen, h_preoff, h_sstart, h_sbase, h_moff, h_msize, h_mrow, h_mlen,
+      h_mbits, h_mstart;
+  std::vector<int32_t> h_slen;
+  std::vector<uint32_t> h_sbits;
+  int64_t i0 = 0;
+  int cur = 0;
+  while (i0 < n) {
+    // rows of this batch: whole members, text <= batch_bytes (estimated
+    // first by the upper bound, then exact)
+    const int64_t rows_cap = std::max<int64_t>(rpc, (batch_bytes / std::max<int64_t>(row_bytes + 8 * r, 1)) / rpc * rpc);
+    const int64_t i1 = std::min(n, i0 + rows_cap);
+    const int64_t nr = i1 - i0;
+    STEP(d_blen.need((size_t)(nr * nblk)));
+    if (r > 0) {
+      for (int64_t y0 = 0; y0 < nr; y0 += 65535) {
+        hipLaunchKernelGGL(k_fmt_len, dim3((unsigned)nblk, (unsigned)std::min<int64_t>(65535, nr - y0)), dim3(256), 0,
+                           st, d_zq, ld_zq, r, i0, nblk, y0, d_blen.p);
+        STEP(hipGetLastError());
+      }
+    } else {
+      STEP(hipMemsetAsync(d_blen.p, 0, (size_t)(nr * nblk) * 8, st));
+    }
+    h_blen.resize((size_t)(nr * nblk));
+    STEP(hipMemcpyAsync(h_blen.data(), d_blen.p, h_blen.size() * 8, hipMemcpyDeviceToHost, st));
+    STEP(hipStreamSynchronize(st));
+    h_rowoff.assign((size_t)nr + 1, 0);
+    h_prelen.resize((size_t)nr);
+    h_preoff.resize((size_t)nr + 1);
+    for (int64_t k = 0; k < nr; k++) {
+      int64_t s = 0;
+      for (int64_t b = 0; b < nblk; b++) s += h_blen[k * nblk + b];
+      h_prelen[k] = preoff[i0 + k + 1] - preoff[i0 + k];
+      h_preoff[k] = preoff[i0 + k];
+      h_rowoff[k + 1] = h_rowoff[k] + h_prelen[k] + s + 1;
+    }
+    h_preoff[nr] = preoff[i1];
+    const int64_t tlen = h_rowoff[nr];
+    STEP(d_text.need((size_t)tlen + 16));
+    STEP(d_rowoff.need((size_t)nr + 1));
+    STEP(d_prelen.need((size_t)nr));
+    STEP(d_preoff.need((size_t)nr + 1));
+    STEP(d_boff.need((size_t)(nr * nblk)));
+    STEP(hipMemcpyAsync(d_rowoff.p, h_rowoff.data(), (nr + 1) * 8, hipMemcpyHostToDevice, st));
+    STEP(hipMemcpyAsync(d_prelen.p, h_prelen.data(), nr * 8, hipMemcpyHostToDevice, st));
+    STEP(hipMemcpyAsync(d_preoff.p, h_preoff.data(), (nr + 1) * 8, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_fmt_scan, dim3((unsigned)nr), dim3(256), 0, st, d_blen.p, nblk, d_rowoff.p, d_prelen.p,
+                       d_boff.p);
+    STEP(hipGetLastError());
+    for (int64_t y0 = 0; y0 < nr; y0 += 65535) {
+      hipLaunchKernelGGL(k_fmt_rows, dim3((unsigned)nblk, (unsigned)std::min<int64_t>(65535, nr - y0)), dim3(256), 0,
+                         st, d_zq, ld_zq, r, i0, nblk, y0, d_boff.p, d_pre.p, d_preoff.p, d_rowoff.p, d_text.p);
+      STEP(hipGetLastError());
+    }
+    if (!have_code) {            // the file's code: histogram of the first batch
+      STEP(d_hist.need(256));
+      STEP(hipMemsetAsync(d_hist.p, 0, 256 * 8, st));
+      const int64_t hb_n = std::min<int64_t>(tlen, 1ll << 30);
+      hipLaunchKernelGGL(k_hist, dim3(1024), dim3(256), 0, st, (const uint8_t *)d_text.p, hb_n, d_hist.p);
+      STEP(hipGetLastError());
+      uint64_t hh[256];
+      STEP(hipMemcpyAsync(hh, d_hist.p, 256 * 8, hipMemcpyDeviceToHost, st));
+      STEP(hipStreamSynchronize(st));
+      build_code(hh, code);
+      CodeDev cdh;
+      memcpy(cdh.len, code.len, 256);
+      memcpy(cdh.rcode, code.rcode, 512);
+      STEP(d_code.need(1));
+      STEP(hipMemcpyAsync(d_code.p, &cdh, sizeof cdh, hipMemcpyHostToDevice, st));
+      STEP(d_hdr.need(code.hdr.size()));
+      STEP(hipMemcpyAsync(d_hdr.p, code.hdr.data(), code.hdr.size() * 4, hipMemcpyHostToDevice, st));
+      have_code = true;
+    }
+    // members and their 4 KiB segments
+    const int64_t nm = (nr + rpc - 1) / rpc;
+    h_mstart.resize((size_t)nm);
+    h_mlen.resize((size_t)nm);
+    h_mrow.resize((size_t)nm);
+    h_sstart.clear();
+    h_slen.clear();
+    std::vector<int64_t> mseg0((size_t)nm + 1, 0);
+    for (int64_t m = 0; m < nm; m++) {
+      const int64_t a = m * rpc, b = std::min(nr, a + rpc);
+      h_mstart[m] = h_rowoff[a];
+      h_mlen[m] = h_rowoff[b] - h_rowoff[a];
+      h_mrow[m] = i0 + a;
+      for (int64_t e = 0; e < h_mlen[m]; e += SEG) {
+        h_sstart.push_back(h_mstart[m] + e);
+        h_slen.push_back((int32_t)std::min<int64_t>(SEG, h_mlen[m] - e));
+      }
+      mseg0[m + 1] = (int64_t)h_sstart.size();
+    }
+    const int64_t ns = (int64_t)h_sstart.size();
+    STEP(d_sstart.need((size_t)ns));
+    STEP(d_slen.need((size_t)ns));
+    STEP(d_sbits.need((size_t)ns));
+    STEP(d_mstart.need((size_t)nm));
+    STEP(d_mlen.need((size_t)nm));
+    STEP(d_crc.need((size_t)nm));
+    STEP(hipMemcpyAsync(d_sstart.p, h_sstart.data(), ns * 8, hipMemcpyHostToDevice, st));
+    STEP(hipMemcpyAsync(d_slen.p, h_slen.data(), ns * 4, hipMemcpyHostToDevice, st));
+    STEP(hipMemcpyAsync(d_mstart.p, h_mstart.data(), nm * 8, hipMemcpyHostToDevice, st));
+    STEP(hipMemcpyAsync(d_mlen.p, h_mlen.data(), nm * 8, hipMemcpyHostToDevice, st));
+    if (ns > 0) {
+      hipLaunchKernelGGL(k_seg_bits, dim3((unsigned)ns), dim3(256), 0, st, (const uint8_t *)d_text.p, d_sstart.p,
+                         d_slen.p, d_code.p, d_sbits.p);
+      STEP(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_member_crc, dim3((unsigned)nm), dim3(64), 0, st, (const uint8_t *)d_text.p, d_mstart.p,
+                       d_mlen.p, d_tab.p, x2n, d_crc.p);
+    STEP(hipGetLastError());
+    h_sbits.resize((size_t)ns);
+    if (ns) STEP(hipMemcpyAsync(h_sbits.data(), d_sbits.p, ns * 4, hipMemcpyDeviceToHost, st));
+    STEP(hipStreamSynchronize(st));
+    // output layout: member sizes and every segment's absolute bit
+    h_moff.resize((size_t)nm);
+    h_msize.resize((size_t)nm);
+    h_mbits.resize((size_t)nm);
+    h_sbase.resize((size_t)ns);
+    int64_t off = 0;
+    const int eob_len = code.len[256];
+    for (int64_t m = 0; m < nm; m++) {
+      h_moff[m] = off;
+      int64_t bits = 0;
+      const int64_t b0 = 8 * (off + GR_HDR) + code.hdr_bits;
+      for (int64_t s = mseg0[m]; s < mseg0[m + 1]; s++) {
+        h_sbase[s] = b0 + bits;
+        bits += h_sbits[s];
+      }
+      h_mbits[m] = bits;
+      h_msize[m] = GR_HDR + (code.hdr_bits + bits + eob_len + 7) / 8 + 8;
+      off += h_msize[m];
+    }
+    const int64_t obytes = off;
+    const size_t owords = (size_t)(obytes + 3) / 4 + 1;
+    STEP(d_out.need(owords));
+    STEP(hipMemsetAsync(d_out.p, 0, owords * 4, st));
+    STEP(d_sbase.need((size_t)ns));
+    STEP(d_moff.need((size_t)nm));
+    STEP(d_msize.need((size_t)nm));
+    STEP(d_mrow.need((size_t)nm));
+    STEP(d_mbits.need((size_t)nm));
+    STEP(hipMemcpyAsync(d_sbase.p, h_sbase.data(), ns * 8, hipMemcpyHostToDevice, st));
+    STEP(hipMemcpyAsync(d_moff.p, h_moff.data(), nm * 8, hipMemcpyHostToDevice, st));
+    STEP(hipMemcpyAsync(d_msize.p, h_msize.data(), nm * 8, hipMemcpyHostToDevice, st));
+    STEP(hipMemcpyAsync(d_mrow.p, h_mrow.data(), nm * 8, hipMemcpyHostToDevice, st));
+    STEP(hipMemcpyAsync(d_mbits.p, h_mbits.data(), nm * 8, hipMemcpyHostToDevice, st));
+    if (ns > 0) {
+      hipLaunchKernelGGL(k_encode, dim3((unsigned)ns), dim3(256), 0, st, (const uint8_t *)d_text.p, d_sstart.p,
+                         d_slen.p, d_sbase.p, d_sbits.p, d_code.p, d_out.p);
+      STEP(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_frame, dim3((unsigned)((nm + 63) / 64)), dim3(64), 0, st, d_out.p, d_moff.p, d_msize.p,
+                       d_mrow.p, d_mlen.p, d_mbits.p, d_crc.p, d_hdr.p, code.hdr_bits, (uint32_t)code.rcode[256],
+                       eob_len, nm);
+    STEP(hipGetLastError());
+    // to pinned host memory (the writer thread must be done with this buffer)
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      cv.wait(lk, [&] { return !busy[cur]; });
+    }
+    STEP(hb[cur].need((size_t)obytes));
+    STEP(hipMemcpyAsync(hb[cur].p, d_out.p, (size_t)obytes, hipMemcpyDeviceToHost, st));
+    STEP(hipStreamSynchronize(st));
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      busy[cur] = 1;
+      q.push_back({cur, (size_t)obytes});
+    }
+    cv.notify_all();
+    cur ^= 1;
+    i0 = i1;
+  }
+#undef STEP
+  (void)threads;
+  return finish(rc);
+}
+
+}  // extern "C"

@@ -293,7 +293,39 @@ bool parse_header_line(const std::string &l, int64_t &n, int64_t &r, std::vector
   return ok;
 }
 
+// The two header lines: f"{N}\t{R}\t" + "\t".join(values) (the tab after R
+// is there even when R == 0), "%.3f" or "NA" (normalize_mosdepth.py:520-530).
+void header_lines(int64_t n, int64_t r, const double *sel_means, const double *sel_ratios, std::string &text) {
+  text.clear();
+  for (int h = 0; h < 2; h++) {
+    text += std::to_string(n) + '\t' + std::to_string(r) + '\t';
+    const double *v = h ? sel_ratios : sel_means;
+    for (int64_t c = 0; c < r; c++) {
+      if (c) text += '\t';
+      if (std::isnan(v[c])) text += "NA";
+      else put_fixed(text, v[c], 3);
+    }
+    text += '\n';
+  }
+}
+
 }  // namespace
+
+// For the device writer (gzwrite.hip): member 0 (the header lines) and a
+// row's "ID \t scale \t" prefix, exactly as the host writer makes them.
+bool grid_textio_header_member(int64_t n, int64_t r, const double *sel_means, const double *sel_ratios, int level,
+                               std::string &out) {
+  std::string text;
+  header_lines(n, r, sel_means, sel_ratios, text);
+  return deflate_member(text.data(), text.size(), level, -1, out);
+}
+
+void grid_textio_row_prefix(const char *id_b, const char *id_e, double raw, std::string &out) {
+  out.append(id_b, (size_t)(id_e - id_b));
+  out += '\t';
+  put_fixed(out, raw, 2);
+  out += '\t';
+}
 
 extern "C" {
 
@@ -347,18 +379,7 @@ int grid_write_normalized_gz(const char *path, int64_t n, int64_t r, const char 
       const char *body = nullptr;
       size_t blen = 0;
       if (k == 0) {
-        text.clear();
-        for (int h = 0; h < 2; h++) {
-          // f"{N}\t{R}\t" + "\t".join(values): the tab after R is there even when R == 0
-          text += std::to_string(n) + '\t' + std::to_string(r) + '\t';
-          const double *v = h ? sel_ratios : sel_means;
-          for (int64_t c = 0; c < r; c++) {
-            if (c) text += '\t';
-            if (std::isnan(v[c])) text += "NA";
-            else put_fixed(text, v[c], 3);
-          }
-          text += '\n';
-        }
+        header_lines(n, r, sel_means, sel_ratios, text);
         body = text.data();
         blen = text.size();
       } else {

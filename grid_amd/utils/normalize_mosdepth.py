@@ -225,13 +225,21 @@ def write_normalized_output(mat, individuals_order, selected_indices, output_fil
             out.write(f"{ind}\t{individual_raw_means[i]:.2f}\t" + "\t".join(vals) + "\n")
 
 
-def _write_normalized_q(path, ids, raw, sel_means, sel_vars, zq, ratio_mult=100.0):
-    """Fast writer: z rows are exact integer hundredths from the device; the
-    text is formatted and deflated by threaded host C++ as a multi-member gzip
-    (grid_write_normalized_gz), identical to the reference's after gunzip."""
+def _write_normalized_q(path, ids, raw, sel_means, sel_vars, zq, ratio_mult=100.0, dev=None):
+    """Fast writer: z rows are exact integer hundredths.  ``zq`` on the device
+    (a DevBuf [n][>= r], with ``dev``): the rows are formatted and Huffman-coded
+    in HBM (grid_write_normalized_gz_dev) and only compressed bytes come back;
+    a host array: threaded host C++ formatting + libdeflate
+    (grid_write_normalized_gz).  Either way a multi-member gzip whose text is
+    the reference's after gunzip."""
     sel_means = np.asarray(sel_means, dtype=np.float64)
     with np.errstate(invalid="ignore", divide="ignore"):
         sel_ratios = np.where(sel_means > 0, ratio_mult * np.asarray(sel_vars, dtype=np.float64) / sel_means, np.nan)
+    if isinstance(zq, _abi.DevBuf):
+        n, r = len(ids), len(sel_means)
+        _abi.write_normalized_gz_dev(dev, path, list(ids), np.asarray(raw, dtype=np.float64), sel_means, sel_ratios,
+                                     zq, n, r, zq.shape[1] if len(zq.shape) == 2 else r, level=GZ_LEVEL)
+        return
     _abi.write_normalized_gz(path, list(ids), np.asarray(raw, dtype=np.float64), sel_means, sel_ratios,
                              np.asarray(zq).reshape(len(ids), len(sel_means)), level=GZ_LEVEL)
 
@@ -456,7 +464,7 @@ def normalize_mosdepth(config, console):
     sel_h = sel.numpy()[:r]
     raw = st.rowmean.numpy()[:n]
     sel_means, sel_vars = st.mu.numpy()[:m][sel_h], st.var.numpy()[:m][sel_h]
-    _write_normalized_q(output_path, ids, raw, sel_means, sel_vars, zq.numpy()[:, :r])
+    _write_normalized_q(output_path, ids, raw, sel_means, sel_vars, zq, dev=dev)     # from HBM (gzwrite.hip)
     # step 5 in this process takes the matrix from here instead of re-parsing
     # the file (values exactly as the text prints them; handoff.py)
     with np.errstate(invalid="ignore", divide="ignore"):

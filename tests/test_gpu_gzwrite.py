@@ -1,0 +1,90 @@
+"""Device writer of the step-4 file (grid_write_normalized_gz_dev): the
+decompressed text must equal the host writer's (which tests/test_textio_cpu.py
+and the e2e goldens pin to the reference) byte for byte, across batch and
+member boundaries, sentinels and wide values; the 'GR' index must let the
+library's reader parse it back."""
+import gzip
+import struct
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    from grid_amd import _abi
+    return _abi.Device(0)
+
+
+def _case(n, r, seed, wide=False):
+    rng = np.random.default_rng(seed)
+    zq = np.clip(np.rint(rng.normal(0, 120, (n, r))), -2 ** 31 + 2, 2 ** 31 - 1).astype(np.int32)
+    if wide and n and r:
+        zq.flat[rng.integers(0, n * r, 50)] = rng.integers(-2 ** 31 + 2, 2 ** 31 - 1, 50)
+        zq.flat[0] = 2 ** 31 - 1
+        zq.flat[-1] = -2 ** 31 + 2
+    if n and r:
+        zq.flat[rng.integers(0, n * r, 30)] = -(2 ** 31)        # NA
+        zq.flat[rng.integers(0, n * r, 30)] = -(2 ** 31) + 1    # -0.00
+    ids = [f"SAMPLE_{i:05d}" for i in range(n)]
+    raw = rng.uniform(5, 90, n)
+    raw[:1] = [1e300] if n else raw[:1]
+    mu = rng.uniform(10, 60, r)
+    ra = rng.uniform(0, 9, r)
+    if r:
+        mu[0] = np.nan
+    return ids, raw, mu, ra, zq
+
+
+def _members(path):
+    """(first row, member size) of every member from the 'GR' subfields."""
+    data = open(path, "rb").read()
+    out, p = [], 0
+    while p < len(data):
+        assert data[p:p + 4] == b"\x1f\x8b\x08\x04"
+        size, row = struct.unpack_from("<Qq", data, p + 16)
+        out.append((row, size))
+        p += size
+    assert p == len(data)
+    return out
+
+
+@pytest.mark.parametrize("n,r,batch,wide", [(7, 5000, 0, False), (33, 3001, 40000, True), (1, 1, 0, False),
+                                            (4, 0, 0, False), (300, 17, 9000, False), (2, 70000, 300000, True),
+                                            (5, 1_500_000, 30_000_000, False)])   # 5 batches of one row
+def test_device_writer_equals_host_writer(tmp_path, n, r, batch, wide):
+    from grid_amd import _abi
+    dev = _dev()
+    ids, raw, mu, ra, zq = _case(n, r, seed=n * 1000 + r, wide=wide)
+    ld = max(r, 1) + 3                      # a row stride wider than r
+    zpad = np.zeros((n, ld), np.int32)
+    zpad[:, :r] = zq
+    dz = dev.upload(zpad)
+    host, devf = tmp_path / "host.tsv.gz", tmp_path / "dev.tsv.gz"
+    _abi.write_normalized_gz(str(host), ids, raw, mu, ra, zq, level=1)
+    _abi.write_normalized_gz_dev(dev, str(devf), ids, raw, mu, ra, dz, n, r, ld, level=1, batch_bytes=batch)
+    a, b = gzip.open(host, "rb").read(), gzip.open(devf, "rb").read()
+    assert a == b
+    mem = _members(devf)
+    assert mem[0][0] == -1 and [m[0] for m in mem[1:]] == sorted(m[0] for m in mem[1:])
+    if r:
+        got = _abi.read_normalized_gz(str(devf))
+        assert got[0] == ids and np.array_equal(got[4], np.where(zq == -(2 ** 31) + 1, 0, zq))
+
+
+def test_device_writer_large_rows_size(tmp_path):
+    """A config-2-like row (2.7 M cells): output within 20 % of the host
+    writer's level-1 size, same text."""
+    from grid_amd import _abi
+    dev = _dev()
+    n, r = 3, 2_700_000
+    rng = np.random.default_rng(5)
+    zq = np.clip(np.rint(rng.normal(0, 100, (n, r))), -200, 200).astype(np.int32)
+    ids, raw = ["A", "B", "C"], np.array([30.0, 31.5, 29.25])
+    mu, ra = rng.uniform(10, 60, r), rng.uniform(0, 9, r)
+    host, devf = tmp_path / "h.gz", tmp_path / "d.gz"
+    _abi.write_normalized_gz(str(host), ids, raw, mu, ra, zq, level=1)
+    _abi.write_normalized_gz_dev(dev, str(devf), ids, raw, mu, ra, dev.upload(zq), n, r, r, level=1)
+    assert gzip.open(host, "rb").read() == gzip.open(devf, "rb").read()
+    assert devf.stat().st_size < 1.2 * host.stat().st_size
