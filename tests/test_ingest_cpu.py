@@ -335,3 +335,21 @@ def test_host_gunzip_and_bgzf_members():
     x[len(x) // 2] ^= 0x10
     assert _abi.gunzip_host(bytes(x), big)[0] == _abi.GZ_EDATA
     assert _abi.gunzip_host(bg + b"junk after the members", big)[0] == _abi.GZ_EDATA
+
+
+def test_find_bed_gz_paths_equals_per_sample_glob(tmp_path):
+    """One directory listing gives every sample the file the reference's
+    per-sample glob (normalize_mosdepth.py:569) finds first, scandir order
+    included (S1 also matches S10...; names with the ID inside; no match)."""
+    from grid_amd.utils import normalize_mosdepth as nm
+    names = ["S10.regions.bed.gz", "S1.regions.bed.gz", "xS3y.regions.bed.gz", "S4.regions.bed.gz.csi",
+             "S5regions.bed.gz", "S6_a.regions.bed.gz", "S6.regions.bed.gz", "a[1].regions.bed.gz",
+             ".S7.regions.bed.gz", "S8.mosdepth.global.dist.txt"]
+    for nmx in names:
+        (tmp_path / nmx).write_bytes(b"")
+    ids = ["S1", "S10", "S3", "S4", "S5", "S6", "S6_a", "a[1]", "S7", "S8", "S9", "regions"]
+    got = nm.find_bed_gz_paths(ids, tmp_path)
+    for i in ids:
+        assert got[i] == nm.find_bed_gz_for_individual(i, tmp_path), i
+    with pytest.raises(ValueError):                  # "**regions.bed.gz": pathlib rejects it, as for the reference
+        nm.find_bed_gz_paths([""], tmp_path)
