@@ -36,6 +36,7 @@ _SIGS = {
     "grid_ctx_set_stream": [_vp, _vp],
     "grid_ctx_own_stream": [_vp],
     "grid_sync": [_vp],
+    "grid_ctx_cu_count": [_vp, C.POINTER(_i32)],
     "grid_dev_alloc": [_vp, C.c_size_t, C.POINTER(_vp)],
     "grid_dev_free": [_vp, _vp],
     "grid_h2d": [_vp, _vp, _vp, C.c_size_t],
@@ -293,6 +294,13 @@ class DevBuf:
                 self.free()
         except Exception:
             pass
+
+
+def device_cu_count(dev) -> int:
+    """Compute units of ``dev``'s GPU (256 on MI355X)."""
+    n = _i32()
+    call("grid_ctx_cu_count", dev.ctx, C.byref(n))
+    return n.value
 
 
 def device_count() -> int:

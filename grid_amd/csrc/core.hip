@@ -91,6 +91,12 @@ int grid_ctx_own_stream(grid_ctx *ctx) {
   return GRID_OK;
 }
 
+int grid_ctx_cu_count(grid_ctx *ctx, int32_t *n) {
+  REQUIRE(ctx && n, "bad args");
+  *n = ctx->ncu;
+  return GRID_OK;
+}
+
 int grid_sync(grid_ctx *ctx) {
   REQUIRE(ctx, "ctx is NULL");
   HIPCHK(hipSetDevice(ctx->device));

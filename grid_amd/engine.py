@@ -343,22 +343,35 @@ def phase(dev: Device, irr: np.ndarray, off: np.ndarray, nbr: np.ndarray, w: np.
     return hap.numpy(), imp.numpy(), float(mean.numpy()[0])
 
 
-def phase_batch(dev: Device, loci, min_nbr: int, n_iters: int, legacy: bool = False, paired: bool = False):
-    """Batched phasing + imputation of L independent loci in one launch (one
-    workgroup per locus; BASELINE config 5).  ``loci``: sequence of
-    (irr [n], off [2n+1], nbr, w) per locus (CSR as csr_from_lists).  Returns
-    a list of (hap [2n], imp [2n], mean) equal to phase() per locus.
+def phase_batch(dev: Device, loci, min_nbr: int, n_iters: int, legacy: bool = False, paired: bool = False,
+                group: int | None = None):
+    """Batched phasing + imputation of L independent loci (one workgroup per
+    locus; BASELINE config 5).  ``loci``: sequence of (irr [n], off [2n+1],
+    nbr, w) per locus (CSR as csr_from_lists).  Returns a list of (hap [2n],
+    imp [2n], mean) equal to phase() per locus.
 
-    Host work is the level schedules (grid_hi_levels, host C++ on a thread
-    pool: the calls release the GIL) and one arena of every locus's inputs,
-    copied to HBM in ONE transfer; the packed neighbour lists are built on the
-    device (grid_hi_pack_batch) and the outputs come back in one transfer.
-    Unit-weight loci share one device vector of ones as their weights."""
+    The loci run in GROUPS of ``group`` (default: the device's CU count, one
+    workgroup per CU, so a group is one round of the launch the whole batch
+    would make).  Host work per group is the level schedules (grid_hi_levels,
+    host C++ on a thread pool: the calls release the GIL) and one arena of the
+    group's inputs, copied to HBM in ONE transfer on a copy stream -- done by a
+    background thread for group g+1 while group g phases on the device.  The
+    packed neighbour lists are built on the device (grid_hi_pack_batch);
+    every group writes into one output arena, copied back once.  Unit-weight
+    loci share one device vector of ones as their weights."""
     import os
     from concurrent.futures import ThreadPoolExecutor
     if not len(loci):
         return []
+    legacy_f = _abi.HI_LEGACY if legacy else 0
+    if group is None:
+        group = max(1, _abi.device_cu_count(dev))
     pool = ThreadPoolExecutor(max(1, min(16, os.cpu_count() or 1)))
+    bg = ThreadPoolExecutor(1)
+    cdev = Device(dev.index)                  # its own non-blocking stream: uploads beside the phasing
+
+    def al(x):
+        return -(-int(x) // 256) * 256
 
     def prep(l):
         irr, off, nbr, w = l
@@ -369,21 +382,21 @@ def phase_batch(dev: Device, loci, min_nbr: int, n_iters: int, legacy: bool = Fa
         lens = np.diff(off) if len(off) > 1 else np.zeros(1, I8)
         return off, nbr, order, loff, nl, unit, int(lens.max()) if lens.size else 0
 
-    try:
-        pre = list(pool.map(prep, loci))
-        flags_all = _abi.HI_UNIT_WEIGHTS if all(p[5] for p in pre) else 0
-        legacy_f = _abi.HI_LEGACY if legacy else 0
-        need_pkw = bool(legacy_f) or not flags_all
-        max_n = max(len(l[0]) for l in loci)
-        max_nlev = max(p[4] for p in pre)
-        max_list = max(p[6] for p in pre)
-        max_nnz = max(len(p[1]) for p in pre)
+    sizes = [len(l[0]) for l in loci]
+    o_hap = np.zeros(len(sizes) + 1, dtype=np.int64)
+    np.cumsum([2 * max(n, 1) for n in sizes], out=o_hap[1:])
+    tot = int(o_hap[-1])
+    d_out = dev.alloc(2 * tot + len(sizes), F8)
 
-        def al(x):
-            return -(-int(x) // 256) * 256
-        # input arena: irr, off, nbr, w (weighted loci only), order, loff per locus
+    def stage(g0, g1):
+        """Host prep + upload of loci [g0, g1); returns what the launches need."""
+        sub = loci[g0:g1]
+        pre = list(pool.map(prep, sub))
+        flags = _abi.HI_UNIT_WEIGHTS if all(p[5] for p in pre) else 0
+        need_pkw = bool(legacy_f) or not flags
+        max_nnz = max(len(p[1]) for p in pre)
         arrs, offs, pos = [], [], 0
-        for (irr, _, _, w), (off, nbr, order, loff, nl, unit, _) in zip(loci, pre):
+        for (irr, _, _, w), (off, nbr, order, loff, nl, unit, _) in zip(sub, pre):
             n = len(irr)
             la = [np.ascontiguousarray(irr if n else np.zeros(1), dtype=F8), off, nbr,
                   None if unit else np.ascontiguousarray(w if len(w) else np.zeros(1), dtype=F8),
@@ -400,47 +413,61 @@ def phase_batch(dev: Device, loci, min_nbr: int, n_iters: int, legacy: bool = Fa
             for x, o in zip(arrs[k], offs[k]):
                 if x is not None:
                     host[o:o + x.nbytes] = x.view(U1).reshape(-1)
-        list(pool.map(fill, range(len(loci))))
+        list(pool.map(fill, range(len(sub))))
+        d_in = cdev.upload(host)
+        ones = cdev.upload(np.ones(max(max_nnz, 1), dtype=F8)) if any(p[5] for p in pre) else None
+        pk_pos, ppos = [], 0
+        for l in sub:
+            n1 = max(len(l[0]), 1)
+            a1 = ppos + al(n1 * 2 * _abi.PACK_CAP * 4)
+            pk_pos.append((ppos, a1, a1 + al(n1 * 8)))
+            ppos = a1 + al(n1 * 8) + (al(n1 * 2 * _abi.PACK_CAP * 8) if need_pkw else 0)
+        d_pk = cdev.alloc(max(ppos, 1), U1)
+        descs = []
+        for k, l in enumerate(sub):
+            n, gk = len(l[0]), g0 + k
+            io = [None if o is None else d_in.ptr + o for o in offs[k]]
+            p0, p1, p2 = (d_pk.ptr + x for x in pk_pos[k])
+            hap = d_out.ptr + 8 * int(o_hap[gk])
+            imp = d_out.ptr + 8 * (tot + int(o_hap[gk]))
+            mean = d_out.ptr + 8 * (2 * tot + gk)
+            w_ptr = io[3] if io[3] is not None else ones.ptr
+            descs.append(_abi.HiLocus(n, io[0], io[1], io[2], w_ptr, io[4], io[5], pre[k][4], 0, p0,
+                                      p2 if need_pkw else None, p1, hap, imp, mean))
+        arr = (_abi.HiLocus * len(descs))(*descs)
+        d_arr = cdev.alloc(C.sizeof(arr), U1)
+        call("grid_h2d", cdev.ctx, d_arr.ptr, C.addressof(arr), C.sizeof(arr))
+        meta = (len(descs), max(len(l[0]) for l in sub), max(p[4] for p in pre), max(p[6] for p in pre), flags)
+        return (d_in, ones, d_pk, d_arr), meta
+
+    bounds = [(g0, min(len(loci), g0 + group)) for g0 in range(0, len(loci), group)]
+    keep = []
+    try:
+        fut = bg.submit(stage, *bounds[0])
+        for gi in range(len(bounds)):
+            bufs, (nd, max_n, max_nlev, max_list, flags) = fut.result()
+            if gi + 1 < len(bounds):
+                fut = bg.submit(stage, *bounds[gi + 1])
+            keep.append(bufs)
+            d_arr = bufs[3]
+            for l0 in range(0, nd, 65535):            # grid.y of the pack launch
+                call("grid_hi_pack_batch", dev.ctx, min(65535, nd - l0), d_arr.ptr + l0 * C.sizeof(_abi.HiLocus),
+                     max_n)
+            call("grid_hi_phase_batch", dev.ctx, nd, d_arr.ptr, max_n, max_nlev, min_nbr, n_iters,
+                 flags | legacy_f | (_abi.HI_PAIRED if paired else 0), max_list)
+        out = d_out.numpy()
     finally:
+        bg.shutdown(wait=True)
         pool.shutdown(wait=True)
-    d_in = dev.upload(host)
-    ones = dev.upload(np.ones(max(max_nnz, 1), dtype=F8)) if any(p[5] for p in pre) else None
-    # device arenas: packed lists (built on the device) and outputs
-    sizes = [len(l[0]) for l in loci]
-    pk_pos, ppos = [], 0
-    for n in sizes:
-        n1 = max(n, 1)
-        pk_pos.append((ppos, ppos + al(n1 * 2 * _abi.PACK_CAP * 4), ppos + al(n1 * 2 * _abi.PACK_CAP * 4) + al(n1 * 8)))
-        ppos = pk_pos[-1][2] + (al(n1 * 2 * _abi.PACK_CAP * 8) if need_pkw else 0)
-    d_pk = dev.alloc(max(ppos, 1), U1)
-    o_hap = np.zeros(len(sizes) + 1, dtype=np.int64)
-    np.cumsum([2 * max(n, 1) for n in sizes], out=o_hap[1:])
-    tot = int(o_hap[-1])
-    d_out = dev.alloc(2 * tot + len(sizes), F8)
-    descs = []
-    for k, n in enumerate(sizes):
-        io = [None if o is None else d_in.ptr + o for o in offs[k]]
-        p0, p1, p2 = (d_pk.ptr + x for x in pk_pos[k])
-        hap = d_out.ptr + 8 * int(o_hap[k])
-        imp = d_out.ptr + 8 * (tot + int(o_hap[k]))
-        mean = d_out.ptr + 8 * (2 * tot + k)
-        w_ptr = io[3] if io[3] is not None else ones.ptr
-        descs.append(_abi.HiLocus(n, io[0], io[1], io[2], w_ptr, io[4], io[5], pre[k][4], 0, p0,
-                                  p2 if need_pkw else None, p1, hap, imp, mean))
-    arr = (_abi.HiLocus * len(descs))(*descs)
-    d_arr = dev.alloc(C.sizeof(arr), U1)
-    call("grid_h2d", dev.ctx, d_arr.ptr, C.addressof(arr), C.sizeof(arr))
-    step = 65535
-    for l0 in range(0, len(descs), step):          # grid.y of the pack launch
-        call("grid_hi_pack_batch", dev.ctx, min(step, len(descs) - l0), d_arr.ptr + l0 * C.sizeof(_abi.HiLocus),
-             max_n)
-    call("grid_hi_phase_batch", dev.ctx, len(descs), d_arr.ptr, max_n, max_nlev, min_nbr, n_iters,
-         flags_all | legacy_f | (_abi.HI_PAIRED if paired else 0), max_list)
-    out = d_out.numpy()
+        dev.sync()
+        for bufs_ in keep:                    # cdev's buffers, freed before its context closes
+            for b_ in bufs_:
+                if b_ is not None:
+                    b_.free()
+        cdev.close()
     res = []
     for k, n in enumerate(sizes):
         h0 = int(o_hap[k])
         res.append((out[h0:h0 + 2 * n].copy(), out[tot + h0:tot + h0 + 2 * n].copy(),
                     float(out[2 * tot + k]) if n else 0.0))
-    del d_in, d_pk, d_arr, ones
     return res

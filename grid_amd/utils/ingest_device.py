@@ -163,6 +163,7 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
     columns per file, status per file: 0 ok, 1 failed, 3 missing); raises
     DeviceIngestUnsupported."""
     nfiles = len(paths)
+    t_start = time.perf_counter()
     keep = []
     opts = _opts(dev, prefix, window, excluded, keep)
     sizes = np.array([os.path.getsize(p) if p else -1 for p in paths], np.int64)
@@ -392,7 +393,8 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
             if TRACE:
                 import sys
                 print(f"[ingest] batch {bi}: {nb} files, wait read {t_b - t_w:.3f} inflate {t_i - t_b:.3f} "
-                      f"parse {time.perf_counter() - t_i:.3f} s", file=sys.stderr, flush=True)
+                      f"parse {time.perf_counter() - t_i:.3f} s (at {time.perf_counter() - t_start:.3f})",
+                      file=sys.stderr, flush=True)
     finally:
         if pending is not None:
             try:
@@ -404,6 +406,9 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
         copier.shutdown(wait=True)
         waiter.shutdown(wait=True)
         cdev.close()
+    if TRACE:
+        import sys
+        print(f"[ingest] batches done at {time.perf_counter() - t_start:.3f} s", file=sys.stderr, flush=True)
     if K is None:
         return [], [], None, status
     rows = np.array([f for f in range(nfiles) if status[f] == 0], np.int32)
@@ -418,6 +423,9 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
     if np.any(pres[rows] != kh[rows]):
         raise DeviceIngestUnsupported("a repeated (start, end) key in a file")
     m = m.value
+    if TRACE:
+        import sys
+        print(f"[ingest] finish done at {time.perf_counter() - t_start:.3f} s", file=sys.stderr, flush=True)
     return rows, (Q, nK, valid, cpos, K, m), nval, status
 
 

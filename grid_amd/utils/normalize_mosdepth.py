@@ -332,10 +332,14 @@ def _ingest_dev(dev, individuals, mosdepth_dir, chromosome, start, end, excluded
                 console=None):
     """R1-R4 on the device (ingest_device.py); same (ids, regions, matrix) as
     ``ingest_native``, the matrix a device buffer."""
+    import time
+    t0 = time.perf_counter()
     inds = list(individuals)
     where = find_bed_gz_paths(inds, mosdepth_dir)
     paths = [str(where[ind]) if where[ind].exists() else None for ind in inds]
     window = (start, end) if start is not None and end is not None else None
+    if ingest_device.TRACE:
+        print(f"[ingest] paths in {time.perf_counter() - t0:.3f} s", file=sys.stderr, flush=True)
     rows, state, nval, status = ingest_device.ingest_device(
         dev, paths, norm_chrom(chromosome) if chromosome else None, window, excluded or {}, min_depth, max_depth,
         threads=max(1, int(threads or 1)))
@@ -348,6 +352,8 @@ def _ingest_dev(dev, individuals, mosdepth_dir, chromosome, start, end, excluded
     if not ids:
         return [], [], np.zeros((0, 0), dtype=np.int32)
     q, regions = ingest_device.gather(dev, state, [keep[i] for i in ids], len(inds))
+    if ingest_device.TRACE:
+        print(f"[ingest] gathered at {time.perf_counter() - t0:.3f} s", file=sys.stderr, flush=True)
     return ids, regions, q
 
 

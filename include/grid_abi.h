@@ -63,6 +63,8 @@ int grid_ctx_destroy(grid_ctx *ctx);
  * grid_ctx_own_stream restores the context's private non-blocking stream. */
 int grid_ctx_set_stream(grid_ctx *ctx, void *hip_stream);
 int grid_ctx_own_stream(grid_ctx *ctx);
+/* Compute units of the context's device (persistent grids, batch sizing). */
+int grid_ctx_cu_count(grid_ctx *ctx, int32_t *n);
 int grid_sync(grid_ctx *ctx);
 int grid_dev_alloc(grid_ctx *ctx, size_t bytes, void **d_ptr);
 int grid_dev_free(grid_ctx *ctx, void *d_ptr);
