@@ -39,6 +39,8 @@ _SIGS = {
     "grid_ctx_cu_count": [_vp, C.POINTER(_i32)],
     "grid_dev_alloc": [_vp, C.c_size_t, C.POINTER(_vp)],
     "grid_dev_free": [_vp, _vp],
+    "grid_host_alloc": [C.c_size_t, C.POINTER(_vp)],
+    "grid_host_free": [_vp],
     "grid_h2d": [_vp, _vp, _vp, C.c_size_t],
     "grid_d2h": [_vp, _vp, _vp, C.c_size_t],
     "grid_d2d": [_vp, _vp, _vp, C.c_size_t],
@@ -195,6 +197,28 @@ def ptr(a) -> int:
     if hasattr(a, "data_ptr"):
         return a.data_ptr()
     return int(a)
+
+
+class PinnedBuf:
+    """Page-locked host memory (grid_host_alloc) viewed as a uint8 array."""
+
+    def __init__(self, nbytes: int):
+        h = _vp()
+        call("grid_host_alloc", int(nbytes), C.byref(h))
+        self.ptr, self.nbytes = h.value, int(nbytes)
+        self.array = np.ctypeslib.as_array((C.c_uint8 * self.nbytes).from_address(self.ptr))
+
+    def free(self):
+        if self.ptr:
+            self.array = None
+            load().grid_host_free(self.ptr)
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 class Device:

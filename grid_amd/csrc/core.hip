@@ -120,6 +120,17 @@ int grid_dev_free(grid_ctx *ctx, void *p) {
   return GRID_OK;
 }
 
+int grid_host_alloc(size_t bytes, void **h) {
+  REQUIRE(h, "bad args");
+  HIPCHK(hipHostMalloc(h, bytes ? bytes : 16, hipHostMallocDefault));
+  return GRID_OK;
+}
+
+int grid_host_free(void *h) {
+  if (h) HIPCHK(hipHostFree(h));
+  return GRID_OK;
+}
+
 int grid_h2d(grid_ctx *ctx, void *d, const void *h, size_t bytes) {
   if (!bytes) return GRID_OK;
   HIPCHK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, ctx->stream));

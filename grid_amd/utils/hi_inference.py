@@ -10,6 +10,7 @@ sequential in-place order.
 """
 from __future__ import annotations
 
+import sys
 from collections import defaultdict
 from pathlib import Path
 
@@ -314,12 +315,11 @@ def _locus_path(template, locus, **kw):
 def _rank_world(comm=None):
     if comm is not None:
         return comm.get_rank(), comm.get_world_size()
-    try:
-        import torch.distributed as dist
-        if dist.is_available() and dist.is_initialized():
-            return dist.get_rank(), dist.get_world_size()
-    except ImportError:
-        pass
+    # an initialised default process group means torch.distributed is already
+    # imported; never import torch just to ask (seconds on a fresh host)
+    dist = sys.modules.get("torch.distributed")
+    if dist is not None and dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
     return 0, 1
 
 

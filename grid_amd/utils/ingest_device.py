@@ -57,16 +57,19 @@ def _align(x, a=256):
 
 
 class _Pinned:
-    """Reusable pinned host staging (torch allocates the page-locked memory)."""
+    """Reusable pinned host staging (grid_host_alloc: page-locked, so the
+    copies to HBM run at PCIe speed; no torch in the step path -- a first
+    ``import torch`` costs seconds on a fresh host)."""
 
     def __init__(self):
-        self.t = None
+        self.b = None
 
     def get(self, n):
-        import torch
-        if self.t is None or self.t.numel() < n:
-            self.t = torch.empty(max(n, 1), dtype=torch.uint8, pin_memory=True)
-        return self.t.numpy()
+        if self.b is None or self.b.nbytes < n:
+            if self.b is not None:
+                self.b.free()
+            self.b = _abi.PinnedBuf(max(int(n), 1))
+        return self.b.array
 
 
 def _opts(dev, prefix, window, excluded, keep):
@@ -187,9 +190,7 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
     rpool = ThreadPoolExecutor(1)         # the next batch's read (its files on `pool`)
     copier = ThreadPoolExecutor(1)        # H2D of CPU-inflated text, on its own stream
     waiter = ThreadPoolExecutor(1)        # notes when the GPU's inflate ends
-    import torch
-    cstream = torch.cuda.Stream(device=dev.index)
-    cdev = _abi.Device(dev.index, cstream)
+    cdev = _abi.Device(dev.index)          # its own non-blocking stream
     split = _Split(nthreads)
 
     def read_batch(bi):

@@ -68,6 +68,9 @@ int grid_ctx_cu_count(grid_ctx *ctx, int32_t *n);
 int grid_sync(grid_ctx *ctx);
 int grid_dev_alloc(grid_ctx *ctx, size_t bytes, void **d_ptr);
 int grid_dev_free(grid_ctx *ctx, void *d_ptr);
+/* Page-locked host memory (copies at PCIe speed; the device ingest stages). */
+int grid_host_alloc(size_t bytes, void **h_ptr);
+int grid_host_free(void *h_ptr);
 int grid_h2d(grid_ctx *ctx, void *d_dst, const void *h_src, size_t bytes);
 int grid_d2h(grid_ctx *ctx, void *h_dst, const void *d_src, size_t bytes);
 int grid_d2d(grid_ctx *ctx, void *d_dst, const void *d_src, size_t bytes);

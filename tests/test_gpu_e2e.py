@@ -20,7 +20,7 @@ def _content(p):
     return open(p).read()
 
 
-def _stage(name, tmp_path, cfgname="config.yaml"):
+def _stage(name, tmp_path, cfgname="config.yaml", device_ingest=None):
     src = os.path.join(G, name)
     shutil.copytree(os.path.join(src, "inputs"), tmp_path / "inputs")
     c = yaml.safe_load(open(os.path.join(src, cfgname)))
@@ -28,6 +28,8 @@ def _stage(name, tmp_path, cfgname="config.yaml"):
     c["output_dir"] = str(tmp_path / "out")
     c["mosdepth"]["work_dir"] = str(tmp_path / c["mosdepth"]["work_dir"])
     c["mosdepth"]["normalize"]["repeat_mask_file"] = str(tmp_path / c["mosdepth"]["normalize"]["repeat_mask_file"])
+    if device_ingest is not None:
+        c["mosdepth"]["normalize"]["device_ingest"] = device_ingest
     hc = c["compute_haploid_genotypes"]
     for k in ("ibs_output", "ibd_output"):
         if k in hc:
@@ -39,10 +41,11 @@ def _stage(name, tmp_path, cfgname="config.yaml"):
     return c, str(p)
 
 
+@pytest.mark.parametrize("device_ingest", [True, False], ids=["device-ingest", "host-ingest"])
 @pytest.mark.parametrize("name", ["g1", "g1b", "g1c"])
-def test_wgs_pipeline_matches_reference(name, tmp_path):
+def test_wgs_pipeline_matches_reference(name, device_ingest, tmp_path):
     from grid_amd.pipeline import run_wgs_pipeline
-    c, p = _stage(name, tmp_path)
+    c, p = _stage(name, tmp_path, device_ingest=device_ingest)
     run_wgs_pipeline(console=None, config=p)
     out = c["output_dir"]
     exp = os.path.join(G, name, "expected")

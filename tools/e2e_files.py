@@ -32,7 +32,9 @@ ap.add_argument("--threads", type=int, default=16)
 ap.add_argument("--json", default=os.path.join(ROOT, "gpurun_out", "e2e_files.json"))
 ap.add_argument("--keep", action="store_true", help="keep the generated cohort")
 ap.add_argument("--bgzf", action="store_true", help="BGZF files (what mosdepth writes) instead of one gzip member")
-ap.add_argument("--device-ingest", action="store_true", help="mosdepth.normalize.device_ingest: inflate + parse in HBM")
+ap.add_argument("--ingest", choices=["device", "host"], default="device",
+                help="mosdepth.normalize.device_ingest true (the default: inflate + parse in HBM) or false")
+ap.add_argument("--device-ingest", action="store_true", help=argparse.SUPPRESS)   # older spelling of --ingest device
 ap.add_argument("--reuse", action="store_true", help="keep the cohort in --data for a later run (implies --keep)")
 a = ap.parse_args()
 
@@ -46,7 +48,7 @@ def rss_gb():
 
 
 res = {"config": {"samples": a.samples, "bins": a.bins, "data": a.data, "out": a.out, "bgzf": a.bgzf,
-                  "device_ingest": a.device_ingest, "threads": a.threads}, "phases_s": {},
+                  "device_ingest": a.ingest == "device", "threads": a.threads}, "phases_s": {},
        "peak_rss_gb_after": {}}
 mos = os.path.join(a.data, "mosdepth")
 os.makedirs(mos, exist_ok=True)
@@ -90,7 +92,7 @@ cfg = {
     "count_reads": {"run": False, "output_file_prefix": "counts"},
     "mosdepth": {"run": False, "work_dir": mos, "remove_intermediate": False,
                  "normalize": {"run": True, "min_depth": 20, "max_depth": 100, "top_frac": 0.1,
-                               "device_ingest": a.device_ingest,
+                               "device_ingest": a.ingest == "device",
                                "output_file_prefix": "normalized",
                                "repeat_mask_file": os.path.join(a.data, "mask.bed")},
                  "neighbors": {"run": True, "output_file_prefix": "neighbors", "num_neighbors": 10, "zmax": 2.0,
