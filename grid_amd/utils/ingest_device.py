@@ -34,6 +34,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 import time
+from collections.abc import Sequence
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -430,6 +431,34 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
     return rows, (Q, nK, valid, cpos, K, m), nval, status
 
 
+class Regions(Sequence):
+    """The valid columns' (start, end) pairs as a read-only sequence built on
+    demand from two int64 arrays (a list of 3 M tuples costs ~1 s, and the
+    step itself never needs it)."""
+
+    def __init__(self, starts, ends):
+        self.s, self.e = starts, ends
+
+    def __len__(self):
+        return len(self.s)
+
+    def __getitem__(self, k):
+        if isinstance(k, slice):
+            return list(zip(self.s[k].tolist(), self.e[k].tolist()))
+        return int(self.s[k]), int(self.e[k])
+
+    def __iter__(self):
+        return zip(self.s.tolist(), self.e.tolist())
+
+    def __eq__(self, other):
+        try:
+            return len(self) == len(other) and list(self) == list(other)
+        except TypeError:
+            return NotImplemented
+
+    __hash__ = None
+
+
 def gather(dev, state, row_files, nfiles):
     """The matrix rows of ``row_files`` (file indices, in output order) and
     the valid columns' (start, end)."""
@@ -441,6 +470,6 @@ def gather(dev, state, row_files, nfiles):
     d_dst = dev.upload(dst)
     call("grid_md_gather", dev.ctx, Q.ptr, nK, nK, nfiles, valid.ptr, cpos.ptr, d_dst.ptr, out.ptr,
          max(m, 1), K.ptr, st.ptr, en.ptr)
-    regions = list(zip(st.numpy()[:m].tolist(), en.numpy()[:m].tolist()))
+    regions = Regions(st.numpy()[:m], en.numpy()[:m])
     out.shape = (len(row_files), m)            # the allocation keeps >= 1 element
     return out, regions
