@@ -119,13 +119,20 @@ def cpu_baseline(q_host, n_total, m_total, k, n_iters, seed=SEED):
     hap, mean = steps.run_phasing(irr, hn, 1, n_iters)
     _ = [steps.compute_imp(i, hap, hn, mean) for i in range(ns)]
     t4 = time.perf_counter()
+    return scale_cpu_baseline((ns, ms, t1 - t0, t2 - t1, t3 - t2, t4 - t3), n_total, m_total)
+
+
+def scale_cpu_baseline(meas, n_total, m_total):
+    """The oracle sample's stage times scaled by complexity to n_total x
+    m_total: normalisation n m, k-NN n^2 m, dipCN and phasing n."""
+    ns, ms, tn, tk, td, tp = meas
     fn, fm = n_total / ns, m_total / ms
-    total = (t1 - t0) * fn * fm + (t2 - t1) * fn * fn * fm + (t3 - t2) * fn + (t4 - t3) * fn
+    total = tn * fn * fm + tk * fn * fn * fm + td * fn + tp * fn
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    return {"value": n_total / total, "unit": "samples/s", "cores": threads, "kind": "port",
+    return {"value": n_total / total, "unit": "samples/s", "cores": threads, "kind": "port", "measured": meas,
             "sample": (f"oracle steps 4-7 on the first {ns} samples x {ms} bins of the same cohort, scaled to "
-                       f"{n_total} x {m_total}: normalise {t1 - t0:.2f}s x{fn * fm:.1f}, kNN {t2 - t1:.2f}s "
-                       f"x{fn * fn * fm:.1f}, dipCN {t3 - t2:.2f}s x{fn:.1f}, phasing {t4 - t3:.2f}s x{fn:.1f} "
+                       f"{n_total} x {m_total}: normalise {tn:.2f}s x{fn * fm:.1f}, kNN {tk:.2f}s "
+                       f"x{fn * fn * fm:.1f}, dipCN {td:.2f}s x{fn:.1f}, phasing {tp:.2f}s x{fn:.1f} "
                        f"(extrapolated; host memory bounds the reference well below this shape)")}
 
 
@@ -211,6 +218,155 @@ def plan_memory(n, ml, world, budget):
     return min(chunk, -(-ml // 8192) * 8192), fixed + per_col * chunk
 
 
+def run_workload(args, n, m, steps, warmup, world, rank, local, dist, comm, dev, note, profile_pass=True):
+    """One workload's timed steps (steps 4-7 of an n x m cohort over `world`
+    ranks): the bench line's fields for it."""
+    import torch
+
+    from grid_amd import _abi
+    from grid_amd.fused import Depth16, HipOps, Steps47, SynthSource, TorchAlloc, shard_range
+
+    c0, c1 = shard_range(m, rank, world)
+    ml = c1 - c0
+    talloc = TorchAlloc(local)
+    ops = HipOps(dev)
+    if args.chunk and (n, m) == (args.samples, args.bins):
+        chunk, _ = args.chunk, None
+    else:
+        chunk, _ = plan_memory(n, ml, world, args.hbm_budget_gb * 1e9)
+    streamed = chunk is not None and chunk < ml
+    depth_format = args.depth_format
+    if depth_format == "auto":
+        depth_format = "int32" if streamed else "q16"
+    if streamed:
+        if depth_format != "int32":
+            raise SystemExit("bench: the compact depth form is resident-only")
+        q, ldq = SynthSource(ops, SEED, n, c0, NCL), None
+    elif depth_format == "q16":
+        # compact depth matrix: uint16 hundredths + escape table (half the HBM
+        # bytes of the four step-4 passes; same int32 values after decoding)
+        q = Depth16.synth(talloc, dev.ctx, SEED, n, ml, c0, NCL)
+        ldq = q.ld
+    else:
+        q = torch.empty((n, max(ml, 1)), dtype=torch.int32, device="cuda")
+        _abi.call("grid_synth_depth", dev.ctx, SEED, n, ml, ml, c0, NCL, q.data_ptr())
+        ldq = ml
+    reads, off, nbr, w = synth_reads_and_ibs(n)
+    # step 7 on its own stream, deferred behind the next pass's Gram (fused.py
+    # Steps47): it overlaps that pass's top-k/dipCN and the next statistics;
+    # every pass's phasing still completes inside the timed region (finish()
+    # before the final synchronize)
+    lane = None
+    if not args.no_overlap:
+        pdev = _abi.Device(local)
+        pstream = torch.cuda.Stream()
+        pdev.set_stream(pstream)
+        lane = (HipOps(pdev), pstream)
+    st = Steps47(ops, talloc, n, m, c0, ml, k=args.k, n_nbr=300, top_frac=0.1, zmax=2.0, sigma2_max=1000.0,
+                 frac_r=1.0, min_nbr=1, n_iters=args.n_iters, comm=comm, phase_lane=lane,
+                 chunk=chunk if streamed else None, keep_z=not streamed)
+    st.set_reads(reads)
+    st.set_phasing_graph(off, nbr, w)
+
+    note(f"{n} x {m}, shard {ml} bins, {st.nch} chunk(s); warmup {warmup}, steps {steps}")
+    for w_ in range(warmup):
+        st.run(q, ldq)
+        st.finish()
+        torch.cuda.synchronize()
+        note(f"warmup {w_} done")
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    gms, glaunch = 0.0, 0
+    gram_pairs = []
+    for s in range(steps):
+        st.run(q, ldq, time_gram=True)
+        gram_pairs += st.gram_evs
+        if st.nch > 1:                          # long streamed steps: progress for the watchdog
+            note(f"step {s} queued")
+    st.finish()                                 # the last step's (deferred) phasing, inside the clock
+    torch.cuda.synchronize()
+    note("timed steps done")
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    el = torch.tensor([t1 - t0], dtype=torch.float64, device="cuda")
+    if dist:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    gms = sum(a.elapsed_time(b) for a, b in gram_pairs) / max(steps, 1)      # Gram ms per step
+    glaunch = len(gram_pairs) // max(steps, 1)
+    stages = None
+    if profile_pass:
+        st.run(q, ldq, profile=True)          # untimed pass: per-stage device times
+        torch.cuda.synchronize()
+        stages = {k: round(v, 3) for k, v in st.stage_ms().items()}
+
+    valid = int(st.valid[:n].sum().item())
+    traffic, tsrc = None, None
+    tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), args.traffic_json)
+    if os.path.exists(tpath):
+        tj = json.load(open(tpath))
+        shape_ok = tj.get("bench", {}).get("samples", 3202) == n and tj.get("bench", {}).get("bins", 3_000_000) == m
+        hits = [v for kk, v in tj["kernels"].items() if kk.startswith(GRAM_KERNEL)]
+        if hits and shape_ok and world == 1 and not streamed:
+            traffic, tsrc = hits[0]["traffic_bytes"], args.traffic_json
+    ruse = st.ruse_loc
+    flops = 2.0 * n * n * ruse                          # SURVEY 8(d): 2 N^2 R_use per step (this rank)
+    nt, ni = st.np_ // 128, st.np_ // 256               # k_gram8: 256x128 tiles (I, j >= 2I)
+    ntiles = sum(nt - 2 * i for i in range(ni))
+    executed = 2.0 * ntiles * 256 * 128 * sum(-(-u // 64) * 64 for u in st.chunk_used)
+    gsec = gms * 1e-3
+    streamed_note = (f", bin-streamed in {st.nch} chunks of {chunk} bins regenerated on the device every pass "
+                     f"(inside the timed region), step-4 output written per chunk") if streamed else ""
+    cfgname = {(3202, 3_000_000): "BASELINE config 2", (50_000, 3_000_000): "BASELINE config 3 shape",
+               (50_000, 30_000_000): "BASELINE config 4 shape"}.get((n, m), "custom")
+    out = {
+        "metric": METRIC,
+        "value": n * steps / elapsed,
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": 1000.0 * elapsed / steps,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64 (statistics) + bf16-MFMA exact-integer (k-NN)",
+        "data": "synthetic (counter-based cohort generated in HBM; 26 ancestry clusters)",
+        "config": {"workload": f"{cfgname}: {n} samples x {m} bins, k={args.k}, n_iters={args.n_iters}, "
+                               f"{world} GPU(s){streamed_note}",
+                   "samples": n, "bins": m, "k": args.k, "n_iters": args.n_iters,
+                   "parallelism": f"bin-sharded x{world}", "depth_format": depth_format,
+                   "streamed": streamed, "chunk_bins": chunk if streamed else None, "chunks": st.nch,
+                   "selected_regions": st.r_loc if world == 1 else None, "R_use_rank0": ruse,
+                   "dipcn_valid": valid, "phasing_levels": st.nlev},
+        "stages_ms": stages,
+        "roofline": {"kernel": "k_gram8 (exact bf16-MFMA Gram)", "bound": "mfma",
+                     "achieved": flops / gsec / 1e12, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": flops / gsec / 1e12 / PEAK_BF16_TFLOPS,
+                     "traffic": traffic, "traffic_source": tsrc,
+                     "hbm_gbs": traffic * glaunch / gsec / 1e9 if traffic else None,
+                     "hbm_frac": traffic * glaunch / gsec / 1e9 / PEAK_HBM_GBS if traffic else None,
+                     "gram_ms": gms, "gram_launches_per_step": glaunch,
+                     "executed_mfma_tflops": executed / gsec / 1e12,
+                     "executed_frac": executed / gsec / 1e12 / PEAK_BF16_TFLOPS,
+                     "flops_def": "2*N^2*R_use per step on this rank (SURVEY 8d), over the summed HIP-event time "
+                                  "of its Gram launches; executed = the 256x128 upper-triangle tiles k_gram8 "
+                                  "computes (the symmetric half is not executed)"},
+    }
+    timing = {"stages": stages, "elapsed": elapsed}
+    # release the workload's device memory before another one
+    del st, q
+    if lane is not None:
+        del lane
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return out, timing
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -229,6 +385,10 @@ def main():
     ap.add_argument("--no-files-baseline", action="store_true",
                     help="skip the from-files oracle run at config 1 (~1 min of host time)")
     ap.add_argument("--no-overlap", action="store_true", help="run step 7 inline on the main stream")
+    ap.add_argument("--config3-steps", type=int, default=1,
+                    help="N=1: timed steps of the BASELINE config-3 shape (50k x 3M, streamed) reported beside the "
+                         "line as config3_1gpu (0 = skip)")
+    ap.add_argument("--config3-warmup", type=int, default=1)
     ap.add_argument("--traffic-json", default=TRAFFIC_JSON,
                     help="rocprofv3 PMC summary (tools/pmc_traffic.py) of this same command, for roofline.traffic")
     ap.add_argument("--depth-format", choices=["auto", "int32", "q16"], default="auto",
@@ -266,150 +426,42 @@ def main():
         comm = TorchComm(dist)
 
     from grid_amd import _abi
-    from grid_amd.fused import Depth16, HipOps, Steps47, SynthSource, TorchAlloc, shard_range
 
     dev = _abi.Device(local)
     dev.set_stream(torch.cuda.current_stream())
-    n, m = args.samples, args.bins
-    c0, c1 = shard_range(m, rank, world)
-    ml = c1 - c0
-    talloc = TorchAlloc(local)
-    ops = HipOps(dev)
-    if args.chunk:
-        chunk, _ = args.chunk, None
-    else:
-        chunk, _ = plan_memory(n, ml, world, args.hbm_budget_gb * 1e9)
-    streamed = chunk is not None and chunk < ml
-    if args.depth_format == "auto":
-        args.depth_format = "int32" if streamed else "q16"
-    if streamed:
-        if args.depth_format != "int32":
-            raise SystemExit("bench: the compact depth form is resident-only")
-        q, ldq = SynthSource(ops, SEED, n, c0, NCL), None
-    elif args.depth_format == "q16":
-        # compact depth matrix: uint16 hundredths + escape table (half the HBM
-        # bytes of the four step-4 passes; same int32 values after decoding)
-        q = Depth16.synth(talloc, dev.ctx, SEED, n, ml, c0, NCL)
-        ldq = q.ld
-    else:
-        q = torch.empty((n, max(ml, 1)), dtype=torch.int32, device="cuda")
-        _abi.call("grid_synth_depth", dev.ctx, SEED, n, ml, ml, c0, NCL, q.data_ptr())
-        ldq = ml
-    reads, off, nbr, w = synth_reads_and_ibs(n)
-    # step 7 on its own stream, deferred behind the next pass's Gram (fused.py
-    # Steps47): it overlaps that pass's top-k/dipCN and the next statistics;
-    # every pass's phasing still completes inside the timed region (finish()
-    # before the final synchronize)
-    lane = None
-    if not args.no_overlap:
-        pdev = _abi.Device(local)
-        pstream = torch.cuda.Stream()
-        pdev.set_stream(pstream)
-        lane = (HipOps(pdev), pstream)
-    st = Steps47(ops, talloc, n, m, c0, ml, k=args.k, n_nbr=300, top_frac=0.1, zmax=2.0, sigma2_max=1000.0,
-                 frac_r=1.0, min_nbr=1, n_iters=args.n_iters, comm=comm, phase_lane=lane,
-                 chunk=chunk if streamed else None, keep_z=not streamed)
-    st.set_reads(reads)
-    st.set_phasing_graph(off, nbr, w)
 
     def note(msg):
         if rank == 0:
             print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
-    note(f"{n} x {m}, shard {ml} bins, {st.nch} chunk(s); warmup {args.warmup}, steps {args.steps}")
-    for w_ in range(args.warmup):
-        st.run(q, ldq)
-        st.finish()
-        torch.cuda.synchronize()
-        note(f"warmup {w_} done")
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    gms, glaunch = 0.0, 0
-    gram_pairs = []
-    for s in range(args.steps):
-        st.run(q, ldq, time_gram=True)
-        gram_pairs += st.gram_evs
-        if st.nch > 1:                          # long streamed steps: progress for the watchdog
-            note(f"step {s} queued")
-    st.finish()                                 # the last step's (deferred) phasing, inside the clock
-    torch.cuda.synchronize()
-    note("timed steps done")
-    if dist:
-        dist.barrier()
-    t1 = time.perf_counter()
-    el = torch.tensor([t1 - t0], dtype=torch.float64, device="cuda")
-    if dist:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed = float(el.item())
-    gms = sum(a.elapsed_time(b) for a, b in gram_pairs) / max(args.steps, 1)      # Gram ms per step
-    glaunch = len(gram_pairs) // max(args.steps, 1)
-    st.run(q, ldq, profile=True)              # untimed pass: per-stage device times
-    torch.cuda.synchronize()
-    stages = {k: round(v, 3) for k, v in st.stage_ms().items()}
-
-    valid = int(st.valid[:n].sum().item())
-    traffic, tsrc = None, None
-    tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), args.traffic_json)
-    if os.path.exists(tpath):
-        tj = json.load(open(tpath))
-        shape_ok = tj.get("bench", {}).get("samples", 3202) == n and tj.get("bench", {}).get("bins", 3_000_000) == m
-        hits = [v for kk, v in tj["kernels"].items() if kk.startswith(GRAM_KERNEL)]
-        if hits and shape_ok and world == 1 and not streamed:
-            traffic, tsrc = hits[0]["traffic_bytes"], args.traffic_json
-    ruse = st.ruse_loc
-    flops = 2.0 * n * n * ruse                          # 2 N^2 R_use per step (this rank)
-    nt, ni = st.np_ // 128, st.np_ // 256               # k_gram8: 256x128 tiles (I, j >= 2I)
-    ntiles = sum(nt - 2 * i for i in range(ni))
-    executed = 2.0 * ntiles * 256 * 128 * sum(-(-u // 64) * 64 for u in st.chunk_used)
-    gsec = gms * 1e-3
-    streamed_note = (f", bin-streamed in {st.nch} chunks of {chunk} bins regenerated on the device every pass "
-                     f"(inside the timed region), step-4 output written per chunk") if streamed else ""
-    cfgname = {(3202, 3_000_000): "BASELINE config 2", (50_000, 3_000_000): "BASELINE config 3 shape",
-               (50_000, 30_000_000): "BASELINE config 4 shape"}.get((n, m), "custom")
-    out = {
-        "metric": METRIC,
-        "value": n * args.steps / elapsed,
-        "unit": "samples/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": 1000.0 * elapsed / args.steps,
-        "higher_is_better": True,
-        "scaling": "strong",
-        "vs_baseline": None,
-        "dtype": "f64 (statistics) + bf16-MFMA exact-integer (k-NN)",
-        "data": "synthetic (counter-based cohort generated in HBM; 26 ancestry clusters)",
-        "config": {"workload": f"{cfgname}: {n} samples x {m} bins, k={args.k}, n_iters={args.n_iters}, "
-                               f"{world} GPU(s){streamed_note}",
-                   "samples": n, "bins": m, "k": args.k, "n_iters": args.n_iters,
-                   "parallelism": f"bin-sharded x{world}", "depth_format": args.depth_format,
-                   "streamed": streamed, "chunk_bins": chunk if streamed else None, "chunks": st.nch,
-                   "selected_regions": st.r_loc if world == 1 else None, "R_use_rank0": ruse,
-                   "dipcn_valid": valid, "phasing_levels": st.nlev},
-        "stages_ms": stages,
-        "roofline": {"kernel": "k_gram8 (exact bf16-MFMA Gram)", "bound": "mfma",
-                     "achieved": flops / gsec / 1e12, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": flops / gsec / 1e12 / PEAK_BF16_TFLOPS,
-                     "traffic": traffic, "traffic_source": tsrc,
-                     "hbm_gbs": traffic * glaunch / gsec / 1e9 if traffic else None,
-                     "hbm_frac": traffic * glaunch / gsec / 1e9 / PEAK_HBM_GBS if traffic else None,
-                     "gram_ms": gms, "gram_launches_per_step": glaunch,
-                     "executed_mfma_tflops": executed / gsec / 1e12,
-                     "executed_frac": executed / gsec / 1e12 / PEAK_BF16_TFLOPS,
-                     "flops_def": "2*N^2*R_use per step on this rank (SURVEY 8d), over the summed HIP-event time "
-                                  "of its Gram launches; executed = the 256x128 upper-triangle tiles k_gram8 "
-                                  "computes (the symmetric half is not executed)"},
-    }
+    n, m = args.samples, args.bins
+    out, timing = run_workload(args, n, m, args.steps, args.warmup, world, rank, local, dist, comm, dev, note)
+    # the metric's own shape (BASELINE config 3: 50k x 3M, streamed on one
+    # GPU): one more timed measurement in the same run, beside the line's
+    # workload (N = 1 only: the scaling runs keep one workload per N)
+    c3 = None
+    if world == 1 and args.config3_steps > 0 and (n, m) != (50_000, 3_000_000):
+        note("config 3 shape (50,000 x 3,000,000, streamed) as a second measurement")
+        o3, _ = run_workload(args, 50_000, 3_000_000, args.config3_steps, args.config3_warmup, world, rank, local, dist,
+                             comm, dev, note, profile_pass=False)
+        c3 = {k: o3[k] for k in ("value", "unit", "steps", "warmup", "ms_per_step")}
+        c3["config"] = o3["config"]
+        c3["gram_ms"] = o3["roofline"]["gram_ms"]
+        c3["gram_frac_2N2R"] = o3["roofline"]["frac"]
+        c3["executed_frac"] = o3["roofline"]["executed_frac"]
+        out["config3_1gpu"] = c3
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        ns, ms = min(args.cpu_samples, n), min(args.cpu_bins, ml)
+        c0 = 0
+        ns, ms = min(args.cpu_samples, n), min(args.cpu_bins, m)
         qs = torch.empty((ns, ms), dtype=torch.int32, device="cuda")   # same cells, int32 form
         _abi.call("grid_synth_depth", dev.ctx, SEED, ns, ms, ms, c0, NCL, qs.data_ptr())
         qh = qs.cpu().numpy()
         del qs
         out["cpu_baseline"] = cpu_baseline(qh, n, m, args.k, args.n_iters)
+        if c3 is not None:
+            cb3 = scale_cpu_baseline(out["cpu_baseline"]["measured"], 50_000, 3_000_000)
+            c3["cpu_baseline"] = {k: cb3[k] for k in ("value", "unit", "cores", "kind", "sample")}
+            c3["speedup_vs_cpu_baseline"] = c3["value"] / cb3["value"]
         if not args.no_files_baseline:
             note("cpu baseline: the oracle from files at config 1")
             out["cpu_baseline"]["from_files"] = cpu_baseline_from_files(n, m, args.k, args.n_iters)

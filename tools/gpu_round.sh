@@ -19,7 +19,7 @@ fi
 timeout -k 10 400 python -u bench.py > $O/bench.json 2> $O/bench.err
 echo "bench ok"; cat $O/bench.json
 cd /tmp && export TMPDIR=/tmp
-B="$R/bench.py --steps 3 --warmup 1 --no-cpu-baseline"
+B="$R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --config3-steps 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -- python3 $B > $O/stats.log 2>&1
 echo "stats ok"
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv --pmc FETCH_SIZE -d $O/pmc_fetch -- python3 $B > $O/pmc_fetch.log 2>&1
