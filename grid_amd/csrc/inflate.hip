@@ -28,7 +28,15 @@
 
 namespace {
 
-constexpr int RING = 32768, RMASK = RING - 1, FLUSH = 4096;
+// The LDS ring holds the last RING bytes of output (every unflushed byte among
+// them: pos - flushed < FLUSH + 266 before a flush), so a match with dist <=
+// RING - 258 copies within the ring; a longer one (up to DEFLATE's 32768)
+// reads its source from the flushed output in HBM (FAR: dist > RING - 258 >
+// pos - flushed + 257, so every source byte is flushed).  An 8 KiB ring puts
+// ~14.5 KiB of LDS on a wave: 11 waves per CU instead of the 4 a 32 KiB window
+// allowed -- the decode chain is latency-bound, one symbol at a time.
+constexpr int RING = 8192, RMASK = RING - 1, FLUSH = 4096, NEAR = RING - 258;
+static_assert(NEAR > FLUSH + 266 + 257, "far copies must read flushed bytes only");
 
 __constant__ uint32_t c_crc_pow[48][32];   // columns of M^(2^k), M = one zero byte
 
@@ -163,6 +171,24 @@ struct DevP {
   // more than the reciprocal's error, so the quotient below is exact
   __device__ __forceinline__ void copy_bytes(uint32_t dist, uint32_t len) {
     const int64_t s0 = pos - dist;
+    if (dist > (uint32_t)NEAR) {       // FAR (rare): no overlap (dist > len); source in HBM
+      // this wave's flush stores must have reached L2, and the loads go to L2
+      // (agent scope): an L1 line of the neighbouring member's wave may hold
+      // these bytes from before they were written
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      for (uint32_t k0 = 0; k0 < len; k0 += 64) {
+        const uint32_t k = k0 + lane;
+        if (k < len) {
+          const uint8_t *a = out + s0 + k;
+          const uint32_t w = __hip_atomic_load(reinterpret_cast<const uint32_t *>((uintptr_t)a & ~(uintptr_t)3),
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ring[(pos + k) & RMASK] = (uint8_t)(w >> (8 * ((uintptr_t)a & 3)));
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      pos += len;
+      return;
+    }
     const float rdist = __builtin_amdgcn_rcpf((float)dist);
     for (uint32_t k0 = 0; k0 < len; k0 += 64) {
       const uint32_t k = k0 + lane;
@@ -359,7 +385,7 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ src,
                                                 int32_t *__restrict__ nmem) {
   __shared__ __attribute__((aligned(16))) uint8_t s_ring[RING];
   __shared__ uint16_t s_tab[icore::T_SIZE];
-  __shared__ uint32_t s_ftab[F_LEN + F_DIST];   // 38.9 KiB in all: 4 waves per CU
+  __shared__ uint32_t s_ftab[F_LEN + F_DIST];   // 14.5 KiB in all: 11 waves per CU
   const int f = blockIdx.x;
   DevP p;
   // the stream starts `skew` bytes into a 4-B aligned word (a BGZF member

@@ -22,6 +22,14 @@ def _variants():
     texts = [b"", b"a", b"hello hello hello hello", bytes(rng.getrandbits(8) for _ in range(70000)),
              b"".join(b"chr1\t%d\t%d\t%.2f\n" % (i * 1000, i * 1000 + 1000, rng.uniform(0, 100)) for i in range(20000)),
              b"A" * 100000, bytes(range(256)) * 300]
+    # matches beyond the LDS ring (inflate.hip: dist > 8192 - 258 reads the
+    # flushed output in HBM), up to DEFLATE's 32768, and both sides of the edge
+    rb = lambda k: bytes(rng.getrandbits(8) for _ in range(k))    # noqa: E731
+    x, y, a, b = rb(12000), rb(5000), rb(16384), rb(16384)
+    texts += [x + y + x, a + b + a]
+    for e in (7933, 7934, 7935, 7936, 8192, 8193):
+        z = rb(e)
+        texts.append(z + z + z[:300])
     out = []
     for t in texts:
         for lvl in (0, 1, 6, 9):
