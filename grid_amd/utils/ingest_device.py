@@ -102,9 +102,9 @@ class _Split:
 
     def __init__(self, threads):
         self.threads = max(1, int(threads))
-        self.gpu = 10.0e9         # B/s, member-parallel
+        self.gpu = 18.0e9         # B/s, member-parallel (8 KiB inflate ring: 10 waves per CU)
         self.wave = 9.0e6         # B/s, one wave on one whole file
-        self.cpu = 0.6e9          # B/s per thread
+        self.cpu = 0.4e9          # B/s per thread while the GPU inflates too (0.6-0.7 alone)
 
     def plan(self, files, text, bgzf):
         g_mem = g_whole = c = 0.0

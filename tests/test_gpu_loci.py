@@ -70,3 +70,27 @@ def test_loci_sharded_world2(tmp_path):
     cfg, _ = write_cohort(str(tmp_path))
     mp.start_processes(_worker, args=(2, _free_port(), cfg), nprocs=2, join=True, start_method="spawn")
     _check(cfg)
+
+
+def test_phase_batch_groups_equal_one_group():
+    """engine.phase_batch in groups of 3 loci (host prep of group g+1 beside
+    group g's phasing, several launches) = one group, bit for bit, with unit
+    and general weights and loci of different sizes."""
+    import numpy as np
+    from grid_amd import engine
+    from grid_amd.device import get_device
+    rng = np.random.default_rng(5)
+    loci = []
+    for k in range(8):
+        n = int(rng.integers(20, 300))
+        irr = rng.choice([1.0, 1.5, 2.0, 2.5, 3.0], size=n) * rng.uniform(0.9, 1.1, n)
+        per = int(rng.integers(1, 12))
+        nbr = rng.integers(0, 2 * n, 2 * n * per).astype(np.int32)
+        off = np.arange(0, 2 * n * per + 1, per, dtype=np.int64)
+        w = np.ones(len(nbr)) if k % 3 else rng.uniform(0.1, 2.0, len(nbr))
+        loci.append((irr, off, nbr, w))
+    dev = get_device()
+    one = engine.phase_batch(dev, loci, 1, 20)
+    grouped = engine.phase_batch(dev, loci, 1, 20, group=3)
+    for (h1, i1, m1), (h2, i2, m2) in zip(one, grouped):
+        assert np.array_equal(h1, h2, equal_nan=True) and np.array_equal(i1, i2, equal_nan=True) and m1 == m2
