@@ -281,9 +281,14 @@ def run(n, m, *, k=10, n_iters=3, n_rows=128, n_blocks=4, n_windows=4, budget_gb
     log(f"selection ok: R={st.r_loc}, R_use={st.ruse_loc}")
     check_dipcn_phasing(st, n, k, 300, reads, off, nbr, n_iters)
     log(f"dipCN + phasing ok; total {time.perf_counter() - t0:.1f}s")
-    return {"n": n, "m": m, "chunks": st.nch, "chunk": chunk, "R": st.r_loc, "R_use": st.ruse_loc,
-            "cells_verified": ck.cells, "escapes_checked": ck.esc_checked, "query_rows": len(rows),
-            "chain_s": t2 - t1, "total_s": time.perf_counter() - t0}
+    res = {"n": n, "m": m, "chunks": st.nch, "chunk": chunk, "R": st.r_loc, "R_use": st.ruse_loc,
+           "cells_verified": ck.cells, "escapes_checked": ck.esc_checked, "query_rows": len(rows),
+           "chain_s": t2 - t1, "total_s": time.perf_counter() - t0}
+    st.on_z_chunk = None                 # st <-> ck cycle: free the ~200 GB of chunk buffers now
+    del ck, st
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return res
 
 
 if __name__ == "__main__":

@@ -16,3 +16,20 @@ def pytest_configure(config):
 @pytest.fixture
 def golden_dir():
     return GOLDEN
+
+
+@pytest.fixture(autouse=True)
+def _release_device_memory(request):
+    """After every GPU test: collect reference cycles (a chain and its chunk
+    callback point at each other) and hand the caching allocator's blocks back,
+    so the next full-shape test (configs 3 and 4 plan ~200 GB of HBM each)
+    starts on an empty device."""
+    yield
+    if request.node.get_closest_marker("gpu") is None or "torch" not in sys.modules:
+        return
+    import gc
+    gc.collect()
+    torch = sys.modules["torch"]
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
