@@ -62,14 +62,17 @@ class _Pinned:
     copies to HBM run at PCIe speed; no torch in the step path -- a first
     ``import torch`` costs seconds on a fresh host)."""
 
-    def __init__(self):
+    def __init__(self, bound):
         self.b = None
+        self.bound = int(bound)        # the size a request normally stays within
 
     def get(self, n):
         if self.b is None or self.b.nbytes < n:
             if self.b is not None:
                 self.b.free()
-            self.b = _abi.PinnedBuf(max(int(n), 1))
+            # room to grow at once: a buffer re-pinned a few MB larger each
+            # batch stalled that batch's copy to HBM by ~1 s (profiles/r03q)
+            self.b = _abi.PinnedBuf(max(int(n), min(2 * int(n), self.bound), 1))
         return self.b.array
 
 
@@ -192,8 +195,8 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
         cin += _align(sizes[f])
     if cur:
         batches.append(cur)
-    pins = [_Pinned(), _Pinned()]
-    stages = [_Pinned(), _Pinned()]
+    pins = [_Pinned(BATCH_IN + 512), _Pinned(BATCH_IN + 512)]
+    stages = [_Pinned(STAGE + 512), _Pinned(STAGE + 512)]
     nthreads = max(1, min(int(threads or 1), 32))
     pool = ThreadPoolExecutor(nthreads)
     rpool = ThreadPoolExecutor(1)         # the next batch's read (its files on `pool`)
@@ -471,13 +474,25 @@ def gather(dev, state, row_files, nfiles):
     """The matrix rows of ``row_files`` (file indices, in output order) and
     the valid columns' (start, end)."""
     Q, nK, valid, cpos, K, m = state
+    if m == nK and m > 0 and len(row_files) == nfiles and np.array_equal(np.asarray(row_files), np.arange(nfiles)):
+        # every key valid and every file a row, already in output order: the
+        # placed matrix IS the result (no 38 GB copy at config 2)
+        kh = K.numpy()[:m]
+        Q.shape = (nfiles, m)
+        return Q, Regions(np.ascontiguousarray(kh[:, 0]), np.ascontiguousarray(kh[:, 1]))
+    t0 = time.perf_counter()
     dst = np.full(max(nfiles, 1), -1, np.int32)
     dst[np.asarray(row_files, np.int64)] = np.arange(len(row_files), dtype=np.int32)
     out = dev.alloc((max(len(row_files), 1), max(m, 1)), np.int32)
     st, en = dev.alloc(max(m, 1), np.int64), dev.alloc(max(m, 1), np.int64)
+    t1 = time.perf_counter()
     d_dst = dev.upload(dst)
     call("grid_md_gather", dev.ctx, Q.ptr, nK, nK, nfiles, valid.ptr, cpos.ptr, d_dst.ptr, out.ptr,
          max(m, 1), K.ptr, st.ptr, en.ptr)
     regions = Regions(st.numpy()[:m], en.numpy()[:m])
+    if TRACE:
+        import sys
+        print(f"[ingest] gather: {len(row_files)} of {nfiles} rows, {m} of {nK} columns; alloc "
+              f"{t1 - t0:.3f} s, gather {time.perf_counter() - t1:.3f} s", file=sys.stderr, flush=True)
     out.shape = (len(row_files), m)            # the allocation keeps >= 1 element
     return out, regions
