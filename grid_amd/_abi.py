@@ -24,6 +24,9 @@ ZQ16_NAN, ZQ16_NEG0, ZQ16_ESC = -32768, -32767, -32766   # GRID_ZQ16_* (grid_nor
 BLOCK = 8192
 KBW = 32                       # K-block width of the k-NN panel (common.hpp KBW)
 SEG_K1 = 16                    # GRID_SEG_K1: candidate keys per row / column (multi-GPU step 5)
+SEL_STATE = 16                 # GRID_SEL_STATE: int64 slots of the device selection state
+SEL_NVALID, SEL_RLOC, SEL_RTOT, SEL_NV, SEL_RUSE, SEL_ERR = 0, 1, 2, 3, 4, 5   # GRID_SEL_* slots
+SEL_THR, SEL_V0, SEL_SMIN, SEL_SMAX = 8, 9, 12, 13
 
 _i64, _i32, _f64, _vp = C.c_int64, C.c_int32, C.c_double, C.c_void_p
 
@@ -58,6 +61,10 @@ _SIGS = {
     "grid_norm_zquant_f64": [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _f64, _vp, _i64, C.POINTER(_i32)],
     "grid_select_kth": [_vp, _vp, _i64, _vp, _i32, _vp],
     "grid_select_gt": [_vp, _vp, _i64, _f64, _vp, C.POINTER(_i64)],
+    "grid_sel_stage1": [_vp, _vp, _i64, _vp, _i64, _i64, _f64, _vp, _vp, _vp],
+    "grid_sel_stage2": [_vp, _vp, _i64, _vp, _i64, _f64, _f64, _vp, _vp],
+    "grid_sel_read": [_vp, _vp, _vp],
+    "grid_status_copy": [_vp, _vp],
     "grid_round_decimals": [_vp, _vp, _i64, C.c_int, _vp],
     "grid_gather_f64": [_vp, _vp, _vp, _i64, _vp],
     "grid_colmap_range": [_vp, _vp, _i64, _f64, _f64, _vp, C.POINTER(_i64)],

@@ -259,40 +259,16 @@ __device__ __forceinline__ uint64_t dkey(double d) {
   return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
 }
 
-__global__ __launch_bounds__(256) void k_kth_hist(const double *__restrict__ v, int64_t n, int nk, int shift,
-                                                  const KthState *__restrict__ st, unsigned *__restrict__ ghist) {
-  __shared__ unsigned h[KTH_MAX][256];
-  for (int t = threadIdx.x; t < KTH_MAX * 256; t += 256) (&h[0][0])[t] = 0;
-  uint64_t pre[KTH_MAX];
-#pragma unroll
-  for (int j = 0; j < KTH_MAX; j++) pre[j] = j < nk ? st[j].prefix : 0;
-  __syncthreads();
-  const int hs = shift + 8;                      // bits above the current digit must match
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const double d = v[i];
-    if (d != d) continue;
-    const uint64_t k = dkey(d);
-    const unsigned dig = (unsigned)(k >> shift) & 255u;
-#pragma unroll
-    for (int j = 0; j < KTH_MAX; j++)
-      if (j < nk && (hs >= 64 || ((k ^ pre[j]) >> hs) == 0)) atomicAdd(&h[j][dig], 1u);
-  }
-  __syncthreads();
-  for (int t = threadIdx.x; t < nk * 256; t += 256) {
-    const unsigned c = (&h[0][0])[t];
-    if (c) atomicAdd(ghist + t, c);
-  }
-}
-
 // one wave per k: the digit holding rank k, the rank within it; clears the histogram
-__global__ __launch_bounds__(64) void k_kth_pick(int shift, KthState *__restrict__ st, unsigned *__restrict__ ghist) {
-  const int j = blockIdx.x, lane = threadIdx.x;
+__device__ __forceinline__ void kth_pick_wave(int j, int lane, int shift, KthState *__restrict__ st,
+                                              unsigned *__restrict__ ghist) {
   unsigned *hj = ghist + j * 256;
   unsigned c[4];
   unsigned s = 0;
 #pragma unroll
   for (int q = 0; q < 4; q++) {
-    c[q] = hj[lane * 4 + q];
+    // agent scope: the other workgroups' histogram atomics, not a stale line
+    c[q] = __hip_atomic_load(hj + lane * 4 + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s += c[q];
   }
   // inclusive prefix over lanes of the 4-bin sums
@@ -314,6 +290,56 @@ __global__ __launch_bounds__(64) void k_kth_pick(int shift, KthState *__restrict
   }
 #pragma unroll
   for (int q = 0; q < 4; q++) hj[lane * 4 + q] = 0;
+}
+
+// One pass of the select: a histogram of the digit at `shift` over the values
+// whose key prefix matches, then the last workgroup to finish its histogram (a
+// ticket after a release fence) picks the digits, wave j for rank j, and
+// resets the ticket (one launch per pass instead of histogram + pick)
+__global__ __launch_bounds__(256) void k_kth_pass(const double *__restrict__ v, int64_t n, int nk, int shift,
+                                                  KthState *__restrict__ st, unsigned *__restrict__ ghist,
+                                                  unsigned *__restrict__ ticket) {
+  __shared__ unsigned h[KTH_MAX][256];
+  __shared__ bool last;
+  for (int t = threadIdx.x; t < KTH_MAX * 256; t += 256) (&h[0][0])[t] = 0;
+  uint64_t pre[KTH_MAX];
+#pragma unroll
+  for (int j = 0; j < KTH_MAX; j++) pre[j] = j < nk ? st[j].prefix : 0;
+  __syncthreads();
+  const int hs = shift + 8;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const double d = v[i];
+    if (d != d) continue;
+    const uint64_t k = dkey(d);
+    const unsigned dig = (unsigned)(k >> shift) & 255u;
+#pragma unroll
+    for (int j = 0; j < KTH_MAX; j++)
+      if (j < nk && (hs >= 64 || ((k ^ pre[j]) >> hs) == 0)) atomicAdd(&h[j][dig], 1u);
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < nk * 256; t += 256) {
+    const unsigned c = (&h[0][0])[t];
+    if (c) atomicAdd(ghist + t, c);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;                                   // workgroup-uniform
+  __threadfence();
+  const int w = threadIdx.x >> 6;
+  if (w < nk) kth_pick_wave(w, threadIdx.x & 63, shift, st, ghist);
+  if (threadIdx.x == 0) *ticket = 0;
+}
+
+// gh: KTH_MAX * 256 zeroed counters followed by a zeroed ticket
+static void kth_passes(grid_ctx *ctx, const double *d_v, int64_t n, int nk, KthState *ks, unsigned *gh) {
+  const int blocks = (int)std::min<int64_t>(ceil_div(n, 256), 4 * ctx->ncu);
+  for (int shift = 56; shift >= 0; shift -= 8)
+    hipLaunchKernelGGL(k_kth_pass, dim3(blocks), dim3(256), 0, ctx->stream, d_v, n, nk, shift, ks, gh,
+                       gh + KTH_MAX * 256);
 }
 
 __global__ __launch_bounds__(256) void k_count_valid(const double *__restrict__ v, int64_t n,
@@ -350,7 +376,7 @@ int grid_select_kth(grid_ctx *ctx, const double *d_v, int64_t n, const int64_t *
   REQUIRE(ctx && h_ks && h_vals && n > 0 && d_v && nk >= 1 && nk <= KTH_MAX, "bad args (1 <= nk <= %d)", KTH_MAX);
   for (int j = 0; j < nk; j++) REQUIRE(h_ks[j] >= 0 && h_ks[j] < n, "k (%lld) out of range", (long long)h_ks[j]);
   void *s = nullptr;
-  const size_t hbytes = (size_t)KTH_MAX * 256 * 4;
+  const size_t hbytes = (size_t)KTH_MAX * 256 * 4 + 256;          // + the k_kth_pass ticket
   int rc = grid_scratch(ctx, 256 + hbytes, &s);
   if (rc) return rc;
   KthState *st = (KthState *)s;
@@ -360,11 +386,7 @@ int grid_select_kth(grid_ctx *ctx, const double *d_v, int64_t n, const int64_t *
   std::memcpy(ctx->pinned, hs, sizeof(KthState) * nk);
   HIPCHK(hipMemcpyAsync(st, ctx->pinned, sizeof(KthState) * nk, hipMemcpyHostToDevice, ctx->stream));
   HIPCHK(hipMemsetAsync(gh, 0, hbytes, ctx->stream));
-  const int blocks = (int)std::min<int64_t>(ceil_div(n, 256), 4 * ctx->ncu);
-  for (int shift = 56; shift >= 0; shift -= 8) {
-    hipLaunchKernelGGL(k_kth_hist, dim3(blocks), dim3(256), 0, ctx->stream, d_v, n, nk, shift, st, gh);
-    hipLaunchKernelGGL(k_kth_pick, dim3(nk), dim3(64), 0, ctx->stream, shift, st, gh);
-  }
+  kth_passes(ctx, d_v, n, nk, st, gh);
   LAUNCHCHK();
   HIPCHK(hipMemcpyAsync(ctx->pinned, st, sizeof(KthState) * nk, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -451,6 +473,207 @@ int grid_colmap_range(grid_ctx *ctx, const double *d_r, int64_t n, double smin, 
   HIPCHK(hipStreamSynchronize(ctx->stream));
   return GRID_OK;
 }
+
+// ---- pass C on the device: the chain's region selection (fused.py run()) as
+// two enqueue-only stages and one read-back, instead of six host round trips
+// (count, two order statistics, the selected count, the kept count).  Every
+// kernel reads its scalars (counts, ranks, threshold, sigma^2 range) from the
+// state slots d_st[GRID_SEL_*]; the values equal the host path's.
+__device__ __forceinline__ double st_f(const int64_t *st, int k) { return __longlong_as_double(st[k]); }
+__device__ __forceinline__ void st_setf(int64_t *st, int k, double v) { st[k] = __double_as_longlong(v); }
+__device__ __forceinline__ double kth_value(uint64_t k) {
+  const uint64_t u = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k;
+  return __longlong_as_double((long long)u);
+}
+
+// ranks of the median pair and the top fraction: sorted(...)[int(top_frac * n)]
+// with Python's index rules (normalize_mosdepth.py:462,495)
+__global__ void k_sel_ranks1(int64_t *st, double top_frac, KthState *ks) {
+  const int64_t nv = st[GRID_SEL_NVALID];
+  int64_t a = 0, b = 0, t = 0;
+  if (nv > 0) {
+    a = nv % 2 ? nv / 2 : nv / 2 - 1;
+    b = nv / 2;
+    const double x = top_frac * (double)nv;
+    t = (x == x && fabs(x) < 9.2e18) ? (int64_t)x : -1 - nv;     // int(): truncation toward zero
+    if (t < 0) t += nv;
+    if (t < 0 || t >= nv) {
+      st[GRID_SEL_ERR] = 1;                                        // IndexError: list index out of range
+      t = 0;
+    }
+  }
+  ks[0] = KthState{0ull, a};
+  ks[1] = KthState{0ull, b};
+  ks[2] = KthState{0ull, t};
+}
+
+__global__ void k_sel_fin1(int64_t *st, const KthState *ks) {
+  const int64_t nv = st[GRID_SEL_NVALID];
+  for (int j = 0; j < 3; j++) st_setf(st, GRID_SEL_V0 + j, nv > 0 ? kth_value(ks[j].prefix) : 0.0);
+  st_setf(st, GRID_SEL_THR, nv > 0 ? kth_value(ks[2].prefix) : __builtin_nan(""));   // NaN: nothing is >
+}
+
+__global__ void k_gt_flags_st(const double *v, int64_t n, const int64_t *st, uint8_t *f) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) f[i] = v[i] > st_f(st, GRID_SEL_THR) ? 1 : 0;
+}
+
+// r3[i] = float("%.3f" % ratio[sel[i]]) for i < r_loc, NaN up to len_pad (the
+// all-gather's padding); r_tot = r_loc (summed over ranks by the caller)
+__global__ void k_sel_r3(const double *ratio, const int32_t *sel, int64_t *st, int64_t len_pad, double *r3) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t rl = st[GRID_SEL_RLOC];
+  if (i == 0) st[GRID_SEL_RTOT] = rl;
+  if (i >= len_pad) return;
+  double out = __builtin_nan("");
+  if (i < rl) {
+    const double x = ratio[sel[i]];
+    out = x;
+    if (x == x && !isinf(x)) {
+      const double k = round_dec_k(x, 1000.0);
+      out = k / 1000.0;
+      if (k == 0.0 && signbit(x)) out = -0.0;
+    }
+  }
+  r3[i] = out;
+}
+
+// sorted(r3)[min(int(r_tot * (1 - frac_r)), nv - 1)] (find_neighbors.py:166-170)
+__global__ void k_sel_ranks2(int64_t *st, double frac_r, KthState *ks) {
+  const int64_t nv = st[GRID_SEL_NV];
+  int64_t k = 0;
+  if (nv > 0) {
+    const double x = (double)st[GRID_SEL_RTOT] * (1.0 - frac_r);
+    k = (x == x && fabs(x) < 9.2e18) ? (int64_t)x : nv - 1;
+    if (k > nv - 1) k = nv - 1;
+    if (k < 0) {
+      st[GRID_SEL_ERR] = 2;
+      k = 0;
+    }
+  }
+  ks[0] = KthState{0ull, k};
+}
+
+__global__ void k_sel_fin2(int64_t *st, const KthState *ks, double sigma2_max) {
+  const bool any = st[GRID_SEL_NV] > 0;
+  st_setf(st, GRID_SEL_SMIN, any ? kth_value(ks[0].prefix) : -__builtin_inf());
+  st_setf(st, GRID_SEL_SMAX, any ? sigma2_max : __builtin_inf());
+}
+
+__global__ void k_keep_flags_st(const double *r, int64_t n, const int64_t *st, int32_t *f) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double x = r[i], lo = st_f(st, GRID_SEL_SMIN), hi = st_f(st, GRID_SEL_SMAX);
+  f[i] = (i < st[GRID_SEL_RLOC] && x == x && !isinf(x) && x >= lo && x <= hi) ? 1 : 0;
+}
+
+// exclusive ranks -> column map (-1 = not kept); the last element's thread
+// records the kept count before overwriting its entry
+__global__ void k_colmap_fix_st(const int32_t *flags, int32_t *map, int64_t n, int64_t *st) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (i == n - 1) st[GRID_SEL_RUSE] = (int64_t)map[i] + flags[i];
+  if (!flags[i]) map[i] = -1;
+}
+
+
+extern "C" {
+
+int grid_sel_stage1(grid_ctx *ctx, const double *d_rall, int64_t rlen, const double *d_ratio, int64_t ml,
+                    int64_t len_pad, double top_frac, int32_t *d_sel, double *d_r3, int64_t *d_st) {
+  REQUIRE(ctx && d_st && rlen >= 0 && ml >= 0 && len_pad >= ml && (rlen == 0 || d_rall) &&
+          (ml == 0 || (d_ratio && d_sel)) && (len_pad == 0 || d_r3), "bad args");
+  REQUIRE(ml < (1ll << 31), "ml >= 2^31");
+  size_t cub = 0;
+  hipcub::CountingInputIterator<int32_t> it(0);
+  if (ml > 0)
+    HIPCHK(hipcub::DeviceSelect::Flagged(nullptr, cub, it, (uint8_t *)nullptr, d_sel, (int64_t *)nullptr, (int)ml,
+                                         ctx->stream));
+  const size_t hbytes = (size_t)KTH_MAX * 256 * 4 + 256;          // + the k_kth_pass ticket
+  const size_t off_h = 256, off_c = off_h + hbytes, off_f = off_c + ((cub + 255) & ~size_t(255));
+  void *s = nullptr;
+  int rc = grid_scratch(ctx, off_f + (size_t)ml + 256, &s);
+  if (rc) return rc;
+  char *base = (char *)s;
+  KthState *ks = (KthState *)base;
+  unsigned *gh = (unsigned *)(base + off_h);
+  HIPCHK(hipMemsetAsync(d_st, 0, GRID_SEL_STATE * 8, ctx->stream));
+  HIPCHK(hipMemsetAsync(gh, 0, hbytes, ctx->stream));
+  if (rlen > 0) {
+    const int blocks = (int)std::min<int64_t>(ceil_div(rlen, 256), 8 * ctx->ncu);
+    hipLaunchKernelGGL(k_count_valid, dim3(blocks), dim3(256), 0, ctx->stream, d_rall, rlen,
+                       (unsigned long long *)(d_st + GRID_SEL_NVALID));
+  }
+  hipLaunchKernelGGL(k_sel_ranks1, dim3(1), dim3(1), 0, ctx->stream, d_st, top_frac, ks);
+  if (rlen > 0) kth_passes(ctx, d_rall, rlen, 3, ks, gh);
+  hipLaunchKernelGGL(k_sel_fin1, dim3(1), dim3(1), 0, ctx->stream, d_st, ks);
+  if (ml > 0) {
+    uint8_t *flags = (uint8_t *)(base + off_f);
+    hipLaunchKernelGGL(k_gt_flags_st, dim3((unsigned)ceil_div(ml, 256)), dim3(256), 0, ctx->stream, d_ratio, ml, d_st,
+                       flags);
+    HIPCHK(hipcub::DeviceSelect::Flagged(base + off_c, cub, it, flags, d_sel, d_st + GRID_SEL_RLOC, (int)ml,
+                                         ctx->stream));
+  }
+  if (len_pad > 0)
+    hipLaunchKernelGGL(k_sel_r3, dim3((unsigned)ceil_div(len_pad, 256)), dim3(256), 0, ctx->stream, d_ratio, d_sel,
+                       d_st, len_pad, d_r3);
+  else
+    hipLaunchKernelGGL(k_sel_r3, dim3(1), dim3(1), 0, ctx->stream, d_ratio, d_sel, d_st, (int64_t)0, d_r3);
+  LAUNCHCHK();
+  return GRID_OK;
+}
+
+int grid_sel_stage2(grid_ctx *ctx, const double *d_r3all, int64_t r3len, const double *d_r3, int64_t ml,
+                    double frac_r, double sigma2_max, int32_t *d_colmap, int64_t *d_st) {
+  REQUIRE(ctx && d_st && r3len >= 0 && ml >= 0 && (r3len == 0 || d_r3all) && (ml == 0 || (d_r3 && d_colmap)),
+          "bad args");
+  REQUIRE(ml < (1ll << 31), "ml >= 2^31");
+  size_t cub = 0;
+  if (ml > 0)
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub, (int32_t *)nullptr, d_colmap, (int)ml, ctx->stream));
+  const size_t hbytes = (size_t)KTH_MAX * 256 * 4 + 256;          // + the k_kth_pass ticket
+  const size_t off_h = 256, off_c = off_h + hbytes, off_f = off_c + ((cub + 255) & ~size_t(255));
+  void *s = nullptr;
+  int rc = grid_scratch(ctx, off_f + (size_t)ml * 4 + 256, &s);
+  if (rc) return rc;
+  char *base = (char *)s;
+  KthState *ks = (KthState *)base;
+  unsigned *gh = (unsigned *)(base + off_h);
+  HIPCHK(hipMemsetAsync(gh, 0, hbytes, ctx->stream));
+  if (r3len > 0) {
+    const int blocks = (int)std::min<int64_t>(ceil_div(r3len, 256), 8 * ctx->ncu);
+    hipLaunchKernelGGL(k_count_valid, dim3(blocks), dim3(256), 0, ctx->stream, d_r3all, r3len,
+                       (unsigned long long *)(d_st + GRID_SEL_NV));
+  }
+  hipLaunchKernelGGL(k_sel_ranks2, dim3(1), dim3(1), 0, ctx->stream, d_st, frac_r, ks);
+  if (r3len > 0) kth_passes(ctx, d_r3all, r3len, 1, ks, gh);
+  hipLaunchKernelGGL(k_sel_fin2, dim3(1), dim3(1), 0, ctx->stream, d_st, ks, sigma2_max);
+  if (ml > 0) {
+    int32_t *flags = (int32_t *)(base + off_f);
+    const unsigned g = (unsigned)ceil_div(ml, 256);
+    hipLaunchKernelGGL(k_keep_flags_st, dim3(g), dim3(256), 0, ctx->stream, d_r3, ml, d_st, flags);
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(base + off_c, cub, flags, d_colmap, (int)ml, ctx->stream));
+    hipLaunchKernelGGL(k_colmap_fix_st, dim3(g), dim3(256), 0, ctx->stream, flags, d_colmap, ml, d_st);
+  }
+  LAUNCHCHK();
+  return GRID_OK;
+}
+
+int grid_status_copy(grid_ctx *ctx, void *d_dst) {
+  REQUIRE(ctx && d_dst && ctx->scratch, "bad args (no status block yet)");
+  HIPCHK(hipMemcpyAsync(d_dst, ctx->scratch, 16, hipMemcpyDeviceToDevice, ctx->stream));
+  return GRID_OK;
+}
+
+int grid_sel_read(grid_ctx *ctx, const int64_t *d_st, int64_t *h_st) {
+  REQUIRE(ctx && d_st && h_st, "bad args");
+  HIPCHK(hipMemcpyAsync(ctx->pinned, d_st, GRID_SEL_STATE * 8, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  std::memcpy(h_st, ctx->pinned, GRID_SEL_STATE * 8);
+  return GRID_OK;
+}
+
+}  // extern "C"
 
 // ------------------------------------------------------ host formatting ----
 int grid_format_hundredths(const int32_t *v, int64_t n, char *out, int64_t cap, int64_t *len) {

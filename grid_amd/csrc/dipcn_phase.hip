@@ -791,14 +791,15 @@ int grid_dipcn(grid_ctx *ctx, int64_t n, const double *d_reads, const uint8_t *d
                const int32_t *d_nbr, const double *d_nscale, const int32_t *d_ncnt, int64_t ld, int64_t n_nbr,
                double *d_out, uint8_t *d_valid, int32_t *h_zerodiv) {
   REQUIRE(ctx && n >= 0 && ld >= 0, "bad args");
-  if (n == 0) {
-    if (h_zerodiv) *h_zerodiv = 0;
-    return GRID_OK;
-  }
   void *s = nullptr;
   int rc = grid_scratch(ctx, 256, &s);
   if (rc) return rc;
   int32_t *d_zd = (int32_t *)s;
+  if (n == 0) {
+    if (h_zerodiv) *h_zerodiv = 0;
+    else HIPCHK(hipMemsetAsync(d_zd, 0, 16, ctx->stream));     // for a deferred grid_status_copy
+    return GRID_OK;
+  }
   HIPCHK(hipMemsetAsync(d_zd, 0, 4, ctx->stream));
   hipLaunchKernelGGL(k_dipcn, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, ctx->stream, n, d_reads, d_has,
                      d_scale, d_nbr, d_nscale, d_ncnt, ld, n_nbr, d_out, d_valid, d_zd);

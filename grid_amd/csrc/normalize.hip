@@ -10,7 +10,10 @@
 // Every arithmetic op is an IEEE fp64 +,-,*,/,sqrt with -ffp-contract=off.
 #include "common.hpp"
 
+#include <algorithm>
+#include <functional>
 #include <type_traits>
+#include <vector>
 
 namespace {
 
@@ -284,6 +287,83 @@ __global__ __launch_bounds__(64) void k_row_block_tail_w(const int32_t *__restri
   if (lane == 0) {
     int k = 0;
     bsum[row * nblk + b] = pairwise_tree(len, [&](int, int) { return s_val[k++]; });
+    bcnt[row * nblk + b] = c;
+  }
+}
+
+
+// The partial last block with its pairwise tree planned on the host (the tail
+// length is the same for every row, so is numpy's recursion): leaves in
+// left-to-right order, internal nodes grouped by height, each the sum of two
+// earlier values.  One wave per row stages the tail in LDS with 16-B loads,
+// sums one leaf per lane (pairwise_leaf's order) and evaluates the tree a
+// height at a time.  k_row_block_tail_w walked the recursion on lane 0 with
+// its stack in scratch: 537 us at 375,000 bins (6,360-element tails).
+constexpr int TP_MAXL = 128, TP_MAXH = 10;
+struct TailPlan {
+  int32_t nleaf, nnode, nh;
+  int16_t lo[TP_MAXL], len[TP_MAXL];        // leaf l covers [lo, lo + len) of the tail
+  uint8_t a[TP_MAXL], b[TP_MAXL];           // node k (value nleaf + k) = v[a[k]] + v[b[k]]
+  uint8_t hend[TP_MAXH];                    // nodes of height h: [hend[h-1], hend[h])
+};
+
+template <bool S16>
+__global__ __launch_bounds__(64) void k_row_block_tail_p(const int32_t *__restrict__ q, Q16 s16, int64_t ld,
+                                                          int64_t m, int64_t nblk, const TailPlan p,
+                                                          double *__restrict__ bsum, int32_t *__restrict__ bcnt) {
+  typedef std::conditional_t<S16, uint16_t, int32_t> T;
+  __shared__ __attribute__((aligned(16))) T s_q[BLK];
+  __shared__ double s_v[2 * TP_MAXL];
+  const int64_t row = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int64_t b = nblk - 1, c0 = b * BLK;
+  const int len = (int)(m - c0);
+  int c = 0;
+  if constexpr (S16) {
+    // row * ld + c0 is a multiple of 8 codes (ld % 8 == 0, c0 % 8192 == 0): 16-B aligned
+    typedef unsigned v4u __attribute__((ext_vector_type(4)));
+    const uint16_t *src = s16.q + row * ld + c0;
+    const int n8 = len >> 3;
+    for (int i = lane; i < n8; i += 64) {
+      const v4u u = reinterpret_cast<const v4u *>(src)[i];
+      *reinterpret_cast<v4u *>(&s_q[8 * i]) = u;
+#pragma unroll
+      for (int k = 0; k < 8; k++) c += ((u[k >> 1] >> (16 * (k & 1))) & 0xFFFFu) != GRID_Q16_MISS;
+    }
+    for (int i = 8 * n8 + lane; i < len; i += 64) {
+      s_q[i] = src[i];
+      c += src[i] != GRID_Q16_MISS;
+    }
+  } else {
+    const int32_t *src = q + row * ld + c0;
+    for (int i = lane; i < len; i += 64) {
+      const int32_t v = src[i];
+      s_q[i] = v;
+      c += v != GRID_MISSING;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
+  __syncthreads();
+  auto val = [&](int e) -> double {
+    if constexpr (S16) {
+      const uint32_t v = s_q[e];
+      if (__builtin_expect(v <= GRID_Q16_MAXV, 1)) return div100_exact((int32_t)v);
+      return v == GRID_Q16_MISS ? 0.0 : qval(q16_lookup(row, c0 + e, s16));
+    } else {
+      return qval(s_q[e]);
+    }
+  };
+  for (int l = lane; l < p.nleaf; l += 64) s_v[l] = pairwise_leaf_v(val, p.lo[l], p.len[l]);
+  __syncthreads();
+  int k0 = 0;
+  for (int h = 0; h < p.nh; h++) {
+    const int k1 = p.hend[h];
+    for (int k = k0 + lane; k < k1; k += 64) s_v[p.nleaf + k] = s_v[p.a[k]] + s_v[p.b[k]];
+    __syncthreads();
+    k0 = k1;
+  }
+  if (lane == 0) {
+    bsum[row * nblk + b] = s_v[p.nleaf + p.nnode - 1];
     bcnt[row * nblk + b] = c;
   }
 }
@@ -1703,6 +1783,59 @@ static bool q16_ok(const grid_depth16 *q, int64_t ld) {
 }
 static Q16 to_q16(const grid_depth16 *q) { return Q16{q->q, q->eoff, q->ecol, q->eval}; }
 
+// numpy's pairwise recursion over [0, len) (pairwise_sum: n <= 128 is a leaf,
+// else halves at n2 = n / 2 rounded down to a multiple of 8) as a TailPlan:
+// leaves numbered left to right, internal nodes ordered by height so one
+// height's nodes are independent.  A tail of <= 128 elements is one leaf and
+// no node (the kernel reads the root as v[nleaf + nnode - 1] = v[0]).
+static bool tail_plan(int len, TailPlan &p) {
+  struct Node { int a, b, h; };                 // children: >= 0 leaf, < 0 node ~idx
+  std::vector<Node> nodes;
+  p.nleaf = 0;
+  bool ok = true;
+  std::function<int(int, int, int &)> rec = [&](int lo, int n, int &h) -> int {
+    if (n <= LEAF) {
+      if (p.nleaf >= TP_MAXL) { ok = false; return 0; }
+      p.lo[p.nleaf] = (int16_t)lo;
+      p.len[p.nleaf] = (int16_t)n;
+      h = 0;
+      return p.nleaf++;
+    }
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    int hl = 0, hr = 0;
+    const int l = rec(lo, n2, hl), r = rec(lo + n2, n - n2, hr);
+    h = std::max(hl, hr) + 1;
+    nodes.push_back({l, r, h});
+    return ~(int)(nodes.size() - 1);
+  };
+  int h = 0;
+  const int root = rec(0, len, h);
+  if (!ok) return false;
+  if (root >= 0) {                              // one leaf, no node
+    p.nnode = 0;
+    p.nh = 0;
+    return p.nleaf == 1;
+  }
+  if (h > TP_MAXH || nodes.size() > (size_t)TP_MAXL) return false;
+  // order by height (stable), then map children to value indices
+  std::vector<int> order(nodes.size()), pos(nodes.size());
+  for (size_t i = 0; i < nodes.size(); i++) order[i] = (int)i;
+  std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return nodes[x].h < nodes[y].h; });
+  for (size_t k = 0; k < order.size(); k++) pos[order[k]] = (int)k;
+  auto vidx = [&](int c) { return c >= 0 ? c : p.nleaf + pos[~c]; };
+  p.nnode = (int)nodes.size();
+  p.nh = h;
+  for (size_t k = 0; k < order.size(); k++) {
+    const Node &nd = nodes[order[k]];
+    p.a[k] = (uint8_t)vidx(nd.a);
+    p.b[k] = (uint8_t)vidx(nd.b);
+    p.hend[nd.h - 1] = (uint8_t)(k + 1);
+  }
+  // the root (greatest height, the only one) must come last
+  return pos[~root] == p.nnode - 1 && p.nleaf + p.nnode <= 2 * TP_MAXL;
+}
+
 // Row blocks from an int32 (d_q) or compact (s16.q) matrix.
 static int row_blocks_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, int64_t n, int64_t m, int64_t ld,
                            double *d_bsum, int32_t *d_bcnt) {
@@ -1732,8 +1865,10 @@ static int row_blocks_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, in
   }
   if (nblk > nfull) {
     REQUIRE(n <= 2147483647, "n too large for one launch");
-    auto kern = c16 ? k_row_block_tail_w<true> : k_row_block_tail_w<false>;
-    hipLaunchKernelGGL(kern, dim3((unsigned)n), dim3(64), 0, ctx->stream, d_q, s16, ld, m, nblk, d_bsum, d_bcnt);
+    TailPlan p;
+    REQUIRE(tail_plan((int)(m - nfull * BLK), p), "tail plan out of range (len %lld)", (long long)(m - nfull * BLK));
+    auto kern = c16 ? k_row_block_tail_p<true> : k_row_block_tail_p<false>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)n), dim3(64), 0, ctx->stream, d_q, s16, ld, m, nblk, p, d_bsum, d_bcnt);
     LAUNCHCHK();
   }
   return GRID_OK;
@@ -1975,6 +2110,13 @@ static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, int64_
   REQUIRE(qmax >= 0 && qmax <= 256, "qmax %d outside the exact-bf16 range [0, 256]", qmax);
   if (n == 0 || r == 0) {
     if (h_overflow) *h_overflow = 0;
+    if (h_nesc) *h_nesc = 0;
+    if (!h_overflow) {          // the deferred read (grid_status_copy) finds a clean block
+      void *s = nullptr;
+      int rc = grid_scratch(ctx, 256, &s);
+      if (rc) return rc;
+      HIPCHK(hipMemsetAsync(s, 0, 16, ctx->stream));
+    }
     return GRID_OK;
   }
   REQUIRE(ceil_div(n, ZR * ZRB) <= 65535, "n too large for one launch");
@@ -2113,7 +2255,7 @@ int grid_norm_zquant_kb16(grid_ctx *ctx, const int32_t *d_q, int64_t n, int64_t 
                           int64_t np_zb, int64_t *d_esc_idx, int32_t *d_esc_val, int64_t esc_cap,
                           int64_t *h_nesc, int32_t *h_overflow) {
   REQUIRE(np_zb >= n && np_zb % 64 == 0, "np_zb must be >= n and a multiple of 64");
-  REQUIRE(d_zq16 && h_overflow && h_nesc && esc_cap >= 0 && (esc_cap == 0 || (d_esc_idx && d_esc_val)),
+  REQUIRE(d_zq16 && (h_overflow == nullptr) == (h_nesc == nullptr) && esc_cap >= 0 && (esc_cap == 0 || (d_esc_idx && d_esc_val)),
           "grid_norm_zquant_kb16: bad escape list / outputs");
   return zquant_impl(ctx, d_q, kNoQ16, n, ld, d_sel, r, d_rm, d_mu, scale, nullptr, ld_zq, d_colmap, qmax, d_zb, KBW,
                      np_zb * KBW, h_overflow, d_zq16, d_esc_idx, d_esc_val, esc_cap, h_nesc);
@@ -2126,7 +2268,7 @@ int grid_norm_zquant_kb16_q16(grid_ctx *ctx, const grid_depth16 *q, int64_t n, i
                               int64_t *h_nesc, int32_t *h_overflow) {
   REQUIRE(q16_ok(q, ld), "compact matrix: 16-byte aligned q, ld %% 8 == 0 and escape offsets required");
   REQUIRE(np_zb >= n && np_zb % 64 == 0, "np_zb must be >= n and a multiple of 64");
-  REQUIRE(d_zq16 && h_overflow && h_nesc && esc_cap >= 0 && (esc_cap == 0 || (d_esc_idx && d_esc_val)),
+  REQUIRE(d_zq16 && (h_overflow == nullptr) == (h_nesc == nullptr) && esc_cap >= 0 && (esc_cap == 0 || (d_esc_idx && d_esc_val)),
           "grid_norm_zquant_kb16_q16: bad escape list / outputs");
   return zquant_impl(ctx, nullptr, to_q16(q), n, ld, d_sel, r, d_rm, d_mu, scale, nullptr, ld_zq, d_colmap, qmax, d_zb,
                      KBW, np_zb * KBW, h_overflow, d_zq16, d_esc_idx, d_esc_val, esc_cap, h_nesc);

@@ -217,6 +217,19 @@ class HipOps:
         call("grid_colmap_range", self.ctx, ptr(r), n, smin, smax, ptr(colmap), C.byref(c))
         return c.value
 
+    # pass C on the device (include/grid_abi.h grid_sel_*): enqueue only, one read-back
+    def sel_stage1(self, rall, rlen, ratio, ml, len_pad, top_frac, sel, r3, st):
+        call("grid_sel_stage1", self.ctx, ptr(rall), rlen, ptr(ratio), ml, len_pad, top_frac, ptr(sel), ptr(r3),
+             ptr(st))
+
+    def sel_stage2(self, r3all, r3len, r3, ml, frac_r, sigma2_max, colmap, st):
+        call("grid_sel_stage2", self.ctx, ptr(r3all), r3len, ptr(r3), ml, frac_r, sigma2_max, ptr(colmap), ptr(st))
+
+    def sel_read(self, st):
+        h = np.zeros(_abi.SEL_STATE, np.int64)
+        call("grid_sel_read", self.ctx, ptr(st), h.ctypes.data)
+        return h
+
     def zquant(self, q, n, ld, sel, r, rm, mu, scale, zq, ld_zq, colmap, qmax, zb, np_zb):
         """z hundredths + the K-blocked bf16 panel [kpad/32][np_zb][32]."""
         of = C.c_int32()
@@ -228,20 +241,26 @@ class HipOps:
                  ld_zq, ptr(colmap), qmax, ptr(zb), np_zb, C.byref(of))
         return of.value
 
-    def zquant16(self, q, n, ld, sel, r, rm, mu, scale, zq16, ld_zq, colmap, qmax, zb, np_zb, esc_idx, esc_val):
+    def zquant16(self, q, n, ld, sel, r, rm, mu, scale, zq16, ld_zq, colmap, qmax, zb, np_zb, esc_idx, esc_val,
+                 defer=None):
         """As zquant with the step-4 output as int16 codes plus an escape list
         for the rare values outside them.  Returns (overflow bits, escapes);
-        bit 1 = the list overflowed (the caller reruns with int32)."""
+        bit 1 = the list overflowed (the caller reruns with int32).  defer: a
+        2-slot int64 device tensor that receives (overflow bits, escapes) on the
+        stream instead (no synchronisation; returns None)."""
         of, ne = C.c_int32(), C.c_int64()
+        h_ne, h_of = (None, None) if defer is not None else (C.byref(ne), C.byref(of))
         cap = 0 if esc_idx is None else esc_idx.numel()
         if isinstance(q, Depth16):
             call("grid_norm_zquant_kb16_q16", self.ctx, C.byref(q.desc), n, q.ld, ptr(sel), r, ptr(rm), ptr(mu),
                  scale, ptr(zq16), ld_zq, ptr(colmap), qmax, ptr(zb), np_zb, ptr(esc_idx), ptr(esc_val), cap,
-                 C.byref(ne), C.byref(of))
+                 h_ne, h_of)
         else:
             call("grid_norm_zquant_kb16", self.ctx, ptr(q), n, ld, ptr(sel), r, ptr(rm), ptr(mu), scale, ptr(zq16),
-                 ld_zq, ptr(colmap), qmax, ptr(zb), np_zb, ptr(esc_idx), ptr(esc_val), cap, C.byref(ne),
-                 C.byref(of))
+                 ld_zq, ptr(colmap), qmax, ptr(zb), np_zb, ptr(esc_idx), ptr(esc_val), cap, h_ne, h_of)
+        if defer is not None:
+            call("grid_status_copy", self.ctx, ptr(defer))
+            return None
         return of.value, ne.value
 
     def gram(self, zb, np_, kpad, qmax, gram):
@@ -268,9 +287,14 @@ class HipOps:
     def synth(self, seed, n, m, ld, col0, ncl, out):
         call("grid_synth_depth", self.ctx, seed, n, m, ld, col0, ncl, ptr(out))
 
-    def dipcn(self, n, reads, has, scale, nbr, nscale, ncnt, ld, n_nbr, out, valid):
+    def dipcn(self, n, reads, has, scale, nbr, nscale, ncnt, ld, n_nbr, out, valid, defer=None):
+        """Returns the zero-division flag; with ``defer`` (a 2-slot int64 device
+        tensor) the flag goes there on the stream instead (returns None)."""
         call("grid_dipcn", self.ctx, n, ptr(reads), ptr(has), ptr(scale), ptr(nbr), ptr(nscale), ptr(ncnt), ld,
-             n_nbr, ptr(out), ptr(valid), C.byref(self.zerodiv))
+             n_nbr, ptr(out), ptr(valid), None if defer is not None else C.byref(self.zerodiv))
+        if defer is not None:
+            call("grid_status_copy", self.ctx, ptr(defer))
+            return None
         return self.zerodiv.value
 
     def phase(self, n, irr, off, nbr, w, min_nbr, iters, sched, hap, imp, mean):
@@ -389,6 +413,11 @@ class Steps47:
         self.sel = a.empty(ml1, I4)
         self.r3 = a.empty(max(self.mlmax, 1), F8)
         self.colmap = a.empty(ml1, I4)
+        self.sel_st = a.empty(_abi.SEL_STATE, I8)             # pass C's device scalars (grid_sel_*)
+        # status blocks read once at the end of a pass (grid_status_copy): slots
+        # 0-1 the step-4 output's (overflow bits, escapes), 2-3 dipCN's zero division
+        self.dstat = a.empty(4, I8)
+        self._zdef = self._ddef = None
         # step-4 output, exact hundredths: int16 codes (GRID_ZQ16_*, half the
         # HBM writes) when the ops support them, int32 otherwise or when a
         # pass has |z| > 327.66 (zq_int32() gives the int32 form either way)
@@ -590,34 +619,36 @@ class Steps47:
             o.col_means(qc, n, b - a, ldc, self.rm, self.mu[a:b])
             o.col_vars(qc, n, b - a, ldc, self.rm, self.mu[a:b], self.var[a:b], self.ratio[a:b])
         self._mark("col_stats")
-        # ---- pass C: median -> scale; sorted(...)[int(top_frac*n)] -> selection ----
+        # ---- pass C: median -> scale; sorted(...)[int(top_frac*n)] -> selection;
+        # step 5's region filter on the "%.3f" ratios (find_neighbors.py:148-171)
+        # and the panel column map -- on the device (grid_sel_stage1/2), with
+        # one read-back of the scalars the later grids need ----
         rall, rlen = self._gather_padded(self.ratio, ml, self.mlmax, float("nan"))
-        # order statistics of the valid ratios (radix select; no sort)
-        nvalid = o.count_valid(rall, rlen)
-        scale, r_loc = 1.0, 0
+        st = self.sel_st
+        pad = self.mlmax if self.comm is not None else ml
+        o.sel_stage1(rall, rlen, self.ratio, ml, pad, self.top_frac, self.sel, self.r3, st)
+        if self.comm is not None:
+            r3all = self.comm.all_gather(self.r3.view(-1)[: self.mlmax]).view(-1)
+            r3len = self.world * self.mlmax
+            self.comm.all_reduce_sum(st[_abi.SEL_RTOT:_abi.SEL_RTOT + 1])
+        else:
+            r3all, r3len = self.r3, ml
+        o.sel_stage2(r3all, r3len, self.r3, ml, self.frac_r, float(self.sigma2_max), self.colmap, st)
+        h = o.sel_read(st)
+        if h[_abi.SEL_ERR] == 1:
+            raise IndexError("list index out of range")
+        if h[_abi.SEL_ERR]:
+            raise _abi.GridNativeError("sigma^2 rank out of range (frac_r > 1)")
+        f = h.view(np.float64)
+        nvalid, r_loc = int(h[_abi.SEL_NVALID]), int(h[_abi.SEL_RLOC])
+        scale = 1.0
         if nvalid:
-            ks = [nvalid // 2] if nvalid % 2 else [nvalid // 2 - 1, nvalid // 2]
-            ks.append(py_index(nvalid, int(self.top_frac * nvalid)))
-            vals = o.select_kth(rall, rlen, ks)
-            med = vals[0] if nvalid % 2 else (vals[0] + vals[1]) / 2.0
+            med = float(f[_abi.SEL_V0]) if nvalid % 2 else (float(f[_abi.SEL_V0]) + float(f[_abi.SEL_V0 + 1])) / 2.0
             if med > 0:
                 scale = 1.0 / math.sqrt(med / 100.0)
-            thr = vals[-1]
-            r_loc = o.select_gt(self.ratio, ml, thr, self.sel)
         self.scale, self.r_loc = scale, r_loc
-        # ---- step 5 region filter on the "%.3f" ratios (find_neighbors.py:148-171) ----
-        o.gather(self.ratio, self.sel, r_loc, self.r3)
-        o.round_decimals(self.r3, r_loc, 3, self.r3)
-        r3all, r3len = self._gather_padded(self.r3, r_loc, self.mlmax, float("nan"))
-        r_tot = r_loc if self.comm is None else self._sum_int(r_loc)
-        self.r_tot = r_tot
-        nv = o.count_valid(r3all, r3len)
-        if nv:
-            smin = o.select_kth(r3all, r3len, [min(int(r_tot * (1.0 - self.frac_r)), nv - 1)])[0]
-            smax = float(self.sigma2_max)
-        else:
-            smin, smax = -math.inf, math.inf
-        self.ruse_loc = o.colmap_range(self.r3, r_loc, smin, smax, self.colmap)
+        self.r_tot = int(h[_abi.SEL_RTOT])
+        self.ruse_loc = int(h[_abi.SEL_RUSE])
         sb, kb = self._chunk_bounds(r_loc)
         self._mark("select_sort")
         # ---- pass D: z (step-4 output) + clipped bf16 panel per chunk, the
@@ -685,8 +716,12 @@ class Steps47:
             self._ev_free[b] = None
         o.round_decimals(self.rm, n, 2, self.scale2)
         o.gather(self.scale2, idx, n * max(self.k, 1), self.nscale)
-        if o.dipcn(n, self.reads, self.has, self.scale2, idx, self.nscale, cnt, max(self.k, 1), self.n_nbr,
-                   self._dips[b], self.valid):
+        if hasattr(o, "sel_read"):
+            o.dipcn(n, self.reads, self.has, self.scale2, idx, self.nscale, cnt, max(self.k, 1), self.n_nbr,
+                    self._dips[b], self.valid, defer=self.dstat[2:4])
+            self._ddef = True
+        elif o.dipcn(n, self.reads, self.has, self.scale2, idx, self.nscale, cnt, max(self.k, 1), self.n_nbr,
+                     self._dips[b], self.valid):
             raise ZeroDivisionError("float division by zero")
         self._cur = b
         self._mark("dipcn")
@@ -698,6 +733,30 @@ class Steps47:
                     self.hap, self.imp, self.mean)
         self._mark("phase")
         self.idx_out, self.cnt_out = idx, cnt
+        self._check_deferred()
+
+    def _check_deferred(self):
+        """The statuses of this pass's zquant and dipCN, read once everything is
+        queued (the host waits for dipCN; the phasing may still run): |z| out
+        of range raises, an overflowed int16 escape list reruns the step-4
+        output as int32 (the panel and the Gram are already right), a zero
+        division raises as the reference does."""
+        zdef, ddef = self._zdef, self._ddef
+        self._zdef = self._ddef = None
+        if zdef is None and ddef is None:
+            return
+        h = self.dstat.cpu().numpy()
+        if zdef is not None:
+            of, ne = int(h[0]) & 0xFFFFFFFF, int(h[1])
+            if of & 1:
+                raise _abi.GridNativeError("z-score outside the int32 hundredths range")
+            if of & 2:
+                q, qc, ldc, a, b, s0, s1, sel_c, cm_c = zdef
+                self._zquant32(q, qc, ldc, a, b, s0, s1, sel_c, cm_c)
+            else:
+                self.nesc = ne
+        if ddef is not None and int(h[2]) & 0xFFFFFFFF:
+            raise ZeroDivisionError("float division by zero")
 
     def _step5_segments(self):
         """Sharded step 5: reduce-scatter the upper-triangle segments (each
@@ -801,6 +860,14 @@ class Steps47:
             e0 = self.nesc if self.keep_z else 0
             cap = self.esc_idx.numel() - e0
             zt = self.zq16.view(-1)[zcol:]
+            if self.nch == 1 and self.on_z_chunk is None and hasattr(o, "sel_read"):
+                # one chunk, nobody consumes the codes before the pass ends: the
+                # status is read at the end of the pass (_check_deferred), so the
+                # Gram and the rest of the pass queue behind zquant without a sync
+                o.zquant16(qc, n, ldc, sel_c, rc, self.rm, mu_c, self.scale, zt, ld_zq, cm_c, self.qmax, self.zb,
+                           self.np_, self.esc_idx[e0:], self.esc_val[e0:], defer=self.dstat[0:2])
+                self._zdef = (q, qc, ldc, a, b, s0, s1, sel_c, cm_c)
+                return
             of, ne = o.zquant16(qc, n, ldc, sel_c, rc, self.rm, mu_c, self.scale, zt, ld_zq, cm_c, self.qmax, self.zb,
                                 self.np_, self.esc_idx[e0:], self.esc_val[e0:])
             if of & 1:
@@ -814,6 +881,12 @@ class Steps47:
                 return
             if self.nch > 1:
                 raise _abi.GridNativeError(f"more than {cap} int16 escapes (|z| > 327.65) in chunk [{s0}, {s1})")
+        self._zquant32(q, qc, ldc, a, b, s0, s1, sel_c, cm_c)
+
+    def _zquant32(self, q, qc, ldc, a, b, s0, s1, sel_c, cm_c):
+        o, n, rc = self.ops, self.n, s1 - s0
+        mu_c = self.mu[a:b]
+        zcol, ld_zq = (s0, max(self.ml, 1)) if self.keep_z else (0, rc)
         self.zq_is16 = False            # int32 output: no int16 codes (unaligned input, or too many escapes)
         if self.zq is None:
             self.zq = self.A.empty(tuple(self.zq16.shape), I4)

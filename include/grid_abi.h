@@ -167,6 +167,41 @@ int grid_gather_f64(grid_ctx *ctx, const double *d_v, const int32_t *d_idx, int6
  * (or -1); *h_ruse = number kept.  keep = finite(r) && r>=smin && r<=smax. */
 int grid_colmap_range(grid_ctx *ctx, const double *d_r, int64_t n, double smin, double smax,
                       int32_t *d_colmap, int64_t *h_ruse);
+/* Region selection on the device (the chain's pass C without host round
+ * trips).  State d_st: GRID_SEL_STATE int64 slots (doubles stored as bits).
+ * Stage 1: nvalid = count of non-NaN d_rall[:rlen]; v0, v1 = the median pair's
+ * order statistics and v2 = thr = sorted(...)[int(top_frac * nvalid)]
+ * (normalize_mosdepth.py:462,495; err = 1 for Python's IndexError);
+ * d_sel = {j < ml : d_ratio[j] > thr} (r_loc of them, :499); d_r3[i] =
+ * float("%.3f" % d_ratio[d_sel[i]]) for i < r_loc and NaN up to len_pad;
+ * r_tot = r_loc (the caller sums it over ranks before stage 2).
+ * Stage 2: nv = count of non-NaN d_r3all[:r3len]; smin = sorted(r3all)
+ * [min(int(r_tot * (1 - frac_r)), nv - 1)], smax = sigma2_max (both +-inf when
+ * nv == 0; find_neighbors.py:166-171); d_colmap as grid_colmap_range over
+ * d_r3[:r_loc] (entries up to ml: -1), ruse = kept count.
+ * grid_sel_read: copy the slots to h_st (synchronises the stream). */
+#define GRID_SEL_STATE 16
+#define GRID_SEL_NVALID 0
+#define GRID_SEL_RLOC 1
+#define GRID_SEL_RTOT 2
+#define GRID_SEL_NV 3
+#define GRID_SEL_RUSE 4
+#define GRID_SEL_ERR 5
+#define GRID_SEL_THR 8
+#define GRID_SEL_V0 9
+#define GRID_SEL_SMIN 12
+#define GRID_SEL_SMAX 13
+int grid_sel_stage1(grid_ctx *ctx, const double *d_rall, int64_t rlen, const double *d_ratio, int64_t ml,
+                    int64_t len_pad, double top_frac, int32_t *d_sel, double *d_r3, int64_t *d_st);
+int grid_sel_stage2(grid_ctx *ctx, const double *d_r3all, int64_t r3len, const double *d_r3, int64_t ml,
+                    double frac_r, double sigma2_max, int32_t *d_colmap, int64_t *d_st);
+int grid_sel_read(grid_ctx *ctx, const int64_t *d_st, int64_t *h_st);
+/* Deferred status: called with h_overflow = h_nesc = NULL (grid_norm_zquant_kb16*)
+ * or h_zerodiv = NULL (grid_dipcn), those calls do not synchronise; this copies
+ * the 16-byte status block the call just left (int32 flags at byte 0, uint64
+ * escape count at byte 8) to d_dst on the stream, to be read later.  Call it
+ * before any other entry point runs on the context. */
+int grid_status_copy(grid_ctx *ctx, void *d_dst);
 /* z_{i,s} = ((q/100/rm_i - mu_j)/sqrt(mu_j))*scale for j = sel[s]
  * (normalize_mosdepth.py:458,470), quantised exactly as "%.2f" into
  * d_zq[i*ld_zq + s] (GRID_ZQ_NAN / GRID_ZQ_NEG0 sentinels; may be NULL), and,

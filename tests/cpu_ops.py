@@ -113,6 +113,57 @@ class NumpyOps:
         _np(colmap)[:n] = np.where(keep, cm, -1)
         return int(keep.sum())
 
+    # grid_sel_stage1 / _stage2 / _read: the device-resident pass C on a state
+    # tensor of GRID_SEL_STATE int64 slots (doubles as bits)
+    @staticmethod
+    def _setf(st, k, x):
+        _np(st)[k] = np.array([x], np.float64).view(np.int64)[0]
+
+    def sel_stage1(self, rall, rlen, ratio, ml, len_pad, top_frac, sel, r3, st):
+        a = _np(st)
+        a[:] = 0
+        nvalid = self.count_valid(rall, rlen) if rlen else 0
+        a[0] = nvalid
+        if nvalid:
+            ks = [nvalid // 2, nvalid // 2] if nvalid % 2 else [nvalid // 2 - 1, nvalid // 2]
+            t = int(top_frac * nvalid)
+            t = t + nvalid if t < 0 else t
+            if not 0 <= t < nvalid:
+                a[5], t = 1, 0
+            vals = self.select_kth(rall, rlen, ks + [t])
+            for j in range(3):
+                self._setf(st, 9 + j, vals[j])
+            self._setf(st, 8, vals[2])
+        else:
+            self._setf(st, 8, float("nan"))
+        r_loc = self.select_gt(ratio, ml, float(np.array([a[8]]).view(np.float64)[0]), sel) if ml else 0
+        a[1] = a[2] = r_loc
+        if len_pad:
+            self.gather(ratio, sel, r_loc, r3)
+            self.round_decimals(r3, r_loc, 3, r3)
+            _np(r3).reshape(-1)[r_loc:len_pad] = np.nan
+
+    def sel_stage2(self, r3all, r3len, r3, ml, frac_r, sigma2_max, colmap, st):
+        a = _np(st)
+        nv = self.count_valid(r3all, r3len) if r3len else 0
+        a[3] = nv
+        if nv:
+            k = min(int(int(a[2]) * (1.0 - frac_r)), nv - 1)
+            if k < 0:
+                a[5], k = 2, 0
+            smin, smax = self.select_kth(r3all, r3len, [k])[0], float(sigma2_max)
+        else:
+            smin, smax = -math.inf, math.inf
+        self._setf(st, 12, smin)
+        self._setf(st, 13, smax)
+        r_loc = int(a[1])
+        ruse = self.colmap_range(r3, r_loc, smin, smax, colmap) if r_loc else 0
+        _np(colmap).reshape(-1)[r_loc:ml] = -1
+        a[4] = ruse
+
+    def sel_read(self, st):
+        return _np(st).copy()
+
     def zquant(self, q, n, ld, sel, r, rm, mu, scale, zq, ld_zq, colmap, qmax, zb, np_zb):
         if r == 0:
             return 0
@@ -226,7 +277,10 @@ class NumpyOps:
                 _np(d2)[r, t] = dd
             _np(cnt)[r] = len(lst)
 
-    def dipcn(self, n, reads, has, scale, nbr, nscale, ncnt, ld, n_nbr, out, valid):
+    def dipcn(self, n, reads, has, scale, nbr, nscale, ncnt, ld, n_nbr, out, valid, defer=None):
+        if defer is not None:                  # HipOps' deferred flag (never set here)
+            _np(defer)[0] = self.dipcn(n, reads, has, scale, nbr, nscale, ncnt, ld, n_nbr, out, valid)
+            return None
         rd, hs, sc = _np(reads), _np(has), _np(scale)
         nb, ns, nc = _np(nbr), _np(nscale), _np(ncnt)
         for i in range(n):

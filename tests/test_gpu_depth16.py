@@ -167,3 +167,62 @@ def test_chain_q16_equals_int32(dev):
                                                st.idx_out[:n], st.d2[:n], st.dip[:n], st.hap[: 2 * n])]
     for a, b in zip(res["i32"], res["q16"]):
         assert np.array_equal(a, b, equal_nan=True)
+
+
+@pytest.mark.parametrize("tail", [1, 7, 8, 9, 127, 128, 129, 136, 255, 257, 1000, 1728, 4095, 4096, 6360, 8191])
+def test_row_means_every_tail_length(dev, tail):
+    """The partial last block's pairwise tree (planned on the host per tail
+    length): row means of both depth forms equal NumPy's nanmean bit for bit,
+    with escapes and missing cells inside the tail."""
+    from grid_amd.fused import Depth16, HipOps
+    from oracle.npsum import nanmean_rows
+    n, m = 70, 8192 + tail
+    q = random_depths(n, m, 100 + tail)
+    q[3, 8192:] = MISSING                       # a row whose tail is all missing
+    q[4, -1] = 300000                           # an escape in the tail's last leaf
+    qd = torch.from_numpy(q).cuda()
+    q16, eoff, ecol, ev, ld16 = encode(dev, qd)
+    d16 = Depth16(q16, eoff, ecol, ev, ld16)
+    ops = HipOps(dev)
+    mat = np.where(q == MISSING, np.nan, q / 100.0)
+    exp = nanmean_rows(mat)
+    for src, ld in ((qd, m), (d16, ld16)):
+        bsum = torch.zeros((n, 2), dtype=torch.float64, device="cuda")
+        bcnt = torch.zeros((n, 2), dtype=torch.int32, device="cuda")
+        ops.row_blocks(src, n, m, ld, bsum, bcnt)
+        rm = torch.zeros(n, dtype=torch.float64, device="cuda")
+        ops.row_means(bsum, bcnt, n, 2, rm)
+        assert np.array_equal(rm.cpu().numpy(), exp, equal_nan=True)
+        assert np.array_equal(bcnt.cpu().numpy()[:, 1], (q[:, 8192:] != MISSING).sum(1))
+
+
+@pytest.mark.parametrize("n,m", [(1, 9), (7, 1001), (8, 64), (33, 777), (257, 4099), (300, 5 * 8192 + 517),
+                                 (520, 2 * 8192 + 1)])
+def test_col_stats_pipelined_equal_int32(dev, n, m):
+    """The pipelined compact column kernel (k_col16_pipe: LDS row windows,
+    groups of 8 rows in flight, ragged last column) gives the int32 column
+    kernels' bits: rows not a multiple of 8 or 32, windows of 256 rows, odd m,
+    missing cells, escapes and a zero-mean row."""
+    from grid_amd.fused import Depth16, HipOps
+    q = random_depths(n, m, 7 * n + m)
+    if n > 3:
+        q[3, :] = 0                                  # row mean 0: a bad row (skipped)
+    qd = torch.from_numpy(q).cuda()
+    q16, eoff, ecol, ev, ld16 = encode(dev, qd)
+    d16 = Depth16(q16, eoff, ecol, ev, ld16)
+    ops = HipOps(dev)
+    nblk = -(-m // 8192)
+    out = {}
+    for name, src, ld in (("i32", qd, m), ("q16", d16, ld16)):
+        bsum = torch.zeros((n, nblk), dtype=torch.float64, device="cuda")
+        bcnt = torch.zeros((n, nblk), dtype=torch.int32, device="cuda")
+        ops.row_blocks(src, n, m, ld, bsum, bcnt)
+        rm = torch.zeros(n, dtype=torch.float64, device="cuda")
+        ops.row_means(bsum, bcnt, n, nblk, rm)
+        mu, var, ratio = (torch.full((m + 1,), -7.0, dtype=torch.float64, device="cuda") for _ in range(3))
+        ops.col_means(src, n, m, ld, rm, mu)
+        ops.col_vars(src, n, m, ld, rm, mu, var, ratio)
+        out[name] = [t.cpu().numpy() for t in (rm, mu, var, ratio)]
+    for a, b in zip(out["i32"], out["q16"]):
+        assert np.array_equal(a, b, equal_nan=True)
+    assert out["q16"][1][m] == -7.0                  # nothing stored past the last column
