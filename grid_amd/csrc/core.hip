@@ -259,16 +259,40 @@ __device__ __forceinline__ uint64_t dkey(double d) {
   return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
 }
 
+__global__ __launch_bounds__(256) void k_kth_hist(const double *__restrict__ v, int64_t n, int nk, int shift,
+                                                  const KthState *__restrict__ st, unsigned *__restrict__ ghist) {
+  __shared__ unsigned h[KTH_MAX][256];
+  for (int t = threadIdx.x; t < KTH_MAX * 256; t += 256) (&h[0][0])[t] = 0;
+  uint64_t pre[KTH_MAX];
+#pragma unroll
+  for (int j = 0; j < KTH_MAX; j++) pre[j] = j < nk ? st[j].prefix : 0;
+  __syncthreads();
+  const int hs = shift + 8;                      // bits above the current digit must match
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const double d = v[i];
+    if (d != d) continue;
+    const uint64_t k = dkey(d);
+    const unsigned dig = (unsigned)(k >> shift) & 255u;
+#pragma unroll
+    for (int j = 0; j < KTH_MAX; j++)
+      if (j < nk && (hs >= 64 || ((k ^ pre[j]) >> hs) == 0)) atomicAdd(&h[j][dig], 1u);
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < nk * 256; t += 256) {
+    const unsigned c = (&h[0][0])[t];
+    if (c) atomicAdd(ghist + t, c);
+  }
+}
+
 // one wave per k: the digit holding rank k, the rank within it; clears the histogram
-__device__ __forceinline__ void kth_pick_wave(int j, int lane, int shift, KthState *__restrict__ st,
-                                              unsigned *__restrict__ ghist) {
+__global__ __launch_bounds__(64) void k_kth_pick(int shift, KthState *__restrict__ st, unsigned *__restrict__ ghist) {
+  const int j = blockIdx.x, lane = threadIdx.x;
   unsigned *hj = ghist + j * 256;
   unsigned c[4];
   unsigned s = 0;
 #pragma unroll
   for (int q = 0; q < 4; q++) {
-    // agent scope: the other workgroups' histogram atomics, not a stale line
-    c[q] = __hip_atomic_load(hj + lane * 4 + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    c[q] = hj[lane * 4 + q];
     s += c[q];
   }
   // inclusive prefix over lanes of the 4-bin sums
@@ -292,54 +316,16 @@ __device__ __forceinline__ void kth_pick_wave(int j, int lane, int shift, KthSta
   for (int q = 0; q < 4; q++) hj[lane * 4 + q] = 0;
 }
 
-// One pass of the select: a histogram of the digit at `shift` over the values
-// whose key prefix matches, then the last workgroup to finish its histogram (a
-// ticket after a release fence) picks the digits, wave j for rank j, and
-// resets the ticket (one launch per pass instead of histogram + pick)
-__global__ __launch_bounds__(256) void k_kth_pass(const double *__restrict__ v, int64_t n, int nk, int shift,
-                                                  KthState *__restrict__ st, unsigned *__restrict__ ghist,
-                                                  unsigned *__restrict__ ticket) {
-  __shared__ unsigned h[KTH_MAX][256];
-  __shared__ bool last;
-  for (int t = threadIdx.x; t < KTH_MAX * 256; t += 256) (&h[0][0])[t] = 0;
-  uint64_t pre[KTH_MAX];
-#pragma unroll
-  for (int j = 0; j < KTH_MAX; j++) pre[j] = j < nk ? st[j].prefix : 0;
-  __syncthreads();
-  const int hs = shift + 8;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const double d = v[i];
-    if (d != d) continue;
-    const uint64_t k = dkey(d);
-    const unsigned dig = (unsigned)(k >> shift) & 255u;
-#pragma unroll
-    for (int j = 0; j < KTH_MAX; j++)
-      if (j < nk && (hs >= 64 || ((k ^ pre[j]) >> hs) == 0)) atomicAdd(&h[j][dig], 1u);
-  }
-  __syncthreads();
-  for (int t = threadIdx.x; t < nk * 256; t += 256) {
-    const unsigned c = (&h[0][0])[t];
-    if (c) atomicAdd(ghist + t, c);
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    last = atomicAdd(ticket, 1u) == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!last) return;                                   // workgroup-uniform
-  __threadfence();
-  const int w = threadIdx.x >> 6;
-  if (w < nk) kth_pick_wave(w, threadIdx.x & 63, shift, st, ghist);
-  if (threadIdx.x == 0) *ticket = 0;
-}
-
-// gh: KTH_MAX * 256 zeroed counters followed by a zeroed ticket
+// 8 passes of histogram + pick (gh: KTH_MAX * 256 zeroed counters).  One
+// launch per pass with a last-workgroup pick was slower (0.29 -> 0.56 ms of
+// selection at 375,000 bins, r03x): every workgroup's agent-scope release
+// fence before its ticket costs more than the second launch.
 static void kth_passes(grid_ctx *ctx, const double *d_v, int64_t n, int nk, KthState *ks, unsigned *gh) {
   const int blocks = (int)std::min<int64_t>(ceil_div(n, 256), 4 * ctx->ncu);
-  for (int shift = 56; shift >= 0; shift -= 8)
-    hipLaunchKernelGGL(k_kth_pass, dim3(blocks), dim3(256), 0, ctx->stream, d_v, n, nk, shift, ks, gh,
-                       gh + KTH_MAX * 256);
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    hipLaunchKernelGGL(k_kth_hist, dim3(blocks), dim3(256), 0, ctx->stream, d_v, n, nk, shift, ks, gh);
+    hipLaunchKernelGGL(k_kth_pick, dim3(nk), dim3(64), 0, ctx->stream, shift, ks, gh);
+  }
 }
 
 __global__ __launch_bounds__(256) void k_count_valid(const double *__restrict__ v, int64_t n,
@@ -376,7 +362,7 @@ int grid_select_kth(grid_ctx *ctx, const double *d_v, int64_t n, const int64_t *
   REQUIRE(ctx && h_ks && h_vals && n > 0 && d_v && nk >= 1 && nk <= KTH_MAX, "bad args (1 <= nk <= %d)", KTH_MAX);
   for (int j = 0; j < nk; j++) REQUIRE(h_ks[j] >= 0 && h_ks[j] < n, "k (%lld) out of range", (long long)h_ks[j]);
   void *s = nullptr;
-  const size_t hbytes = (size_t)KTH_MAX * 256 * 4 + 256;          // + the k_kth_pass ticket
+  const size_t hbytes = (size_t)KTH_MAX * 256 * 4;
   int rc = grid_scratch(ctx, 256 + hbytes, &s);
   if (rc) return rc;
   KthState *st = (KthState *)s;
@@ -589,7 +575,7 @@ int grid_sel_stage1(grid_ctx *ctx, const double *d_rall, int64_t rlen, const dou
   if (ml > 0)
     HIPCHK(hipcub::DeviceSelect::Flagged(nullptr, cub, it, (uint8_t *)nullptr, d_sel, (int64_t *)nullptr, (int)ml,
                                          ctx->stream));
-  const size_t hbytes = (size_t)KTH_MAX * 256 * 4 + 256;          // + the k_kth_pass ticket
+  const size_t hbytes = (size_t)KTH_MAX * 256 * 4;
   const size_t off_h = 256, off_c = off_h + hbytes, off_f = off_c + ((cub + 255) & ~size_t(255));
   void *s = nullptr;
   int rc = grid_scratch(ctx, off_f + (size_t)ml + 256, &s);
@@ -631,7 +617,7 @@ int grid_sel_stage2(grid_ctx *ctx, const double *d_r3all, int64_t r3len, const d
   size_t cub = 0;
   if (ml > 0)
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub, (int32_t *)nullptr, d_colmap, (int)ml, ctx->stream));
-  const size_t hbytes = (size_t)KTH_MAX * 256 * 4 + 256;          // + the k_kth_pass ticket
+  const size_t hbytes = (size_t)KTH_MAX * 256 * 4;
   const size_t off_h = 256, off_c = off_h + hbytes, off_f = off_c + ((cub + 255) & ~size_t(255));
   void *s = nullptr;
   int rc = grid_scratch(ctx, off_f + (size_t)ml * 4 + 256, &s);
