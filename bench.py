@@ -399,6 +399,12 @@ def main():
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
+    # ONE JSON line on stdout: whatever libraries write to fd 1 (RCCL prints
+    # its version banner there at communicator init, once per rank) goes to
+    # stderr; the result line is written to a saved copy of the real stdout
+    result_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
         raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}")
@@ -466,7 +472,7 @@ def main():
             note("cpu baseline: the oracle from files at config 1")
             out["cpu_baseline"]["from_files"] = cpu_baseline_from_files(n, m, args.k, args.n_iters)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=result_out, flush=True)
     if dist:
         dist.barrier()
         dist.destroy_process_group()
