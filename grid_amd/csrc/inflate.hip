@@ -32,12 +32,13 @@ namespace {
 // them: pos - flushed < FLUSH + 266 before a flush), so a match with dist <=
 // RING - 258 copies within the ring; a longer one (up to DEFLATE's 32768)
 // reads its source from the flushed output in HBM (FAR: dist > RING - 258 >
-// pos - flushed + 257, so every source byte is flushed).  A 4 KiB ring with
-// 2 KiB flushes puts ~10.5 KiB of LDS on a wave: 15 waves per CU (VGPRs allow
-// 16) instead of the 4 a 32 KiB window allowed -- the decode chain is
-// latency-bound, one symbol at a time.  (8 KiB ring / 4 KiB flushes: 10 waves
-// per CU, 18.8 GB/s of text at 1,024 files, profiles/r03o_*.)
-constexpr int RING = 4096, RMASK = RING - 1, FLUSH = 2048, NEAR = RING - 258;
+// pos - flushed + 257, so every source byte is flushed).  A 2 KiB ring with
+// 1 KiB flushes puts ~8.4 KiB of LDS on a wave: 18 waves per CU with the
+// kernel held to 5 waves per SIMD (92 VGPRs), instead of the 4 a 32 KiB window
+// allowed -- the decode chain is latency-bound, one symbol at a time.  (8 KiB
+// ring: 10 waves per CU, 18.8 GB/s of text at 1,024 files, profiles/r03o_*;
+// 4 KiB ring: 15 waves, r03r.)
+constexpr int RING = 2048, RMASK = RING - 1, FLUSH = 1024, NEAR = RING - 258;
 static_assert(NEAR > FLUSH + 266 + 257, "far copies must read flushed bytes only");
 
 __constant__ uint32_t c_crc_pow[48][32];   // columns of M^(2^k), M = one zero byte
@@ -379,7 +380,7 @@ struct DevP {
 };
 
 // One wave per file.  status: 0 ok, else an icore::Status (or GRID_GZ_E_*).
-__global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ src, const int64_t *__restrict__ in_off,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_inflate(const uint8_t *__restrict__ src, const int64_t *__restrict__ in_off,
                                                 const int64_t *__restrict__ in_len, uint8_t *__restrict__ out,
                                                 const int64_t *__restrict__ out_off,
                                                 const int64_t *__restrict__ out_cap, grid_gz_member *mem, int mcap,
@@ -387,7 +388,7 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ src,
                                                 int32_t *__restrict__ nmem) {
   __shared__ __attribute__((aligned(16))) uint8_t s_ring[RING];
   __shared__ uint16_t s_tab[icore::T_SIZE];
-  __shared__ uint32_t s_ftab[F_LEN + F_DIST];   // 10.5 KiB in all: 15 waves per CU
+  __shared__ uint32_t s_ftab[F_LEN + F_DIST];   // 8.4 KiB in all: 18 waves per CU
   const int f = blockIdx.x;
   DevP p;
   // the stream starts `skew` bytes into a 4-B aligned word (a BGZF member
