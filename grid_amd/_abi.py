@@ -49,6 +49,7 @@ _SIGS = {
     "grid_d2d": [_vp, _vp, _vp, C.c_size_t],
     "grid_memset": [_vp, _vp, C.c_int, C.c_size_t],
     "grid_event_record": [_vp, C.c_int],
+    "grid_stream_after": [_vp, _vp],
     "grid_event_elapsed": [_vp, C.c_int, C.c_int, C.POINTER(C.c_float)],
     "grid_norm_row_blocks": [_vp, _vp, _i64, _i64, _i64, _vp, _vp],
     "grid_norm_row_means": [_vp, _vp, _vp, _i64, _i64, _vp],

@@ -163,6 +163,20 @@ int grid_event_record(grid_ctx *ctx, int slot) {
   return GRID_OK;
 }
 
+int grid_stream_after(grid_ctx *ctx, grid_ctx *src) {
+  REQUIRE(ctx && src, "ctx is NULL");
+  REQUIRE(ctx->device == src->device, "contexts on different devices");
+  HIPCHK(hipSetDevice(ctx->device));
+  hipEvent_t ev;
+  HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  hipError_t e = hipEventRecord(ev, src->stream);
+  if (e == hipSuccess) e = hipStreamWaitEvent(ctx->stream, ev, 0);
+  const hipError_t d = hipEventDestroy(ev);     // released once the wait has been satisfied
+  HIPCHK(e);
+  HIPCHK(d);
+  return GRID_OK;
+}
+
 int grid_event_elapsed(grid_ctx *ctx, int a, int b, float *ms) {
   REQUIRE(ctx && a >= 0 && a < 8 && b >= 0 && b < 8 && ms, "bad event slot");
   HIPCHK(hipEventSynchronize(ctx->ev[b]));

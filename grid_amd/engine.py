@@ -450,6 +450,9 @@ def phase_batch(dev: Device, loci, min_nbr: int, n_iters: int, legacy: bool = Fa
                 fut = bg.submit(stage, *bounds[gi + 1])
             keep.append(bufs)
             d_arr = bufs[3]
+            # the group's inputs were copied on cdev's stream: order the launches
+            # behind them through the runtime, not only through the host's wait
+            call("grid_stream_after", dev.ctx, cdev.ctx)
             for l0 in range(0, nd, 65535):            # grid.y of the pack launch
                 call("grid_hi_pack_batch", dev.ctx, min(65535, nd - l0), d_arr.ptr + l0 * C.sizeof(_abi.HiLocus),
                      max_n)

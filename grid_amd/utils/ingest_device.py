@@ -47,6 +47,7 @@ BATCH_IN = 4 << 30              # compressed bytes per batch
 BATCH_TEXT = 24 << 30           # inflated bytes per batch
 STAGE = 1 << 30                 # pinned staging per CPU sub-batch (two of them)
 TRACE = bool(os.environ.get("GRID_INGEST_TRACE"))   # per-batch phase times on stderr
+XSTREAM_WAIT = True             # dev's stream waits for the copy stream (False only in a GPU test's control arm)
 
 
 class DeviceIngestUnsupported(Exception):
@@ -300,6 +301,12 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
         for p_ in pend:
             if p_ is not None:
                 p_.result()
+        if on_cpu and XSTREAM_WAIT:
+            # the parse kernels on dev's stream read text the copy stream wrote
+            # over d_text -- lines the previous batch's kernels had cached: order
+            # the stream behind the copies through the runtime (event + wait), not
+            # through the host's view of their completion alone
+            call("grid_stream_after", dev.ctx, cdev.ctx)
         g_mem = g_whole = 0
         t_gpu = 0.0
         if launched:

@@ -79,6 +79,11 @@ int grid_memset(grid_ctx *ctx, void *d_dst, int value, size_t bytes);
  * recorded markers. */
 int grid_event_record(grid_ctx *ctx, int slot);
 int grid_event_elapsed(grid_ctx *ctx, int slot_a, int slot_b, float *ms);
+/* Order ctx's stream after everything enqueued so far on src's stream (an
+ * event recorded on src, waited on by ctx): the runtime's own cross-stream
+ * dependency, so work on ctx sees memory src's copies wrote (the device
+ * ingest's CPU-inflated text, copied on its own stream). */
+int grid_stream_after(grid_ctx *ctx, grid_ctx *src);
 
 /* --------------------------------------------------------- step 4: normalize
  * Replaces grid/utils/normalize_mosdepth.py normalize_matrix :419-476 and

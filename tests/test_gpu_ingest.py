@@ -37,9 +37,20 @@ SPLITS = {
 }
 
 
-@pytest.fixture(params=["model", "gpu", "cpu", "alternate"])
+def _batch_alternate(self, files, text, bgzf):
+    # whole batches alternate between the sides: the text of a GPU-inflated
+    # batch is then overwritten in d_text by the next batch's copy stream
+    self.calls = getattr(self, "calls", 0) + 1
+    return (sorted(files), []) if self.calls % 2 else ([], sorted(files))
+
+
+SPLITS["batches"] = _batch_alternate
+
+
+@pytest.fixture(params=["model", "gpu", "cpu", "alternate", "batches"])
 def split(request, monkeypatch):
-    """Which side inflates: the cost model, or forced GPU / CPU / every other file."""
+    """Which side inflates: the cost model, or forced GPU / CPU / every other
+    file / every other batch."""
     if request.param != "model":
         monkeypatch.setattr(ingest_device._Split, "plan", SPLITS[request.param])
     return request.param

@@ -49,11 +49,13 @@ def test_gram_k_loops_fixed_barriers_and_no_spills(report):
     the tail of each unit (<= 8 K-steps) reload more -- both recorded here so
     a code-generation change shows up as a test failure."""
     grams = {k: v for k, v in report.items() if k.startswith("k_gram8<0,")}
-    assert len(grams) == 8, sorted(grams)
+    assert len(grams) == 9, sorted(grams)                  # LAY 4 (16x16x32 MFMAs) ships for FL = 1 only
     for name, v in grams.items():
         fl, lay = (int(x) for x in name.rstrip(">").split(",")[-2:])
+        assert fl == 1 or lay != 4, name
         per_step = 2 if lay >= 2 else 1                      # half-split ring: two barriers per K-step
-        ring = [l for l in v["loops"] if l["lds_dma"] == 36 and l["mfma"] == 96 and l["innermost"]]
+        mfma = 192 if lay == 4 else 96                       # 6 K-steps of 16x16x32 (4x4 per wave) or 32x32x16 (2x2)
+        ring = [l for l in v["loops"] if l["lds_dma"] == 36 and l["mfma"] == mfma and l["innermost"]]
         assert ring and all(l["barriers_per_iter"] == [6 * per_step] * 2 for l in ring), (name, ring)
         steady = min(ring, key=lambda l: l["vmcnt"])       # the loop with no tail conditions
         if fl == 1:

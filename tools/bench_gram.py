@@ -43,12 +43,13 @@ zbb = None
 if any(v.startswith("kb") for v in a.variants.split(",")):   # K-blocked [kpad/KBW][np][KBW]
     zbb = zb[:, :kpad].reshape(np_, kpad // _abi.KBW, _abi.KBW).permute(1, 0, 2).contiguous()
 res = {}
+first = None
 flops = 2.0 * a.n * a.n * a.k
 for rep in range(a.reps):
     for vv in a.variants.split(","):
         # "kb21:LAG=2:KC=9" -> variant kb21 with GRID_GRAM_LAG=2, GRID_GRAM_KC=9 (performance knobs)
         v, *knobs = vv.split(":")
-        for kv in ("LAG", "SPIN", "KC", "KX", "QL", "UF", "DYN", "PART_MB"):
+        for kv in ("LAG", "SPIN", "KC", "KX", "QL", "UF", "DYN", "PART_MB", "Q16"):
             os.environ.pop("GRID_GRAM_" + kv, None)
         for kv in knobs:
             key, val = kv.split("=")
@@ -70,7 +71,14 @@ for rep in range(a.reps):
             zz = zb[:256, :kpad].view(torch.bfloat16).double()
             ref = (zz @ zz.T).long()
             ok = torch.equal(gram[:128, :256], ref[:128, :256])
-            print(f"variant {vv}: tile check {'OK' if ok else 'MISMATCH'}", flush=True)
+            # every variant's whole Gram (upper tiles) against the first variant's
+            if first is None:
+                first = gram.clone()
+                same = True
+            else:
+                same = torch.equal(gram, first)
+            print(f"variant {vv}: tile check {'OK' if ok else 'MISMATCH'}, "
+                  f"whole Gram {'equal to' if same else 'DIFFERENT from'} the first variant", flush=True)
 for v, t in res.items():
     ms = min(t)
     print(f"variant {v}: min {ms:.2f} ms  median {np.median(t):.2f} ms  "
