@@ -39,7 +39,7 @@ PEAK_BF16_TFLOPS = 2516.6     # 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz (dense
 PEAK_HBM_GBS = 8000.0
 # HBM bytes per Gram launch from the rocprofv3 FETCH_SIZE / WRITE_SIZE passes
 # of this same command (tools/gpu_round.sh -> tools/pmc_traffic.py)
-TRAFFIC_JSON = "profiles/r03y_pmc_traffic.json"
+TRAFFIC_JSON = "profiles/r03ai_pmc_traffic.json"
 GRAM_KERNEL = "k_gram8<0, true"
 SEED = 20260821
 NCL = 26
