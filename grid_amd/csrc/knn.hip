@@ -1787,7 +1787,11 @@ static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_
   }
   unsigned *rounds = (unsigned *)((char *)ctx->aux + GRID_AUX_BYTES / 2);
   HIPCHK(hipMemsetAsync(rounds, 0, (128 + 8 * 16) * 4, ctx->stream));   // round and unit counters
-  const int per = ctx->ncu >= 8 ? ctx->ncu / 8 : 1;
+  int per = ctx->ncu >= 8 ? ctx->ncu / 8 : 1;
+  // tools A/B (GRID_GRAM_PER: workgroups per XCD below the CU count): how the
+  // feed rate per CU changes with the number of CUs streaming at once
+  const char *pere = GRID_AB_KNOB("GRID_GRAM_PER");
+  if (pere && atoi(pere) >= 1 && atoi(pere) < per) per = atoi(pere);
   const int64_t ngroups = ceil_div(nt6, per);
   // (kx, kc): cost = the longest XCD's sequential work per workgroup in
   // K-step units: rounds x (steps per unit + UF), where UF prices a unit's
