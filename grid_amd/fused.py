@@ -126,9 +126,16 @@ class TorchComm:
         self.host = dist.get_backend() == "gloo"
 
     def all_gather(self, t):
+        """[world, *t.shape]: rank r's t at index r.  Device tensors over RCCL
+        land in that tensor directly (one collective, no stacking copy); gloo
+        stages on the host."""
         import torch
         t = t.contiguous()
-        src = t.cpu() if self.host and t.is_cuda else t
+        if not (self.host and t.is_cuda) and t.is_cuda:
+            out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+            self.dist.all_gather_into_tensor(out, t)
+            return out
+        src = t.cpu() if t.is_cuda else t
         parts = [torch.empty_like(src) for _ in range(self.world)]
         self.dist.all_gather(parts, src)
         return torch.stack(parts).to(t.device)
