@@ -62,3 +62,13 @@ def test_gram_k_loops_fixed_barriers_and_no_spills(report):
             assert steady["scratch"] == 0 and steady["vmcnt"] == 6 * per_step, (name, steady)
         else:
             assert steady["scratch"] <= 11, (name, steady)
+
+
+def test_round2_no_flush_probe_has_the_production_skeleton():
+    """the no-flush Gram probe that hung in round 2, rebuilt
+    (knn.hip -DGRID_ISA_PROBE, compile only) -- its MFMAs are dead code, but its
+    barriers, vmcnt waits and LDS-DMA per steady K-loop trip equal production
+    k_gram8<0, true, 1, 3>'s and no EXEC-divergent branch separates a barrier."""
+    if not os.path.exists("/opt/rocm/bin/hipcc"):
+        pytest.skip("hipcc not present")
+    assert isa_barriers.probe_compare() == 0

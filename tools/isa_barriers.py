@@ -277,13 +277,48 @@ def check(funcs: dict[str, list[Insn]], pattern: str) -> dict:
     return res
 
 
+def probe_compare() -> int:
+    """The round-2 no-flush probe of the half-split ring, rebuilt (knn.hip
+    with -DGRID_ISA_PROBE: k_gram8<9, true, 1, 3>, results dropped so every
+    MFMA is dead), against production k_gram8<0, true, 1, 3> from the same
+    object: frontier errors, and the steady K loop's barriers and vmcnt waits
+    per 6-step trip (compile only; nothing runs on a GPU)."""
+    src = Path(__file__).resolve().parent.parent / "grid_amd" / "csrc"
+    with tempfile.TemporaryDirectory() as td:
+        obj = Path(td) / "knn_probe.o"
+        subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC",
+                        "-ffp-contract=off", "-I" + str(src.parent.parent / "include"), "-DGRID_ISA_PROBE", "-c",
+                        str(src / "knn.hip"), "-o", str(obj)], check=True, capture_output=True)
+        funcs = {}
+        for co in code_objects(str(obj)):
+            funcs.update(parse_functions(disassemble(co)))
+    res = check(funcs, "k_gram8<")
+    rows = {}
+    for name in ("k_gram8<0, true, 1, 3>", "k_gram8<9, true, 1, 3>"):
+        v = res[name]
+        ring = [l for l in v["loops"] if l["lds_dma"] == 36 and l["innermost"]]
+        steady = min(ring, key=lambda l: l["vmcnt"])
+        rows[name] = (v["errors"], steady["barriers_per_iter"], steady["vmcnt"], steady["mfma"], steady["scratch"])
+        print(f"{name}: frontier errors {len(v['errors'])}; steady trip: barriers {steady['barriers_per_iter']}, "
+              f"vmcnt {steady['vmcnt']}, lgkmcnt {steady['lgkmcnt']}, dma {steady['lds_dma']}, "
+              f"mfma {steady['mfma']}, scratch {steady['scratch']}")
+    (e0, b0, v0, _, _), (e9, b9, v9, _, _) = rows.values()
+    same = not e0 and not e9 and b0 == b9 and v0 == v9
+    print("same barrier / vmcnt skeleton" if same else "SKELETONS DIFFER")
+    return 0 if same else 1
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("lib", nargs="?", default="grid_amd/_lib/libgridhip.so")
     ap.add_argument("--kernels", default="", help="comma-separated name substrings (default: every kernel "
                                                   "that has a barrier)")
     ap.add_argument("--json", action="store_true")
+    ap.add_argument("--probe", action="store_true", help="rebuild the round-2 no-flush Gram probe and compare "
+                                                         "its ISA skeleton with production")
     a = ap.parse_args()
+    if a.probe:
+        sys.exit(probe_compare())
     funcs = {}
     for co in code_objects(a.lib):
         funcs.update(parse_functions(disassemble(co)))
