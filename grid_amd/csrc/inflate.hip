@@ -33,9 +33,10 @@ namespace {
 // RING - 258 copies within the ring; a longer one (up to DEFLATE's 32768)
 // reads its source from the flushed output in HBM (FAR: dist > RING - 258 >
 // pos - flushed + 257, so every source byte is flushed).  A 2 KiB ring with
-// 1 KiB flushes puts ~8.4 KiB of LDS on a wave: 18 waves per CU with the
-// kernel held to 5 waves per SIMD (92 VGPRs), instead of the 4 a 32 KiB window
-// allowed -- the decode chain is latency-bound, one symbol at a time.  (8 KiB
+// 1 KiB flushes and a 2^8-entry literal/length fast table put ~5.4 KiB of LDS
+// on a wave: 28 waves per CU with the kernel held to 7 waves per SIMD (72
+// VGPRs; 18 with the 2^10 table at 5 per SIMD), instead of the 4 a 32 KiB
+// window allowed -- the decode chain is latency-bound, one symbol at a time.  (8 KiB
 // ring: 10 waves per CU, 18.8 GB/s of text at 1,024 files, profiles/r03o_*;
 // 4 KiB ring: 15 waves, r03r.)
 constexpr int RING = 2048, RMASK = RING - 1, FLUSH = 1024, NEAR = RING - 258;
@@ -380,7 +381,10 @@ struct DevP {
 };
 
 // One wave per file.  status: 0 ok, else an icore::Status (or GRID_GZ_E_*).
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_inflate(const uint8_t *__restrict__ src, const int64_t *__restrict__ in_off,
+#ifndef GRID_INFLATE_WPE
+#define GRID_INFLATE_WPE 7            // 72 VGPRs: 7 waves per SIMD (LDS 5.4 KiB per wave: 29 per CU)
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GRID_INFLATE_WPE))) void k_inflate(const uint8_t *__restrict__ src, const int64_t *__restrict__ in_off,
                                                 const int64_t *__restrict__ in_len, uint8_t *__restrict__ out,
                                                 const int64_t *__restrict__ out_off,
                                                 const int64_t *__restrict__ out_cap, grid_gz_member *mem, int mcap,
@@ -388,7 +392,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
                                                 int32_t *__restrict__ nmem) {
   __shared__ __attribute__((aligned(16))) uint8_t s_ring[RING];
   __shared__ uint16_t s_tab[icore::T_SIZE];
-  __shared__ uint32_t s_ftab[F_LEN + F_DIST];   // 8.4 KiB in all: 18 waves per CU
+  __shared__ uint32_t s_ftab[F_LEN + F_DIST];   // 5.4 KiB in all: 28 waves per CU
   const int f = blockIdx.x;
   DevP p;
   // the stream starts `skew` bytes into a 4-B aligned word (a BGZF member

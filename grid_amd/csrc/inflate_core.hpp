@@ -33,7 +33,14 @@
 
 namespace icore {
 
-constexpr int LFAST = 10, DFAST = 8;
+// fast-table bits.  2^8 literal/length entries (round 3): the smaller table lets
+// 28 waves share a CU instead of 18 (k_inflate is latency-bound per wave), and
+// the codes longer than 8 bits it sends to the canonical walk cost less than
+// that buys: 36.2 vs 33.5 GB/s of text at 256 BGZF files (2^9: 35.1; r03am)
+#ifndef GRID_INFLATE_LFAST
+#define GRID_INFLATE_LFAST 8
+#endif
+constexpr int LFAST = GRID_INFLATE_LFAST, DFAST = 8;
 constexpr int FT_LEN = 0, FT_DIST = 1;   // the fast tables (policy-owned)
 // u16 slots of the table area: litlen count/symbols, dist count/symbols,
 // code-length code count/symbols, lengths scratch, offsets scratch
