@@ -106,7 +106,7 @@ class _Split:
 
     def __init__(self, threads):
         self.threads = max(1, int(threads))
-        self.gpu = 18.0e9         # B/s, member-parallel (8 KiB inflate ring: 10 waves per CU)
+        self.gpu = 18.0e9         # B/s, member-parallel, as seen by a batch (beside its disk reads; learned)
         self.wave = 9.0e6         # B/s, one wave on one whole file
         self.cpu = 0.4e9          # B/s per thread while the GPU inflates too (0.6-0.7 alone)
 
