@@ -133,7 +133,8 @@ _SIGS = {
     "grid_gunzip_batch": [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp],
     "grid_gz_text_size": [_vp, _i64, C.POINTER(_i64), C.POINTER(_i32)],
     "grid_gz_members": [_vp, _i64, _vp, _vp, _vp, _i32, C.POINTER(_i32)],
-    "grid_gunzip_host": [_vp, _i64, _vp, _i64, C.POINTER(_i64), C.POINTER(_i32)],
+    "grid_gunzip_host": [_vp, _i64, _vp, _i64, C.POINTER(_i64), C.POINTER(_i32), C.POINTER(C.c_uint32)],
+    "grid_text_crc32": [_vp, _vp, _vp, _vp, _i64, _vp],
     "grid_md_count": [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp],
     "grid_md_parse_ref": [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp,
                           C.POINTER(_i64), C.POINTER(_i32)],
@@ -551,14 +552,26 @@ def gz_members(buf):
     raise GridNativeError("grid_gz_members: member count changed")
 
 
-def gunzip_host(src, out) -> tuple[int, int]:
+def gunzip_host(src, out, with_crc=False):
     """Inflate the gzip file in ``src`` into the uint8 array ``out`` (host,
-    libdeflate or zlib; releases the GIL).  Returns (status GZ_*, bytes)."""
+    libdeflate or zlib; releases the GIL).  Returns (status GZ_*, bytes), and
+    with ``with_crc`` the text's CRC-32 from the members' trailers as well."""
     a = np.frombuffer(src, np.uint8) if not isinstance(src, np.ndarray) else src
-    n, st = _i64(), _i32()
+    n, st, crc = _i64(), _i32(), C.c_uint32()
     call("grid_gunzip_host", a.ctypes.data if a.size else None, a.size, out.ctypes.data if out.size else None,
-         out.size, C.byref(n), C.byref(st))
-    return st.value, n.value
+         out.size, C.byref(n), C.byref(st), C.byref(crc))
+    return (st.value, n.value, crc.value) if with_crc else (st.value, n.value)
+
+
+def text_crc32(dev, base_ptr, offs, lens) -> np.ndarray:
+    """CRC-32 of the device byte ranges base_ptr + offs[i], lens[i] bytes
+    (grid_text_crc32; synchronises dev's stream)."""
+    o = np.ascontiguousarray(offs, np.int64)
+    ln = np.ascontiguousarray(lens, np.int64)
+    out = np.zeros(max(len(o), 1), np.uint32)
+    if len(o):
+        call("grid_text_crc32", dev.ctx, base_ptr, o.ctypes.data, ln.ctypes.data, len(o), out.ctypes.data)
+    return out[:len(o)]
 
 
 class Depth16Desc(C.Structure):

@@ -950,4 +950,49 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
   return finish(rc);
 }
 
+
+int grid_text_crc32(grid_ctx *ctx, const uint8_t *d_base, const int64_t *h_off, const int64_t *h_len, int64_t n,
+                    uint32_t *h_crc) {
+  REQUIRE(ctx && n >= 0 && (n == 0 || (d_base && h_off && h_len && h_crc)), "bad args");
+  if (n == 0) return GRID_OK;
+  constexpr int64_t PIECE = 1 << 20;         // one wave per piece: 16 KiB per lane
+  std::vector<int64_t> ps, pl, first(n + 1);
+  for (int64_t i = 0; i < n; i++) {
+    REQUIRE(h_len[i] >= 0 && h_off[i] >= 0, "range %lld: negative offset or length", (long long)i);
+    first[i] = (int64_t)ps.size();
+    for (int64_t a = 0; a < h_len[i]; a += PIECE) {
+      ps.push_back(h_off[i] + a);
+      pl.push_back(std::min(PIECE, h_len[i] - a));
+    }
+  }
+  first[n] = (int64_t)ps.size();
+  const int64_t np = (int64_t)ps.size();
+  for (int64_t i = 0; i < n; i++) h_crc[i] = 0;         // the empty text
+  if (np == 0) return GRID_OK;
+  REQUIRE(np <= 0x7fffffff, "too many pieces");
+  std::vector<uint32_t> tab(1024), pc(np);
+  crc_tables(tab.data());
+  const X2N x2n = make_x2n();
+  hipStream_t st = ctx->stream;
+  DBuf<int64_t> d_s, d_l;
+  DBuf<uint32_t> d_tab, d_c;
+  HIPCHK(d_s.need((size_t)np));
+  HIPCHK(d_l.need((size_t)np));
+  HIPCHK(d_tab.need(1024));
+  HIPCHK(d_c.need((size_t)np));
+  HIPCHK(hipMemcpyAsync(d_s.p, ps.data(), np * 8, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(d_l.p, pl.data(), np * 8, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(d_tab.p, tab.data(), 4096, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_member_crc, dim3((unsigned)np), dim3(64), 0, st, d_base, d_s.p, d_l.p, d_tab.p, x2n, d_c.p);
+  LAUNCHCHK();
+  HIPCHK(hipMemcpyAsync(pc.data(), d_c.p, np * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  for (int64_t i = 0; i < n; i++) {
+    uint32_t acc = 0;
+    for (int64_t p = first[i]; p < first[i + 1]; p++) acc = crc_combine(acc, pc[p], (uint64_t)pl[p], x2n);
+    h_crc[i] = acc;
+  }
+  return GRID_OK;
+}
+
 }  // extern "C"

@@ -877,8 +877,16 @@ bool bgzf_walk(const uint8_t *buf, int64_t n, F fn) {
   return true;
 }
 
+// a member's trailer CRC-32 appended to the text's CRC so far (the text of
+// several members is their texts back to back: crc32_combine over them)
+inline uint32_t crc_append(uint32_t acc, int64_t acc_len, const uint8_t *trailer, int64_t mlen) {
+  uint32_t c;
+  memcpy(&c, trailer, 4);
+  return acc_len ? (uint32_t)crc32_combine64(acc, c, (z_off64_t)mlen) : c;
+}
+
 // every member of in[0, n) through zlib into out[0, cap)
-int gunzip_zlib(const uint8_t *in, int64_t n, uint8_t *out, int64_t cap, int64_t *out_len) {
+int gunzip_zlib(const uint8_t *in, int64_t n, uint8_t *out, int64_t cap, int64_t *out_len, uint32_t *crc) {
   z_stream z{};
   if (inflateInit2(&z, 16 + 15) != Z_OK) return GRID_GZ_EDATA;
   int64_t pos = 0, got = 0;
@@ -904,6 +912,7 @@ int gunzip_zlib(const uint8_t *in, int64_t n, uint8_t *out, int64_t cap, int64_t
       rc = zr == Z_MEM_ERROR ? GRID_GZ_ESPACE : GRID_GZ_EDATA;
       break;
     }
+    *crc = crc_append(*crc, got, in + in0 - 8, out0 - got);
     pos = in0;
     got = out0;
     while (pos < n && in[pos] == 0) pos++;
@@ -913,8 +922,11 @@ int gunzip_zlib(const uint8_t *in, int64_t n, uint8_t *out, int64_t cap, int64_t
   *out_len = got;
   return rc;
 }
-// every member of in[0, n) into out[0, cap): libdeflate, else zlib; a GRID_GZ_* status
-int gunzip_any(const uint8_t *in, int64_t n, uint8_t *out, int64_t cap, int64_t *out_len) {
+// every member of in[0, n) into out[0, cap): libdeflate, else zlib; a GRID_GZ_* status;
+// *crc = the CRC-32 of the whole text, from the members' trailers (each checked
+// against its member's text by the inflater)
+int gunzip_any(const uint8_t *in, int64_t n, uint8_t *out, int64_t cap, int64_t *out_len, uint32_t *crc) {
+  *crc = 0;
   if (n < 18 || in[0] != 0x1f || in[1] != 0x8b) return GRID_GZ_EHEADER;
   const fastgz::Api &a = fastgz::api();
   if (a.ok) {
@@ -929,6 +941,7 @@ int gunzip_any(const uint8_t *in, int64_t n, uint8_t *out, int64_t cap, int64_t 
           rc = r == 3 ? GRID_GZ_ESPACE : GRID_GZ_EDATA;
           break;
         }
+        *crc = crc_append(*crc, got, in + pos + used - 8, (int64_t)g);
         got += (int64_t)g;
         pos += (int64_t)used;
         while (pos < n && in[pos] == 0) pos++;
@@ -938,7 +951,7 @@ int gunzip_any(const uint8_t *in, int64_t n, uint8_t *out, int64_t cap, int64_t 
       return rc;
     }
   }
-  return gunzip_zlib(in, n, out, cap, out_len);
+  return gunzip_zlib(in, n, out, cap, out_len, crc);
 }
 }  // namespace
 
@@ -989,13 +1002,16 @@ int grid_gz_members(const uint8_t *buf, int64_t n, int64_t *start, int64_t *len,
   return ok ? GRID_OK : GRID_EUNSUPPORTED;
 }
 
-int grid_gunzip_host(const uint8_t *in, int64_t n, uint8_t *out, int64_t cap, int64_t *out_len, int32_t *status) {
+int grid_gunzip_host(const uint8_t *in, int64_t n, uint8_t *out, int64_t cap, int64_t *out_len, int32_t *status,
+                     uint32_t *crc) {
   if (!out_len || !status || n < 0 || cap < 0 || (n > 0 && !in) || (cap > 0 && !out)) {
     grid_set_error("grid_gunzip_host: bad args");
     return GRID_EINVAL;
   }
   *out_len = 0;
-  *status = gunzip_any(in, n, out, cap, out_len);
+  uint32_t c = 0;
+  *status = gunzip_any(in, n, out, cap, out_len, &c);
+  if (crc) *crc = c;
   return GRID_OK;
 }
 

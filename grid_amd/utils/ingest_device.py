@@ -21,6 +21,12 @@ means in file order, the valid columns, the empty-sample filter and the rows
 in sorted-ID order (grid_md_finish / grid_md_gather) -- the matrix never
 exists on the host.
 
+Text the host threads inflated is checked where it sits in HBM before it is
+parsed: the CRC-32 of each such file's text in d_text (grid_text_crc32) must
+equal the CRC its gzip trailers give (the GPU-inflated members are checked the
+same way by grid_gunzip_batch's k_gz_crc); a mismatch hands the cohort to the
+host parser.
+
 Anything outside the common shape -- a line outside the canonical mosdepth
 grammar or a non-ASCII byte, reference keys that are not strictly
 increasing, a key outside K, a repeated key, a file of plain gzip members
@@ -48,6 +54,7 @@ BATCH_TEXT = 24 << 30           # inflated bytes per batch
 STAGE = 1 << 30                 # pinned staging per CPU sub-batch (two of them)
 TRACE = bool(os.environ.get("GRID_INGEST_TRACE"))   # per-batch phase times on stderr
 XSTREAM_WAIT = True             # dev's stream waits for the copy stream (False only in a GPU test's control arm)
+AFTER_HOST_TEXT = None          # test seam: called (dev, d_text, toff, files) once host text is in HBM
 
 
 class DeviceIngestUnsupported(Exception):
@@ -196,6 +203,7 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
         cin += _align(sizes[f])
     if cur:
         batches.append(cur)
+    in_need = 256 + max((sum(_align(max(sizes[f], 1)) for f in b) for b in batches), default=0)
     pins = [_Pinned(BATCH_IN + 512), _Pinned(BATCH_IN + 512)]
     stages = [_Pinned(STAGE + 512), _Pinned(STAGE + 512)]
     nthreads = max(1, min(int(threads or 1), 32))
@@ -230,6 +238,7 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
         nb = len(fs)
         gst = np.zeros(nb, np.int32)
         tlen = np.zeros(nb, np.int64)
+        hcrc = np.zeros(nb, np.uint32)
         todo = [k for k in range(nb) if gz[k] and sizes[fs[k]] > 0]
         for k in range(nb):
             if not sizes[fs[k]]:
@@ -285,10 +294,10 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
             def one(t, grp=grp, stage=stage, soff=soff):
                 k = grp[t]
                 v = buf[off[k]:off[k] + sizes[fs[k]]]
-                return _abi.gunzip_host(v, stage[soff[t]:soff[t] + caps_[k]])
+                return _abi.gunzip_host(v, stage[soff[t]:soff[t] + caps_[k]], with_crc=True)
             res = list(pool.map(one, range(len(grp))))
             for t, k in enumerate(grp):
-                gst[k], tlen[k] = res[t]
+                gst[k], tlen[k], hcrc[k] = res[t]
                 c_bytes += int(tlen[k])
 
             def h2d(grp=grp, stage=stage, soff=soff, res=res):
@@ -307,6 +316,17 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
             # the stream behind the copies through the runtime (event + wait), not
             # through the host's view of their completion alone
             call("grid_stream_after", dev.ctx, cdev.ctx)
+        hk = [k for k in on_cpu if gst[k] == 0 and tlen[k] > 0]
+        if hk:
+            # the guard: the host-inflated text as it sits in HBM against the CRC
+            # of its gzip trailers, read on dev's stream (where the parse runs)
+            if AFTER_HOST_TEXT is not None:
+                AFTER_HOST_TEXT(dev, d_text, toff, hk)
+            got = _abi.text_crc32(dev, d_text.ptr, toff[hk], tlen[hk])
+            bad = [fs[k] for k, c in zip(hk, got) if int(c) != int(hcrc[k])]
+            if bad:
+                raise DeviceIngestUnsupported(f"{paths[bad[0]]}: its text in HBM does not match its gzip CRC "
+                                              f"({len(bad)} host-inflated file(s))")
         g_mem = g_whole = 0
         t_gpu = 0.0
         if launched:
@@ -349,10 +369,14 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
             toff[1:] = np.cumsum(tcap)
             if toff[-1] > BATCH_TEXT * 2:
                 raise DeviceIngestUnsupported("a batch of files inflates beyond the device text buffer")
-            if d_in is None or d_in.nbytes < off[-1] + 256:
-                d_in = dev.alloc(int(max(off[-1] + 256, BATCH_IN + 256)), np.uint8)
+            # device buffers sized from the cohort, not from the batch bounds: the
+            # compressed bytes of the largest batch (known from the file sizes), the
+            # text grown with 1/8 headroom as batches need it
+            if d_in is None:
+                d_in = dev.alloc(in_need, np.uint8)
             if d_text is None or d_text.nbytes < toff[-1] + 256:
-                d_text = dev.alloc(int(max(toff[-1] + 256, min(BATCH_TEXT, 1 << 34))), np.uint8)
+                d_text = None
+                d_text = dev.alloc(int(min(toff[-1] + 256 + toff[-1] // 8, 2 * BATCH_TEXT + 256)), np.uint8)
             t_b = time.perf_counter()
             gst, tlen = inflate(buf, off, fs, caps_, gz, members, toff, d_in, d_text)
             t_i = time.perf_counter()

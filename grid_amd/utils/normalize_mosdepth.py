@@ -317,6 +317,11 @@ def ingest(individuals, mosdepth_dir, chromosome, start, end, excluded, min_dept
         except ingest_device.DeviceIngestUnsupported as e:
             msg = f"device mosdepth parser: {e}; using the host parser"
             log(console, msg, style="warning") if console else print(msg)
+        except _abi.GridNativeError as e:
+            # e.g. the device buffers do not fit (a smaller GPU, ranks sharing
+            # one): the device path's buffers are released with its frame
+            msg = f"device mosdepth ingest failed ({e}); using the host parser"
+            log(console, msg, style="warning") if console else print(msg)
     if ints:
         try:
             return ingest_native(individuals, mosdepth_dir, chromosome, start, end, excluded, min_depth,

@@ -604,9 +604,16 @@ int grid_gz_members(const uint8_t *h_buf, int64_t n, int64_t *h_start, int64_t *
 /* host: inflate a gzip file in memory (every member, zero padding after a member skipped, as
  * CPython's gzip reader) into h_out[0, cap): libdeflate when the system library loads, else
  * zlib; *out_len bytes; *status 0, or GRID_GZ_ESPACE (cap too small), GRID_GZ_EHEADER (not
- * gzip), GRID_GZ_EDATA (anything else: corrupt, truncated, CRC) */
+ * gzip), GRID_GZ_EDATA (anything else: corrupt, truncated, CRC); *crc (may be NULL) = the
+ * CRC-32 of the whole text, combined from the members' trailers -- what the device ingest
+ * checks the text against once it sits in HBM (grid_text_crc32) */
 int grid_gunzip_host(const uint8_t *h_in, int64_t n, uint8_t *h_out, int64_t cap, int64_t *out_len,
-                     int32_t *status);
+                     int32_t *status, uint32_t *crc);
+/* CRC-32 (gzip) of n byte ranges of device memory, d_base + h_off[i] for h_len[i] bytes
+ * (host arrays), into h_crc[i]: one wave per <= 1 MiB piece, the pieces folded on the host.
+ * Synchronises the stream.  The device ingest's guard over host-inflated text in HBM. */
+int grid_text_crc32(grid_ctx *ctx, const uint8_t *d_base, const int64_t *h_off, const int64_t *h_len, int64_t n,
+                    uint32_t *h_crc);
 /* Inflate n_files gzip streams (each: every member back to back) in one launch,
  * one wave per stream (a whole file, or one BGZF member of one).  d_src +
  * d_in_off[f] (4-B aligned) holds d_in_len[f] bytes; the text goes to d_out +

@@ -155,3 +155,68 @@ def test_outside_the_common_case_hands_over(dev, tmp_path):
             nm.ingest_py(inds, d, None, None, None, {}, 20, 100, 2)
         assert got[0] == exp[0] and got[1] == exp[1]
         assert np.array_equal(np.asarray(got[2]), np.asarray(exp[2]))
+
+
+def test_host_text_guard_catches_a_corrupt_byte(dev, tmp_path, monkeypatch):
+    """The guard over host-inflated text: a byte of
+    d_text overwritten after the copy to HBM is caught by the CRC check before
+    the parse (DeviceIngestUnsupported), and ingest() then returns the host
+    parser's result.  Without the corruption the guard passes and the device
+    path gives the host parser's result itself."""
+    monkeypatch.setattr(ingest_device._Split, "plan", SPLITS["cpu"])
+    rng = np.random.default_rng(11)
+    files = {f"S{i:03d}": _rand_lines(rng, 2000) for i in range(5)}
+    d = _cohort(tmp_path, files, members=1)
+    samples = sorted(files)
+    _dev_vs_host(dev, d, samples)                      # clean: the guard passes
+    hits = []
+
+    def corrupt(dev_, d_text, toff, ks):
+        k = ks[len(ks) // 2]
+        pos = int(toff[k]) + 700
+        b = np.zeros(1, np.uint8)
+        _abi.call("grid_d2h", dev_.ctx, b.ctypes.data, d_text.ptr + pos, 1)
+        b[0] = ord("7") if b[0] != ord("7") else ord("3")      # a digit for a digit: still parses
+        _abi.call("grid_h2d", dev_.ctx, d_text.ptr + pos, b.ctypes.data, 1)
+        hits.append(k)
+
+    monkeypatch.setattr(ingest_device, "AFTER_HOST_TEXT", corrupt)
+    inds = nm.map_mosdepth_files_to_samples(d, samples)
+    with pytest.raises(ingest_device.DeviceIngestUnsupported, match="gzip CRC"):
+        nm._ingest_dev(dev, inds, d, None, None, None, {}, 20, 100, 2)
+    assert hits
+    got = nm.ingest(inds, d, None, None, None, {}, 20, 100, 2, dev=dev)
+    exp = nm.ingest_native(inds, d, None, None, None, {}, 20, 100, 2)
+    assert got[0] == exp[0] and got[1] == exp[1]
+    assert np.array_equal(np.asarray(got[2]), np.asarray(exp[2]))
+
+
+def test_device_error_hands_over_to_the_host_parser(dev, tmp_path, monkeypatch):
+    """a native error in the device path (here: the device buffers
+    cannot be allocated) is logged and the host parser reads the cohort."""
+    rng = np.random.default_rng(12)
+    files = {f"S{i:03d}": _rand_lines(rng, 1500) for i in range(3)}
+    d = _cohort(tmp_path, files, members=1)
+    inds = nm.map_mosdepth_files_to_samples(d, sorted(files))
+
+    def no_room(*a, **k):
+        raise _abi.GridNativeError("hipMalloc: out of memory (test)")
+
+    monkeypatch.setattr(dev, "alloc", no_room)
+    got = nm.ingest(inds, d, None, None, None, {}, 20, 100, 2, dev=dev)
+    exp = nm.ingest_native(inds, d, None, None, None, {}, 20, 100, 2)
+    assert got[0] == exp[0] and got[1] == exp[1]
+    assert np.array_equal(np.asarray(got[2]), np.asarray(exp[2]))
+
+
+def test_text_crc32_matches_zlib(dev):
+    """grid_text_crc32 (the guard's device CRC) against zlib over ranges that
+    cross its 1 MiB pieces, empty ones and unaligned starts."""
+    import zlib
+    rng = np.random.default_rng(13)
+    data = rng.integers(0, 256, 5 << 20, dtype=np.uint8)
+    buf = dev.upload(data)
+    offs = [0, 1, 3, 4096, (1 << 20) - 1, 12345, 0, 77]
+    lens = [0, 1, 17, 1 << 20, (1 << 20) + 2, (3 << 20) + 5, 5 << 20, 100]
+    got = _abi.text_crc32(dev, buf.ptr, offs, lens)
+    assert [int(c) for c in got] == [zlib.crc32(data[o:o + n].tobytes()) for o, n in zip(offs, lens)]

@@ -322,10 +322,17 @@ def test_host_gunzip_and_bgzf_members():
     assert _abi.gz_members(gzip.compress(t)) is None
     cases = [bg, gzip.compress(t, 1), gzip.compress(t[:999]) + b"\0\0" + gzip.compress(t[999:]),
              bg + b"\0" * 7]
+    import zlib
     for b in cases:
         out = np.empty(len(t) + 3, np.uint8)
         st, n = _abi.gunzip_host(b, out)
         assert st == 0 and out[:n].tobytes() == t
+        # the CRC the device ingest's guard checks HBM against: the members'
+        # trailer CRCs combined = the CRC of the whole text
+        st, n, crc = _abi.gunzip_host(b, out, with_crc=True)
+        assert st == 0 and crc == zlib.crc32(t)
+    one = gzip.compress(b"") + gzip.compress(t[:5])            # an empty first member
+    assert _abi.gunzip_host(one, np.empty(16, np.uint8), with_crc=True) == (0, 5, zlib.crc32(t[:5]))
     small = np.empty(100, np.uint8)
     assert _abi.gunzip_host(bg, small)[0] == _abi.GZ_ESPACE
     assert _abi.gunzip_host(b"plain text, not gzip", small)[0] == _abi.GZ_EHEADER

@@ -1,6 +1,6 @@
 """Multi-GPU path on CPU: the bin-sharded steps 4-7 chain (grid_amd/fused.py)
-run under torch.distributed with the gloo backend at world sizes 2 and 3
-must give bit-identical results to one rank, and to the oracle.
+run under torch.distributed with the gloo backend at world sizes 2, 3, 4, 5
+and 8 must give bit-identical results to one rank, and to the oracle.
 
 The compute ops are the CPU restatement in tests/cpu_ops.py (the product
 always uses HipOps); what is under test is the sharding: 8192-aligned
@@ -17,9 +17,14 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 N, M, K, ITERS = 20, 3 * 8192 + 517, 4, 6
+# the world-4/5/8 cohort: every rank of 8 owns bins (9 blocks of 8192, the last
+# partial), np = 512 rows in 2W segment blocks -- at W = 8 blocks 10-15 hold
+# only padding rows (n = 300), at W = 5 2W*B = 520 > np (padded blocks)
+WIDE = (300, 8 * 8192 + 517)
 
 
-def cohort():
+def cohort(n=N, m=M):
+    N, M = n, m
     rng = np.random.default_rng(11)
     base = rng.uniform(25, 55, M)
     clus = rng.integers(0, 3, N)
@@ -38,10 +43,11 @@ def cohort():
     return q, reads, offs, np.array(nbr, dtype=np.int32), np.ones(len(nbr))
 
 
-def run_chain(rank, world, comm, chunk=None, source="resident"):
+def run_chain(rank, world, comm, chunk=None, source="resident", shape=(N, M)):
     from grid_amd.fused import HostSource, Steps47, TorchAlloc, shard_range
     from tests.cpu_ops import NumpyOps
-    q, reads, off, nbr, w = cohort()
+    N, M = shape
+    q, reads, off, nbr, w = cohort(N, M)
     c0, c1 = shard_range(M, rank, world)
     qs = torch.from_numpy(np.ascontiguousarray(q[:, c0:c1]))
     st = Steps47(NumpyOps(), TorchAlloc("cpu"), N, M, c0, c1 - c0, k=K, n_nbr=3, n_iters=ITERS, comm=comm,
@@ -59,11 +65,12 @@ def run_chain(rank, world, comm, chunk=None, source="resident"):
     }
 
 
-def _worker(rank, world, port, out_path, chunk):
+def _worker(rank, world, port, out_path, chunk, shape=(N, M)):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from grid_amd.fused import TorchComm
-    res = run_chain(rank, world, TorchComm(dist), chunk=chunk)
+    res = run_chain(rank, world, TorchComm(dist), chunk=chunk, shape=shape)
     np.savez(f"{out_path}.{rank}.npz", **{k: np.asarray(v) for k, v in res.items()})
     dist.barrier()
     dist.destroy_process_group()
@@ -104,12 +111,46 @@ def test_streamed_equals_single(single, chunk, source):
         assert np.array_equal(np.asarray(res[key]), np.asarray(single[key]), equal_nan=True), key
 
 
-@pytest.mark.parametrize("world,chunk", [(2, None), (3, None), (2, 8192)])
-def test_sharded_equals_single(single, world, chunk, tmp_path):
+@pytest.fixture(scope="module")
+def single_wide():
+    return run_chain(0, 1, None, shape=WIDE)
+
+
+def _run_world(world, chunk, shape, tmp_path):
     port = _free_port()
     out = str(tmp_path / "res")
-    mp.start_processes(_worker, args=(world, port, out, chunk), nprocs=world, join=True, start_method="spawn")
-    parts = [dict(np.load(f"{out}.{r}.npz")) for r in range(world)]
+    mp.start_processes(_worker, args=(world, port, out, chunk, shape), nprocs=world, join=True,
+                       start_method="spawn")
+    return [dict(np.load(f"{out}.{r}.npz")) for r in range(world)]
+
+
+@pytest.mark.parametrize("world,chunk", [(2, None), (3, None), (2, 8192)])
+def test_sharded_equals_single(single, world, chunk, tmp_path):
+    _check_parts(_run_world(world, chunk, (N, M), tmp_path), single)
+
+
+@pytest.mark.parametrize("world,chunk", [(4, None), (5, None), (8, None), (8, 8192)])
+def test_sharded_world_4_5_8_equals_single(single_wide, world, chunk, tmp_path):
+    """the driver's 8-GPU layout (blocks r and 2W-1-r of
+    B = np/2W rows, the all-padding blocks of ranks 5-7 at n = 300, one or
+    two 8192-blocks of bins per rank) and a world (5) whose 2W*B exceeds np."""
+    from grid_amd.fused import shard_range
+    assert all(shard_range(WIDE[1], r, world)[1] > shard_range(WIDE[1], r, world)[0] for r in range(world))
+    _check_parts(_run_world(world, chunk, WIDE, tmp_path), single_wide)
+
+
+def test_wide_single_rank_matches_oracle_neighbours(single_wide):
+    """The world-1 reference of the wide cases against the oracle's exact
+    k-NN on the printed step-4 values (so the bit-identity above is anchored)."""
+    from oracle import steps
+    q = cohort(*WIDE)[0]
+    mat = np.where(q == -(2 ** 31), np.nan, q / 100.0)
+    z, ratios, mu, var, scale = steps.normalize_matrix(mat)
+    assert single_wide["scale"] == scale
+    assert single_wide["sel"].tolist() == steps.select_high_variance_regions(ratios, 0.1)
+
+
+def _check_parts(parts, single):
     for key in ("rm", "idx", "d2", "dip", "hap", "imp"):
         for p in parts:
             assert np.array_equal(p[key], single[key], equal_nan=True), key
