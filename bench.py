@@ -183,6 +183,54 @@ def cpu_baseline_from_files(n_target, m_target, k, n_iters):
                       "(single-threaded Python/NumPy, as the reference runs with threads=1)"}
 
 
+def from_files_config2(args, note):
+    """SURVEY 8(d)'s second number: BASELINE config 2 end to end FROM FILES --
+    `grid wgs` steps 4-7 through the drop-in step API (tools/e2e_files.py, a
+    child process: mosdepth BGZF regions.bed.gz files -> normalised gz text ->
+    neighbours -> dipCN -> haploid calls, every output file written) on a
+    synthetic 3,202-sample x 3 M-bin cohort written to /dev/shm before the
+    clock (tools/gen_cohort, the bench's depth model as mosdepth text).  The
+    record carries the per-step wall times and content digests of the output
+    files (runs compare byte for byte)."""
+    import shutil
+    import tempfile
+    root = os.path.dirname(os.path.abspath(__file__))
+    data = os.path.join(args.files_dir, "grid_bench_cfg2")
+    out = os.path.join(tempfile.gettempdir(), "grid_bench_cfg2_out")
+    js = os.path.join(tempfile.gettempdir(), f"grid_bench_cfg2_{os.getpid()}.json")
+    try:
+        free = shutil.disk_usage(args.files_dir).free
+    except OSError as e:
+        return {"skipped": f"{args.files_dir}: {e}"}
+    if free < 100e9:
+        return {"skipped": f"{args.files_dir} has {free / 1e9:.0f} GB free; the BGZF cohort needs ~76 GB"}
+    cmd = [sys.executable, "-u", os.path.join(root, "tools", "e2e_files.py"), "--bgzf", "--samples", "3202",
+           "--bins", "3000000", "--data", data, "--out", out, "--json", js, "--threads", str(args.files_threads)]
+    note("from files, config 2: generating the BGZF cohort (outside the clock), then grid wgs steps 4-7")
+    try:
+        rc = subprocess.run(cmd, stdout=subprocess.DEVNULL, timeout=args.files_timeout).returncode
+    except subprocess.TimeoutExpired:
+        rc = "timeout"
+    finally:
+        shutil.rmtree(data, ignore_errors=True)
+        shutil.rmtree(out, ignore_errors=True)
+    if rc != 0 or not os.path.exists(js):
+        return {"skipped": f"tools/e2e_files.py exited with {rc}"}
+    r = json.load(open(js))
+    os.remove(js)
+    ph = r["phases_s"]
+    stages = {k: round(v, 3) for k, v in ph.items() if k.startswith("step")}
+    return {"value": r["samples_per_s_from_files"], "unit": "samples/s", "steps_4_7_s": r["steps_4_7_s"],
+            "samples": 3202, "bins": 3_000_000, "stages_s": stages,
+            "cohort_generation_s": round(ph.get("generate_cohort", 0.0), 1), "cohort_bytes": r.get("cohort_bytes"),
+            "outputs_bytes": r.get("outputs"), "outputs_xxh3_64": r.get("outputs_xxh3_64"),
+            "peak_rss_gb": max(r.get("peak_rss_gb_after", {0: 0}).values()),
+            "workload": "BASELINE config 2 from files: 3202 mosdepth BGZF regions.bed.gz (3 M x 1 kb bins, '%.2f' "
+                        "depths) -> `grid wgs` steps 4-7 (drop-in step API, device ingest, every output file written "
+                        "to " + os.path.dirname(out) + "); cohort generated before the clock in " + args.files_dir,
+            "timed": "wall clock of the four step functions in one process (tools/e2e_files.py)"}
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -385,6 +433,12 @@ def main():
     ap.add_argument("--no-files-baseline", action="store_true",
                     help="skip the from-files oracle run at config 1 (~1 min of host time)")
     ap.add_argument("--no-overlap", action="store_true", help="run step 7 inline on the main stream")
+    ap.add_argument("--no-files-config2", action="store_true",
+                    help="N=1: skip the from-files config-2 record (BGZF cohort generated in --files-dir, ~1 min, "
+                         "then grid wgs steps 4-7 timed)")
+    ap.add_argument("--files-dir", default="/dev/shm")
+    ap.add_argument("--files-threads", type=int, default=16)
+    ap.add_argument("--files-timeout", type=float, default=360.0)
     ap.add_argument("--config3-steps", type=int, default=1,
                     help="N=1: timed steps of the BASELINE config-3 shape (50k x 3M, streamed) reported beside the "
                          "line as config3_1gpu (0 = skip)")
@@ -471,6 +525,8 @@ def main():
         if not args.no_files_baseline:
             note("cpu baseline: the oracle from files at config 1")
             out["cpu_baseline"]["from_files"] = cpu_baseline_from_files(n, m, args.k, args.n_iters)
+    if rank == 0 and world == 1 and not args.no_files_config2 and (n, m) == (3202, 3_000_000):
+        out["from_files_config2"] = from_files_config2(args, note)
     if rank == 0:
         print(json.dumps(out), file=result_out, flush=True)
     if dist:

@@ -135,11 +135,19 @@ _SIGS = {
     "grid_gz_members": [_vp, _i64, _vp, _vp, _vp, _i32, C.POINTER(_i32)],
     "grid_gunzip_host": [_vp, _i64, _vp, _i64, C.POINTER(_i64), C.POINTER(_i32), C.POINTER(C.c_uint32)],
     "grid_text_crc32": [_vp, _vp, _vp, _vp, _i64, _vp],
-    "grid_md_count": [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp],
+    "grid_md_count": [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp],
+    "grid_file_status": [_vp, _vp, _vp, _i64, _vp, _i64],
+    "grid_h2d_async": [_vp, _vp, _vp, C.c_size_t],
+    "grid_d2h_async": [_vp, _vp, _vp, C.c_size_t],
+    "grid_event_new": [C.POINTER(_vp)],
+    "grid_event_free": [_vp],
+    "grid_event_put": [_vp, _vp],
+    "grid_event_wait": [_vp, _vp],
+    "grid_event_host_wait": [_vp],
     "grid_md_parse_ref": [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp,
                           C.POINTER(_i64), C.POINTER(_i32)],
     "grid_md_parse_map": [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp,
-                          _vp],
+                          _vp, _vp],
     "grid_fill_i32": [_vp, _vp, _i64, _i32],
     "grid_md_finish": [_vp, _vp, _i64, _i64, _i64, _vp, _i32, _f64, _f64, _vp, _vp, _vp, _vp, _vp, C.POINTER(_i64)],
     "grid_md_gather": [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp],
@@ -284,6 +292,33 @@ class Device:
         f = C.c_float()
         call("grid_event_elapsed", self.ctx, a, b, C.byref(f))
         return float(f.value)
+
+
+class Event:
+    """A HIP event (timing disabled) for ordering streams and the host
+    (grid_event_*)."""
+
+    def __init__(self):
+        h = _vp()
+        call("grid_event_new", C.byref(h))
+        self.h = h.value
+
+    def put(self, dev: "Device"):
+        call("grid_event_put", dev.ctx, self.h)
+
+    def wait(self, dev: "Device"):
+        call("grid_event_wait", dev.ctx, self.h)
+
+    def host_wait(self):
+        call("grid_event_host_wait", self.h)
+
+    def __del__(self):
+        try:
+            if self.h:
+                load().grid_event_free(self.h)
+                self.h = None
+        except Exception:
+            pass
 
 
 class DevBuf:

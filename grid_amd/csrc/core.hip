@@ -138,6 +138,49 @@ int grid_h2d(grid_ctx *ctx, void *d, const void *h, size_t bytes) {
   return GRID_OK;
 }
 
+int grid_h2d_async(grid_ctx *ctx, void *d, const void *h, size_t bytes) {
+  if (!bytes) return GRID_OK;
+  HIPCHK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, ctx->stream));
+  return GRID_OK;
+}
+
+int grid_d2h_async(grid_ctx *ctx, void *h, const void *d, size_t bytes) {
+  if (!bytes) return GRID_OK;
+  HIPCHK(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  return GRID_OK;
+}
+
+int grid_event_new(void **ev) {
+  REQUIRE(ev, "ev is NULL");
+  hipEvent_t e;
+  HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  *ev = (void *)e;
+  return GRID_OK;
+}
+
+int grid_event_free(void *ev) {
+  if (ev) HIPCHK(hipEventDestroy((hipEvent_t)ev));
+  return GRID_OK;
+}
+
+int grid_event_put(grid_ctx *ctx, void *ev) {
+  REQUIRE(ctx && ev, "bad args");
+  HIPCHK(hipEventRecord((hipEvent_t)ev, ctx->stream));
+  return GRID_OK;
+}
+
+int grid_event_wait(grid_ctx *ctx, void *ev) {
+  REQUIRE(ctx && ev, "bad args");
+  HIPCHK(hipStreamWaitEvent(ctx->stream, (hipEvent_t)ev, 0));
+  return GRID_OK;
+}
+
+int grid_event_host_wait(void *ev) {
+  REQUIRE(ev, "ev is NULL");
+  HIPCHK(hipEventSynchronize((hipEvent_t)ev));
+  return GRID_OK;
+}
+
 int grid_d2h(grid_ctx *ctx, void *h, const void *d, size_t bytes) {
   if (!bytes) return GRID_OK;
   HIPCHK(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, ctx->stream));

@@ -75,8 +75,9 @@ __device__ __forceinline__ bool md_masked(const MdOpts &o, const uint8_t *c, int
 __global__ __launch_bounds__(256) void k_md_count(const uint8_t *__restrict__ text, const int64_t *__restrict__ toff,
                                                   const int64_t *__restrict__ tlen, const int32_t *__restrict__ cfile,
                                                   const int64_t *__restrict__ cstart, int32_t *__restrict__ cnl,
-                                                  int32_t *__restrict__ flags) {
+                                                  int32_t *__restrict__ flags, const int32_t *__restrict__ fst) {
   const int c = blockIdx.x, f = cfile[c];
+  if (fst && fst[f]) return;            // a file that did not inflate: dropped, its text never read
   const int64_t a = cstart[c], b = min(tlen[f], a + CH);
   const uint8_t *t = text + toff[f];
   int n = 0, hi = 0;
@@ -207,11 +208,13 @@ __global__ __launch_bounds__(PTH) void k_md_parse(const uint8_t *__restrict__ te
                                                   const int32_t *__restrict__ ref_kidx, int64_t ref_nlines,
                                                   int32_t *__restrict__ Q, int64_t ldq,
                                                   const int32_t *__restrict__ qrow,
-                                                  unsigned long long *__restrict__ kept) {
+                                                  unsigned long long *__restrict__ kept,
+                                                  const int32_t *__restrict__ fst) {
   constexpr int HALO = 16, SPAN = HALO + CH + MAXLINE + 16;   // bytes a-16 .. a+CH+MAXLINE (+16 slack)
   __shared__ __attribute__((aligned(16))) uint8_t s_t[SPAN];
   __shared__ int s_wsum[PTH / 64];
   const int c = blockIdx.x, f = cfile[c], tid = threadIdx.x;
+  if (fst && fst[f]) return;            // a file that did not inflate: dropped
   const int64_t L = tlen[f], a = cstart[c], b = min(L, a + CH);
   const uint8_t *t = text + toff[f];
   // load [a - 16, min(L, b + MAXLINE)): whole 16-byte words inside the file
@@ -348,6 +351,13 @@ __global__ __launch_bounds__(PTH) void k_md_parse(const uint8_t *__restrict__ te
   }
 }
 
+// per batch file: nonzero if any of its inflate units (BGZF members) failed
+__global__ void k_file_status(const int32_t *__restrict__ ust, const int64_t *__restrict__ owner, int64_t n,
+                              int32_t *__restrict__ fst) {
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u < n && ust[u] != 0) atomicOr(fst + owner[u], 1);
+}
+
 // K from the reference file: kept keys in line order, their K index per line
 __global__ void k_md_ref_index(const uint8_t *__restrict__ kept, const int64_t *__restrict__ pos, int64_t n,
                                const Key2 *__restrict__ keys, Key2 *__restrict__ K, int32_t *__restrict__ kidx) {
@@ -478,11 +488,11 @@ extern "C" {
 
 int grid_md_count(grid_ctx *ctx, const uint8_t *d_text, const int64_t *d_toff, const int64_t *d_tlen,
                   int64_t nchunks, const int32_t *d_cfile, const int64_t *d_cstart, const int32_t *d_cfirst,
-                  int64_t nfiles, int32_t *d_cnl, int64_t *d_cline0, int32_t *d_flags) {
+                  int64_t nfiles, int32_t *d_cnl, int64_t *d_cline0, int32_t *d_flags, const int32_t *d_fstatus) {
   REQUIRE(ctx && nchunks >= 0 && nchunks <= 0x7fffffff && nfiles >= 0, "bad args");
   if (nchunks == 0) return GRID_OK;
   hipLaunchKernelGGL(k_md_count, dim3((unsigned)nchunks), dim3(256), 0, ctx->stream, d_text, d_toff, d_tlen, d_cfile,
-                     d_cstart, d_cnl, d_flags);
+                     d_cstart, d_cnl, d_flags, d_fstatus);
   LAUNCHCHK();
   hipLaunchKernelGGL(k_md_scan, dim3((unsigned)((nfiles + 63) / 64)), dim3(64), 0, ctx->stream, d_cfirst, d_cnl,
                      d_cline0, (int)nfiles);
@@ -501,7 +511,7 @@ int grid_md_parse_ref(grid_ctx *ctx, const uint8_t *d_text, const int64_t *d_tof
   HIPCHK(hipMemsetAsync(d_kept_line, 0, (size_t)nlines, ctx->stream));
   hipLaunchKernelGGL(k_md_parse<0>, dim3((unsigned)nchunks), dim3(PTH), 0, ctx->stream, d_text, d_toff, d_tlen,
                      d_cfile, d_cstart, d_cline0, to_opts(opts), d_flags, d_kept_line, (Key2 *)d_keys_line, nlines,
-                     nullptr, (int64_t)0, nullptr, (int64_t)0, nullptr, (int64_t)0, nullptr, nullptr);
+                     nullptr, (int64_t)0, nullptr, (int64_t)0, nullptr, (int64_t)0, nullptr, nullptr, nullptr);
   LAUNCHCHK();
   // positions of the kept lines: exclusive scan of the flags (int64 output)
   void *s = nullptr;
@@ -538,12 +548,24 @@ int grid_md_parse_map(grid_ctx *ctx, const uint8_t *d_text, const int64_t *d_tof
                       int64_t nchunks, const int32_t *d_cfile, const int64_t *d_cstart, const int64_t *d_cline0,
                       const grid_md_opts *opts, int32_t *d_flags, const void *d_K, int64_t nK,
                       const int32_t *d_kidx, int64_t ref_nlines, int32_t *d_Q, int64_t ldq, const int32_t *d_qrow,
-                      uint64_t *d_kept) {
+                      uint64_t *d_kept, const int32_t *d_fstatus) {
   REQUIRE(ctx && opts && nchunks >= 0 && nK >= 0 && ldq >= nK, "bad args");
   if (nchunks == 0) return GRID_OK;
   hipLaunchKernelGGL(k_md_parse<1>, dim3((unsigned)nchunks), dim3(PTH), 0, ctx->stream, d_text, d_toff, d_tlen,
                      d_cfile, d_cstart, d_cline0, to_opts(opts), d_flags, nullptr, nullptr, (int64_t)0,
-                     (const Key2 *)d_K, nK, d_kidx, ref_nlines, d_Q, ldq, d_qrow, (unsigned long long *)d_kept);
+                     (const Key2 *)d_K, nK, d_kidx, ref_nlines, d_Q, ldq, d_qrow, (unsigned long long *)d_kept,
+                     d_fstatus);
+  LAUNCHCHK();
+  return GRID_OK;
+}
+
+int grid_file_status(grid_ctx *ctx, const int32_t *d_unit_status, const int64_t *d_owner, int64_t n_units,
+                     int32_t *d_fstatus, int64_t n_files) {
+  REQUIRE(ctx && n_units >= 0 && n_files >= 0, "bad args");
+  if (n_files > 0) HIPCHK(hipMemsetAsync(d_fstatus, 0, (size_t)n_files * 4, ctx->stream));
+  if (n_units == 0) return GRID_OK;
+  hipLaunchKernelGGL(k_file_status, dim3((unsigned)((n_units + 255) / 256)), dim3(256), 0, ctx->stream,
+                     d_unit_status, d_owner, n_units, d_fstatus);
   LAUNCHCHK();
   return GRID_OK;
 }

@@ -39,6 +39,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import threading
 import time
 from collections.abc import Sequence
 from concurrent.futures import ThreadPoolExecutor
@@ -51,6 +52,8 @@ from .._abi import MdOpts, call
 CH = 65536                      # parse chunk (mosdepth_dev.hip CH)
 BATCH_IN = 4 << 30              # compressed bytes per batch
 BATCH_TEXT = 24 << 30           # inflated bytes per batch
+FIRST_BATCH_IN = 256 << 20      # the first batch (read and inflated synchronously: the reference key list)
+PIPELINE = True                 # BGZF batches after the first: enqueued without host round trips (_Async)
 STAGE = 1 << 30                 # pinned staging per CPU sub-batch (two of them)
 TRACE = bool(os.environ.get("GRID_INGEST_TRACE"))   # per-batch phase times on stderr
 XSTREAM_WAIT = True             # dev's stream waits for the copy stream (False only in a GPU test's control arm)
@@ -180,6 +183,162 @@ def _chunks(files, tlen):
             len(cfile))
 
 
+def _release_pinned(held):
+    for pb in held:
+        if pb.b is not None:
+            pb.b.free()
+            pb.b = None
+
+
+class _Async:
+    """The device ingest's pipelined batches (every file BGZF, all inflated by
+    the GPU; after the first batch, which builds the key list K synchronously).
+    Per batch, with no host round trip:
+      copy stream:  [wait: batch b-2's parse done] compressed input + the batch's
+                    tables (member units, files, 64 KiB chunks: one pinned arena)
+                    -> HBM (d_in / tables of parity b % 2); event h2d[b % 2];
+      main stream:  [wait h2d] grid_gunzip_batch (inflate + CRC) -> grid_file_status
+                    (files with a failed member are skipped by the parse, as the
+                    reference drops them) -> grid_md_count -> grid_md_parse_map;
+                    event done[b % 2].
+    So batch b+1's 4 GB copy runs under batch b's inflate, and the host only
+    builds tables.  A file's text length is the sum of its members' ISIZEs
+    (the inflater checks every member against its ISIZE and CRC).  Statuses,
+    lengths, flags and kept counts stay on the device per batch and are read
+    once at the end (results)."""
+
+    def __init__(self, dev, cdev, opts, K, nK, kidx, ref_nlines, Q):
+        self.dev, self.cdev, self.opts = dev, cdev, opts
+        self.K, self.nK, self.kidx, self.ref_nlines, self.Q = K, nK, kidx, ref_nlines, Q
+        self.h2d = [_abi.Event(), _abi.Event()]
+        self.done = [_abi.Event(), _abi.Event()]
+        self.issued = [False, False]
+        self.arena_h = [_Pinned(64 << 20), _Pinned(64 << 20)]
+        self.arena_d = [None, None]
+        self.scr = [None, None]                 # per parity: member table, chunk counts/lines, file status
+        self.out = []                           # per batch: (fs, owner, unit status, unit length, flags, kept, okb)
+
+    @staticmethod
+    def _pack(parts):
+        offs, pos = [], 0
+        for a in parts:
+            offs.append(pos)
+            pos += _align(a.nbytes)
+        return offs, pos
+
+    def batch(self, bi, fs, buf, off, caps_, gz, members, toff, d_in, d_text, fsizes):
+        dev, cdev, p = self.dev, self.cdev, bi % 2
+        nb = len(fs)
+        mu = [k for k in range(nb) if gz[k] and fsizes[k] > 0 and members[k] is not None]
+        uo, ul, to, tc, owner = [], [], [], [], []
+        for k in mu:
+            ms, ml, mi = members[k]
+            uo.append(off[k] + ms)
+            ul.append(ml)
+            cum = np.zeros(len(mi), np.int64)
+            np.cumsum(mi[:-1], out=cum[1:])
+            to.append(toff[k] + cum)
+            tc.append(mi.astype(np.int64))
+            owner.append(np.full(len(mi), k, np.int64))
+        cat = (lambda x: np.concatenate(x) if x else np.zeros(0, np.int64))
+        units = [cat(x) for x in (uo, ul, to, tc, owner)]
+        nu = len(units[0])
+        tlen = np.zeros(nb, np.int64)               # text of a file that inflates: its members' ISIZEs
+        for k in mu:
+            tlen[k] = int(members[k][2].astype(np.int64).sum())
+        okb = [k for k in mu if tlen[k] > 0]
+        cfile, cstart, cfirst, nch = _chunks(okb, tlen)
+        parts = units + [tlen, np.ascontiguousarray(toff[:nb]), np.asarray(fs, np.int32), cfile, cstart, cfirst]
+        offs, nbytes = self._pack(parts)
+        # the arena of parity p: its previous copy (batch bi-2) must be done
+        if self.issued[p]:
+            self.h2d[p].host_wait()
+        host = self.arena_h[p].get(nbytes + 256)
+        for a, o in zip(parts, offs):
+            host[o:o + a.nbytes] = a.view(np.uint8).reshape(-1)
+        if self.arena_d[p] is None or self.arena_d[p].nbytes < nbytes + 256:
+            self.drain()
+            self.arena_d[p] = None
+            self.arena_d[p] = dev.alloc(max(nbytes + 256, 16 << 20) * 5 // 4, np.uint8)
+        need = (nu * _abi.GZ_MEMBER_BYTES, nu * 4, nch * 4, nch * 8, nb * 4)
+        sc = self.scr[p]
+        if sc is None or any(b.nbytes < n + 256 for b, n in zip(sc, need)):
+            self.drain()
+            self.scr[p] = None
+            self.scr[p] = sc = [dev.alloc(max(n + 256, 4096) * 5 // 4, np.uint8) for n in need]
+        mem, unm, cnl, cline0, fst = sc
+        # per-batch outputs read at the end (small)
+        ust, uln = dev.alloc(max(nu, 1), np.int32), dev.alloc(max(nu, 1), np.int64)
+        bflags, bk = dev.zeros(nb, np.int32), dev.zeros(nb, np.uint64)
+        # copy stream: after batch bi-2's parse (same parity buffers), the input and the tables
+        if self.issued[p]:
+            self.done[p].wait(cdev)
+        call("grid_h2d_async", cdev.ctx, d_in.ptr, buf.ctypes.data, int(off[-1]))
+        call("grid_h2d_async", cdev.ctx, self.arena_d[p].ptr, host.ctypes.data, nbytes)
+        self.h2d[p].put(cdev)
+        # main stream
+        self.h2d[p].wait(dev)
+        A = self.arena_d[p].ptr
+        d_uo, d_ul, d_to, d_tc, d_own, d_tl, d_toff, d_qrow, d_cf, d_cs, d_c1 = (A + o for o in offs)
+        if nu:
+            call("grid_gunzip_batch", dev.ctx, d_in.ptr, d_uo, d_ul, nu, d_text.ptr, d_to, d_tc, mem.ptr, 1,
+                 ust.ptr, uln.ptr, unm.ptr)
+        call("grid_file_status", dev.ctx, ust.ptr, d_own, nu, fst.ptr, nb)
+        if nch:
+            call("grid_md_count", dev.ctx, d_text.ptr, d_toff, d_tl, nch, d_cf, d_cs, d_c1, len(okb), cnl.ptr,
+                 cline0.ptr, bflags.ptr, fst.ptr)
+            call("grid_md_parse_map", dev.ctx, d_text.ptr, d_toff, d_tl, nch, d_cf, d_cs, cline0.ptr,
+                 C.byref(self.opts), bflags.ptr, self.K.ptr, self.nK, self.kidx.ptr, self.ref_nlines, self.Q.ptr,
+                 self.nK, d_qrow, bk.ptr, fst.ptr)
+        self.done[p].put(dev)
+        self.issued[p] = True
+        # not gzip at all: dropped (GZ_EHEADER in the synchronous path)
+        hdr_bad = [k for k in range(nb) if not gz[k] and fsizes[k] > 0]
+        self.out.append((list(fs), units[4], ust, uln, bflags, bk, okb, nu, hdr_bad))
+        return self.h2d[p]
+
+    def drain(self):
+        self.dev.sync()
+        self.cdev.sync()
+
+    def results(self, paths):
+        """(file, status 0/1, kept) per file of the pipelined batches; raises
+        DeviceIngestUnsupported for a parse flag, as the synchronous path."""
+        res = []
+        self.kept = []
+        for fs, owner, ust, uln, bflags, bk, okb, nu, hdr_bad in self.out:
+            nb = len(fs)
+            bad = np.zeros(nb, np.int32)
+            bad[hdr_bad] = _abi.GZ_EHEADER
+            if nu:
+                st = ust.numpy()[:nu]
+                # a member past its BGZF size is corrupt (dropped), not several members
+                np.maximum.at(bad, owner, np.where(st == _abi.GZ_ESPACE, _abi.GZ_EDATA, st))
+            bf, bkv = bflags.numpy(), bk.numpy()
+            for k in okb:
+                if bad[k] == 0 and bf[k]:
+                    why = "a line outside the mosdepth grammar" if bf[k] & _abi.MD_EXOTIC else "a key outside K"
+                    raise DeviceIngestUnsupported(f"{paths[fs[k]]}: {why}")
+            for k, f in enumerate(fs):
+                res.append((f, 0 if bad[k] == 0 else 1, int(bkv[k])))
+            self.kept.append((np.asarray(fs), bkv))
+        return res
+
+    def kept_total(self, nfiles):
+        tot = np.zeros(max(nfiles, 1), np.uint64)
+        for fs, bkv in self.kept:
+            tot[fs] += bkv
+        return tot
+
+    def close(self):
+        try:
+            self.drain()
+        finally:
+            self.out = []
+            self.arena_d = [None, None]
+            self.scr = [None, None]
+
+
 def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, threads=16):
     """paths: one per individual in file order (None = no file).  Returns
     (ok files in file order, the device state for ``gather``, records in valid
@@ -196,7 +355,8 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
     # batches in file order
     batches, cur, cin = [], [], 0
     for f in order:
-        if cur and cin + _align(sizes[f]) > BATCH_IN:
+        lim = min(FIRST_BATCH_IN, BATCH_IN) if not batches else BATCH_IN
+        if cur and cin + _align(sizes[f]) > lim:
             batches.append(cur)
             cur, cin = [], 0
         cur.append(f)
@@ -214,10 +374,14 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
     cdev = _abi.Device(dev.index)          # its own non-blocking stream
     split = _Split(nthreads)
 
+    h2d_done = [None] * len(batches)       # per pipelined batch: the event after its copies to HBM
+
     def read_batch(bi):
         fs = batches[bi]
         off = np.zeros(len(fs) + 1, np.int64)
         off[1:] = np.cumsum([_align(max(sizes[f], 1)) for f in fs])
+        if bi >= 2 and h2d_done[bi - 2] is not None:
+            h2d_done[bi - 2].host_wait()        # pins[bi % 2] still feeds batch bi-2's copy
         buf = pins[bi % 2].get(int(off[-1]) + 256)
 
         def one(k):
@@ -233,7 +397,7 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
         info = list(pool.map(one, range(len(fs))))
         return buf, off, [i[0] for i in info], [i[1] for i in info]
 
-    def inflate(buf, off, fs, caps_, gz, members, toff, d_in, d_text):
+    def inflate(buf, off, fs, caps_, gz, members, toff, d_in, d_text, plan):
         """Inflate the batch's files into d_text + toff[k]; (status, length) per file."""
         nb = len(fs)
         gst = np.zeros(nb, np.int32)
@@ -246,7 +410,7 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
             elif not gz[k]:
                 gst[k] = _abi.GZ_EHEADER
         bgzf = {k: members[k] is not None for k in todo}
-        on_gpu, on_cpu = split.plan(todo, caps_, bgzf)
+        on_gpu, on_cpu = plan
         t0 = time.perf_counter()
         launched = []
         if on_gpu:
@@ -354,7 +518,9 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
 
     K = kidx = Q = None
     nK = ref_nlines = 0
-    d_in = d_text = None
+    d_text = None
+    d_ins = [None, None]
+    pipe = None
     pending = rpool.submit(read_batch, 0) if batches else None
     try:
         for bi, fs in enumerate(batches):
@@ -372,13 +538,36 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
             # device buffers sized from the cohort, not from the batch bounds: the
             # compressed bytes of the largest batch (known from the file sizes), the
             # text grown with 1/8 headroom as batches need it
-            if d_in is None:
-                d_in = dev.alloc(in_need, np.uint8)
+            if d_ins[bi % 2] is None or d_ins[bi % 2].nbytes < off[-1] + 256:
+                if pipe is not None:
+                    pipe.drain()
+                d_ins[bi % 2] = None
+                d_ins[bi % 2] = dev.alloc(in_need if bi else int(off[-1]) + 256, np.uint8)
             if d_text is None or d_text.nbytes < toff[-1] + 256:
+                if pipe is not None:
+                    pipe.drain()
                 d_text = None
                 d_text = dev.alloc(int(min(toff[-1] + 256 + toff[-1] // 8, 2 * BATCH_TEXT + 256)), np.uint8)
+            d_in = d_ins[bi % 2]
+            todo = [k for k in range(nb) if gz[k] and sizes[fs[k]] > 0]
+            bgzf = {k: members[k] is not None for k in todo}
+            plan = split.plan(todo, caps_, bgzf)
+            if PIPELINE and K is not None and all(bgzf.values()) and not plan[1]:
+                # every file BGZF (what mosdepth writes): the GPU inflates all of
+                # them, and the batch is enqueued behind the previous one
+                if pipe is None:
+                    pipe = _Async(dev, cdev, opts, K, nK, kidx, ref_nlines, Q)
+                h2d_done[bi] = pipe.batch(bi, fs, buf, off, caps_, gz, members, toff, d_in, d_text,
+                                          [sizes[f] for f in fs])
+                if TRACE:
+                    import sys
+                    print(f"[ingest] batch {bi}: {nb} files enqueued, wait read {time.perf_counter() - t_w:.3f} s "
+                          f"(at {time.perf_counter() - t_start:.3f})", file=sys.stderr, flush=True)
+                continue
+            if pipe is not None:
+                pipe.drain()
             t_b = time.perf_counter()
-            gst, tlen = inflate(buf, off, fs, caps_, gz, members, toff, d_in, d_text)
+            gst, tlen = inflate(buf, off, fs, caps_, gz, members, toff, d_in, d_text, plan)
             t_i = time.perf_counter()
             for k, f in enumerate(fs):
                 if gst[k] == _abi.GZ_ESPACE:
@@ -394,7 +583,7 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
             # flags per batch file, folded into the cohort's afterwards
             bflags = dev.zeros(nb, np.int32)
             call("grid_md_count", dev.ctx, d_text.ptr, d_toff.ptr, d_tl.ptr, nch, d_cfile.ptr, d_cstart.ptr,
-                 d_cfirst.ptr, len(okb), cnl.ptr, cline0.ptr, bflags.ptr)
+                 d_cfirst.ptr, len(okb), cnl.ptr, cline0.ptr, bflags.ptr, None)
             if K is None:
                 # the reference key list: the first file that inflated with text
                 r = okb[0]
@@ -425,7 +614,8 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
             qrow = dev.upload(np.asarray(fs, np.int32))
             bk = dev.zeros(nb, np.uint64)
             call("grid_md_parse_map", dev.ctx, d_text.ptr, d_toff.ptr, d_tl.ptr, nch, d_cfile.ptr, d_cstart.ptr,
-                 cline0.ptr, C.byref(opts), bflags.ptr, K.ptr, nK, kidx.ptr, ref_nlines, Q.ptr, nK, qrow.ptr, bk.ptr)
+                 cline0.ptr, C.byref(opts), bflags.ptr, K.ptr, nK, kidx.ptr, ref_nlines, Q.ptr, nK, qrow.ptr, bk.ptr,
+                 None)
             bf, bkv = bflags.numpy(), bk.numpy()
             for k in okb:
                 if bf[k]:
@@ -439,12 +629,25 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
                 print(f"[ingest] batch {bi}: {nb} files, wait read {t_b - t_w:.3f} inflate {t_i - t_b:.3f} "
                       f"parse {time.perf_counter() - t_i:.3f} s (at {time.perf_counter() - t_start:.3f})",
                       file=sys.stderr, flush=True)
+        if pipe is not None:
+            t_d = time.perf_counter()
+            pipe.drain()
+            for f, st_, kp in pipe.results(paths):
+                status[f] = st_
+            kept_h = kept.numpy()
+            kept_h += pipe.kept_total(nfiles)
+            kept.copy_from(kept_h)
+            if TRACE:
+                import sys
+                print(f"[ingest] pipeline drained in {time.perf_counter() - t_d:.3f} s", file=sys.stderr, flush=True)
     finally:
         if pending is not None:
             try:
                 pending.result()
             except Exception:
                 pass
+        if pipe is not None:
+            pipe.close()
         rpool.shutdown(wait=True)
         pool.shutdown(wait=True)
         copier.shutdown(wait=True)
@@ -452,7 +655,18 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
         cdev.close()
     if TRACE:
         import sys
-        print(f"[ingest] batches done at {time.perf_counter() - t_start:.3f} s", file=sys.stderr, flush=True)
+        print(f"[ingest] batches done (threads joined, copy context closed) at {time.perf_counter() - t_start:.3f} s",
+              file=sys.stderr, flush=True)
+    # the staging buffers: GBs of page-locked memory whose release (unpinning)
+    # takes a fraction of a second -- done on a thread of its own, off the step's path
+    held = [pb for grp in ([pins, stages] + ([pipe.arena_h] if pipe is not None else [])) for pb in grp]
+    threading.Thread(target=_release_pinned, args=(held,), daemon=True).start()
+    held = None
+    d_ins = d_text = pipe = None
+    if TRACE:
+        import sys
+        print(f"[ingest] input/text buffers freed at {time.perf_counter() - t_start:.3f} s", file=sys.stderr,
+              flush=True)
     if K is None:
         return [], [], None, status
     rows = np.array([f for f in range(nfiles) if status[f] == 0], np.int32)

@@ -348,6 +348,8 @@ def _ingest_dev(dev, individuals, mosdepth_dir, chromosome, start, end, excluded
     rows, state, nval, status = ingest_device.ingest_device(
         dev, paths, norm_chrom(chromosome) if chromosome else None, window, excluded or {}, min_depth, max_depth,
         threads=max(1, int(threads or 1)))
+    if ingest_device.TRACE:
+        print(f"[ingest] device ingest returned at {time.perf_counter() - t0:.3f} s", file=sys.stderr, flush=True)
     keep = {ind: i for i, ind in enumerate(inds) if status[i] == 0 and state is not None and nval[i] > 0}
     removed = len(inds) - len(keep)
     if removed > 0:                           # filter_empty_samples (:576-600)

@@ -74,6 +74,19 @@ int grid_host_free(void *h_ptr);
 int grid_h2d(grid_ctx *ctx, void *d_dst, const void *h_src, size_t bytes);
 int grid_d2h(grid_ctx *ctx, void *h_dst, const void *d_src, size_t bytes);
 int grid_d2d(grid_ctx *ctx, void *d_dst, const void *d_src, size_t bytes);
+/* Asynchronous copies on the context stream (page-locked host memory; the
+ * caller keeps the host buffer unchanged until an event after the copy). */
+int grid_h2d_async(grid_ctx *ctx, void *d_dst, const void *h_src, size_t bytes);
+int grid_d2h_async(grid_ctx *ctx, void *h_dst, const void *d_src, size_t bytes);
+/* Named events for stream-to-stream and stream-to-host ordering (the device
+ * ingest's pipeline: copy stream -> inflate/parse stream -> host reuse of the
+ * staging buffers).  put = record on ctx's stream; wait = ctx's stream waits;
+ * host_wait = the calling thread blocks until the event completes. */
+int grid_event_new(void **ev);
+int grid_event_free(void *ev);
+int grid_event_put(grid_ctx *ctx, void *ev);
+int grid_event_wait(grid_ctx *ctx, void *ev);
+int grid_event_host_wait(void *ev);
 int grid_memset(grid_ctx *ctx, void *d_dst, int value, size_t bytes);
 /* Event timing on the context stream (for bench.py): returns ms between two
  * recorded markers. */
@@ -569,7 +582,7 @@ typedef struct grid_md_opts {
 /* newlines per chunk and their per-file prefix; flags |= GRID_MD_EXOTIC for bytes >= 0x80 */
 int grid_md_count(grid_ctx *ctx, const uint8_t *d_text, const int64_t *d_toff, const int64_t *d_tlen,
                   int64_t nchunks, const int32_t *d_cfile, const int64_t *d_cstart, const int32_t *d_cfirst,
-                  int64_t nfiles, int32_t *d_cnl, int64_t *d_cline0, int32_t *d_flags);
+                  int64_t nfiles, int32_t *d_cnl, int64_t *d_cline0, int32_t *d_flags, const int32_t *d_fstatus);
 /* the reference file (one file, nlines lines): its kept keys in line order -> the key list
  * d_K ((start, end) int64 pairs, *h_nK of them), d_kidx[line] = K index or -1; *h_unsorted = 1
  * when the keys are not strictly increasing (the caller then uses the host parser) */
@@ -582,7 +595,14 @@ int grid_md_parse_map(grid_ctx *ctx, const uint8_t *d_text, const int64_t *d_tof
                       int64_t nchunks, const int32_t *d_cfile, const int64_t *d_cstart, const int64_t *d_cline0,
                       const grid_md_opts *opts, int32_t *d_flags, const void *d_K, int64_t nK,
                       const int32_t *d_kidx, int64_t ref_nlines, int32_t *d_Q, int64_t ldq, const int32_t *d_qrow,
-                      uint64_t *d_kept);
+                      uint64_t *d_kept, const int32_t *d_fstatus);
+/* d_fstatus (may be NULL in grid_md_count / grid_md_parse_map: every file parsed) = per batch
+ * file, nonzero when any of its inflate units failed (the file is dropped, as the reference
+ * drops a sample whose gzip does not read): grid_file_status folds the units' statuses of a
+ * grid_gunzip_batch launch (d_owner[u] = the unit's batch file) on the stream, so the parse
+ * needs no host round trip to know which files inflated */
+int grid_file_status(grid_ctx *ctx, const int32_t *d_unit_status, const int64_t *d_owner, int64_t n_units,
+                     int32_t *d_fstatus, int64_t n_files);
 int grid_fill_i32(grid_ctx *ctx, int32_t *d_p, int64_t n, int32_t v);
 /* population means over the rows d_rows (file order), valid columns, their positions
  * (*h_m valid), per row: entries present and entries present in valid columns */

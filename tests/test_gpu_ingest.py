@@ -57,7 +57,13 @@ def split(request, monkeypatch):
 
 
 def _dev_vs_host(dev, d, samples, chrom=None, start=None, end=None, excluded=None, lo=20, hi=100):
-    inds = nm.map_mosdepth_files_to_samples(d, samples)
+    # the file order is the caller's sample order, not the directory's glob
+    # order: the device path takes the first file that inflates as its key
+    # list, and a later file with a key outside it hands the cohort to the host
+    # parser (test_subset_reference_file_hands_over) -- the r03af failure was
+    # exactly that, a shorter file first in one box's directory order
+    m = nm.map_mosdepth_files_to_samples(d, samples)
+    inds = {s: m[s] for s in samples if s in m}
     ex = excluded or {}
     a = nm._ingest_dev(dev, inds, d, chrom, start, end, ex, lo, hi, 4)
     b = nm.ingest_native(inds, d, chrom, start, end, ex, lo, hi, 4)
@@ -128,6 +134,30 @@ def test_subsets_bgzf_empty_corrupt_and_zero_depth(dev, tmp_path, split, monkeyp
     samples = sorted(files) + ["E000", "C000", "N000", "B000"]
     a = _dev_vs_host(dev, d, samples)
     assert len(a[0]) == 8
+
+
+def test_subset_reference_file_hands_over(dev, tmp_path):
+    """The cause of the r03af failure, shown deterministically: when the first
+    file that inflates (the device path's key list K) holds only a subset of
+    the bins, a later file's record has a key outside K, and the device path
+    hands the cohort over (DeviceIngestUnsupported); ingest() then returns the
+    host parser's result.  Which file is first follows the directory's glob
+    order (map_mosdepth_files_to_samples, reference normalize_mosdepth.py:162),
+    so the earlier test met this case only on some boxes."""
+    rng = np.random.default_rng(2)
+    base = _rand_lines(rng, 3000)
+    files = {"A_short": base[:2500], "B_full": base, "C_full": list(base)}
+    d = _cohort(tmp_path, files, members=1)
+    m = nm.map_mosdepth_files_to_samples(d, list(files))
+    inds = {k: m[k] for k in ("A_short", "B_full", "C_full")}
+    with pytest.raises(ingest_device.DeviceIngestUnsupported, match="a key outside K"):
+        nm._ingest_dev(dev, inds, d, None, None, None, {}, 20, 100, 2)
+    got = nm.ingest(inds, d, None, None, None, {}, 20, 100, 2, dev=dev)
+    exp = nm.ingest_native(inds, d, None, None, None, {}, 20, 100, 2)
+    assert got[0] == exp[0] and got[1] == exp[1]
+    assert np.array_equal(np.asarray(got[2]), np.asarray(exp[2]))
+    # the full file first: the device path itself
+    _dev_vs_host(dev, d, ["B_full", "A_short", "C_full"])
 
 
 def test_outside_the_common_case_hands_over(dev, tmp_path):
@@ -220,3 +250,46 @@ def test_text_crc32_matches_zlib(dev):
     lens = [0, 1, 17, 1 << 20, (1 << 20) + 2, (3 << 20) + 5, 5 << 20, 100]
     got = _abi.text_crc32(dev, buf.ptr, offs, lens)
     assert [int(c) for c in got] == [zlib.crc32(data[o:o + n].tobytes()) for o, n in zip(offs, lens)]
+
+
+def test_pipelined_batches_equal_the_host_parser(dev, tmp_path, monkeypatch):
+    """The pipelined BGZF batches (ingest_device._Async: copies on their own
+    stream, no host round trip per batch, failed files skipped on the device)
+    against the host parser, and against the synchronous path, over several
+    batches with a corrupt member, a truncated file, an empty file and a file
+    that is not gzip in later batches."""
+    monkeypatch.setattr(ingest_device, "BATCH_IN", 40 << 10)
+    rng = np.random.default_rng(21)
+    base = _rand_lines(rng, 3000)
+    files = {}
+    for i in range(10):
+        lines = list(base)
+        for j in rng.choice(len(lines), 30, replace=False):
+            lines[j] = lines[j].rsplit("\t", 1)[0] + "\t0.00\n"
+        files[f"S{i:03d}"] = lines
+    d = tmp_path / "md"
+    d.mkdir()
+    for name, lines in files.items():
+        (d / f"{name}.regions.bed.gz").write_bytes(_bgzf("".join(lines).encode()))
+    bg = bytearray(_bgzf("".join(files["S004"]).encode()))
+    bg[len(bg) // 2] ^= 0x55
+    (d / "X001.regions.bed.gz").write_bytes(bytes(bg))                  # corrupt member: dropped
+    good = (d / "S002.regions.bed.gz").read_bytes()
+    (d / "X002.regions.bed.gz").write_bytes(good[: len(good) // 2])     # truncated: dropped
+    (d / "X003.regions.bed.gz").write_bytes(b"")                        # empty: no lines
+    (d / "X004.regions.bed.gz").write_bytes(b"not gzip")                # dropped
+    samples = sorted(files)[:3] + ["X001", "X002"] + sorted(files)[3:] + ["X003", "X004"]
+    calls = []
+    orig = ingest_device._Async.batch
+
+    def counted(self, *a, **k):
+        calls.append(1)
+        return orig(self, *a, **k)
+
+    monkeypatch.setattr(ingest_device._Async, "batch", counted)
+    a = _dev_vs_host(dev, d, samples)
+    assert len(calls) >= 3, "the pipelined path did not run"
+    monkeypatch.setattr(ingest_device, "PIPELINE", False)
+    b = _dev_vs_host(dev, d, samples)
+    assert a[0] == b[0] and a[1] == b[1]
+    assert np.array_equal(a[2].numpy(), b[2].numpy())

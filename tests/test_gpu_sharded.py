@@ -1,5 +1,5 @@
 """Multi-GPU path with the real HIP kernels: the bin-sharded steps 4-7 chain
-at world sizes 2 and 3 (ranks sharing the one visible GPU, gloo standing in
+at world sizes 2, 3, 4 and 8 (ranks sharing the one visible GPU, gloo standing in
 for RCCL, which needs a GPU per rank) must give bit-identical neighbours,
 dipCN and phasing to one rank, with step 7 on its own stream (the bench's
 overlapped configuration) on every rank."""
@@ -14,7 +14,7 @@ import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
 
-N, M, K, ITERS = 300, 5 * 8192 + 517, 6, 12
+N, M, K, ITERS = 300, 8 * 8192 + 517, 6, 12     # 9 bin blocks: every rank of 8 owns bins
 
 
 def cohort():
@@ -90,7 +90,7 @@ def single():
     return run_chain(0, 1, None, lane=False)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_gpu_sharded_equals_single(single, world, tmp_path):
     port = _free_port()
     out = str(tmp_path / "res")

@@ -147,7 +147,17 @@ def test_wide_single_rank_matches_oracle_neighbours(single_wide):
     mat = np.where(q == -(2 ** 31), np.nan, q / 100.0)
     z, ratios, mu, var, scale = steps.normalize_matrix(mat)
     assert single_wide["scale"] == scale
-    assert single_wide["sel"].tolist() == steps.select_high_variance_regions(ratios, 0.1)
+    sel = steps.select_high_variance_regions(ratios, 0.1)
+    assert single_wide["sel"].tolist() == sel
+    # step 5 on the printed values, as smoke() does
+    raw = np.nanmean(mat, axis=1)
+    lines = steps.normalized_lines(z, [f"S{i}" for i in range(WIDE[0])], sel, mu, var, raw)
+    ids, r5, z5, sc5 = steps.parse_normalized(lines)
+    idx5, _ = steps.filter_regions_by_variance(r5, 1.0, 1000.0)
+    qz = np.rint(np.nan_to_num(np.clip(z5, -2.0, 2.0), nan=0.0)[:, idx5] * 100).astype(np.int64)
+    nb = steps.knn_exact(qz, K)
+    for i in range(WIDE[0]):
+        assert single_wide["idx"][i, : len(nb[i])].tolist() == [j for j, _ in nb[i]], i
 
 
 def _check_parts(parts, single):

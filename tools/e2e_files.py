@@ -58,17 +58,14 @@ ids = [f"S{i:05d}" for i in range(a.samples)]
 # ---- inputs --------------------------------------------------------------
 t0 = time.perf_counter()
 gen = os.path.join(ROOT, "tools", "gen_cohort")
-if not os.path.exists(gen):
-    subprocess.run(["g++", "-O3", "-std=c++17", "-pthread", "-o", gen, gen + ".cpp", "-lz"], check=True)
+if not os.path.exists(gen) or os.path.getmtime(gen) < os.path.getmtime(gen + ".cpp"):
+    subprocess.run(["g++", "-O3", "-std=c++17", "-pthread", "-o", gen, gen + ".cpp", "-lz", "-ldl"], check=True)
 have = len([f for f in os.listdir(mos) if f.endswith(".regions.bed.gz")])
 if have != a.samples:
     note(f"generating {a.samples} x {a.bins} mosdepth files in {mos}")
-    step = 200
-    for i0 in range(0, a.samples, step):        # batches: progress lines for the watchdog
-        n_b = min(step, a.samples - i0)
-        subprocess.run([gen, mos, str(n_b), str(a.bins), "20260821", str(a.threads), str(i0)]
-                       + (["bgzf"] if a.bgzf else []), check=True)
-        note(f"  {i0 + n_b} files")
+    # one call (the per-bin tables once); it prints a progress line per 200 files
+    subprocess.run([gen, mos, str(a.samples), str(a.bins), "20260821", str(a.threads), "0"]
+                   + (["bgzf"] if a.bgzf else []), check=True)
 res["phases_s"]["generate_cohort"] = time.perf_counter() - t0
 res["cohort_bytes"] = sum(os.path.getsize(os.path.join(mos, f)) for f in os.listdir(mos))
 
@@ -144,6 +141,24 @@ for step, fun in (("step4", lambda: nm.normalize_mosdepth(cfg, None)), ("step5",
     note(f"{step} done in {res['phases_s'][step + '_total']:.1f} s, peak RSS {rss_gb():.1f} GB")
 
 res["outputs"] = {f: os.path.getsize(os.path.join(a.out, f)) for f in sorted(os.listdir(a.out))}
+try:                                    # content digests (outside the timed steps): runs compare byte for byte
+    import xxhash
+
+    def digest(path):
+        # a small .gz (Python's gzip.open, as the reference's writers) carries
+        # its write time in the header: digest its text; the device writer's
+        # large file has MTIME 0: its bytes
+        h = xxhash.xxh3_64()
+        small_gz = path.endswith(".gz") and os.path.getsize(path) < (64 << 20)
+        with (gzip.open(path, "rb") if small_gz else open(path, "rb")) as fh:
+            for blk in iter(lambda: fh.read(1 << 26), b""):
+                h.update(blk)
+        return h.hexdigest()
+    t = time.perf_counter()
+    res["outputs_xxh3_64"] = {f: digest(os.path.join(a.out, f)) for f in sorted(os.listdir(a.out))}
+    res["phases_s"]["digest_outputs"] = time.perf_counter() - t
+except ImportError:
+    pass
 res["steps_4_7_s"] = sum(res["phases_s"][s + "_total"] for s in ("step4", "step5", "step6", "step7"))
 res["samples_per_s_from_files"] = a.samples / res["steps_4_7_s"]
 os.makedirs(os.path.dirname(a.json), exist_ok=True)

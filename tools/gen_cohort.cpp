@@ -7,9 +7,10 @@
 // one gzip member per file, or with "bgzf" BGZF (what mosdepth writes through
 // htslib: 65280-byte blocks, each its own member with the "BC" length field,
 // then the 28-byte end-of-file member).
-//   g++ -O3 -std=c++17 -pthread -o tools/gen_cohort tools/gen_cohort.cpp -lz
+//   g++ -O3 -std=c++17 -pthread -o tools/gen_cohort tools/gen_cohort.cpp -lz -ldl
 //   tools/gen_cohort DIR N_SAMPLES N_BINS SEED THREADS [FIRST_SAMPLE [bgzf]]
 // (samples FIRST_SAMPLE .. FIRST_SAMPLE + N_SAMPLES - 1: batches of one cohort)
+#include <dlfcn.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -30,23 +31,57 @@ static inline uint64_t mix(uint64_t z) {
   return z ^ (z >> 31);
 }
 static inline float unif(uint64_t h) { return (float)(h >> 40) * (1.0f / 16777216.0f); }
+// libdeflate (the system library, loaded at run time; its header is not in the
+// image) for the BGZF blocks: ~3x zlib's level-1 rate; zlib without it
+struct Ldf {
+  void *(*alloc_c)(int) = nullptr;
+  size_t (*deflate_c)(void *, const void *, size_t, void *, size_t) = nullptr;
+  void (*free_c)(void *) = nullptr;
+  uint32_t (*crc)(uint32_t, const void *, size_t) = nullptr;
+  bool ok = false;
+  Ldf() {
+    if (getenv("GRID_NO_LIBDEFLATE")) return;
+    void *h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return;
+    alloc_c = (void *(*)(int))dlsym(h, "libdeflate_alloc_compressor");
+    deflate_c = (size_t (*)(void *, const void *, size_t, void *, size_t))dlsym(h, "libdeflate_deflate_compress");
+    free_c = (void (*)(void *))dlsym(h, "libdeflate_free_compressor");
+    crc = (uint32_t (*)(uint32_t, const void *, size_t))dlsym(h, "libdeflate_crc32");
+    ok = alloc_c && deflate_c && free_c && crc;
+  }
+};
+static const Ldf g_ldf;
 // BGZF writer: text in, 65280-byte blocks out as gzip members
 struct Bgzf {
   FILE *f = nullptr;
   std::vector<char> blk;
   std::vector<unsigned char> z;
+  void *comp = nullptr;           // libdeflate compressor (level 1), one per writer
   bool ok = true;
-  explicit Bgzf(FILE *ff) : f(ff), z(70000) { blk.reserve(65280); }
+  explicit Bgzf(FILE *ff) : f(ff), z(70000) {
+    blk.reserve(65280);
+    if (g_ldf.ok) comp = g_ldf.alloc_c(1);
+  }
+  ~Bgzf() {
+    if (comp) g_ldf.free_c(comp);
+  }
   void block(const char *p, size_t n, int level) {
-    z_stream s{};
-    deflateInit2(&s, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY);
-    s.next_in = (Bytef *)p;
-    s.avail_in = (uInt)n;
-    s.next_out = z.data() + 18;
-    s.avail_out = (uInt)(z.size() - 26);
-    const int rc = deflate(&s, Z_FINISH);
-    const size_t c = z.size() - 26 - s.avail_out;
-    deflateEnd(&s);
+    size_t c = 0;
+    int rc = Z_STREAM_END;
+    if (comp && level) {
+      c = g_ldf.deflate_c(comp, p, n, z.data() + 18, 65536 - 26);
+      if (c == 0) rc = Z_BUF_ERROR;        // did not fit: stored below
+    } else {
+      z_stream s{};
+      deflateInit2(&s, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY);
+      s.next_in = (Bytef *)p;
+      s.avail_in = (uInt)n;
+      s.next_out = z.data() + 18;
+      s.avail_out = (uInt)(z.size() - 26);
+      rc = deflate(&s, Z_FINISH);
+      c = z.size() - 26 - s.avail_out;
+      deflateEnd(&s);
+    }
     if (rc != Z_STREAM_END || c + 26 > 65536) {
       if (level) block(p, n, 0);   // incompressible: stored
       else ok = false;
@@ -55,7 +90,8 @@ struct Bgzf {
     const unsigned char h[18] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 'B', 'C', 2, 0,
                                  (unsigned char)((c + 25) & 255), (unsigned char)((c + 25) >> 8)};
     memcpy(z.data(), h, 18);
-    const uint32_t crc = (uint32_t)crc32(0, (const Bytef *)p, (uInt)n), isz = (uint32_t)n;
+    const uint32_t crc = g_ldf.ok ? g_ldf.crc(0, p, n) : (uint32_t)crc32(0, (const Bytef *)p, (uInt)n);
+    const uint32_t isz = (uint32_t)n;
     memcpy(z.data() + 18 + c, &crc, 4);
     memcpy(z.data() + 22 + c, &isz, 4);
     ok = ok && fwrite(z.data(), 1, c + 26, f) == c + 26;
@@ -103,12 +139,20 @@ int main(int argc, char **argv) {
   const int ncl = 26;
   // per-bin parts, shared by every sample
   std::vector<float> base(m), off((size_t)m * ncl);
-  for (int64_t b = 0; b < m; b++) {
-    base[b] = 25.0f + 30.0f * unif(mix(seed ^ ((uint64_t)b * 0x9E37ull) ^ 0x1234ull));
-    for (int c = 0; c < ncl; c++)
-      off[(size_t)b * ncl + c] = 0.16f * (unif(mix(seed ^ ((uint64_t)b << 8) ^ (uint64_t)c ^ 0x77ull)) - 0.5f);
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; t++)
+      th.emplace_back([&, t]() {
+        for (int64_t b = t; b < m; b += nt) {
+          base[b] = 25.0f + 30.0f * unif(mix(seed ^ ((uint64_t)b * 0x9E37ull) ^ 0x1234ull));
+          for (int c = 0; c < ncl; c++)
+            off[(size_t)b * ncl + c] = 0.16f * (unif(mix(seed ^ ((uint64_t)b << 8) ^ (uint64_t)c ^ 0x77ull)) - 0.5f);
+        }
+      });
+    for (auto &t : th) t.join();
   }
-  std::atomic<int64_t> next{0}, failed{0};
+  const bool dry = getenv("GEN_COHORT_DRY") != nullptr;   // timing: text only, nothing compressed or written
+  std::atomic<int64_t> next{0}, failed{0}, done{0};
   auto work = [&]() {
     std::vector<char> buf(1 << 20);
     for (;;) {
@@ -131,6 +175,7 @@ int main(int argc, char **argv) {
         gzbuffer(f, 1 << 20);
       }
       auto emit = [&](const char *p, size_t k) {
+        if (dry) return;
         if (bw) bw->write(p, k);
         else gzwrite(f, p, (unsigned)k);
       };
@@ -167,6 +212,11 @@ int main(int argc, char **argv) {
         delete bw;
       } else if (gzclose(f) != Z_OK) {
         failed++;
+      }
+      const int64_t d = ++done;
+      if (d % 200 == 0 || d == n) {          // progress for a caller's watchdog
+        fprintf(stderr, "[gen_cohort] %lld of %lld files\n", (long long)d, (long long)n);
+        fflush(stderr);
       }
     }
   };
