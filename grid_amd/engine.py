@@ -204,6 +204,8 @@ def _knn_zq(dev: Device, zq: np.ndarray, cols: np.ndarray, k: int, zmax: float, 
       * otherwise (clips are not hundredths): fixed-order fp64 distances.
     Returns (idx, d2, cnt); d2 is float64 in value^2 units when ``values``,
     else int64 hundredths^2 (integer paths only)."""
+    if isinstance(zq, list):                    # a holder: this call takes the only reference
+        zq = zq.pop()
     if isinstance(zq, DevBuf):                  # already on the device (step-4 hand-off)
         assert zq.dtype == np.int32 and len(zq.shape) == 2
     else:
@@ -222,7 +224,7 @@ def _knn_zq(dev: Device, zq: np.ndarray, cols: np.ndarray, k: int, zmax: float, 
         kpad = pad_to(max(r, 1), 64)
         zb = dev.alloc((kpad // KBW, np_, KBW), U2)
         call("grid_knn_panel_i32", dev.ctx, dz.ptr, n, ld, dcols.ptr, r, q, zb.ptr, np_, kpad)
-        del dz
+        del dz, zq                              # step 4's matrix is freed before the Gram is allocated
         idx, d2, cnt = knn(dev, zb, n, np_, kpad, kpad, q, k, r, kblocked=True)
         return idx, (d2 / 10000.0 if values else d2), cnt
     d2m = dev.alloc((np_, np_), F8)
@@ -231,14 +233,14 @@ def _knn_zq(dev: Device, zq: np.ndarray, cols: np.ndarray, k: int, zmax: float, 
             raise GridNativeError("zmax too large for exact int64 distances stored as fp64")
         g = dev.alloc((n, max(r, 1)), I4)
         call("grid_knn_gather_i32", dev.ctx, dz.ptr, n, ld, dcols.ptr, r, q, g.ptr)
-        del dz
+        del dz, zq
         call("grid_knn_dist_i32", dev.ctx, g.ptr, n, r, max(r, 1), d2m.ptr, np_)
         scale = _dist_key_scale(4.0 * q * q * max(r, 1), True)
         unit = 10000.0
     else:
         g = dev.alloc((n, max(r, 1)), F8)
         call("grid_knn_gather_f64", dev.ctx, dz.ptr, n, ld, dcols.ptr, r, float(zmax), g.ptr)
-        del dz
+        del dz, zq
         call("grid_knn_dist_f64", dev.ctx, g.ptr, n, r, max(r, 1), d2m.ptr, np_)
         scale = _dist_key_scale(4.0 * zmax * zmax * max(r, 1) + 1.0, False)
         unit = 1.0
@@ -255,7 +257,10 @@ def _knn_zq(dev: Device, zq: np.ndarray, cols: np.ndarray, k: int, zmax: float, 
 
 def knn_from_zq(dev: Device, zq: np.ndarray, cols: np.ndarray, k: int, zmax: float):
     """find_neighbors.py:57-65 + find_neighbors_sklearn on the step-4
-    hundredths: (idx, squared distances in value^2 units, cnt)."""
+    hundredths: (idx, squared distances in value^2 units, cnt).  ``zq`` may be
+    a one-element list holding the matrix: the call then owns it and frees it
+    once the k-NN panel is built (step 5's peak HBM is max(zq + panel,
+    panel + Gram), not their sum)."""
     return _knn_zq(dev, zq, cols, k, zmax, True)
 
 
@@ -448,6 +453,15 @@ def phase_batch(dev: Device, loci, min_nbr: int, n_iters: int, legacy: bool = Fa
             bufs, (nd, max_n, max_nlev, max_list, flags) = fut.result()
             if gi + 1 < len(bounds):
                 fut = bg.submit(stage, *bounds[gi + 1])
+            if keep:
+                # the previous groups' inputs are dead once their phasing ends: device
+                # memory follows the group in flight, not the number of loci
+                dev.sync()
+                for bufs_ in keep:
+                    for b_ in bufs_:
+                        if b_ is not None:
+                            b_.free()
+                keep = []
             keep.append(bufs)
             d_arr = bufs[3]
             # the group's inputs were copied on cdev's stream: order the launches

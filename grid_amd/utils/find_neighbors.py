@@ -153,9 +153,13 @@ def find_neighbors(config, console):
 
     # clip (:57), NaN -> 0 (:58) and the column filter (:171) run on the device
     # over the int32 hundredths (no host copies of the matrix)
+    # the matrix goes to the k-NN in a holder: the call owns it and frees it
+    # once the panel is built (a device hand-off is GBs of HBM)
+    holder = [zq.reshape(N, -1) if N and got is None else zq]
+    del zq, got
     with progress_bar(console, total=N, description="Finding neighbors...") as (progress, task):
-        idx, d2, cnt = engine.knn_from_zq(get_device(config), zq.reshape(N, -1) if N and got is None else zq,
-                                          np.asarray(valid, dtype=np.int32), int(n_neighbors), float(zmax))
+        idx, d2, cnt = engine.knn_from_zq(get_device(config), holder, np.asarray(valid, dtype=np.int32),
+                                          int(n_neighbors), float(zmax))
         progress.advance(task, N)
 
     nbrs = {ind: [(ids[int(idx[i, t])], float(d2[i, t])) for t in range(cnt[i])]

@@ -88,3 +88,32 @@ def test_config5_734_loci_x_50k():
         ei = [steps.compute_imp(i, eh, hn, em) for i in range(n)]
         assert np.array_equal(imp, np.array(ei).reshape(-1), equal_nan=True)
     bigcheck.log("config 5: 2 loci == oracle (3 sweeps)")
+
+
+@pytest.mark.timeout(600)
+def test_config5_batch_loci_100_sweeps_vs_oracle():
+    """the batched launch at the full n_iters = 100 against
+    the oracle's _run_phasing/_compute_imp (hi_inference.py:175-250) on
+    1000G-sized loci (3,202 samples: hap vectors in LDS) and a small one, in a
+    batch that also holds a 50k-sample locus (hap vectors in global memory),
+    which must equal its own single-locus launch."""
+    from grid_amd import _abi, engine
+    from oracle import steps
+    rng = np.random.default_rng(3202)
+    sizes = [3202, 50_000, 3202, 777]
+    loci = [_locus(rng, n) for n in sizes]
+    dev = _abi.Device(0)
+    dev.set_stream(torch.cuda.current_stream())
+    res = engine.phase_batch(dev, loci, 1, 100)
+    hap, imp, mean = engine.phase(dev, *loci[1], 1, 100)
+    assert np.array_equal(res[1][0], hap, equal_nan=True) and np.array_equal(res[1][1], imp, equal_nan=True)
+    assert res[1][2] == mean
+    for li in (0, 2, 3):
+        irr, off, nbr, w = loci[li]
+        n = len(irr)
+        hn = [[(int(nbr[t]), 1.0) for t in range(off[h], off[h + 1])] for h in range(2 * n)]
+        eh, em = steps.run_phasing(list(irr), hn, 1, 100)
+        assert np.array_equal(res[li][0], np.array(eh), equal_nan=True), f"locus {li}: hap"
+        assert res[li][2] == em
+        ei = [steps.compute_imp(i, eh, hn, em) for i in range(n)]
+        assert np.array_equal(res[li][1], np.array(ei).reshape(-1), equal_nan=True), f"locus {li}: imp"

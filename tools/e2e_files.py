@@ -36,6 +36,7 @@ ap.add_argument("--ingest", choices=["device", "host"], default="device",
                 help="mosdepth.normalize.device_ingest true (the default: inflate + parse in HBM) or false")
 ap.add_argument("--device-ingest", action="store_true", help=argparse.SUPPRESS)   # older spelling of --ingest device
 ap.add_argument("--reuse", action="store_true", help="keep the cohort in --data for a later run (implies --keep)")
+ap.add_argument("--generate-only", action="store_true", help="write the cohort and inputs into --data, then exit")
 a = ap.parse_args()
 
 
@@ -100,6 +101,9 @@ cfg = {
                                   "ibs_output": os.path.join(a.data, "ibs.tsv.gz")},
 }
 res["phases_s"]["write_inputs"] = time.perf_counter() - t0 - res["phases_s"]["generate_cohort"]
+if a.generate_only:
+    note("cohort written")
+    sys.exit(0)
 
 # ---- timed steps ---------------------------------------------------------
 from grid_amd import engine  # noqa: E402
@@ -164,7 +168,9 @@ res["samples_per_s_from_files"] = a.samples / res["steps_4_7_s"]
 os.makedirs(os.path.dirname(a.json), exist_ok=True)
 json.dump(res, open(a.json, "w"), indent=1)
 print(json.dumps(res), flush=True)
+import shutil  # noqa: E402  (no child process once the GPU is in use)
 if not (a.keep or a.reuse):
-    subprocess.run(["rm", "-rf", a.data, a.out])
+    shutil.rmtree(a.data, ignore_errors=True)
+    shutil.rmtree(a.out, ignore_errors=True)
 elif a.reuse:
-    subprocess.run(["rm", "-rf", a.out])
+    shutil.rmtree(a.out, ignore_errors=True)
