@@ -19,9 +19,10 @@
 //      segment's absolute output bit); k_encode: each segment packs its codes
 //      into an LDS word image and stores it, atomically only on the two edge
 //      words it may share with a neighbour;
-//   4. k_member_crc: CRC-32 per member, one wave per member, lanes on equal
-//      slices (slicing-by-4 tables in LDS) folded with the GF(2) shift
-//      x^(8 len) mod P (zlib's crc32_combine algorithm, restated);
+//   4. k_seg_crc / k_seg_fold: CRC-32 of every 4 KiB text segment (a wave
+//      each: 64-byte lane slices, slicing-by-4 tables in LDS, a tree of the
+//      fixed GF(2) shift operators x^(8 len) mod P -- zlib's crc32_combine
+//      algorithm, restated), then the segments folded per member;
 //   5. k_frame: gzip header, block header bits, end-of-block code, CRC and
 //      ISIZE of every member.
 // The compressed batch is copied to pinned host memory and written by a host
@@ -227,10 +228,6 @@ __host__ __device__ inline uint32_t x8n(uint64_t n, const X2N &x) {
     k++;
   }
   return p;
-}
-// crc(A || B) from crc(A), crc(B), |B|
-__host__ __device__ inline uint32_t crc_combine(uint32_t ca, uint32_t cb, uint64_t lb, const X2N &x) {
-  return multmodp(x8n(lb, x), ca) ^ cb;
 }
 void crc_tables(uint32_t *t /* [4][256] */) {
   for (uint32_t i = 0; i < 256; i++) {
@@ -504,37 +501,83 @@ __device__ __forceinline__ void glb_byte(uint32_t *out, uint64_t byte, uint32_t 
   atomicOr(&out[byte >> 2], (v & 0xffu) << (8 * (byte & 3)));
 }
 
-// CRC-32 of every member text [mstart, mstart + mlen): one wave per member,
-// lane l on its 1/64 slice (slicing-by-4), folded in order by crc_combine.
-__global__ __launch_bounds__(64) void k_member_crc(const uint8_t *__restrict__ text, const int64_t *__restrict__ mstart,
-                                                   const int64_t *__restrict__ mlen, const uint32_t *__restrict__ tab,
-                                                   X2N x2n, uint32_t *__restrict__ crc) {
+// ---- segment-parallel CRC-32 --------------------------------------------
+// CRC(A || B) = M_|B| crc(A) ^ crc(B), M_L the GF(2) operator x^(8L) mod P as
+// 32 columns; the operators of 64 * 2^k bytes (k = 0..6: 64 .. 4096) are
+// precomputed on the host.  A 4 KiB segment: lane l of one wave takes bytes
+// [64 l, 64 l + 64) (four 16-B loads, slicing-by-4 in LDS), then a 6-level
+// tree of the fixed operators gives the segment's CRC in lane 0; a segment
+// shorter than 4 KiB (a member's or a range's last) is folded by lane 0 with
+// the general operator.  Then one thread per member folds its segments.
+constexpr int CSEG = 4096;
+struct CrcOps {
+  uint32_t m[7][32];     // M_(64 * 2^k), k = 0..6
+};
+CrcOps make_crc_ops(const X2N &x) {
+  CrcOps o;
+  for (int k = 0; k < 7; k++) {
+    const uint32_t op = x8n((uint64_t)64 << k, x);
+    for (int b = 0; b < 32; b++) o.m[k][b] = multmodp(op, 1u << b);
+  }
+  return o;
+}
+__device__ __forceinline__ uint32_t gf2_mul(const uint32_t *m, uint32_t c) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int b = 0; b < 32; b++) r ^= (0u - ((c >> b) & 1u)) & m[b];
+  return r;
+}
+
+__global__ __launch_bounds__(256) void k_seg_crc(const uint8_t *__restrict__ text, const int64_t *__restrict__ sstart,
+                                                 const int32_t *__restrict__ slen, int64_t ns,
+                                                 const uint32_t *__restrict__ tab, CrcOps ops, X2N x2n,
+                                                 uint32_t *__restrict__ scrc) {
   __shared__ uint32_t t[4][256];
-  __shared__ uint32_t s_c[64];
-  __shared__ int64_t s_l[64];
-  const int lane = threadIdx.x;
-  for (int e = lane; e < 1024; e += 64) t[e >> 8][e & 255] = tab[e];
+  __shared__ uint32_t s_m[7][32];
+  for (int e = threadIdx.x; e < 1024; e += 256) t[e >> 8][e & 255] = tab[e];
+  for (int e = threadIdx.x; e < 7 * 32; e += 256) s_m[e >> 5][e & 31] = ops.m[e >> 5][e & 31];
   __syncthreads();
-  const int64_t m = blockIdx.x, L = mlen[m];
-  const uint8_t *base = text + mstart[m];
-  const int64_t per = (L + 63) / 64;
-  const int64_t a = min(L, per * lane), b = min(L, per * (lane + 1));
-  uint32_t c = 0xffffffffu;
-  int64_t e = a;
-  for (; e < b && ((uintptr_t)(base + e) & 3); e++) c = t[0][(c ^ base[e]) & 0xff] ^ (c >> 8);
-  for (; e + 4 <= b; e += 4) {
-    c ^= *(const uint32_t *)(base + e);
-    c = t[3][c & 0xff] ^ t[2][(c >> 8) & 0xff] ^ t[1][(c >> 16) & 0xff] ^ t[0][c >> 24];
+  const int lane = threadIdx.x & 63;
+  const int64_t sg = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (sg >= ns) return;                      // whole waves only: no barrier below
+  const uint8_t *base = text + sstart[sg];
+  const int L = slen[sg];
+  auto crc_bytes = [&](const uint8_t *p, int n) {
+    uint32_t c = 0xffffffffu;
+    int e = 0;
+    for (; e < n && ((uintptr_t)(p + e) & 3); e++) c = t[0][(c ^ p[e]) & 0xff] ^ (c >> 8);
+    for (; e + 4 <= n; e += 4) {
+      c ^= *(const uint32_t *)(p + e);
+      c = t[3][c & 0xff] ^ t[2][(c >> 8) & 0xff] ^ t[1][(c >> 16) & 0xff] ^ t[0][c >> 24];
+    }
+    for (; e < n; e++) c = t[0][(c ^ p[e]) & 0xff] ^ (c >> 8);
+    return c ^ 0xffffffffu;
+  };
+  if (L == CSEG) {
+    uint32_t c = crc_bytes(base + 64 * lane, 64);
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      const uint32_t o = __shfl_down(c, 1 << k, 64);
+      if ((lane & ((2 << k) - 1)) == 0) c = gf2_mul(s_m[k], c) ^ o;
+    }
+    if (lane == 0) scrc[sg] = c;
+  } else if (lane == 0) {
+    scrc[sg] = crc_bytes(base, L);           // the short last segment: serial
   }
-  for (; e < b; e++) c = t[0][(c ^ base[e]) & 0xff] ^ (c >> 8);
-  s_c[lane] = c ^ 0xffffffffu;
-  s_l[lane] = b - a;
-  __syncthreads();
-  if (lane == 0) {
-    uint32_t acc = 0;                 // crc of the empty string
-    for (int l = 0; l < 64; l++) acc = crc_combine(acc, s_c[l], (uint64_t)s_l[l], x2n);
-    crc[m] = acc;
+}
+
+// one thread per group (member / range): its segments [g0[i], g0[i + 1]) in order
+__global__ void k_seg_fold(const uint32_t *__restrict__ scrc, const int32_t *__restrict__ slen,
+                           const int64_t *__restrict__ g0, int64_t ng, CrcOps ops, X2N x2n,
+                           uint32_t *__restrict__ crc) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ng) return;
+  uint32_t acc = 0;
+  for (int64_t s = g0[g]; s < g0[g + 1]; s++) {
+    const int L = slen[s];
+    acc = (L == CSEG ? gf2_mul(ops.m[6], acc) : multmodp(x8n((uint64_t)L, x2n), acc)) ^ scrc[s];
   }
+  crc[g] = acc;
 }
 
 // gzip framing of member m at byte moff[m]: header with the GR index, the
@@ -686,10 +729,11 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
   std::vector<uint32_t> crctab(1024);
   crc_tables(crctab.data());
   const X2N x2n = make_x2n();
+  const CrcOps cops = make_crc_ops(x2n);
   DBuf<int64_t> d_blen, d_boff, d_rowoff, d_prelen, d_preoff, d_sstart, d_sbase, d_moff, d_msize, d_mrow, d_mlen,
-      d_mbits, d_mstart;
+      d_mbits, d_mstart, d_mseg0;
   DBuf<int32_t> d_slen;
-  DBuf<uint32_t> d_sbits, d_crc, d_hdr, d_tab, d_out;
+  DBuf<uint32_t> d_sbits, d_crc, d_hdr, d_tab, d_out, d_scrc;
   DBuf<char> d_pre, d_text;
   DBuf<CodeDev> d_code;
   DBuf<unsigned long long> d_hist;
@@ -881,8 +925,16 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
                          d_slen.p, d_code.p, d_sbits.p);
       STEP(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_member_crc, dim3((unsigned)nm), dim3(64), 0, st, (const uint8_t *)d_text.p, d_mstart.p,
-                       d_mlen.p, d_tab.p, x2n, d_crc.p);
+    STEP(d_scrc.need((size_t)std::max<int64_t>(ns, 1)));
+    STEP(d_mseg0.need((size_t)nm + 1));
+    STEP(hipMemcpyAsync(d_mseg0.p, mseg0.data(), (nm + 1) * 8, hipMemcpyHostToDevice, st));
+    if (ns > 0) {
+      hipLaunchKernelGGL(k_seg_crc, dim3((unsigned)((ns + 3) / 4)), dim3(256), 0, st, (const uint8_t *)d_text.p,
+                         d_sstart.p, d_slen.p, ns, d_tab.p, cops, x2n, d_scrc.p);
+      STEP(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_seg_fold, dim3((unsigned)((nm + 63) / 64)), dim3(64), 0, st, d_scrc.p, d_slen.p,
+                       d_mseg0.p, nm, cops, x2n, d_crc.p);
     STEP(hipGetLastError());
     h_sbits.resize((size_t)ns);
     if (ns) STEP(hipMemcpyAsync(h_sbits.data(), d_sbits.p, ns * 4, hipMemcpyDeviceToHost, st));
@@ -955,43 +1007,49 @@ int grid_text_crc32(grid_ctx *ctx, const uint8_t *d_base, const int64_t *h_off, 
                     uint32_t *h_crc) {
   REQUIRE(ctx && n >= 0 && (n == 0 || (d_base && h_off && h_len && h_crc)), "bad args");
   if (n == 0) return GRID_OK;
-  constexpr int64_t PIECE = 1 << 20;         // one wave per piece: 16 KiB per lane
-  std::vector<int64_t> ps, pl, first(n + 1);
+  // 4 KiB segments of every range (k_seg_crc), folded per range (k_seg_fold)
+  std::vector<int64_t> ss, g0(n + 1);
+  std::vector<int32_t> sl;
   for (int64_t i = 0; i < n; i++) {
     REQUIRE(h_len[i] >= 0 && h_off[i] >= 0, "range %lld: negative offset or length", (long long)i);
-    first[i] = (int64_t)ps.size();
-    for (int64_t a = 0; a < h_len[i]; a += PIECE) {
-      ps.push_back(h_off[i] + a);
-      pl.push_back(std::min(PIECE, h_len[i] - a));
+    g0[i] = (int64_t)ss.size();
+    for (int64_t a = 0; a < h_len[i]; a += CSEG) {
+      ss.push_back(h_off[i] + a);
+      sl.push_back((int32_t)std::min<int64_t>(CSEG, h_len[i] - a));
     }
   }
-  first[n] = (int64_t)ps.size();
-  const int64_t np = (int64_t)ps.size();
-  for (int64_t i = 0; i < n; i++) h_crc[i] = 0;         // the empty text
-  if (np == 0) return GRID_OK;
-  REQUIRE(np <= 0x7fffffff, "too many pieces");
-  std::vector<uint32_t> tab(1024), pc(np);
+  g0[n] = (int64_t)ss.size();
+  const int64_t ns = (int64_t)ss.size();
+  std::vector<uint32_t> tab(1024);
   crc_tables(tab.data());
   const X2N x2n = make_x2n();
+  const CrcOps cops = make_crc_ops(x2n);
   hipStream_t st = ctx->stream;
-  DBuf<int64_t> d_s, d_l;
-  DBuf<uint32_t> d_tab, d_c;
-  HIPCHK(d_s.need((size_t)np));
-  HIPCHK(d_l.need((size_t)np));
+  DBuf<int64_t> d_s, d_g0;
+  DBuf<int32_t> d_l;
+  DBuf<uint32_t> d_tab, d_sc, d_c;
+  HIPCHK(d_s.need((size_t)std::max<int64_t>(ns, 1)));
+  HIPCHK(d_l.need((size_t)std::max<int64_t>(ns, 1)));
+  HIPCHK(d_g0.need((size_t)n + 1));
   HIPCHK(d_tab.need(1024));
-  HIPCHK(d_c.need((size_t)np));
-  HIPCHK(hipMemcpyAsync(d_s.p, ps.data(), np * 8, hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(d_l.p, pl.data(), np * 8, hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(d_tab.p, tab.data(), 4096, hipMemcpyHostToDevice, st));
-  hipLaunchKernelGGL(k_member_crc, dim3((unsigned)np), dim3(64), 0, st, d_base, d_s.p, d_l.p, d_tab.p, x2n, d_c.p);
-  LAUNCHCHK();
-  HIPCHK(hipMemcpyAsync(pc.data(), d_c.p, np * 4, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  for (int64_t i = 0; i < n; i++) {
-    uint32_t acc = 0;
-    for (int64_t p = first[i]; p < first[i + 1]; p++) acc = crc_combine(acc, pc[p], (uint64_t)pl[p], x2n);
-    h_crc[i] = acc;
+  HIPCHK(d_sc.need((size_t)std::max<int64_t>(ns, 1)));
+  HIPCHK(d_c.need((size_t)n));
+  if (ns) {
+    HIPCHK(hipMemcpyAsync(d_s.p, ss.data(), ns * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_l.p, sl.data(), ns * 4, hipMemcpyHostToDevice, st));
   }
+  HIPCHK(hipMemcpyAsync(d_g0.p, g0.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(d_tab.p, tab.data(), 4096, hipMemcpyHostToDevice, st));
+  if (ns) {
+    hipLaunchKernelGGL(k_seg_crc, dim3((unsigned)((ns + 3) / 4)), dim3(256), 0, st, d_base, d_s.p, d_l.p, ns,
+                       d_tab.p, cops, x2n, d_sc.p);
+    LAUNCHCHK();
+  }
+  hipLaunchKernelGGL(k_seg_fold, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, d_sc.p, d_l.p, d_g0.p, n, cops,
+                     x2n, d_c.p);
+  LAUNCHCHK();
+  HIPCHK(hipMemcpyAsync(h_crc, d_c.p, n * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
   return GRID_OK;
 }
 

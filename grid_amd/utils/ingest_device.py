@@ -365,6 +365,14 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
         batches.append(cur)
     in_need = 256 + max((sum(_align(max(sizes[f], 1)) for f in b) for b in batches), default=0)
     pins = [_Pinned(BATCH_IN + 512), _Pinned(BATCH_IN + 512)]
+    # page-locking GBs of staging takes ~0.15 s per GB: both input buffers are
+    # pinned at full size on threads of their own while the (small) first
+    # batch is read into a buffer of its own and inflated
+    first = _Pinned(FIRST_BATCH_IN + 512)
+    prepin = None
+    if len(batches) > 1:
+        prepin = ThreadPoolExecutor(2)
+        pin_jobs = [prepin.submit(pins[k].get, in_need + 256) for k in (1, 0)]
     stages = [_Pinned(STAGE + 512), _Pinned(STAGE + 512)]
     nthreads = max(1, min(int(threads or 1), 32))
     pool = ThreadPoolExecutor(nthreads)
@@ -382,7 +390,12 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
         off[1:] = np.cumsum([_align(max(sizes[f], 1)) for f in fs])
         if bi >= 2 and h2d_done[bi - 2] is not None:
             h2d_done[bi - 2].host_wait()        # pins[bi % 2] still feeds batch bi-2's copy
-        buf = pins[bi % 2].get(int(off[-1]) + 256)
+        if bi == 0:
+            buf = first.get(int(off[-1]) + 256)
+        else:
+            if prepin is not None:
+                pin_jobs[0 if bi % 2 else 1].result()
+            buf = pins[bi % 2].get(int(off[-1]) + 256)
 
         def one(k):
             f = fs[k]
@@ -659,7 +672,9 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
               file=sys.stderr, flush=True)
     # the staging buffers: GBs of page-locked memory whose release (unpinning)
     # takes a fraction of a second -- done on a thread of its own, off the step's path
-    held = [pb for grp in ([pins, stages] + ([pipe.arena_h] if pipe is not None else [])) for pb in grp]
+    if prepin is not None:
+        prepin.shutdown(wait=True)
+    held = [pb for grp in ([pins, stages, [first]] + ([pipe.arena_h] if pipe is not None else [])) for pb in grp]
     threading.Thread(target=_release_pinned, args=(held,), daemon=True).start()
     held = None
     d_ins = d_text = pipe = None

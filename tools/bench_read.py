@@ -68,3 +68,13 @@ for threads in (8, 16, 32):
             dt = run(buf, threads, how)
             print(json.dumps({"method": how, "buffer": name, "threads": threads, "s": dt, "GBps": tot / dt / 1e9}),
                   flush=True)
+
+# host -> HBM copy rate from each buffer (grid_h2d: hipMemcpyAsync + sync)
+dev = _abi.Device(0)
+d = dev.alloc(int(off[-1]) + 256, np.uint8)
+for name, buf in (("pinned", pin.array), ("pageable", page)):
+    for rep in range(2):
+        t = time.perf_counter()
+        _abi.call("grid_h2d", dev.ctx, d.ptr, buf.ctypes.data, int(off[-1]))
+        dt = time.perf_counter() - t
+        print(json.dumps({"h2d": name, "rep": rep, "s": dt, "GBps": off[-1] / dt / 1e9}), flush=True)

@@ -1,0 +1,21 @@
+#!/bin/bash
+# round 4: segment-parallel CRC in the device writer and the ingest guard, pre-pinned ingest staging:
+# writer/ingest GPU tests, then the from-files config-2 steps under rocprofv3 (kernel stats)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r04h
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 500 python -u -m pytest -x -v --timeout 200 --timeout-method thread -p no:cacheprovider \
+  tests/test_gpu_gzwrite.py tests/test_gpu_ingest.py tests/test_gpu_e2e.py > $O/pytest.log 2>&1 || { tail -n 40 $O/pytest.log; exit 1; }
+tail -n 3 $O/pytest.log
+timeout -k 10 300 python -u tools/e2e_files.py --bgzf --generate-only > $O/gen.log 2>&1 || { tail -n 20 $O/gen.log; exit 1; }
+GRID_INGEST_TRACE=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -- \
+  python3 -u tools/e2e_files.py --bgzf --reuse --json $O/e2e.json > $O/e2e.log 2>&1
+rc=$?
+rm -rf /dev/shm/grid_e2e
+grep -E "e2e\] .*(step4_ingest|step4_write|done in)" $O/e2e.log | tail -n 8
+find $O/stats -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats.csv \;
+find $O/stats -name "*kernel_trace.csv" -exec gzip -c {} \; > $O/kernel_trace.csv.gz
+rm -rf $O/stats
+exit $rc
