@@ -69,13 +69,17 @@ def _align(x, a=256):
 
 
 class _Pinned:
-    """Reusable pinned host staging (grid_host_alloc: page-locked, so the
-    copies to HBM run at PCIe speed; no torch in the step path -- a first
-    ``import torch`` costs seconds on a fresh host)."""
+    """Reusable host staging.  Page-locked (grid_host_alloc: no torch in the
+    step path -- a first ``import torch`` costs seconds on a fresh host) for
+    the asynchronous copies of host-inflated text; PAGEABLE (``pinned=False``)
+    for the compressed input: the runtime copies pageable memory to HBM as fast
+    as page-locked here (56 vs 52-58 GB/s, profiles/r04i_host_read_h2d.jsonl),
+    while page-locking 4 GB costs ~0.65 s that stalls every other HIP call."""
 
-    def __init__(self, bound):
+    def __init__(self, bound, pinned=True):
         self.b = None
         self.bound = int(bound)        # the size a request normally stays within
+        self.pinned = pinned
 
     def get(self, n):
         if self.b is None or self.b.nbytes < n:
@@ -83,8 +87,18 @@ class _Pinned:
                 self.b.free()
             # room to grow at once: a buffer re-pinned a few MB larger each
             # batch stalled that batch's copy to HBM by ~1 s (profiles/r03q)
-            self.b = _abi.PinnedBuf(max(int(n), min(2 * int(n), self.bound), 1))
+            nb = max(int(n), min(2 * int(n), self.bound), 1)
+            self.b = _abi.PinnedBuf(nb) if self.pinned else _Pageable(nb)
         return self.b.array
+
+
+class _Pageable:
+    def __init__(self, nbytes):
+        self.array = np.empty(int(nbytes), np.uint8)
+        self.nbytes = int(nbytes)
+
+    def free(self):
+        self.array = None
 
 
 def _opts(dev, prefix, window, excluded, keep):
@@ -213,7 +227,7 @@ class _Async:
         self.h2d = [_abi.Event(), _abi.Event()]
         self.done = [_abi.Event(), _abi.Event()]
         self.issued = [False, False]
-        self.arena_h = [_Pinned(64 << 20), _Pinned(64 << 20)]
+        self.arena_h = [_Pinned(64 << 20, pinned=False), _Pinned(64 << 20, pinned=False)]
         self.arena_d = [None, None]
         self.scr = [None, None]                 # per parity: member table, chunk counts/lines, file status
         self.out = []                           # per batch: (fs, owner, unit status, unit length, flags, kept, okb)
@@ -270,11 +284,13 @@ class _Async:
         # per-batch outputs read at the end (small)
         ust, uln = dev.alloc(max(nu, 1), np.int32), dev.alloc(max(nu, 1), np.int64)
         bflags, bk = dev.zeros(nb, np.int32), dev.zeros(nb, np.uint64)
-        # copy stream: after batch bi-2's parse (same parity buffers), the input and the tables
+        # copy context: after batch bi-2's parse (same parity buffers), the input
+        # and the tables, from pageable staging (the call returns once they are in
+        # HBM; it runs while the device inflates batch bi-1)
         if self.issued[p]:
-            self.done[p].wait(cdev)
-        call("grid_h2d_async", cdev.ctx, d_in.ptr, buf.ctypes.data, int(off[-1]))
-        call("grid_h2d_async", cdev.ctx, self.arena_d[p].ptr, host.ctypes.data, nbytes)
+            self.done[p].host_wait()
+        call("grid_h2d", cdev.ctx, d_in.ptr, buf.ctypes.data, int(off[-1]))
+        call("grid_h2d", cdev.ctx, self.arena_d[p].ptr, host.ctypes.data, nbytes)
         self.h2d[p].put(cdev)
         # main stream
         self.h2d[p].wait(dev)
@@ -364,15 +380,8 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
     if cur:
         batches.append(cur)
     in_need = 256 + max((sum(_align(max(sizes[f], 1)) for f in b) for b in batches), default=0)
-    pins = [_Pinned(BATCH_IN + 512), _Pinned(BATCH_IN + 512)]
-    # page-locking GBs of staging takes ~0.15 s per GB: both input buffers are
-    # pinned at full size on threads of their own while the (small) first
-    # batch is read into a buffer of its own and inflated
-    first = _Pinned(FIRST_BATCH_IN + 512)
-    prepin = None
-    if len(batches) > 1:
-        prepin = ThreadPoolExecutor(2)
-        pin_jobs = [prepin.submit(pins[k].get, in_need + 256) for k in (1, 0)]
+    pins = [_Pinned(BATCH_IN + 512, pinned=False), _Pinned(BATCH_IN + 512, pinned=False)]
+    first = _Pinned(FIRST_BATCH_IN + 512, pinned=False)    # the (small) first batch: K, quickly
     stages = [_Pinned(STAGE + 512), _Pinned(STAGE + 512)]
     nthreads = max(1, min(int(threads or 1), 32))
     pool = ThreadPoolExecutor(nthreads)
@@ -390,12 +399,7 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
         off[1:] = np.cumsum([_align(max(sizes[f], 1)) for f in fs])
         if bi >= 2 and h2d_done[bi - 2] is not None:
             h2d_done[bi - 2].host_wait()        # pins[bi % 2] still feeds batch bi-2's copy
-        if bi == 0:
-            buf = first.get(int(off[-1]) + 256)
-        else:
-            if prepin is not None:
-                pin_jobs[0 if bi % 2 else 1].result()
-            buf = pins[bi % 2].get(int(off[-1]) + 256)
+        buf = (first if bi == 0 else pins[bi % 2]).get(int(off[-1]) + 256)
 
         def one(k):
             f = fs[k]
@@ -672,8 +676,6 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
               file=sys.stderr, flush=True)
     # the staging buffers: GBs of page-locked memory whose release (unpinning)
     # takes a fraction of a second -- done on a thread of its own, off the step's path
-    if prepin is not None:
-        prepin.shutdown(wait=True)
     held = [pb for grp in ([pins, stages, [first]] + ([pipe.arena_h] if pipe is not None else [])) for pb in grp]
     threading.Thread(target=_release_pinned, args=(held,), daemon=True).start()
     held = None
