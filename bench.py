@@ -40,6 +40,9 @@ PEAK_HBM_GBS = 8000.0
 # HBM bytes per Gram launch from the rocprofv3 FETCH_SIZE / WRITE_SIZE passes
 # of this same command (tools/gpu_round.sh -> tools/pmc_traffic.py)
 TRAFFIC_JSON = "profiles/r03ai_pmc_traffic.json"
+# the oracle from files over N x M, per-stage fits (tools/cpu_sweep.py,
+# run on a GPU box's host cores); reported beside the live bounded sample
+CPU_SWEEP_JSON = "profiles/r04k_cpu_sweep.json"
 GRAM_KERNEL = "k_gram8<0, true"
 SEED = 20260821
 NCL = 26
@@ -229,6 +232,28 @@ def from_files_config2(args, note):
                         "depths) -> `grid wgs` steps 4-7 (drop-in step API, device ingest, every output file written "
                         "to " + os.path.dirname(out) + "); cohort generated before the clock in " + args.files_dir,
             "timed": "wall clock of the four step functions in one process (tools/e2e_files.py)"}
+
+
+def cpu_sweep_fit():
+    """The committed CPU-baseline sweep (tools/cpu_sweep.py: the oracle from
+    files at N in {100, 400, 1600} x M in {30k, 100k}, one single-threaded
+    process per point) and its per-stage fits extrapolated to configs 2 and 3
+    -- measured offline on a GPU box's host cores, not in this run."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), CPU_SWEEP_JSON)
+    if not os.path.exists(path):
+        return None
+    d = json.load(open(path))
+    return {"source": CPU_SWEEP_JSON, "cores_per_point": d["cores_per_point"], "host_cpus": d.get("host_cpus"),
+            "points": [{"samples": p["n"], "bins": p["m"], "total_s": round(p["total_s"], 2),
+                        "stages_s": {k: round(v, 3) for k, v in p["stages_s"].items()}} for p in d["points"]],
+            "fit_seconds_per_unit": d["fit_seconds_per_unit"], "fit_units": d["fit_units"],
+            "fit_check": d["fit_check"],
+            "config2_samples_per_s": d["extrapolated"]["config2_3202x3M"]["samples_per_s"],
+            "config3_samples_per_s": d["extrapolated"]["config3_50kx3M"]["samples_per_s"],
+            "config2_total_s": d["extrapolated"]["config2_3202x3M"]["total_s"],
+            "kind": "port", "note": "oracle/pipeline.py from mosdepth files to output files (the reference's step "
+                                    "functions restated), fitted per stage and extrapolated: the reference's fp64 "
+                                    "matrix does not fit host memory at configs 2-3"}
 
 
 def _free_port():
@@ -525,6 +550,9 @@ def main():
         if not args.no_files_baseline:
             note("cpu baseline: the oracle from files at config 1")
             out["cpu_baseline"]["from_files"] = cpu_baseline_from_files(n, m, args.k, args.n_iters)
+        sweep = cpu_sweep_fit()
+        if sweep is not None:
+            out["cpu_baseline"]["sweep"] = sweep
     if rank == 0 and world == 1 and not args.no_files_config2 and (n, m) == (3202, 3_000_000):
         out["from_files_config2"] = from_files_config2(args, note)
     if rank == 0:

@@ -504,6 +504,63 @@ __global__ __launch_bounds__(CT) void k_gz_crc(const uint8_t *__restrict__ out, 
   if (tid == 0 && s_bad) status[f] = GRID_GZ_ECRC;
 }
 
+// BGZF units (one member each, mcap == 1; a member's text is <= 64 KiB): one
+// WAVE per member instead of one workgroup -- lane l takes bytes [1 KiB l,
+// 1 KiB (l + 1)) (slicing by 4, tables in LDS), a 6-level tree of the fixed
+// operators M^(1 KiB 2^k) = c_crc_pow[10 + k] joins the lanes (the general
+// shift where a subtree is short), lane 0 adds the initial register; longer
+// members take several 64 KiB rounds.  The raw-register convention of k_gz_crc.
+__global__ __launch_bounds__(256) void k_member_check(const uint8_t *__restrict__ out,
+                                                      const int64_t *__restrict__ out_off,
+                                                      const grid_gz_member *__restrict__ mem,
+                                                      const int32_t *__restrict__ nmem, int64_t n,
+                                                      int32_t *__restrict__ status) {
+  __shared__ uint32_t t4[4][256];
+  {
+    const int i = threadIdx.x;
+    uint32_t c = (uint32_t)i;
+    for (int k = 0; k < 8; k++) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
+    t4[0][i] = c;
+  }
+  __syncthreads();
+  for (int sl = 1; sl < 4; sl++) {
+    const int i = threadIdx.x;
+    t4[sl][i] = (t4[sl - 1][i] >> 8) ^ t4[0][t4[sl - 1][i] & 255];
+    __syncthreads();
+  }
+  const int lane = threadIdx.x & 63;
+  const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (u >= n) return;                                   // whole waves: no barrier below
+  if (__builtin_amdgcn_readfirstlane(status[u]) != 0 || __builtin_amdgcn_readfirstlane(nmem[u]) < 1) return;
+  const grid_gz_member g = mem[u];
+  const uint8_t *base = out + out_off[u] + g.start;
+  const int64_t L = g.end - g.start;
+  uint32_t acc = 0xFFFFFFFFu;                           // raw register before the member's bytes
+  for (int64_t r0 = 0; r0 < L; r0 += 65536) {
+    const int64_t RL = min((int64_t)65536, L - r0);
+    const int64_t a = min(RL, (int64_t)1024 * lane), b = min(RL, a + 1024);
+    const uint8_t *p = base + r0;
+    uint32_t c = 0;
+    int64_t e = a;
+    for (; e < b && ((uintptr_t)(p + e) & 3); e++) c = t4[0][(c ^ p[e]) & 255] ^ (c >> 8);
+    for (; e + 4 <= b; e += 4) {
+      c ^= *(const uint32_t *)(p + e);
+      c = t4[3][c & 255] ^ t4[2][(c >> 8) & 255] ^ t4[1][(c >> 16) & 255] ^ t4[0][c >> 24];
+    }
+    for (; e < b; e++) c = t4[0][(c ^ p[e]) & 255] ^ (c >> 8);
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      const uint32_t o = __shfl_down(c, 1 << k, 64);
+      const int64_t rs = (int64_t)1024 * (lane + (1 << k));
+      const int64_t lr = rs >= RL ? 0 : min(RL - rs, (int64_t)1024 << k);
+      if ((lane & ((2 << k) - 1)) == 0 && lr > 0)
+        c = (lr == ((int64_t)1024 << k) ? gf2_apply(c_crc_pow[10 + k], c) : crc_shift(c, (uint64_t)lr)) ^ o;
+    }
+    acc = crc_shift(acc, (uint64_t)RL) ^ c;            // lane 0's c is the round's
+  }
+  if (lane == 0 && (acc ^ 0xFFFFFFFFu) != g.crc) status[u] = GRID_GZ_ECRC;
+}
+
 bool g_crc_ready = false;
 
 int crc_tables_once() {
@@ -548,8 +605,13 @@ int grid_gunzip_batch(grid_ctx *ctx, const uint8_t *d_src, const int64_t *d_in_o
   hipLaunchKernelGGL(k_inflate, dim3((unsigned)n_files), dim3(64), 0, ctx->stream, d_src, d_in_off, d_in_len,
                      d_out, d_out_off, d_out_cap, d_mem, mcap, d_status, d_out_len, d_nmem);
   LAUNCHCHK();
-  hipLaunchKernelGGL(k_gz_crc, dim3((unsigned)n_files), dim3(CT), 0, ctx->stream, d_out, d_out_off, d_mem, mcap,
-                     d_nmem, d_status);
+  if (mcap == 1) {   // BGZF members (one per unit): a wave per member
+    hipLaunchKernelGGL(k_member_check, dim3((unsigned)((n_files + 3) / 4)), dim3(256), 0, ctx->stream, d_out,
+                       d_out_off, d_mem, d_nmem, n_files, d_status);
+  } else {
+    hipLaunchKernelGGL(k_gz_crc, dim3((unsigned)n_files), dim3(CT), 0, ctx->stream, d_out, d_out_off, d_mem, mcap,
+                       d_nmem, d_status);
+  }
   LAUNCHCHK();
   return GRID_OK;
 }

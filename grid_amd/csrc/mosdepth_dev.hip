@@ -15,7 +15,7 @@
 //   * population means: per column, the files in FILE ORDER (the reference's
 //     threads=1 order, as ingest.cpp), q / 100.0 exactly (div100_exact).
 //
-// Kernels per batch of files: k_md_count (newlines per 64 KiB chunk, any
+// Kernels per batch of files: k_md_count (newlines per 16 KiB chunk, any
 // byte >= 0x80), k_md_scan (per-file prefix of the chunk counts), k_md_parse
 // (one workgroup per chunk: the chunk in LDS, one thread per 256-byte
 // segment, each line parsed by the thread whose segment holds its first
@@ -26,7 +26,10 @@
 
 namespace {
 
-constexpr int CH = 65536, SEG = 256, PTH = CH / SEG, MAXLINE = 256;
+// 16 KiB chunks, a 64-byte segment per thread: 16.7 KiB of LDS per workgroup,
+// so ~9 workgroups per CU hide the per-line latencies (64 KiB chunks held 2
+// per CU: 52 ms per 17.5 GB batch at config 2, profiles/r04h_*)
+constexpr int CH = 16384, SEG = 64, PTH = CH / SEG, MAXLINE = 256;
 
 struct MdOpts {
   const char *prefix;       // device bytes (npre of them)

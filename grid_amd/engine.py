@@ -349,7 +349,7 @@ def phase(dev: Device, irr: np.ndarray, off: np.ndarray, nbr: np.ndarray, w: np.
 
 
 def phase_batch(dev: Device, loci, min_nbr: int, n_iters: int, legacy: bool = False, paired: bool = False,
-                group: int | None = None):
+                group: int | None = None, inflight: int = 3):
     """Batched phasing + imputation of L independent loci (one workgroup per
     locus; BASELINE config 5).  ``loci``: sequence of (irr [n], off [2n+1],
     nbr, w) per locus (CSR as csr_from_lists).  Returns a list of (hap [2n],
@@ -363,7 +363,13 @@ def phase_batch(dev: Device, loci, min_nbr: int, n_iters: int, legacy: bool = Fa
     background thread for group g+1 while group g phases on the device.  The
     packed neighbour lists are built on the device (grid_hi_pack_batch);
     every group writes into one output arena, copied back once.  Unit-weight
-    loci share one device vector of ones as their weights."""
+    loci share one device vector of ones as their weights.
+
+    Up to ``inflight`` groups run at once, each on a stream of its own: a
+    50k-sample locus keeps its haplotypes in global memory and its workgroup
+    waits on gathers, and a CU holds up to three of these workgroups (75
+    VGPRs, 512 threads), so groups launched one after another on one stream
+    left two thirds of every CU idle."""
     import os
     from concurrent.futures import ThreadPoolExecutor
     if not len(loci):
@@ -374,6 +380,7 @@ def phase_batch(dev: Device, loci, min_nbr: int, n_iters: int, legacy: bool = Fa
     pool = ThreadPoolExecutor(max(1, min(16, os.cpu_count() or 1)))
     bg = ThreadPoolExecutor(1)
     cdev = Device(dev.index)                  # its own non-blocking stream: uploads beside the phasing
+    lanes = [dev] + [Device(dev.index) for _ in range(max(1, int(inflight)) - 1)]   # launch streams
 
     def al(x):
         return -(-int(x) // 256) * 256
@@ -446,42 +453,46 @@ def phase_batch(dev: Device, loci, min_nbr: int, n_iters: int, legacy: bool = Fa
         return (d_in, ones, d_pk, d_arr), meta
 
     bounds = [(g0, min(len(loci), g0 + group)) for g0 in range(0, len(loci), group)]
-    keep = []
+    keep = [None] * len(lanes)                # per launch stream: the inputs of its group in flight
     try:
         fut = bg.submit(stage, *bounds[0])
         for gi in range(len(bounds)):
             bufs, (nd, max_n, max_nlev, max_list, flags) = fut.result()
             if gi + 1 < len(bounds):
                 fut = bg.submit(stage, *bounds[gi + 1])
-            if keep:
-                # the previous groups' inputs are dead once their phasing ends: device
-                # memory follows the group in flight, not the number of loci
-                dev.sync()
-                for bufs_ in keep:
-                    for b_ in bufs_:
-                        if b_ is not None:
-                            b_.free()
-                keep = []
-            keep.append(bufs)
+            ln = lanes[gi % len(lanes)]
+            if keep[gi % len(lanes)] is not None:
+                # that stream's previous group's inputs are dead once its phasing ends:
+                # device memory follows the groups in flight, not the number of loci
+                ln.sync()
+                for b_ in keep[gi % len(lanes)]:
+                    if b_ is not None:
+                        b_.free()
+            keep[gi % len(lanes)] = bufs
             d_arr = bufs[3]
             # the group's inputs were copied on cdev's stream: order the launches
             # behind them through the runtime, not only through the host's wait
-            call("grid_stream_after", dev.ctx, cdev.ctx)
+            call("grid_stream_after", ln.ctx, cdev.ctx)
             for l0 in range(0, nd, 65535):            # grid.y of the pack launch
-                call("grid_hi_pack_batch", dev.ctx, min(65535, nd - l0), d_arr.ptr + l0 * C.sizeof(_abi.HiLocus),
+                call("grid_hi_pack_batch", ln.ctx, min(65535, nd - l0), d_arr.ptr + l0 * C.sizeof(_abi.HiLocus),
                      max_n)
-            call("grid_hi_phase_batch", dev.ctx, nd, d_arr.ptr, max_n, max_nlev, min_nbr, n_iters,
+            call("grid_hi_phase_batch", ln.ctx, nd, d_arr.ptr, max_n, max_nlev, min_nbr, n_iters,
                  flags | legacy_f | (_abi.HI_PAIRED if paired else 0), max_list)
+        for ln in lanes:
+            ln.sync()
         out = d_out.numpy()
     finally:
         bg.shutdown(wait=True)
         pool.shutdown(wait=True)
-        dev.sync()
+        for ln in lanes:
+            ln.sync()
         for bufs_ in keep:                    # cdev's buffers, freed before its context closes
-            for b_ in bufs_:
+            for b_ in bufs_ or ():
                 if b_ is not None:
                     b_.free()
         cdev.close()
+        for ln in lanes[1:]:
+            ln.close()
     res = []
     for k, n in enumerate(sizes):
         h0 = int(o_hap[k])

@@ -49,7 +49,7 @@ import numpy as np
 from .. import _abi
 from .._abi import MdOpts, call
 
-CH = 65536                      # parse chunk (mosdepth_dev.hip CH)
+CH = 16384                      # parse chunk (mosdepth_dev.hip CH)
 BATCH_IN = 4 << 30              # compressed bytes per batch
 BATCH_TEXT = 24 << 30           # inflated bytes per batch
 FIRST_BATCH_IN = 256 << 20      # the first batch (read and inflated synchronously: the reference key list)
@@ -186,15 +186,18 @@ def _gpu_inflate(dev, d_in, d_text, units, mcap):
 
 
 def _chunks(files, tlen):
-    """Chunk table of the files (batch-local indices) with text."""
-    cfile, cstart, cfirst = [], [], [0]
-    for f in files:
-        n = -(-int(tlen[f]) // CH)
-        cfile += [f] * n
-        cstart += list(range(0, n * CH, CH))
-        cfirst.append(len(cfile))
-    return (np.asarray(cfile or [0], np.int32), np.asarray(cstart or [0], np.int64), np.asarray(cfirst, np.int32),
-            len(cfile))
+    """Chunk table of the files (batch-local indices) with text: per chunk its
+    file and start; per file its first chunk (cfirst[k], k in file order)."""
+    files = np.asarray(files, np.int64)
+    n = -(-np.asarray(tlen, np.int64)[files] // CH) if len(files) else np.zeros(0, np.int64)
+    cfirst = np.zeros(len(files) + 1, np.int32)
+    np.cumsum(n, out=cfirst[1:])
+    tot = int(cfirst[-1])
+    if tot == 0:
+        return np.zeros(1, np.int32), np.zeros(1, np.int64), cfirst, 0
+    cfile = np.repeat(files, n).astype(np.int32)
+    cstart = (np.arange(tot, dtype=np.int64) - np.repeat(cfirst[:-1].astype(np.int64), n)) * CH
+    return cfile, cstart, cfirst, tot
 
 
 def _release_pinned(held):

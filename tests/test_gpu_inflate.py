@@ -128,10 +128,13 @@ def test_inflate_rejects_exactly_what_zlib_rejects(dev):
             assert st[f] == 0 and got[f] == r, (f, st[f])
 
 
-def test_streams_at_any_offset(dev):
+@pytest.mark.parametrize("mcap", [4, 1])
+def test_streams_at_any_offset(dev, mcap):
     """The ingest's member-granular launch: every BGZF member is its own
     stream, packed at any byte offset, its text at any byte offset (the
-    members of a file back to back) -- and the reject cases with them."""
+    members of a file back to back) -- and the reject cases with them.
+    mcap = 1 is the ingest's launch (k_member_check: a wave per member); a
+    member whose trailer CRC is changed must be rejected (GZ_ECRC)."""
     rng = random.Random(11)
     texts = [b"".join(b"chr1\t%d\t%d\t%.2f\n" % (i * 1000, i * 1000 + 1000, rng.uniform(0, 90))
                       for i in range(n)) for n in (1, 700, 9000)]
@@ -145,6 +148,11 @@ def test_streams_at_any_offset(dev):
             assert len(refs[-1]) == i_
     streams.append(gzip.compress(texts[1], 1)[:-9])        # truncated
     refs.append(None)
+    for k in (1, len(streams) // 2, len(streams) - 2):    # a wrong trailer CRC: every byte decodes
+        x = bytearray(streams[k])
+        x[-8 + rng.randrange(4)] ^= 1 << rng.randrange(8)
+        streams.append(bytes(x))
+        refs.append(None)
     src = bytearray(b"\x00" * 3)
     in_off, out_off, caps = [], [], []
     opos = 5
@@ -160,11 +168,12 @@ def test_streams_at_any_offset(dev):
     d_io, d_il = dev.upload(np.array(in_off, np.int64)), dev.upload(np.array([len(b) for b in streams], np.int64))
     d_oo, d_cap = dev.upload(np.array(out_off, np.int64)), dev.upload(np.array(caps, np.int64))
     out = dev.alloc(opos + 256, np.uint8)
-    mem = dev.alloc(n * 4 * _abi.GZ_MEMBER_BYTES, np.uint8)
+    mem = dev.alloc(n * mcap * _abi.GZ_MEMBER_BYTES, np.uint8)
     st, ln, nm = dev.alloc(n, np.int32), dev.alloc(n, np.int64), dev.alloc(n, np.int32)
     _abi.call("grid_gunzip_batch", dev.ctx, d_src.ptr, d_io.ptr, d_il.ptr, n, out.ptr, d_oo.ptr, d_cap.ptr, mem.ptr,
-              4, st.ptr, ln.ptr, nm.ptr)
+              mcap, st.ptr, ln.ptr, nm.ptr)
     st, ln, host = st.numpy(), ln.numpy(), out.numpy()
+    assert all(st[f] == _abi.GZ_ECRC for f in range(n - 3, n))
     for f, r in enumerate(refs):
         if r is None:
             assert st[f] != 0

@@ -360,3 +360,21 @@ def test_find_bed_gz_paths_equals_per_sample_glob(tmp_path):
         assert got[i] == nm.find_bed_gz_for_individual(i, tmp_path), i
     with pytest.raises(ValueError):                  # "**regions.bed.gz": pathlib rejects it, as for the reference
         nm.find_bed_gz_paths([""], tmp_path)
+
+
+def test_device_ingest_chunk_table():
+    """ingest_device._chunks (the parse kernels' chunk table, built with numpy
+    per pipelined batch): every file with text cut in CH-byte chunks, in file
+    order, its first chunk in cfirst."""
+    from grid_amd.utils import ingest_device as d
+    rng = np.random.default_rng(3)
+    for _ in range(100):
+        nb = int(rng.integers(1, 12))
+        tlen = rng.integers(0, 5 * d.CH, nb)
+        tlen[rng.random(nb) < 0.2] = 0
+        files = [f for f in range(nb) if tlen[f] > 0 and rng.random() < 0.8]
+        cfile, cstart, cfirst, tot = d._chunks(files, tlen)
+        exp = [(f, s) for f in files for s in range(0, int(tlen[f]), d.CH)]
+        assert tot == len(exp)
+        assert [(int(a), int(b)) for a, b in zip(cfile[:tot], cstart[:tot])] == exp
+        assert cfirst.tolist() == [0] + list(np.cumsum([-(-int(tlen[f]) // d.CH) for f in files]))

@@ -31,6 +31,8 @@ ap.add_argument("--per-hap", type=int, default=10)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--cpu-samples", type=int, default=1000)
 ap.add_argument("--paired", action="store_true", help="A/B: the two-haplotypes-per-lane kernel")
+ap.add_argument("--inflight", type=int, default=3, help="groups of loci running at once (engine.phase_batch)")
+ap.add_argument("--group", type=int, default=0, help="loci per group (0: the CU count)")
 a = ap.parse_args()
 
 
@@ -58,7 +60,7 @@ res, times = None, []
 for rep in range(a.reps + 1):          # first call: schedules, uploads and warm-up
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    res = engine.phase_batch(dev, loci, 1, a.iters, paired=a.paired)
+    res = engine.phase_batch(dev, loci, 1, a.iters, paired=a.paired, group=a.group or None, inflight=a.inflight)
     torch.cuda.synchronize()
     times.append(time.perf_counter() - t1)
 
@@ -106,7 +108,7 @@ si = a.loci * a.samples * a.iters
 print(json.dumps({
     "metric": "loci/s batched haplotype phasing (config 5)", "value": a.loci / (gpu_ms * 1e-3), "unit": "loci/s",
     "config": {"loci": a.loci, "samples": a.samples, "n_iters": a.iters, "per_hap": a.per_hap,
-               "max_levels": max_nl},
+               "max_levels": max_nl, "inflight": a.inflight, "group": a.group},
     "device_ms": gpu_ms, "sample_iters_per_s": si / (gpu_ms * 1e-3),
     "end_to_end_s": min(times[1:]), "first_call_s": times[0], "synthetic_generation_s": gen_s,
     "cpu_baseline": {"sample_iters_per_s": 1.0 / cpu_per_si, "cores": 1, "kind": "port",
