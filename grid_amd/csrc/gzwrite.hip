@@ -34,6 +34,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <cstdio>
 #include <cstring>
@@ -721,6 +722,18 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
     grid_set_error("cannot open %s for writing", path);
     return GRID_EINVAL;
   }
+  // The batches go to the file through a second descriptor opened O_DIRECT
+  // where the file system allows it: 4 KiB-aligned ranges straight from the
+  // pinned buffers, no page-cache copy and no dirty-page throttling (the
+  // overlay disk of the MI355X boxes: 4.6 GB/s through the page cache with a
+  // final sync, 5.5 GB/s direct, profiles/r04l_disk.txt).  Each batch is
+  // copied to host memory FA bytes into its buffer, FA = its file offset mod
+  // 4 KiB, so the buffer starts on a 4 KiB file boundary once the previous
+  // batch's unaligned tail (the carry, < 4 KiB) is put in front of it; the
+  // last carry goes through the ordinary descriptor.  Without O_DIRECT every
+  // batch is written whole through the ordinary descriptor.
+  constexpr size_t FA = 4096;
+  std::atomic<int> fdd{open(path, O_WRONLY | O_DIRECT)};
   hipStream_t st = ctx->stream;
   const int64_t nblk = std::max<int64_t>(1, (r + CPB - 1) / CPB);
   // rows per member (the host writer's rule: ~8 MB of text per member)
@@ -743,19 +756,24 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
   // writer thread: member 0 first, then the batches in order
   std::mutex mu;
   std::condition_variable cv;
-  std::deque<std::pair<int, size_t>> q;      // (pinned buffer, bytes); -1 = end
+  std::deque<std::pair<int, size_t>> q;      // (pinned buffer, bytes after its front gap); -1 = end
   int busy[2] = {0, 0};
+  size_t gap[2] = {0, 0};                    // bytes in front of a buffer's batch: its file offset mod FA
+  int64_t hdr_size = -1;                     // known once the writer thread has the header member
   // pwrite of [p, p + len) at file offset o by up to 4 threads (page-cache
   // copies: one thread moves ~5 GB/s)
-  auto pwrite_all = [&](const char *p, size_t len, int64_t o) {
+  // pwrite of [p, p + len) at file offset o by up to 4 threads (page-cache
+  // copies: one thread moves ~5 GB/s); on the direct descriptor the pieces
+  // split at FA multiples
+  auto pwrite_all = [&](int f, const char *p, size_t len, int64_t o, size_t unit) {
     const int W = (int)std::max<size_t>(1, std::min<size_t>(4, len >> 26));
     std::vector<std::thread> ws;
     std::vector<char> ok((size_t)W, 1);
     for (int t = 0; t < W; t++)
       ws.emplace_back([&, t] {
-        size_t a = len * t / W, b = len * (t + 1) / W;
+        size_t a = (len / unit) * t / W * unit, b = t + 1 == W ? len : (len / unit) * (t + 1) / W * unit;
         while (a < b) {
-          const ssize_t k = pwrite(fd, p + a, b - a, o + (int64_t)a);
+          const ssize_t k = pwrite(f, p + a, b - a, o + (int64_t)a);
           if (k <= 0) { ok[(size_t)t] = 0; return; }
           a += (size_t)k;
         }
@@ -765,11 +783,21 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
       if (!c) return false;
     return true;
   };
-  int64_t foff = 0;
+  int64_t foff = 0;                          // file bytes written (direct: up to the carry)
+  int64_t out_done = 0;                      // batch bytes handed to the writer (main thread)
+  std::string carry;                         // direct mode: the written batches' unaligned tail
   std::thread wr([&] {
     hdr_thr.join();
-    if (!hdr_ok || !pwrite_all(hdr_member.data(), hdr_member.size(), 0)) io_ok = false;
-    foff = (int64_t)hdr_member.size();
+    const size_t hs = hdr_member.size();
+    const size_t ha = fdd >= 0 ? hs / FA * FA : hs;
+    if (!hdr_ok || !pwrite_all(fd, hdr_member.data(), ha, 0, 1)) io_ok = false;
+    carry.assign(hdr_member.data() + ha, hs - ha);
+    foff = (int64_t)ha;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      hdr_size = (int64_t)hs;
+    }
+    cv.notify_all();
     for (;;) {
       std::pair<int, size_t> job;
       {
@@ -779,8 +807,28 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
         q.pop_front();
       }
       if (job.first < 0) return;
-      if (io_ok && !pwrite_all((const char *)hb[job.first].p, job.second, foff)) io_ok = false;
-      foff += (int64_t)job.second;
+      char *b = (char *)hb[job.first].p;
+      const size_t g = gap[job.first];
+      if (io_ok && fdd >= 0 && carry.size() == g) {
+        memcpy(b, carry.data(), g);          // the buffer now starts at file offset foff (FA-aligned)
+        const size_t tot = g + job.second, da = tot / FA * FA;
+        if (da && !pwrite_all(fdd, b, da, foff, FA)) {
+          close(fdd.exchange(-1));           // direct I/O refused: this batch and the rest the ordinary way
+          if (!pwrite_all(fd, b, tot, foff, 1)) io_ok = false;
+          carry.clear();
+          foff += (int64_t)tot;
+        } else {
+          carry.assign(b + da, tot - da);
+          foff += (int64_t)da;
+        }
+      } else if (io_ok) {
+        // the ordinary descriptor: the carry (if direct I/O stopped), then the batch after its gap
+        if (!carry.empty() && !pwrite_all(fd, carry.data(), carry.size(), foff, 1)) io_ok = false;
+        foff += (int64_t)carry.size();
+        carry.clear();
+        if (io_ok && !pwrite_all(fd, b + g, job.second, foff, 1)) io_ok = false;
+        foff += (int64_t)job.second;
+      }
       {
         std::lock_guard<std::mutex> lk(mu);
         busy[job.first] = 0;
@@ -795,6 +843,8 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
     }
     cv.notify_all();
     wr.join();
+    if (io_ok && !carry.empty() && !pwrite_all(fd, carry.data(), carry.size(), foff, 1)) io_ok = false;
+    if (fdd >= 0 && close(fdd.exchange(-1)) != 0) io_ok = false;
     if (close(fd) != 0) io_ok = false;
     if (code == GRID_OK && !io_ok) {
       grid_set_error("grid_write_normalized_gz_dev: %s failed", hdr_ok ? "write" : "header deflate");
@@ -981,17 +1031,22 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
                        d_mrow.p, d_mlen.p, d_mbits.p, d_crc.p, d_hdr.p, code.hdr_bits, (uint32_t)code.rcode[256],
                        eob_len, nm);
     STEP(hipGetLastError());
-    // to pinned host memory (the writer thread must be done with this buffer)
+    // to pinned host memory (the writer thread must be done with this buffer),
+    // gap bytes into it: the batch's file offset mod FA (the header's size is
+    // needed for the first batch)
     {
       std::unique_lock<std::mutex> lk(mu);
-      cv.wait(lk, [&] { return !busy[cur]; });
+      cv.wait(lk, [&] { return !busy[cur] && hdr_size >= 0; });
     }
-    STEP(hb[cur].need((size_t)obytes));
-    STEP(hipMemcpyAsync(hb[cur].p, d_out.p, (size_t)obytes, hipMemcpyDeviceToHost, st));
+    const size_t g = fdd >= 0 ? (size_t)((hdr_size + out_done) % (int64_t)FA) : 0;
+    STEP(hb[cur].need((size_t)obytes + FA));
+    STEP(hipMemcpyAsync((char *)hb[cur].p + g, d_out.p, (size_t)obytes, hipMemcpyDeviceToHost, st));
     STEP(hipStreamSynchronize(st));
+    out_done += obytes;
     {
       std::lock_guard<std::mutex> lk(mu);
       busy[cur] = 1;
+      gap[cur] = g;
       q.push_back({cur, (size_t)obytes});
     }
     cv.notify_all();

@@ -504,12 +504,14 @@ __global__ __launch_bounds__(CT) void k_gz_crc(const uint8_t *__restrict__ out, 
   if (tid == 0 && s_bad) status[f] = GRID_GZ_ECRC;
 }
 
-// BGZF units (one member each, mcap == 1; a member's text is <= 64 KiB): one
-// WAVE per member instead of one workgroup -- lane l takes bytes [1 KiB l,
-// 1 KiB (l + 1)) (slicing by 4, tables in LDS), a 6-level tree of the fixed
-// operators M^(1 KiB 2^k) = c_crc_pow[10 + k] joins the lanes (the general
-// shift where a subtree is short), lane 0 adds the initial register; longer
-// members take several 64 KiB rounds.  The raw-register convention of k_gz_crc.
+// BGZF units (one member each, mcap == 1): one WAVE per member.  The text is
+// read in 1 KiB rows, lane l taking the 16 bytes [16 l, 16 l + 16) of every
+// row -- each wave load is 1 KiB contiguous -- and keeping the raw register
+// (from state 0) of its column of blocks: acc_l = M^1024 acc_l ^ crc0(block).
+// A 6-level tree of M^(16 2^k) (c_crc_pow[4 + k]) joins the columns (lane l's
+// last block is followed by 63 - l blocks of its row), lane 0 adds the tail
+// row byte by byte and the initial register.  Same raw-register convention as
+// k_gz_crc; a member whose CRC differs gets GRID_GZ_ECRC.
 __global__ __launch_bounds__(256) void k_member_check(const uint8_t *__restrict__ out,
                                                       const int64_t *__restrict__ out_off,
                                                       const grid_gz_member *__restrict__ mem,
@@ -534,31 +536,38 @@ __global__ __launch_bounds__(256) void k_member_check(const uint8_t *__restrict_
   if (__builtin_amdgcn_readfirstlane(status[u]) != 0 || __builtin_amdgcn_readfirstlane(nmem[u]) < 1) return;
   const grid_gz_member g = mem[u];
   const uint8_t *base = out + out_off[u] + g.start;
-  const int64_t L = g.end - g.start;
-  uint32_t acc = 0xFFFFFFFFu;                           // raw register before the member's bytes
-  for (int64_t r0 = 0; r0 < L; r0 += 65536) {
-    const int64_t RL = min((int64_t)65536, L - r0);
-    const int64_t a = min(RL, (int64_t)1024 * lane), b = min(RL, a + 1024);
-    const uint8_t *p = base + r0;
-    uint32_t c = 0;
-    int64_t e = a;
-    for (; e < b && ((uintptr_t)(p + e) & 3); e++) c = t4[0][(c ^ p[e]) & 255] ^ (c >> 8);
-    for (; e + 4 <= b; e += 4) {
-      c ^= *(const uint32_t *)(p + e);
-      c = t4[3][c & 255] ^ t4[2][(c >> 8) & 255] ^ t4[1][(c >> 16) & 255] ^ t4[0][c >> 24];
+  const int64_t L = g.end - g.start, R = L >> 10;
+  auto step4 = [&](uint32_t c, uint32_t w) {
+    c ^= w;
+    return t4[3][c & 255] ^ t4[2][(c >> 8) & 255] ^ t4[1][(c >> 16) & 255] ^ t4[0][c >> 24];
+  };
+  uint32_t acc = 0;
+  const bool al = ((uintptr_t)base & 15) == 0;
+  for (int64_t k = 0; k < R; k++) {
+    const uint8_t *p = base + (k << 10) + 16 * lane;
+    uint32_t w0, w1, w2, w3;
+    if (al) {
+      const uint4 v = *reinterpret_cast<const uint4 *>(p);
+      w0 = v.x; w1 = v.y; w2 = v.z; w3 = v.w;
+    } else {                                            // a member's text at any byte offset
+      uint32_t b[4] = {0, 0, 0, 0};
+      for (int e = 0; e < 16; e++) b[e >> 2] |= (uint32_t)p[e] << (8 * (e & 3));
+      w0 = b[0]; w1 = b[1]; w2 = b[2]; w3 = b[3];
     }
-    for (; e < b; e++) c = t4[0][(c ^ p[e]) & 255] ^ (c >> 8);
-#pragma unroll
-    for (int k = 0; k < 6; k++) {
-      const uint32_t o = __shfl_down(c, 1 << k, 64);
-      const int64_t rs = (int64_t)1024 * (lane + (1 << k));
-      const int64_t lr = rs >= RL ? 0 : min(RL - rs, (int64_t)1024 << k);
-      if ((lane & ((2 << k) - 1)) == 0 && lr > 0)
-        c = (lr == ((int64_t)1024 << k) ? gf2_apply(c_crc_pow[10 + k], c) : crc_shift(c, (uint64_t)lr)) ^ o;
-    }
-    acc = crc_shift(acc, (uint64_t)RL) ^ c;            // lane 0's c is the round's
+    const uint32_t c = step4(step4(step4(step4(0u, w0), w1), w2), w3);
+    acc = gf2_apply(c_crc_pow[10], acc) ^ c;
   }
-  if (lane == 0 && (acc ^ 0xFFFFFFFFu) != g.crc) status[u] = GRID_GZ_ECRC;
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    const uint32_t o = __shfl_down(acc, 1 << k, 64);
+    if ((lane & ((2 << k) - 1)) == 0) acc = gf2_apply(c_crc_pow[4 + k], acc) ^ o;
+  }
+  if (lane == 0) {
+    uint32_t c = acc;                                   // raw CRC of the R full rows, from state 0
+    for (int64_t e = R << 10; e < L; e++) c = t4[0][(c ^ base[e]) & 255] ^ (c >> 8);
+    c ^= crc_shift(0xFFFFFFFFu, (uint64_t)L);
+    if ((c ^ 0xFFFFFFFFu) != g.crc) status[u] = GRID_GZ_ECRC;
+  }
 }
 
 bool g_crc_ready = false;

@@ -88,3 +88,31 @@ def test_device_writer_large_rows_size(tmp_path):
     _abi.write_normalized_gz_dev(dev, str(devf), ids, raw, mu, ra, dev.upload(zq), n, r, r, level=1)
     assert gzip.open(host, "rb").read() == gzip.open(devf, "rb").read()
     assert devf.stat().st_size < 1.2 * host.stat().st_size
+
+
+@pytest.mark.parametrize("where", ["tmp", "shm"])
+def test_device_writer_direct_and_buffered(tmp_path, where):
+    """The writer's two ways to the file -- O_DIRECT for 4 KiB-aligned ranges
+    with the unaligned carry through the ordinary descriptor (a disk file
+    system), or the ordinary descriptor only (where O_DIRECT is refused) -- give
+    the same bytes, over many batches whose sizes are not multiples of 4 KiB."""
+    import os
+    import tempfile
+    from grid_amd import _abi
+    dev = _dev()
+    n, r = 40, 20011
+    ids, raw, mu, ra, zq = _case(n, r, seed=77)
+    dz = dev.upload(zq)
+    d = tmp_path if where == "tmp" else tempfile.mkdtemp(dir="/dev/shm") if os.path.isdir("/dev/shm") else tmp_path
+    outs = []
+    for batch in (0, 123457):                     # one batch; ~20 batches of odd sizes
+        f = os.path.join(str(d), f"o{batch}.gz")
+        _abi.write_normalized_gz_dev(dev, f, ids, raw, mu, ra, dz, n, r, r, level=1, batch_bytes=batch)
+        outs.append(open(f, "rb").read())
+        _members(f)
+        os.remove(f)
+    if str(d) != str(tmp_path):
+        os.rmdir(d)
+    host = tmp_path / "host.gz"
+    _abi.write_normalized_gz(str(host), ids, raw, mu, ra, zq, level=1)
+    assert gzip.decompress(outs[0]) == gzip.decompress(outs[1]) == gzip.open(host, "rb").read()

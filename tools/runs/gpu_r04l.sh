@@ -9,9 +9,9 @@ export TMPDIR=/tmp
 timeout -k 10 500 python -u -m pytest -x -v --timeout 200 --timeout-method thread -p no:cacheprovider \
   tests/test_gpu_inflate.py tests/test_gpu_ingest.py tests/test_gpu_e2e.py > $O/pytest.log 2>&1 || { tail -n 40 $O/pytest.log; exit 1; }
 tail -n 3 $O/pytest.log
-{ df -h /tmp; for m in buffered direct; do
-    if [ $m = direct ]; then f="oflag=direct"; else f="conv=fdatasync"; fi
-    /usr/bin/time -f "$m %e s" dd if=/dev/zero of=/tmp/ddtest bs=64M count=96 $f 2>&1 | tail -n 2; rm -f /tmp/ddtest; done; } > $O/disk.txt 2>&1
+{ df -h /tmp; for m in buffered fdatasync direct; do
+    case $m in direct) f="oflag=direct";; fdatasync) f="conv=fdatasync";; *) f="";; esac
+    echo "== $m"; timeout -k 5 120 dd if=/dev/zero of=/tmp/ddtest bs=64M count=96 $f 2>&1 | tail -n 1; rm -f /tmp/ddtest; done; } > $O/disk.txt 2>&1
 cat $O/disk.txt
 timeout -k 10 300 python -u tools/e2e_files.py --bgzf --generate-only > $O/gen.log 2>&1 || { tail -n 20 $O/gen.log; exit 1; }
 GRID_INGEST_TRACE=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -- \
