@@ -531,6 +531,24 @@ __device__ __forceinline__ int32_t q_at(const int32_t *__restrict__ q, const Q16
   else return q[i * ld + j];
 }
 
+// Raw compact words of CUN rows, 2 codes (columns j0, j0 + 1) per 4-byte word.
+template <int CUN, bool NTL>
+__device__ __forceinline__ void ld_raw(const Q16 &s16, int64_t i0, int64_t ld, int64_t j0, uint32_t (&w)[CUN]) {
+#pragma unroll
+  for (int u = 0; u < CUN; u++) {
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(s16.q + (i0 + u) * ld + j0);
+    w[u] = NTL ? __builtin_nontemporal_load(p) : *p;
+  }
+}
+template <int CUN>
+__device__ __forceinline__ void unpack_raw(const uint32_t (&w)[CUN], int32_t (&v)[CUN][2]) {
+#pragma unroll
+  for (int u = 0; u < CUN; u++) {
+    v[u][0] = (int32_t)(w[u] & 0xFFFFu);
+    v[u][1] = (int32_t)(w[u] >> 16);
+  }
+}
+
 // PF: software-pipelined row groups (the next group's loads issued before
 // this group is summed; the summation order is unchanged).
 template <int VW, bool S16, int CUN = CU, bool NTL = false, bool PF = false>
@@ -586,7 +604,21 @@ __global__ __launch_bounds__(256) void k_col_means(const int32_t *__restrict__ q
   };
   const int64_t ng = n / CUN;
   int64_t i = 0;
-  if constexpr (PF) {
+  if constexpr (PF && S16 && VW == 2) {
+    // the next group's codes in flight while this group is summed (same order),
+    // held as the raw 4-byte words (2 codes each): 8 registers per group, so the
+    // pipelined loop keeps the occupancy of the plain one
+    uint32_t wa[CUN], wb[CUN];
+    if (ng > 0) ld_raw<CUN, NTL>(s16, 0, ld, j0, wa);
+    for (int64_t g = 0; g < ng; g += 2) {
+      if (g + 1 < ng) ld_raw<CUN, NTL>(s16, (g + 1) * CUN, ld, j0, wb);
+      { int32_t v[CUN][VW]; unpack_raw<CUN>(wa, v); do_grp(v, g * CUN); }
+      if (g + 1 >= ng) break;
+      if (g + 2 < ng) ld_raw<CUN, NTL>(s16, (g + 2) * CUN, ld, j0, wa);
+      { int32_t v[CUN][VW]; unpack_raw<CUN>(wb, v); do_grp(v, (g + 1) * CUN); }
+    }
+    i = ng * CUN;
+  } else if constexpr (PF) {
     // the next group's loads are in flight while this group is summed (same order)
     int32_t va[CUN][VW], vb[CUN][VW];
     if (ng > 0) ld_grp(va, 0);
@@ -682,7 +714,18 @@ __global__ __launch_bounds__(256) void k_col_vars(const int32_t *__restrict__ q,
   };
   const int64_t ng = n / CUN;
   int64_t i = 0;
-  if constexpr (PF) {
+  if constexpr (PF && S16 && VW == 2) {
+    uint32_t wa[CUN], wb[CUN];
+    if (ng > 0) ld_raw<CUN, NTL>(s16, 0, ld, j0, wa);
+    for (int64_t g = 0; g < ng; g += 2) {
+      if (g + 1 < ng) ld_raw<CUN, NTL>(s16, (g + 1) * CUN, ld, j0, wb);
+      { int32_t v[CUN][VW]; unpack_raw<CUN>(wa, v); do_grp(v, g * CUN); }
+      if (g + 1 >= ng) break;
+      if (g + 2 < ng) ld_raw<CUN, NTL>(s16, (g + 2) * CUN, ld, j0, wa);
+      { int32_t v[CUN][VW]; unpack_raw<CUN>(wb, v); do_grp(v, (g + 1) * CUN); }
+    }
+    i = ng * CUN;
+  } else if constexpr (PF) {
     int32_t va[CUN][VW], vb[CUN][VW];
     if (ng > 0) ld_grp(va, 0);
     for (int64_t g = 0; g < ng; g += 2) {

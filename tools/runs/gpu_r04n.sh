@@ -16,3 +16,10 @@ for f in 1 3; do
     > $O/loci_50k_inflight$f.json 2> $O/loci_50k_inflight$f.err || { tail -n 20 $O/loci_50k_inflight$f.err; exit 1; }
   python -c "import json; d=json.load(open('$O/loci_50k_inflight$f.json')); print($f, 'device_ms', round(d['device_ms'],1), 'e2e', round(d['end_to_end_s'],3))"
 done
+# column statistics: raw-word software-pipelined row groups (GRID_COL_PF=1, tools build) vs the default
+for v in 0 1 0 1; do
+  GRID_AMD_LIB=grid_amd/_lib/libgridhip_probes.so GRID_COL_PF=$v timeout -k 10 200 python -u bench.py --steps 10 \
+    --warmup 2 --no-cpu-baseline --config3-steps 0 --no-files-config2 > $O/colpf$v.json 2> $O/colpf$v.err \
+    || { tail -n 20 $O/colpf$v.err; exit 1; }
+  python -c "import json; d=json.load(open('$O/colpf$v.json')); print('PF', $v, d['ms_per_step'], d['stages_ms']['col_stats'])"
+done
