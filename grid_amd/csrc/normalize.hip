@@ -531,21 +531,28 @@ __device__ __forceinline__ int32_t q_at(const int32_t *__restrict__ q, const Q16
   else return q[i * ld + j];
 }
 
-// Raw compact words of CUN rows, 2 codes (columns j0, j0 + 1) per 4-byte word.
-template <int CUN, bool NTL>
+// Raw compact codes of CUN rows: one 2-byte code (VW 1) or 2 codes (columns
+// j0, j0 + 1) per 4-byte word (VW 2), one register per row either way.
+template <int VW, int CUN, bool NTL>
 __device__ __forceinline__ void ld_raw(const Q16 &s16, int64_t i0, int64_t ld, int64_t j0, uint32_t (&w)[CUN]) {
+  static_assert(VW == 1 || VW == 2, "raw rows of 1 or 2 compact codes");
 #pragma unroll
   for (int u = 0; u < CUN; u++) {
-    const uint32_t *p = reinterpret_cast<const uint32_t *>(s16.q + (i0 + u) * ld + j0);
-    w[u] = NTL ? __builtin_nontemporal_load(p) : *p;
+    const uint16_t *p16 = s16.q + (i0 + u) * ld + j0;
+    if constexpr (VW == 2) {
+      const uint32_t *p = reinterpret_cast<const uint32_t *>(p16);
+      w[u] = NTL ? __builtin_nontemporal_load(p) : *p;
+    } else {
+      w[u] = NTL ? __builtin_nontemporal_load(p16) : *p16;
+    }
   }
 }
-template <int CUN>
-__device__ __forceinline__ void unpack_raw(const uint32_t (&w)[CUN], int32_t (&v)[CUN][2]) {
+template <int VW, int CUN>
+__device__ __forceinline__ void unpack_raw(const uint32_t (&w)[CUN], int32_t (&v)[CUN][VW]) {
 #pragma unroll
   for (int u = 0; u < CUN; u++) {
     v[u][0] = (int32_t)(w[u] & 0xFFFFu);
-    v[u][1] = (int32_t)(w[u] >> 16);
+    if constexpr (VW == 2) v[u][1] = (int32_t)(w[u] >> 16);
   }
 }
 
@@ -604,18 +611,18 @@ __global__ __launch_bounds__(256) void k_col_means(const int32_t *__restrict__ q
   };
   const int64_t ng = n / CUN;
   int64_t i = 0;
-  if constexpr (PF && S16 && VW == 2) {
+  if constexpr (PF && S16 && VW <= 2) {
     // the next group's codes in flight while this group is summed (same order),
     // held as the raw 4-byte words (2 codes each): 8 registers per group, so the
     // pipelined loop keeps the occupancy of the plain one
     uint32_t wa[CUN], wb[CUN];
-    if (ng > 0) ld_raw<CUN, NTL>(s16, 0, ld, j0, wa);
+    if (ng > 0) ld_raw<VW, CUN, NTL>(s16, 0, ld, j0, wa);
     for (int64_t g = 0; g < ng; g += 2) {
-      if (g + 1 < ng) ld_raw<CUN, NTL>(s16, (g + 1) * CUN, ld, j0, wb);
-      { int32_t v[CUN][VW]; unpack_raw<CUN>(wa, v); do_grp(v, g * CUN); }
+      if (g + 1 < ng) ld_raw<VW, CUN, NTL>(s16, (g + 1) * CUN, ld, j0, wb);
+      { int32_t v[CUN][VW]; unpack_raw<VW, CUN>(wa, v); do_grp(v, g * CUN); }
       if (g + 1 >= ng) break;
-      if (g + 2 < ng) ld_raw<CUN, NTL>(s16, (g + 2) * CUN, ld, j0, wa);
-      { int32_t v[CUN][VW]; unpack_raw<CUN>(wb, v); do_grp(v, (g + 1) * CUN); }
+      if (g + 2 < ng) ld_raw<VW, CUN, NTL>(s16, (g + 2) * CUN, ld, j0, wa);
+      { int32_t v[CUN][VW]; unpack_raw<VW, CUN>(wb, v); do_grp(v, (g + 1) * CUN); }
     }
     i = ng * CUN;
   } else if constexpr (PF) {
@@ -714,15 +721,15 @@ __global__ __launch_bounds__(256) void k_col_vars(const int32_t *__restrict__ q,
   };
   const int64_t ng = n / CUN;
   int64_t i = 0;
-  if constexpr (PF && S16 && VW == 2) {
+  if constexpr (PF && S16 && VW <= 2) {
     uint32_t wa[CUN], wb[CUN];
-    if (ng > 0) ld_raw<CUN, NTL>(s16, 0, ld, j0, wa);
+    if (ng > 0) ld_raw<VW, CUN, NTL>(s16, 0, ld, j0, wa);
     for (int64_t g = 0; g < ng; g += 2) {
-      if (g + 1 < ng) ld_raw<CUN, NTL>(s16, (g + 1) * CUN, ld, j0, wb);
-      { int32_t v[CUN][VW]; unpack_raw<CUN>(wa, v); do_grp(v, g * CUN); }
+      if (g + 1 < ng) ld_raw<VW, CUN, NTL>(s16, (g + 1) * CUN, ld, j0, wb);
+      { int32_t v[CUN][VW]; unpack_raw<VW, CUN>(wa, v); do_grp(v, g * CUN); }
       if (g + 1 >= ng) break;
-      if (g + 2 < ng) ld_raw<CUN, NTL>(s16, (g + 2) * CUN, ld, j0, wa);
-      { int32_t v[CUN][VW]; unpack_raw<CUN>(wb, v); do_grp(v, (g + 1) * CUN); }
+      if (g + 2 < ng) ld_raw<VW, CUN, NTL>(s16, (g + 2) * CUN, ld, j0, wa);
+      { int32_t v[CUN][VW]; unpack_raw<VW, CUN>(wb, v); do_grp(v, (g + 1) * CUN); }
     }
     i = ng * CUN;
   } else if constexpr (PF) {
@@ -2099,7 +2106,7 @@ static int col_stats_impl(grid_ctx *ctx, bool vars, const int32_t *d_q, const Q1
   const char *cu = GRID_AB_KNOB("GRID_COL16_CU");   // compact codes: 16 rows in flight (timing only)
   const bool cu16 = s16.q && cu && atoi(cu) == 16;
 #endif
-  const char *cpf = GRID_AB_KNOB("GRID_COL_PF");  // software-pipelined row groups, compact 2-column path (A/B)
+  const char *cpf = GRID_AB_KNOB("GRID_COL_PF");  // software-pipelined row groups, compact 1- and 2-column paths (A/B)
   const bool pf = cpf ? atoi(cpf) != 0 : COL_PF;
   const char *cn = getenv("GRID_COL_NT");   // streaming (nontemporal) loads, 1-column path (A/B)
   const bool nt = cn ? atoi(cn) != 0 : COL_NT;
@@ -2113,19 +2120,21 @@ static int col_stats_impl(grid_ctx *ctx, bool vars, const int32_t *d_q, const Q1
   const dim3 grid((unsigned)ceil_div(ceil_div(m, vw), 256));
   if (!vars) {
     auto kern = s16.q ? (vw == 8 ? (nt ? k_col_means<8, true, CU, true> : k_col_means<8, true>) : vw == 4 ? k_col_means<4, true>
-                         : vw == 2 ? (cu16 ? k_col_means<2, true, 16, true>
-                                      : nt ? (pf ? k_col_means<2, true, CU, true, true> : k_col_means<2, true, CU, true>)
-                                           : k_col_means<2, true>)
-                                   : (nt ? k_col_means<1, true, CU, true> : k_col_means<1, true>))
+                         : vw == 2 ? (pf ? (cu16 ? k_col_means<2, true, 16, true, true> : k_col_means<2, true, CU, true, true>)
+                                      : cu16 ? k_col_means<2, true, 16, true>
+                                      : nt ? k_col_means<2, true, CU, true> : k_col_means<2, true>)
+                                   : pf ? (cu16 ? k_col_means<1, true, 16, true, true> : k_col_means<1, true, CU, true, true>)
+                                        : (nt ? k_col_means<1, true, CU, true> : k_col_means<1, true>))
                 : vw == 4 ? k_col_means<4, false> : vw == 2 ? k_col_means<2, false>
                 : cu16 ? k_col_means<1, false, 16> : nt ? k_col_means<1, false, CU, true> : k_col_means<1, false>;
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, ctx->stream, d_q, s16, n, m, ld, d_rm, rinv, rbad, d_out);
   } else {
     auto kern = s16.q ? (vw == 8 ? (nt ? k_col_vars<8, true, CU, true> : k_col_vars<8, true>) : vw == 4 ? k_col_vars<4, true>
-                         : vw == 2 ? (cu16 ? k_col_vars<2, true, 16, true>
-                                      : nt ? (pf ? k_col_vars<2, true, CU, true, true> : k_col_vars<2, true, CU, true>)
-                                           : k_col_vars<2, true>)
-                                   : (nt ? k_col_vars<1, true, CU, true> : k_col_vars<1, true>))
+                         : vw == 2 ? (pf ? (cu16 ? k_col_vars<2, true, 16, true, true> : k_col_vars<2, true, CU, true, true>)
+                                      : cu16 ? k_col_vars<2, true, 16, true>
+                                      : nt ? k_col_vars<2, true, CU, true> : k_col_vars<2, true>)
+                                   : pf ? (cu16 ? k_col_vars<1, true, 16, true, true> : k_col_vars<1, true, CU, true, true>)
+                                        : (nt ? k_col_vars<1, true, CU, true> : k_col_vars<1, true>))
                 : vw == 4 ? k_col_vars<4, false> : vw == 2 ? k_col_vars<2, false>
                 : cu16 ? k_col_vars<1, false, 16> : nt ? k_col_vars<1, false, CU, true> : k_col_vars<1, false>;
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, ctx->stream, d_q, s16, n, m, ld, d_rm, rinv, rbad, d_mu, d_out,

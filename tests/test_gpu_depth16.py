@@ -85,11 +85,19 @@ def test_synth_q16_equals_encoded_synth(dev):
     assert torch.equal(d.ecol[:k], ecol) and torch.equal(d.evals[:k], ev)
 
 
+# raw-code software-pipelined column kernels (GRID_COL_PF; 1 or 2 columns per
+# thread, 8 or 16 rows per group); the knobs take effect in the tools build
+# (GRID_AMD_LIB=.../libgridhip_probes.so), the product library runs its defaults
+PF_KNOBS = [{"GRID_COL_PF": "1"}, {"GRID_COL_PF": "1", "GRID_COL16_VW": "1"},
+            {"GRID_COL_PF": "1", "GRID_COL16_VW": "1", "GRID_COL16_CU": "16"},
+            {"GRID_COL_PF": "1", "GRID_COL16_CU": "16"}]
+
+
 @pytest.mark.parametrize("knobs", [{}, {"GRID_COL16_VW": "1", "GRID_ROWBLK16_PB": "1"},
                                    {"GRID_COL16_VW": "4", "GRID_ROWBLK16_PB": "4", "GRID_ROWBLK_NT": "0",
                                     "GRID_COL_NT": "0", "GRID_ZQUANT_NT": "0", "GRID_ZQUANT_GROUPS": "3"},
                                    {"GRID_COL16_CU": "16", "GRID_ROWBLK16_PB": "2", "GRID_ZQUANT_GROUPS": "5"},
-                                   {"GRID_ZQUANT7": "0"}])
+                                   {"GRID_ZQUANT7": "0"}] + PF_KNOBS)
 @pytest.mark.parametrize("pattern", ["every3", "dense"])
 def test_step4_kernels_q16_equal_int32(dev, knobs, pattern, monkeypatch):
     """Every q16 kernel variant (columns per thread, blocks per workgroup,
@@ -196,14 +204,17 @@ def test_row_means_every_tail_length(dev, tail):
         assert np.array_equal(bcnt.cpu().numpy()[:, 1], (q[:, 8192:] != MISSING).sum(1))
 
 
+@pytest.mark.parametrize("knobs", [{}] + PF_KNOBS)
 @pytest.mark.parametrize("n,m", [(1, 9), (7, 1001), (8, 64), (33, 777), (257, 4099), (300, 5 * 8192 + 517),
                                  (520, 2 * 8192 + 1)])
-def test_col_stats_pipelined_equal_int32(dev, n, m):
+def test_col_stats_pipelined_equal_int32(dev, n, m, knobs, monkeypatch):
     """The pipelined compact column kernel (k_col16_pipe: LDS row windows,
     groups of 8 rows in flight, ragged last column) gives the int32 column
     kernels' bits: rows not a multiple of 8 or 32, windows of 256 rows, odd m,
     missing cells, escapes and a zero-mean row."""
     from grid_amd.fused import Depth16, HipOps
+    for k_, v_ in knobs.items():
+        monkeypatch.setenv(k_, v_)
     q = random_depths(n, m, 7 * n + m)
     if n > 3:
         q[3, :] = 0                                  # row mean 0: a bad row (skipped)
