@@ -201,6 +201,7 @@ __global__ __launch_bounds__(NT, 2) void k_gram_dma(const uint16_t *__restrict__
 }
 
 constexpr int BM3 = 256, BN3 = 128;
+constexpr bool GRAM_WIDE = false;   // default for GRID_GRAM_WIDE (16x16 layout: flush in 512-B row segments)
 constexpr int SLOT3 = (BM3 + BN3) * BK * 2;     // 48 KiB
 constexpr int QSA = BM3 * BK * 2, QSB = BN3 * BK * 2;   // quad-row image: A / B slot bytes
 
@@ -1183,6 +1184,47 @@ __device__ __forceinline__ void g8q_atomics(int32_t (&iacc)[4][4][4], int I, int
       }
 }
 
+// The same drain with 512-B row segments: per (a, r) the four 16x16 blocks'
+// registers are transposed across the wave's four 16-lane groups (a 4x4
+// transpose of (lane group, block): two exchange stages, lanes xor 32 then
+// xor 16, two shuffles each), after which register b of lane l holds row
+// 16 a + 4 b + r, column 64 wc + l -- one wave-instruction covers one row's 64
+// consecutive int64 (4 rows x 128 B before).  The same 64 atomics per wave.
+__device__ __forceinline__ void g8q_atomics_wide(int32_t (&iacc)[4][4][4], int I, int tj, int64_t np_,
+                                                 unsigned long long *__restrict__ gram) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const bool g1 = (lane >> 5) & 1, g0 = (lane >> 4) & 1;
+#pragma unroll
+  for (int a = 0; a < 4; a++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      int32_t v[4] = {iacc[a][0][r], iacc[a][1][r], iacc[a][2][r], iacc[a][3][r]};
+      // stage 1: swap bit 1 of the lane group with bit 1 of the block index
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        const int32_t snd = g1 ? v[j] : v[j | 2];
+        const int32_t rcv = __shfl_xor(snd, 32, 64);
+        if (g1) v[j] = rcv; else v[j | 2] = rcv;
+      }
+      // stage 2: bit 0 with bit 0
+#pragma unroll
+      for (int j = 0; j < 4; j += 2) {
+        const int32_t snd = g0 ? v[j] : v[j | 1];
+        const int32_t rcv = __shfl_xor(snd, 16, 64);
+        if (g0) v[j] = rcv; else v[j | 1] = rcv;
+      }
+      const int col = tj * BN3 + wc * 64 + lane;
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        const int row = I * BM3 + wr * 64 + a * 16 + 4 * b + r;
+        if (v[b] != 0) atomicAdd(gram + (int64_t)row * np_ + col, (unsigned long long)(long long)v[b]);
+      }
+#pragma unroll
+      for (int b = 0; b < 4; b++) iacc[a][b][r] = 0;
+    }
+}
+
 // kx = the number of K-ranges the XCDs split the K axis into (8, 4, 2 or 1):
 // XCD x runs K-range x % kx of the tile groups g = x / kx (mod 8 / kx).  A
 // small cohort (fewer tile groups than XCDs) splits K eight ways; a large one
@@ -1217,7 +1259,7 @@ __global__ __launch_bounds__(512, 1) void k_gram8(const uint16_t *__restrict__ z
   // the launch open for its fixed share
   for (int64_t r = 0;; r++) {
     int64_t u = r * per + l;
-    if (dyn) {
+    if (dyn & 1) {
       if (threadIdx.x == 0)
         s_unit = (int64_t)__hip_atomic_fetch_add(rounds + 128 + xcd * 16, 1u, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT);
@@ -1260,7 +1302,10 @@ __global__ __launch_bounds__(512, 1) void k_gram8(const uint16_t *__restrict__ z
 #pragma unroll
             for (int r = 0; r < 4; r++) { acc[a][b][r] = 0.0f; iacc[a][b][r] = 0; }
         g8q_run<MODE, FL>(z, ld, I, tj, s0, s1, smem, acc, iacc);
-        if constexpr (MODE != 9) g8q_atomics(iacc, I, tj, np_, gram);
+        if constexpr (MODE != 9) {
+          if (dyn & 2) g8q_atomics_wide(iacc, I, tj, np_, gram);
+          else g8q_atomics(iacc, I, tj, np_, gram);
+        }
       }
     } else if (s1 > s0) {
       f32x16 acc[2][2];
@@ -1831,7 +1876,9 @@ static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_
   const char *xe = getenv("GRID_GRAM_KX");
   const int lag = le ? atoi(le) : 1, spin = se ? atoi(se) : 20000;
   const char *dye = GRID_AB_KNOB("GRID_GRAM_DYN");      // units from a per-XCD counter (1) or fixed per workgroup (0)
-  const int dyn = dye ? atoi(dye) != 0 : 1;
+  // bit 1: the 16x16 layout's flush in 512-B row segments (g8q_atomics_wide; A/B GRID_GRAM_WIDE)
+  const char *wde = GRID_AB_KNOB("GRID_GRAM_WIDE");
+  const int dyn = (dye ? atoi(dye) != 0 : 1) | ((wde ? atoi(wde) != 0 : GRAM_WIDE) ? 2 : 0);
   if (xe && (atoi(xe) == 1 || atoi(xe) == 2 || atoi(xe) == 4 || atoi(xe) == 8)) {
     bkx = atoi(xe);
     bkc = ceil_div(ceil_div(nsteps, bkx), sps_max);

@@ -150,12 +150,16 @@ def test_gram_exact_worst_case(dev):
                                       ref[ti*128:(ti+1)*128, tj*128:(tj+1)*128])
 
 
+@pytest.mark.parametrize("wide", ["0", "1"])
 @pytest.mark.parametrize("qmax", [200, 256])
-def test_gram_kblocked_multi_slice(dev, qmax):
+def test_gram_kblocked_multi_slice(dev, qmax, wide, monkeypatch):
     """grid_knn_gram_kb (k_gram8 on the K-blocked panel zquant_kb writes) on
     several int32 K-slices with a partial last 6-step group, both fp32 chunk
-    lengths (qmax 200: 384 products, 256: 192), all-|qmax| worst-case rows."""
+    lengths (qmax 200: 384 products, 256: 192), all-|qmax| worst-case rows;
+    wide: the 16x16 layout's flush in 512-B row segments (GRID_GRAM_WIDE, live
+    in the tools build)."""
     from grid_amd._abi import call
+    monkeypatch.setenv("GRID_GRAM_WIDE", wide)
     n, np_ = 600, 768
     r = 64 * (2 * (((1 << 31) - 1) // (qmax * qmax * 64)) + 7)
     rng = np.random.default_rng(qmax)

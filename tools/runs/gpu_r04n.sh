@@ -16,23 +16,6 @@ for f in 1 3; do
     > $O/loci_50k_inflight$f.json 2> $O/loci_50k_inflight$f.err || { tail -n 20 $O/loci_50k_inflight$f.err; exit 1; }
   python -c "import json; d=json.load(open('$O/loci_50k_inflight$f.json')); print($f, 'device_ms', round(d['device_ms'],1), 'e2e', round(d['end_to_end_s'],3))"
 done
-# the column kernel variants' bits (tools build, knobs live) before their timing
-GRID_AMD_LIB=grid_amd/_lib/libgridhip_probes.so timeout -k 10 300 python -u -m pytest -x -v --timeout 120 \
-  --timeout-method thread -p no:cacheprovider tests/test_gpu_depth16.py > $O/pytest_depth16_probes.log 2>&1 \
-  || { tail -n 40 $O/pytest_depth16_probes.log; exit 1; }
-tail -n 2 $O/pytest_depth16_probes.log
-# column statistics (tools build): columns per thread (GRID_COL16_VW), raw-code software-pipelined row groups
-# (GRID_COL_PF), rows per group (GRID_COL16_CU), at config 2 and at the 1/8-bins per-rank shape
-for bins in 375000 3000000; do
-  for c in "2 0 8" "2 1 8" "1 1 8" "1 1 16" "2 1 16" "2 0 8"; do
-    set -- $c
-    tag=b${bins}_vw$1_pf$2_cu$3
-    GRID_AMD_LIB=grid_amd/_lib/libgridhip_probes.so GRID_COL16_VW=$1 GRID_COL_PF=$2 GRID_COL16_CU=$3 \
-      timeout -k 10 200 python -u bench.py --bins $bins --steps 10 --warmup 2 --no-cpu-baseline --config3-steps 0 \
-      --no-files-config2 > $O/col_$tag.json 2> $O/col_$tag.err || { tail -n 20 $O/col_$tag.err; exit 1; }
-    python -c "import json; d=json.load(open('$O/col_$tag.json')); print('$tag', d['ms_per_step'], d['stages_ms']['col_stats'])"
-  done
-done
 # bench.py --gpus 8 rehearsal, 8 ranks sharing the one GPU over gloo, reduced shape
 GRID_BENCH_SHARE_GPU=1 GRID_DIST_BACKEND=gloo timeout -k 10 400 python -u bench.py --gpus 8 --steps 3 --warmup 1 \
   --samples 1024 --bins 524288 --hbm-budget-gb 20 --no-cpu-baseline --config3-steps 0 \
