@@ -556,6 +556,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_files_config2 and (n, m) == (3202, 3_000_000):
         out["from_files_config2"] = from_files_config2(args, note)
     if rank == 0:
+        out["build"] = _abi.build_info()          # the library's source sha256 = this tree's (checked at load)
         print(json.dumps(out), file=result_out, flush=True)
     if dist:
         dist.barrier()

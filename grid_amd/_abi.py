@@ -152,7 +152,7 @@ _SIGS = {
     "grid_md_finish": [_vp, _vp, _i64, _i64, _i64, _vp, _i32, _f64, _f64, _vp, _vp, _vp, _vp, _vp, C.POINTER(_i64)],
     "grid_md_gather": [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp],
 }
-EXPORTS = tuple(_SIGS) + ("grid_last_error",)
+EXPORTS = tuple(_SIGS) + ("grid_last_error", "grid_build_info")
 
 
 class GridNativeError(RuntimeError):
@@ -184,8 +184,47 @@ def load():
         f.restype = C.c_int
     lib.grid_last_error.argtypes = []
     lib.grid_last_error.restype = C.c_char_p
+    info = _build_info(lib)
+    want = source_sha256()
+    if want is not None and info.get("src_sha256") != want:
+        raise GridNativeError(f"{LIB_PATH} was built from other sources (library {info.get('src_sha256')}, "
+                              f"tree {want}): rebuild with `make -C grid_amd/csrc`")
     _lib = lib
     return lib
+
+
+# the files grid_amd/csrc/Makefile hashes into the library (HASHED), in its sorted order
+_CSRC = _HERE / "csrc"
+_HASHED = sorted(["core.hip", "normalize.hip", "knn.hip", "dipcn_phase.hip", "synth.hip", "depth16.hip",
+                  "inflate.hip", "mosdepth_dev.hip", "gzwrite.hip", "ingest.cpp", "textio.cpp", "hapnbr.cpp",
+                  "common.hpp", "synth_model.hpp", "inflate_core.hpp", "fastgz.hpp"])
+
+
+def source_sha256():
+    """sha256 of the native sources as the Makefile hashes them (None when the
+    tree holds no sources, e.g. an installed copy)."""
+    import hashlib
+    files = [_CSRC / f for f in _HASHED] + [_HERE.parent / "include" / "grid_abi.h"]
+    if not all(f.exists() for f in files):
+        return None
+    h = hashlib.sha256()
+    for f in files:
+        h.update(f.read_bytes())
+    return h.hexdigest()
+
+
+def _build_info(lib):
+    import json
+    lib.grid_build_info.argtypes = [C.c_char_p, C.c_int64]
+    lib.grid_build_info.restype = C.c_int
+    buf = C.create_string_buffer(512)
+    lib.grid_build_info(buf, 512)
+    return json.loads(buf.value.decode())
+
+
+def build_info():
+    """The loaded library's provenance: source sha256, compiler, arch, build time."""
+    return _build_info(load())
 
 
 def check(rc: int, what: str = ""):

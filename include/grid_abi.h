@@ -54,6 +54,12 @@ typedef struct grid_ctx grid_ctx;
 
 /* ---------------------------------------------------------------- runtime */
 const char *grid_last_error(void);
+/* Provenance of this build (no reference counterpart): a JSON object with the
+ * sha256 of the native sources it was compiled from (grid_amd/csrc/Makefile
+ * HASHED), the compiler, the target arch and the UTC build time, written into
+ * out (NUL-terminated, truncated to cap - 1); returns the full length.
+ * grid_amd/_abi.py refuses a library whose hash is not the tree's. */
+int grid_build_info(char *out, int64_t cap);
 int grid_abi_version(void);
 int grid_device_count(int *n);
 int grid_ctx_create(int device, grid_ctx **out);

@@ -115,3 +115,17 @@ def test_product_library_has_no_probe_selectors():
     # through GRID_AB_KNOB, which the product build compiles to "unset"
     names = set(re.findall(rb"\x00(GRID_[A-Z0-9_]+)\x00", blob))
     assert names <= allowed | {b"GRID_NO_LIBDEFLATE"}, sorted(names - allowed)
+
+
+def test_library_provenance_matches_the_tree(monkeypatch):
+    """The loaded library was compiled from the sources in this tree (the
+    Makefile's sha256 of them is compiled in), and a library built from other
+    sources is refused at load instead of running."""
+    from grid_amd import _abi
+    info = _abi.build_info()
+    assert info["src_sha256"] == _abi.source_sha256()
+    assert info["arch"] == "gfx950" and info["built_utc"]
+    monkeypatch.setattr(_abi, "_lib", None)
+    monkeypatch.setattr(_abi, "source_sha256", lambda: "0" * 64)
+    with pytest.raises(_abi.GridNativeError, match="other sources"):
+        _abi.load()
