@@ -81,6 +81,68 @@ __device__ __forceinline__ void rb_finish(const T *s_q, const DEC &dec, double *
   }
 }
 
+// Lane exchanges for the fixed sums below (doubles as two dwords): xor 1 and
+// xor 2 by DPP quad permutes (no LDS traffic), xor 4 / 8 / 16 by ds_swizzle
+// bit-mask mode (within 32 lanes, no address operand).
+__device__ __forceinline__ double lane_xor_d(double v, int k) {
+  int lo = __double2loint(v), hi = __double2hiint(v);
+  if (k == 1) {
+    lo = __builtin_amdgcn_mov_dpp(lo, 0xB1, 0xF, 0xF, false);
+    hi = __builtin_amdgcn_mov_dpp(hi, 0xB1, 0xF, 0xF, false);
+  } else if (k == 2) {
+    lo = __builtin_amdgcn_mov_dpp(lo, 0x4E, 0xF, 0xF, false);
+    hi = __builtin_amdgcn_mov_dpp(hi, 0x4E, 0xF, 0xF, false);
+  } else if (k == 4) {
+    lo = __builtin_amdgcn_ds_swizzle(lo, 0x101F);
+    hi = __builtin_amdgcn_ds_swizzle(hi, 0x101F);
+  } else if (k == 8) {
+    lo = __builtin_amdgcn_ds_swizzle(lo, 0x201F);
+    hi = __builtin_amdgcn_ds_swizzle(hi, 0x201F);
+  } else {
+    lo = __builtin_amdgcn_ds_swizzle(lo, 0x401F);
+    hi = __builtin_amdgcn_ds_swizzle(hi, 0x401F);
+  }
+  return __hiloint2double(hi, lo);
+}
+
+// rb_finish for a block of plain compact codes (no missing cell, no escape:
+// count 8192).  The same additions with the same operands as rb_finish (IEEE
+// addition is commutative, so a + b and b + a are the same bits): the 8
+// chains of a leaf meet by xor-1/2/4 exchanges, ((a0+a1)+(a2+a3)) +
+// ((a4+a5)+(a6+a7)) in lane 8k; the 64 leaves' tree level by level by xor
+// 1..16 exchanges among 32 lanes, pairs in order, the root in lane 0.
+__device__ __forceinline__ void rb_finish16_plain(const uint16_t *s_q, double *s_leaf, int64_t row, int64_t b,
+                                                  int64_t nblk, double *__restrict__ bsum,
+                                                  int32_t *__restrict__ bcnt) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int c = 0; c < 2; c++) {
+    const int chain = tid + c * 256;
+    const int leaf = chain >> 3, j = chain & 7;
+    const uint16_t *lp = &s_q[leaf * LEAF_PAD + j];
+    double acc = div100_exact((int32_t)lp[0]);
+#pragma unroll
+    for (int st = 1; st < 16; st++) acc = acc + div100_exact((int32_t)lp[8 * st]);
+    double t = acc + lane_xor_d(acc, 1);
+    t = t + lane_xor_d(t, 2);
+    t = t + lane_xor_d(t, 4);
+    if ((tid & 7) == 0) s_leaf[leaf] = t;
+  }
+  __syncthreads();
+  if (tid < 32) {
+    double v = s_leaf[2 * tid] + s_leaf[2 * tid + 1];
+    v = v + lane_xor_d(v, 1);
+    v = v + lane_xor_d(v, 2);
+    v = v + lane_xor_d(v, 4);
+    v = v + lane_xor_d(v, 8);
+    v = v + lane_xor_d(v, 16);
+    if (tid == 0) {
+      bsum[row * nblk + b] = v;
+      bcnt[row * nblk + b] = BLK;
+    }
+  }
+}
+
 // ---- full 8192-element blocks: one 256-thread workgroup per (row, block) ----
 // 64 leaves x 8 chains = 512 chains, 2 per thread; leaf results combined in
 // the fixed binary tree of pairwise(8192).
@@ -130,61 +192,110 @@ __global__ __launch_bounds__(256) void k_row_blocks_full(const int32_t *__restri
 // an escape (rare) is looked up out of line.  PB blocks' codes are loaded up
 // front (PB x 4 uint4 per thread).
 constexpr int RB16_PB = 1;   // default for GRID_ROWBLK16_PB (timing only)
-template <int PB, bool NT>
+typedef unsigned rb_v4u __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ __forceinline__ void rb16_load(const Q16 &s16, int64_t ld, int64_t row, int64_t b, rb_v4u (&raw)[4]) {
+  const rb_v4u *src = reinterpret_cast<const rb_v4u *>(s16.q + row * ld + b * BLK);
+#pragma unroll
+  for (int it = 0; it < 4; it++) {
+    if constexpr (NT) raw[it] = __builtin_nontemporal_load(src + it * 256 + threadIdx.x);
+    else raw[it] = src[it * 256 + threadIdx.x];
+  }
+}
+
+// One full block (row, b) from its codes in registers: LDS image, then the
+// chains and tree of rb_finish.  Ends with every LDS read done.
+template <bool RB16_XOR>
+__device__ __forceinline__ void rb16_block(const rb_v4u (&raw)[4], const Q16 &s16, int64_t row, int64_t b,
+                                           int64_t nblk, uint16_t *s_q, double *s_leaf, int *s_cnt,
+                                           double *__restrict__ bsum, int32_t *__restrict__ bcnt) {
+  const int tid = threadIdx.x;
+  // the largest of this thread's 32 codes by packed 16-bit maxima (a code
+  // above GRID_Q16_MAXV is a missing cell or an escape)
+  typedef unsigned short rb_us2 __attribute__((ext_vector_type(2)));
+  rb_us2 mx = {0, 0};
+#pragma unroll
+  for (int it = 0; it < 4; it++) {
+    const int e = (it * 256 + tid) * 8;           // first of this thread's 8 codes
+    const rb_v4u u = raw[it];
+#pragma unroll
+    for (int k = 0; k < 4; k++) mx = __builtin_elementwise_max(mx, __builtin_bit_cast(rb_us2, u[k]));
+    *reinterpret_cast<rb_v4u *>(&s_q[(e >> 7) * LEAF_PAD + (e & 127)]) = u;
+  }
+  const int special = (mx.x > GRID_Q16_MAXV) | (mx.y > GRID_Q16_MAXV);
+  // blocks without a missing cell or an escape (the common case) read the
+  // codes as plain hundredths
+  // __syncthreads_or is workgroup-uniform but returns a VGPR value;
+  // readfirstlane makes the branch scalar, so no wave can skip the
+  // barriers of either side (tools/isa_barriers.py)
+  if (__builtin_expect(!__builtin_amdgcn_readfirstlane(__syncthreads_or(special)), 1)) {
+    if constexpr (RB16_XOR) {
+      rb_finish16_plain(s_q, s_leaf, row, b, nblk, bsum, bcnt);
+    } else {
+      rb_finish(s_q, [](uint16_t c, int) { return div100_exact((int32_t)c); }, s_leaf, s_cnt, BLK / 256, row, b,
+                nblk, bsum, bcnt);
+    }
+  } else {
+    int cnt = 0;
+#pragma unroll
+    for (int it = 0; it < 4; it++)
+#pragma unroll
+      for (int k = 0; k < 8; k++) cnt += ((raw[it][k >> 1] >> (16 * (k & 1))) & 0xFFFFu) != GRID_Q16_MISS;
+    const int64_t c0 = b * BLK;
+    auto dec = [&](uint16_t c, int e) -> double {
+      if (c == GRID_Q16_ESC) return qval(q16_lookup(row, c0 + e, s16));
+      return c == GRID_Q16_MISS ? 0.0 : div100_exact((int32_t)c);
+    };
+    rb_finish<uint16_t, decltype(dec), 1>(s_q, dec, s_leaf, s_cnt, cnt, row, b, nblk, bsum, bcnt);   // rare
+  }
+}
+
+template <int PB, bool NT, bool XOR = true>
 __global__ __launch_bounds__(256) void k_row_blocks16(Q16 s16, int64_t ld, int64_t nblk_full, int64_t nblk,
                                                       double *__restrict__ bsum, int32_t *__restrict__ bcnt) {
   __shared__ __attribute__((aligned(16))) uint16_t s_q[64 * LEAF_PAD];
   __shared__ double s_leaf[64];
   __shared__ int s_cnt[4];
   const int64_t row = blockIdx.y, b0 = (int64_t)blockIdx.x * PB;
-  const int tid = threadIdx.x;
-  typedef unsigned v4u __attribute__((ext_vector_type(4)));
-  v4u raw[PB][4];
+  rb_v4u raw[PB][4];
 #pragma unroll
-  for (int h = 0; h < PB; h++) {
-    const v4u *src = reinterpret_cast<const v4u *>(s16.q + row * ld + (b0 + h) * BLK);
-    if (b0 + h < nblk_full) {
-#pragma unroll
-      for (int it = 0; it < 4; it++) {
-        if constexpr (NT) raw[h][it] = __builtin_nontemporal_load(src + it * 256 + tid);
-        else raw[h][it] = src[it * 256 + tid];
-      }
-    }
-  }
+  for (int h = 0; h < PB; h++)
+    if (b0 + h < nblk_full) rb16_load<NT>(s16, ld, row, b0 + h, raw[h]);
 #pragma unroll
   for (int h = 0; h < PB; h++) {
     const int64_t b = b0 + h;
     if (b >= nblk_full) break;                      // workgroup-uniform
     if (h > 0) __syncthreads();                     // the previous block's LDS reads are done
-    int cnt = 0, special = 0;
+    rb16_block<XOR>(raw[h], s16, row, b, nblk, s_q, s_leaf, s_cnt, bsum, bcnt);
+  }
+}
+
+// Streamed form (GRID_ROWBLK16_PB=0): a grid of resident workgroups walks the
+// (row, block) units u = blockIdx.x, + gridDim.x, ... (row-major, so the
+// workgroups in flight read neighbouring blocks of a row), holding the next
+// unit's codes in registers while this one is summed: the loads of one unit
+// overlap the chains of the previous one inside every workgroup, instead of
+// a workgroup per unit that waits for its loads before any work.
+template <bool NT, bool XOR = true>
+__global__ __launch_bounds__(256) void k_row_blocks16s(Q16 s16, int64_t ld, int64_t n, int64_t nblk_full,
+                                                       int64_t nblk, double *__restrict__ bsum,
+                                                       int32_t *__restrict__ bcnt) {
+  __shared__ __attribute__((aligned(16))) uint16_t s_q[64 * LEAF_PAD];
+  __shared__ double s_leaf[64];
+  __shared__ int s_cnt[4];
+  const int64_t total = n * nblk_full, step = gridDim.x;
+  int64_t u = blockIdx.x;
+  if (u >= total) return;                           // workgroup-uniform
+  rb_v4u cur[4], nxt[4];
+  rb16_load<NT>(s16, ld, u / nblk_full, u % nblk_full, cur);
+  for (; u < total; u += step) {
+    const int64_t un = u + step;
+    if (un < total) rb16_load<NT>(s16, ld, un / nblk_full, un % nblk_full, nxt);
+    rb16_block<XOR>(cur, s16, u / nblk_full, u % nblk_full, nblk, s_q, s_leaf, s_cnt, bsum, bcnt);
+    __syncthreads();                                // this unit's LDS reads are done before the next image
 #pragma unroll
-    for (int it = 0; it < 4; it++) {
-      const int e = (it * 256 + tid) * 8;           // first of this thread's 8 codes
-      const v4u u = raw[h][it];
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const uint32_t c = (u[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
-        cnt += c != GRID_Q16_MISS;
-        special |= c > GRID_Q16_MAXV;
-      }
-      *reinterpret_cast<v4u *>(&s_q[(e >> 7) * LEAF_PAD + (e & 127)]) = u;
-    }
-    // blocks without a missing cell or an escape (the common case) read the
-    // codes as plain hundredths
-    // __syncthreads_or is workgroup-uniform but returns a VGPR value;
-    // readfirstlane makes the branch scalar, so no wave can skip the
-    // barriers of either side (tools/isa_barriers.py)
-    if (__builtin_expect(!__builtin_amdgcn_readfirstlane(__syncthreads_or(special)), 1)) {
-      rb_finish(s_q, [](uint16_t c, int) { return div100_exact((int32_t)c); }, s_leaf, s_cnt, cnt, row, b, nblk,
-                bsum, bcnt);
-    } else {
-      const int64_t c0 = b * BLK;
-      auto dec = [&](uint16_t c, int e) -> double {
-        if (c == GRID_Q16_ESC) return qval(q16_lookup(row, c0 + e, s16));
-        return c == GRID_Q16_MISS ? 0.0 : div100_exact((int32_t)c);
-      };
-      rb_finish<uint16_t, decltype(dec), 1>(s_q, dec, s_leaf, s_cnt, cnt, row, b, nblk, bsum, bcnt);   // rare
-    }
+    for (int it = 0; it < 4; it++) cur[it] = nxt[it];
   }
 }
 
@@ -1917,12 +2028,25 @@ static int row_blocks_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, in
     if (c16) {
       const char *pe = GRID_AB_KNOB("GRID_ROWBLK16_PB");
       const int pb = pe ? atoi(pe) : RB16_PB;
-      REQUIRE(pb == 1 || pb == 2 || pb == 4, "GRID_ROWBLK16_PB must be 1, 2 or 4 (got %d)", pb);
-      auto kern = pb == 1 ? (nt ? k_row_blocks16<1, true> : k_row_blocks16<1, false>)
-                : pb == 2 ? (nt ? k_row_blocks16<2, true> : k_row_blocks16<2, false>)
-                          : (nt ? k_row_blocks16<4, true> : k_row_blocks16<4, false>);
-      hipLaunchKernelGGL(kern, dim3((unsigned)ceil_div(nfull, pb), (unsigned)n), dim3(256), 0, ctx->stream, s16, ld,
-                         nfull, nblk, d_bsum, d_bcnt);
+      REQUIRE(pb == 0 || pb == 1 || pb == 2 || pb == 4, "GRID_ROWBLK16_PB must be 0, 1, 2 or 4 (got %d)", pb);
+      if (pb == 0) {
+        // streamed: 8 resident workgroups per CU (17.9 KiB of LDS each), at most one per unit
+        const char *we = GRID_AB_KNOB("GRID_ROWBLK16_WPC");
+        const int64_t wpc = we && atoi(we) > 0 ? atoi(we) : 8;
+        const int64_t g = std::min<int64_t>(n * nfull, (int64_t)ctx->ncu * wpc);
+        hipLaunchKernelGGL(nt ? k_row_blocks16s<true> : k_row_blocks16s<false>, dim3((unsigned)g), dim3(256), 0,
+                           ctx->stream, s16, ld, n, nfull, nblk, d_bsum, d_bcnt);
+      } else {
+        // the plain blocks' sums by lane exchanges (default) or by rb_finish's broadcasts (A/B)
+        const char *xe = GRID_AB_KNOB("GRID_ROWBLK16_XOR");
+        const bool xr = xe ? atoi(xe) != 0 : true;
+        auto kern = pb == 1 ? (nt ? (xr ? k_row_blocks16<1, true> : k_row_blocks16<1, true, false>)
+                                  : k_row_blocks16<1, false>)
+                  : pb == 2 ? (nt ? k_row_blocks16<2, true> : k_row_blocks16<2, false>)
+                            : (nt ? k_row_blocks16<4, true> : k_row_blocks16<4, false>);
+        hipLaunchKernelGGL(kern, dim3((unsigned)ceil_div(nfull, pb), (unsigned)n), dim3(256), 0, ctx->stream, s16,
+                           ld, nfull, nblk, d_bsum, d_bcnt);
+      }
     } else {
       auto kern = vec4_ok(d_q, ld) ? (nt ? k_row_blocks_full<3> : k_row_blocks_full<0>) : k_row_blocks_full<1>;
       hipLaunchKernelGGL(kern, dim3((unsigned)nfull, (unsigned)n), dim3(256), 0, ctx->stream, d_q, s16, ld, nfull,

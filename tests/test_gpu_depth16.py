@@ -86,9 +86,12 @@ def test_synth_q16_equals_encoded_synth(dev):
 
 
 # raw-code software-pipelined column kernels (GRID_COL_PF; 1 or 2 columns per
-# thread, 8 or 16 rows per group); the knobs take effect in the tools build
+# thread, 8 or 16 rows per group) and the streamed row-block kernel
+# (GRID_ROWBLK16_PB=0; GRID_ROWBLK16_WPC=1: one workgroup per CU, many units
+# each); the knobs take effect in the tools build
 # (GRID_AMD_LIB=.../libgridhip_probes.so), the product library runs its defaults
-PF_KNOBS = [{"GRID_COL_PF": "1"}, {"GRID_COL_PF": "1", "GRID_COL16_VW": "1"},
+PF_KNOBS = [{"GRID_COL_PF": "0", "GRID_ROWBLK16_PB": "0"}, {"GRID_ROWBLK16_PB": "0", "GRID_ROWBLK16_WPC": "1"},
+            {"GRID_ROWBLK16_XOR": "0"}, {"GRID_COL_PF": "1"}, {"GRID_COL_PF": "1", "GRID_COL16_VW": "1"},
             {"GRID_COL_PF": "1", "GRID_COL16_VW": "1", "GRID_COL16_CU": "16"},
             {"GRID_COL_PF": "1", "GRID_COL16_CU": "16"}]
 
