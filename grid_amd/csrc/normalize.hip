@@ -220,7 +220,11 @@ __device__ __forceinline__ void rb16_block(const rb_v4u (&raw)[4], const Q16 &s1
     const int e = (it * 256 + tid) * 8;           // first of this thread's 8 codes
     const rb_v4u u = raw[it];
 #pragma unroll
-    for (int k = 0; k < 4; k++) mx = __builtin_elementwise_max(mx, __builtin_bit_cast(rb_us2, u[k]));
+    for (int k = 0; k < 4; k++) {
+      const uint32_t w = u[k];
+      const rb_us2 h = {(unsigned short)(w & 0xFFFFu), (unsigned short)(w >> 16)};
+      mx = __builtin_elementwise_max(mx, h);
+    }
     *reinterpret_cast<rb_v4u *>(&s_q[(e >> 7) * LEAF_PAD + (e & 127)]) = u;
   }
   const int special = (mx.x > GRID_Q16_MAXV) | (mx.y > GRID_Q16_MAXV);
