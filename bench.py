@@ -329,12 +329,16 @@ def run_workload(args, n, m, steps, warmup, world, rank, local, dist, comm, dev,
     # Steps47): it overlaps that pass's top-k/dipCN and the next statistics;
     # every pass's phasing still completes inside the timed region (finish()
     # before the final synchronize)
+    # two lanes, one per dipCN buffer: the last two passes' phasings (the
+    # deferred one and finish()'s) overlap instead of queueing at the end
     lane = None
     if not args.no_overlap:
-        pdev = _abi.Device(local)
-        pstream = torch.cuda.Stream()
-        pdev.set_stream(pstream)
-        lane = (HipOps(pdev), pstream)
+        lane = []
+        for _ in range(2):
+            pdev = _abi.Device(local)
+            pstream = torch.cuda.Stream()
+            pdev.set_stream(pstream)
+            lane.append((HipOps(pdev), pstream))
     st = Steps47(ops, talloc, n, m, c0, ml, k=args.k, n_nbr=300, top_frac=0.1, zmax=2.0, sigma2_max=1000.0,
                  frac_r=1.0, min_nbr=1, n_iters=args.n_iters, comm=comm, phase_lane=lane,
                  chunk=chunk if streamed else None, keep_z=not streamed)

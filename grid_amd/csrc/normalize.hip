@@ -111,15 +111,17 @@ __device__ __forceinline__ double lane_xor_d(double v, int k) {
 // chains of a leaf meet by xor-1/2/4 exchanges, ((a0+a1)+(a2+a3)) +
 // ((a4+a5)+(a6+a7)) in lane 8k; the 64 leaves' tree level by level by xor
 // 1..16 exchanges among 32 lanes, pairs in order, the root in lane 0.
-__device__ __forceinline__ void rb_finish16_plain(const uint16_t *s_q, double *s_leaf, int64_t row, int64_t b,
-                                                  int64_t nblk, double *__restrict__ bsum,
-                                                  int32_t *__restrict__ bcnt) {
+// T: the LDS element (uint16 compact code or int32 hundredths, never missing here).
+template <class T>
+__device__ __forceinline__ void rb_finish_plain(const T *s_q, double *s_leaf, int64_t row, int64_t b,
+                                                int64_t nblk, double *__restrict__ bsum,
+                                                int32_t *__restrict__ bcnt) {
   const int tid = threadIdx.x;
 #pragma unroll
   for (int c = 0; c < 2; c++) {
     const int chain = tid + c * 256;
     const int leaf = chain >> 3, j = chain & 7;
-    const uint16_t *lp = &s_q[leaf * LEAF_PAD + j];
+    const T *lp = &s_q[leaf * LEAF_PAD + j];
     double acc = div100_exact((int32_t)lp[0]);
 #pragma unroll
     for (int st = 1; st < 16; st++) acc = acc + div100_exact((int32_t)lp[8 * st]);
@@ -147,8 +149,10 @@ __device__ __forceinline__ void rb_finish16_plain(const uint16_t *s_q, double *s
 // 64 leaves x 8 chains = 512 chains, 2 per thread; leaf results combined in
 // the fixed binary tree of pairwise(8192).
 // SRC: 0 = int32 (int4 loads), 1 = int32 (scalar loads), 3 = int32 (streaming / nontemporal int4 loads; GRID_ROWBLK_NT A/B)
+// XOR: blocks without a missing cell (found by a minimum: GRID_MISSING is
+// INT32_MIN) take rb_finish_plain; the others count their cells from LDS.
 constexpr bool ROWBLK_NT = true;   // default for GRID_ROWBLK_NT
-template <int SRC>
+template <int SRC, bool XOR = true>
 __global__ __launch_bounds__(256) void k_row_blocks_full(const int32_t *__restrict__ q, Q16 s16, int64_t ld,
                                                          int64_t nblk_full, int64_t nblk,
                                                          double *__restrict__ bsum,
@@ -159,7 +163,7 @@ __global__ __launch_bounds__(256) void k_row_blocks_full(const int32_t *__restri
   const int64_t b = blockIdx.x;
   const int64_t row = blockIdx.y;
   const int tid = threadIdx.x;
-  int cnt = 0;
+  int cnt = 0, mn = 0;
   {
     const int32_t *srcp = q + row * ld + b * BLK;
     const int4 *src = reinterpret_cast<const int4 *>(srcp);
@@ -179,6 +183,20 @@ __global__ __launch_bounds__(256) void k_row_blocks_full(const int32_t *__restri
       int e = e4 * 4;
       int leaf = e >> 7, w = e & 127;
       *reinterpret_cast<int4 *>(&s_q[leaf * LEAF_PAD + w]) = v;
+      if constexpr (XOR) mn = min(mn, min(min(v.x, v.y), min(v.z, v.w)));
+      else cnt += (v.x != GRID_MISSING) + (v.y != GRID_MISSING) + (v.z != GRID_MISSING) + (v.w != GRID_MISSING);
+    }
+  }
+  if constexpr (XOR) {
+    // workgroup-uniform branch (readfirstlane of the barrier's OR, see k_row_blocks16)
+    if (__builtin_expect(!__builtin_amdgcn_readfirstlane(__syncthreads_or(mn == GRID_MISSING)), 1)) {
+      rb_finish_plain(s_q, s_leaf, row, b, nblk, bsum, bcnt);
+      return;
+    }
+#pragma unroll
+    for (int it = 0; it < 8; it++) {
+      const int e = (it * 256 + tid) * 4;
+      const int4 v = *reinterpret_cast<const int4 *>(&s_q[(e >> 7) * LEAF_PAD + (e & 127)]);
       cnt += (v.x != GRID_MISSING) + (v.y != GRID_MISSING) + (v.z != GRID_MISSING) + (v.w != GRID_MISSING);
     }
   }
@@ -235,7 +253,7 @@ __device__ __forceinline__ void rb16_block(const rb_v4u (&raw)[4], const Q16 &s1
   // barriers of either side (tools/isa_barriers.py)
   if (__builtin_expect(!__builtin_amdgcn_readfirstlane(__syncthreads_or(special)), 1)) {
     if constexpr (RB16_XOR) {
-      rb_finish16_plain(s_q, s_leaf, row, b, nblk, bsum, bcnt);
+      rb_finish_plain(s_q, s_leaf, row, b, nblk, bsum, bcnt);
     } else {
       rb_finish(s_q, [](uint16_t c, int) { return div100_exact((int32_t)c); }, s_leaf, s_cnt, BLK / 256, row, b,
                 nblk, bsum, bcnt);
@@ -2052,7 +2070,11 @@ static int row_blocks_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, in
                            ld, nfull, nblk, d_bsum, d_bcnt);
       }
     } else {
-      auto kern = vec4_ok(d_q, ld) ? (nt ? k_row_blocks_full<3> : k_row_blocks_full<0>) : k_row_blocks_full<1>;
+      const char *xe = GRID_AB_KNOB("GRID_ROWBLK16_XOR");   // the same A/B for the int32 kernel
+      const bool xr = xe ? atoi(xe) != 0 : true;
+      auto kern = vec4_ok(d_q, ld) ? (nt ? (xr ? k_row_blocks_full<3> : k_row_blocks_full<3, false>)
+                                         : k_row_blocks_full<0>)
+                                   : k_row_blocks_full<1>;
       hipLaunchKernelGGL(kern, dim3((unsigned)nfull, (unsigned)n), dim3(256), 0, ctx->stream, d_q, s16, ld, nfull,
                          nblk, d_bsum, d_bcnt);
     }

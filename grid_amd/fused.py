@@ -380,8 +380,12 @@ class Steps47:
         writes alternate buffers; ``finish()`` issues the last pass's phasing
         (call it before reading ``hap`` / ``imp`` or stopping a clock)."""
         self.ops, self.A, self.comm = ops, alloc, comm
+        # one lane, or two: the phasing of _dips[b] then runs on lane b, so the
+        # last two passes' phasings (finish()) overlap instead of queueing
         self.phase_lane = phase_lane
-        self.ev_phase = None
+        self._lanes = None if phase_lane is None else (list(phase_lane) if isinstance(phase_lane, list)
+                                                       else [phase_lane])
+        self._ev_phase = {}
         self.rank = comm.rank if comm else 0
         self.world = comm.world if comm else 1
         self.n, self.m, self.col0, self.ml = n, m_total, col0, m_local
@@ -481,9 +485,11 @@ class Steps47:
         self._ev_free = [None, None]        # event: the phasing that read _dips[b] is done
         self._pending = None                 # dipCN buffer whose phasing is not issued yet
         self.valid = a.empty(n1, U1)
-        self.hap = a.empty(2 * n1, F8)
-        self.imp = a.empty(2 * n1, F8)
-        self.mean = a.empty(1, F8)
+        # phasing outputs, double-buffered with the dipCN buffer they come from
+        self._haps = [a.empty(2 * n1, F8), a.empty(2 * n1, F8)]
+        self._imps = [a.empty(2 * n1, F8), a.empty(2 * n1, F8)]
+        self._means = [a.empty(1, F8), a.empty(1, F8)]
+        self._out = 0                        # the buffer set of the last issued phasing
         self.marks = None
         self.gram_evs = None
 
@@ -505,6 +511,19 @@ class Steps47:
     def dip(self):
         """dipCN values of the last pass."""
         return self._dips[self._cur]
+
+    @property
+    def hap(self):
+        """Phased haplotype values of the last pass (after finish())."""
+        return self._haps[self._out]
+
+    @property
+    def imp(self):
+        return self._imps[self._out]
+
+    @property
+    def mean(self):
+        return self._means[self._out]
 
     def set_reads(self, reads):
         self.reads = self.A.upload(np.asarray(reads, F8))
@@ -713,7 +732,7 @@ class Steps47:
         idx, self.d2, cnt = self.idx_l, self.d2_l, self.cnt_l
         self._mark("topk")
         # ---- step 6: dipCN (scales as printed "%.2f", neighbour gather) ----
-        lane = None if profile else self.phase_lane
+        lane = None if profile else self._lanes
         if lane is None:
             self.finish()                     # a deferred phasing of an earlier pass first
         b = self._cur ^ 1 if lane is not None else self._cur
@@ -737,7 +756,8 @@ class Steps47:
             self._pending = b                 # issued by the next pass after its Gram, or by finish()
         else:
             o.phase(n, self._dips[b], self.off, self.nbr, self.w, self.min_nbr, self.n_iters, self.sched,
-                    self.hap, self.imp, self.mean)
+                    self._haps[b], self._imps[b], self._means[b])
+            self._out = b
         self._mark("phase")
         self.idx_out, self.cnt_out = idx, cnt
         self._check_deferred()
@@ -811,26 +831,28 @@ class Steps47:
             return
         import torch
         b, self._pending = self._pending, None
-        pops, pstream = self.phase_lane
+        pops, pstream = self._lanes[b % len(self._lanes)]
         ev = torch.cuda.Event()
         ev.record()
         pstream.wait_event(ev)
         pops.phase(self.n, self._dips[b], self.off, self.nbr, self.w, self.min_nbr, self.n_iters, self.sched,
-                   self.hap, self.imp, self.mean)
+                   self._haps[b], self._imps[b], self._means[b])
         done = torch.cuda.Event()
         done.record(pstream)
         self._ev_free[b] = done
-        self.ev_phase = done
+        self._ev_phase[b] = done
+        self._out = b
 
     def finish(self):
         """Issue the last pass's deferred phasing and order the main stream
-        after it (hap / imp / mean are then the last pass's once the stream
-        syncs)."""
+        after every phasing still running (hap / imp / mean are then the last
+        pass's once the stream syncs)."""
         self._issue_pending()
-        if self.ev_phase is not None:
+        if self._ev_phase:
             import torch
-            torch.cuda.current_stream().wait_event(self.ev_phase)
-            self.ev_phase = None
+            for ev in self._ev_phase.values():
+                torch.cuda.current_stream().wait_event(ev)
+            self._ev_phase = {}
 
     def _chunk_bounds(self, r_loc):
         """Per chunk: the range [sb[c], sb[c+1]) of selected indices whose

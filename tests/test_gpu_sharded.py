@@ -45,11 +45,14 @@ def run_chain(rank, world, comm, lane):
     dev.set_stream(torch.cuda.current_stream())
     qs = torch.from_numpy(np.ascontiguousarray(q[:, c0:c1])).cuda()
     pl = None
-    if lane:
-        pdev = _abi.Device(0)
-        ps = torch.cuda.Stream()
-        pdev.set_stream(ps)
-        pl = (HipOps(pdev), ps)
+    if lane:                             # lane = 1 or 2 phasing lanes (two: one per dipCN buffer)
+        pl = []
+        for _ in range(lane):
+            pdev = _abi.Device(0)
+            ps = torch.cuda.Stream()
+            pdev.set_stream(ps)
+            pl.append((HipOps(pdev), ps))
+        pl = pl[0] if lane == 1 else pl
     st = Steps47(HipOps(dev), TorchAlloc(0), N, M, c0, c1 - c0, k=K, n_nbr=4, n_iters=ITERS, comm=comm,
                  phase_lane=pl)
     st.set_reads(reads)
@@ -71,7 +74,7 @@ def _worker(rank, world, port, out_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from grid_amd.fused import TorchComm
-    res = run_chain(rank, world, TorchComm(dist), lane=True)
+    res = run_chain(rank, world, TorchComm(dist), lane=2 if world % 2 == 0 else 1)
     np.savez(f"{out_path}.{rank}.npz", **{k: np.asarray(v) for k, v in res.items()})
     dist.barrier()
     dist.destroy_process_group()
