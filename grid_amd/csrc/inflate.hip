@@ -382,7 +382,10 @@ struct DevP {
 
 // One wave per file.  status: 0 ok, else an icore::Status (or GRID_GZ_E_*).
 #ifndef GRID_INFLATE_WPE
-#define GRID_INFLATE_WPE 7            // 72 VGPRs: 7 waves per SIMD (LDS 5.4 KiB per wave: 29 per CU)
+// 64 VGPRs: 8 waves per SIMD with the 2^7 distance fast table (LDS 4.9 KiB per
+// wave: 32 per CU); 7 waves (72 VGPRs, 2^8 table) measured 37.0 vs 37.5-37.6 GB/s
+// of BGZF text (r04w, 256 files, interleaved)
+#define GRID_INFLATE_WPE 8
 #endif
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GRID_INFLATE_WPE))) void k_inflate(const uint8_t *__restrict__ src, const int64_t *__restrict__ in_off,
                                                 const int64_t *__restrict__ in_len, uint8_t *__restrict__ out,

@@ -40,7 +40,10 @@ namespace icore {
 #ifndef GRID_INFLATE_LFAST
 #define GRID_INFLATE_LFAST 8
 #endif
-constexpr int LFAST = GRID_INFLATE_LFAST, DFAST = 8;
+#ifndef GRID_INFLATE_DFAST
+#define GRID_INFLATE_DFAST 7   // distance codes longer than 7 bits (rare) take the canonical walk (r04w)
+#endif
+constexpr int LFAST = GRID_INFLATE_LFAST, DFAST = GRID_INFLATE_DFAST;
 constexpr int FT_LEN = 0, FT_DIST = 1;   // the fast tables (policy-owned)
 // u16 slots of the table area: litlen count/symbols, dist count/symbols,
 // code-length code count/symbols, lengths scratch, offsets scratch
