@@ -58,6 +58,9 @@ STAGE = 1 << 30                 # pinned staging per CPU sub-batch (two of them)
 TRACE = bool(os.environ.get("GRID_INGEST_TRACE"))   # per-batch phase times on stderr
 XSTREAM_WAIT = True             # dev's stream waits for the copy stream (False only in a GPU test's control arm)
 AFTER_HOST_TEXT = None          # test seam: called (dev, d_text, toff, files) once host text is in HBM
+# pipelined BGZF batches: the fraction of each batch's text the host threads
+# inflate beside the GPU (files spread over the batch; 0 = the GPU inflates all)
+HOST_FRAC = float(os.environ.get("GRID_INGEST_HOST_FRAC", "0"))
 
 
 class DeviceIngestUnsupported(Exception):
@@ -234,6 +237,9 @@ class _Async:
         self.arena_d = [None, None]
         self.scr = [None, None]                 # per parity: member table, chunk counts/lines, file status
         self.out = []                           # per batch: (fs, owner, unit status, unit length, flags, kept, okb)
+        self.htext = [_abi.Event(), _abi.Event()]   # host-inflated text of parity p is in HBM
+        self.hbad = []                          # host-share files whose text failed its CRC in HBM
+        self.one = None                         # page-locked int32 1: a failed host-share file's device status
 
     @staticmethod
     def _pack(parts):
@@ -243,12 +249,20 @@ class _Async:
             pos += _align(a.nbytes)
         return offs, pos
 
-    def batch(self, bi, fs, buf, off, caps_, gz, members, toff, d_in, d_text, fsizes):
+    def batch(self, bi, fs, buf, off, caps_, gz, members, toff, d_in, d_text, fsizes, host=None):
+        """host: (files, future) -- files of the batch the host threads inflate
+        (the future returns per file (status, length, crc, staging, offset));
+        their text is copied into d_text once the previous batch's parse is done
+        and checked there against its gzip CRC on the copy stream, while the
+        GPU inflates the rest; the parse waits for the copy (event htext)."""
         dev, cdev, p = self.dev, self.cdev, bi % 2
         nb = len(fs)
         mu = [k for k in range(nb) if gz[k] and fsizes[k] > 0 and members[k] is not None]
+        hset = set(host[0]) if host else set()
         uo, ul, to, tc, owner = [], [], [], [], []
         for k in mu:
+            if k in hset:
+                continue
             ms, ml, mi = members[k]
             uo.append(off[k] + ms)
             ul.append(ml)
@@ -302,7 +316,41 @@ class _Async:
         if nu:
             call("grid_gunzip_batch", dev.ctx, d_in.ptr, d_uo, d_ul, nu, d_text.ptr, d_to, d_tc, mem.ptr, 1,
                  ust.ptr, uln.ptr, unm.ptr)
+        hfail = []
+        if hset:
+            res = host[1].result()
+            # the previous batch's parse reads d_text: its regions are free once it is done
+            q = 1 - p
+            if self.issued[q]:
+                self.done[q].host_wait()
+            hk = []
+            for k in sorted(hset):
+                st_, ln_, crc_, stage, so = res[k]
+                if st_ != 0 or ln_ != tlen[k]:
+                    hfail.append(k)              # dropped, as a file with a failed member on the GPU
+                    continue
+                if ln_:
+                    call("grid_h2d", cdev.ctx, d_text.ptr + int(toff[k]), stage.ctypes.data + int(so), int(ln_))
+                    hk.append(k)
+            self.htext[p].put(cdev)
+            self.htext[p].wait(dev)
+            if hk and AFTER_HOST_TEXT is not None:
+                AFTER_HOST_TEXT(cdev, d_text, toff, hk)
+            if hk:
+                # the guard, on the copy stream (it wrote the text): a mismatch hands
+                # the cohort to the host parser once the batches are done
+                got = _abi.text_crc32(cdev, d_text.ptr, toff[hk], tlen[hk])
+                for k, c in zip(hk, got):
+                    if int(c) != int(res[k][2]):
+                        self.hbad.append((fs[k], "its text in HBM does not match its gzip CRC"))
         call("grid_file_status", dev.ctx, ust.ptr, d_own, nu, fst.ptr, nb)
+        if hfail:
+            # the parse skips them: their device status set after grid_file_status (stream order)
+            if self.one is None:
+                self.one = _abi.PinnedBuf(64)
+                self.one.array[:4] = np.array([1], np.int32).view(np.uint8)
+            for k in hfail:
+                call("grid_h2d_async", dev.ctx, fst.ptr + 4 * k, self.one.ptr, 4)
         if nch:
             call("grid_md_count", dev.ctx, d_text.ptr, d_toff, d_tl, nch, d_cf, d_cs, d_c1, len(okb), cnl.ptr,
                  cline0.ptr, bflags.ptr, fst.ptr)
@@ -313,7 +361,7 @@ class _Async:
         self.issued[p] = True
         # not gzip at all: dropped (GZ_EHEADER in the synchronous path)
         hdr_bad = [k for k in range(nb) if not gz[k] and fsizes[k] > 0]
-        self.out.append((list(fs), units[4], ust, uln, bflags, bk, okb, nu, hdr_bad))
+        self.out.append((list(fs), units[4], ust, uln, bflags, bk, okb, nu, hdr_bad, hfail))
         return self.h2d[p]
 
     def drain(self):
@@ -323,12 +371,16 @@ class _Async:
     def results(self, paths):
         """(file, status 0/1, kept) per file of the pipelined batches; raises
         DeviceIngestUnsupported for a parse flag, as the synchronous path."""
+        if self.hbad:
+            f, why = self.hbad[0]
+            raise DeviceIngestUnsupported(f"{paths[f]}: {why} ({len(self.hbad)} host-inflated file(s))")
         res = []
         self.kept = []
-        for fs, owner, ust, uln, bflags, bk, okb, nu, hdr_bad in self.out:
+        for fs, owner, ust, uln, bflags, bk, okb, nu, hdr_bad, hfail in self.out:
             nb = len(fs)
             bad = np.zeros(nb, np.int32)
             bad[hdr_bad] = _abi.GZ_EHEADER
+            bad[hfail] = _abi.GZ_EDATA
             if nu:
                 st = ust.numpy()[:nu]
                 # a member past its BGZF size is corrupt (dropped), not several members
@@ -353,6 +405,9 @@ class _Async:
         try:
             self.drain()
         finally:
+            if self.one is not None:
+                self.one.free()
+                self.one = None
             self.out = []
             self.arena_d = [None, None]
             self.scr = [None, None]
@@ -391,6 +446,8 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
     rpool = ThreadPoolExecutor(1)         # the next batch's read (its files on `pool`)
     copier = ThreadPoolExecutor(1)        # H2D of CPU-inflated text, on its own stream
     waiter = ThreadPoolExecutor(1)        # notes when the GPU's inflate ends
+    hctl = ThreadPoolExecutor(1)          # pipelined batches: the host share's inflate (its files on `pool`)
+    hstages = [_Pinned(8 << 30, pinned=False), _Pinned(8 << 30, pinned=False)]
     cdev = _abi.Device(dev.index)          # its own non-blocking stream
     split = _Split(nthreads)
 
@@ -577,8 +634,27 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
                 # them, and the batch is enqueued behind the previous one
                 if pipe is None:
                     pipe = _Async(dev, cdev, opts, K, nK, kidx, ref_nlines, Q)
+                host = None
+                if HOST_FRAC > 0 and len(todo) > 1:
+                    # every step-th file to the host threads (they start now, beside the
+                    # GPU's work on the previous batch and this batch's copies)
+                    step = max(2, int(round(1.0 / HOST_FRAC)))
+                    hfiles = todo[step - 1::step]
+                    so, pos = {}, 0
+                    for k in hfiles:
+                        so[k] = pos
+                        pos += _align(int(caps_[k]))
+                    harr = hstages[bi % 2].get(pos + 256)
+
+                    def run_host(hfiles=hfiles, harr=harr, so=so, buf=buf, off=off, fs=fs, caps_=caps_):
+                        def one(k):
+                            v = buf[off[k]:off[k] + sizes[fs[k]]]
+                            st_, ln_, crc_ = _abi.gunzip_host(v, harr[so[k]:so[k] + int(caps_[k])], with_crc=True)
+                            return k, (int(st_), int(ln_), int(crc_), harr, so[k])
+                        return dict(pool.map(one, hfiles))
+                    host = (hfiles, hctl.submit(run_host))
                 h2d_done[bi] = pipe.batch(bi, fs, buf, off, caps_, gz, members, toff, d_in, d_text,
-                                          [sizes[f] for f in fs])
+                                          [sizes[f] for f in fs], host=host)
                 if TRACE:
                     import sys
                     print(f"[ingest] batch {bi}: {nb} files enqueued, wait read {time.perf_counter() - t_w:.3f} s "
@@ -672,6 +748,7 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
         pool.shutdown(wait=True)
         copier.shutdown(wait=True)
         waiter.shutdown(wait=True)
+        hctl.shutdown(wait=True)
         cdev.close()
     if TRACE:
         import sys

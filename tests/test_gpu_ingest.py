@@ -252,13 +252,18 @@ def test_text_crc32_matches_zlib(dev):
     assert [int(c) for c in got] == [zlib.crc32(data[o:o + n].tobytes()) for o, n in zip(offs, lens)]
 
 
-def test_pipelined_batches_equal_the_host_parser(dev, tmp_path, monkeypatch):
+@pytest.mark.parametrize("host_frac", [0.0, 0.5])
+def test_pipelined_batches_equal_the_host_parser(dev, tmp_path, monkeypatch, host_frac):
     """The pipelined BGZF batches (ingest_device._Async: copies on their own
     stream, no host round trip per batch, failed files skipped on the device)
     against the host parser, and against the synchronous path, over several
     batches with a corrupt member, a truncated file, an empty file and a file
-    that is not gzip in later batches."""
+    that is not gzip in later batches.  host_frac 0.5: every second file of a
+    batch inflated by the host threads beside the GPU (its text copied into
+    HBM behind the previous batch's parse and CRC-checked there; a host file
+    that fails to inflate is dropped like a GPU one)."""
     monkeypatch.setattr(ingest_device, "BATCH_IN", 40 << 10)
+    monkeypatch.setattr(ingest_device, "HOST_FRAC", host_frac)
     rng = np.random.default_rng(21)
     base = _rand_lines(rng, 3000)
     files = {}
@@ -293,3 +298,36 @@ def test_pipelined_batches_equal_the_host_parser(dev, tmp_path, monkeypatch):
     b = _dev_vs_host(dev, d, samples)
     assert a[0] == b[0] and a[1] == b[1]
     assert np.array_equal(a[2].numpy(), b[2].numpy())
+
+
+def test_pipelined_host_share_guard(dev, tmp_path, monkeypatch):
+    """The pipelined batches' host share: a byte of host-inflated text changed
+    in HBM after its copy is caught by the CRC check on the copy stream, and
+    the device path hands the cohort over (DeviceIngestUnsupported); clean, the
+    same cohort gives the host parser's result on the device path."""
+    monkeypatch.setattr(ingest_device, "BATCH_IN", 40 << 10)
+    monkeypatch.setattr(ingest_device, "HOST_FRAC", 0.5)
+    rng = np.random.default_rng(23)
+    base = _rand_lines(rng, 3000)
+    d = tmp_path / "md"
+    d.mkdir()
+    for i in range(8):
+        (d / f"S{i:03d}.regions.bed.gz").write_bytes(_bgzf("".join(base).encode()))
+    samples = [f"S{i:03d}" for i in range(8)]
+    _dev_vs_host(dev, d, samples)
+    hits = []
+
+    def corrupt(dev_, d_text, toff, ks):
+        k = ks[0]
+        pos = int(toff[k]) + 900
+        b = np.zeros(1, np.uint8)
+        _abi.call("grid_d2h", dev_.ctx, b.ctypes.data, d_text.ptr + pos, 1)
+        b[0] = ord("7") if b[0] != ord("7") else ord("3")
+        _abi.call("grid_h2d", dev_.ctx, d_text.ptr + pos, b.ctypes.data, 1)
+        hits.append(k)
+
+    monkeypatch.setattr(ingest_device, "AFTER_HOST_TEXT", corrupt)
+    inds = nm.map_mosdepth_files_to_samples(d, samples)
+    with pytest.raises(ingest_device.DeviceIngestUnsupported, match="gzip CRC"):
+        nm._ingest_dev(dev, inds, d, None, None, None, {}, 20, 100, 2)
+    assert hits
