@@ -262,7 +262,8 @@ def test_pipelined_batches_equal_the_host_parser(dev, tmp_path, monkeypatch, hos
     batch inflated by the host threads beside the GPU (its text copied into
     HBM behind the previous batch's parse and CRC-checked there; a host file
     that fails to inflate is dropped like a GPU one)."""
-    monkeypatch.setattr(ingest_device, "BATCH_IN", 40 << 10)
+    # batches of a few files (one file each when host_frac is 0: many batches)
+    monkeypatch.setattr(ingest_device, "BATCH_IN", (120 if host_frac else 40) << 10)
     monkeypatch.setattr(ingest_device, "HOST_FRAC", host_frac)
     rng = np.random.default_rng(21)
     base = _rand_lines(rng, 3000)
@@ -288,12 +289,13 @@ def test_pipelined_batches_equal_the_host_parser(dev, tmp_path, monkeypatch, hos
     orig = ingest_device._Async.batch
 
     def counted(self, *a, **k):
-        calls.append(1)
+        calls.append(len(k["host"][0]) if k.get("host") else 0)
         return orig(self, *a, **k)
 
     monkeypatch.setattr(ingest_device._Async, "batch", counted)
     a = _dev_vs_host(dev, d, samples)
-    assert len(calls) >= 3, "the pipelined path did not run"
+    assert len(calls) >= 2, "the pipelined path did not run"
+    assert (sum(calls) > 0) == (host_frac > 0), calls
     monkeypatch.setattr(ingest_device, "PIPELINE", False)
     b = _dev_vs_host(dev, d, samples)
     assert a[0] == b[0] and a[1] == b[1]
@@ -305,7 +307,7 @@ def test_pipelined_host_share_guard(dev, tmp_path, monkeypatch):
     in HBM after its copy is caught by the CRC check on the copy stream, and
     the device path hands the cohort over (DeviceIngestUnsupported); clean, the
     same cohort gives the host parser's result on the device path."""
-    monkeypatch.setattr(ingest_device, "BATCH_IN", 40 << 10)
+    monkeypatch.setattr(ingest_device, "BATCH_IN", 120 << 10)
     monkeypatch.setattr(ingest_device, "HOST_FRAC", 0.5)
     rng = np.random.default_rng(23)
     base = _rand_lines(rng, 3000)
