@@ -249,8 +249,8 @@ class _Async:
             pos += _align(a.nbytes)
         return offs, pos
 
-    def batch(self, bi, fs, buf, off, caps_, gz, members, toff, d_in, d_text, fsizes, host=None):
-        """host: (files, future) -- files of the batch the host threads inflate
+    def batch(self, bi, fs, buf, off, caps_, gz, members, toff, d_in, d_text, fsizes, hshare=None):
+        """hshare: (files, future) -- files of the batch the host threads inflate
         (the future returns per file (status, length, crc, staging, offset));
         their text is copied into d_text once the previous batch's parse is done
         and checked there against its gzip CRC on the copy stream, while the
@@ -258,7 +258,7 @@ class _Async:
         dev, cdev, p = self.dev, self.cdev, bi % 2
         nb = len(fs)
         mu = [k for k in range(nb) if gz[k] and fsizes[k] > 0 and members[k] is not None]
-        hset = set(host[0]) if host else set()
+        hset = set(hshare[0]) if hshare else set()
         uo, ul, to, tc, owner = [], [], [], [], []
         for k in mu:
             if k in hset:
@@ -318,7 +318,7 @@ class _Async:
                  ust.ptr, uln.ptr, unm.ptr)
         hfail = []
         if hset:
-            res = host[1].result()
+            res = hshare[1].result()
             # the previous batch's parse reads d_text: its regions are free once it is done
             q = 1 - p
             if self.issued[q]:
@@ -634,7 +634,7 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
                 # them, and the batch is enqueued behind the previous one
                 if pipe is None:
                     pipe = _Async(dev, cdev, opts, K, nK, kidx, ref_nlines, Q)
-                host = None
+                hshare = None
                 if HOST_FRAC > 0 and len(todo) > 1:
                     # every step-th file to the host threads (they start now, beside the
                     # GPU's work on the previous batch and this batch's copies)
@@ -652,9 +652,9 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
                             st_, ln_, crc_ = _abi.gunzip_host(v, harr[so[k]:so[k] + int(caps_[k])], with_crc=True)
                             return k, (int(st_), int(ln_), int(crc_), harr, so[k])
                         return dict(pool.map(one, hfiles))
-                    host = (hfiles, hctl.submit(run_host))
+                    hshare = (hfiles, hctl.submit(run_host))
                 h2d_done[bi] = pipe.batch(bi, fs, buf, off, caps_, gz, members, toff, d_in, d_text,
-                                          [sizes[f] for f in fs], host=host)
+                                          [sizes[f] for f in fs], hshare=hshare)
                 if TRACE:
                     import sys
                     print(f"[ingest] batch {bi}: {nb} files enqueued, wait read {time.perf_counter() - t_w:.3f} s "

@@ -289,7 +289,7 @@ def test_pipelined_batches_equal_the_host_parser(dev, tmp_path, monkeypatch, hos
     orig = ingest_device._Async.batch
 
     def counted(self, *a, **k):
-        calls.append(len(k["host"][0]) if k.get("host") else 0)
+        calls.append(len(k["hshare"][0]) if k.get("hshare") else 0)
         return orig(self, *a, **k)
 
     monkeypatch.setattr(ingest_device._Async, "batch", counted)
