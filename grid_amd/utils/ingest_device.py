@@ -95,13 +95,33 @@ class _Pinned:
         return self.b.array
 
 
+_libc = C.CDLL(None)
+_libc.malloc.restype = C.c_void_p
+_libc.malloc.argtypes = [C.c_size_t]
+_libc.free.argtypes = [C.c_void_p]
+
+
 class _Pageable:
+    """Pageable staging from libc malloc: freed through a foreign call, so the
+    multi-GB munmap runs without the GIL (a NumPy array's free holds it, and
+    the staging released on a background thread stalled the step's own thread
+    for ~0.5 s at the end of the config-2 ingest)."""
+
     def __init__(self, nbytes):
-        self.array = np.empty(int(nbytes), np.uint8)
         self.nbytes = int(nbytes)
+        self.ptr = _libc.malloc(max(self.nbytes, 1))
+        if not self.ptr:
+            raise MemoryError(f"staging of {self.nbytes} bytes")
+        self.array = np.ctypeslib.as_array((C.c_uint8 * self.nbytes).from_address(self.ptr))
 
     def free(self):
-        self.array = None
+        if self.ptr:
+            self.array = None
+            _libc.free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        self.free()
 
 
 def _opts(dev, prefix, window, excluded, keep):
@@ -756,7 +776,8 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
               file=sys.stderr, flush=True)
     # the staging buffers: GBs of page-locked memory whose release (unpinning)
     # takes a fraction of a second -- done on a thread of its own, off the step's path
-    held = [pb for grp in ([pins, stages, [first]] + ([pipe.arena_h] if pipe is not None else [])) for pb in grp]
+    held = [pb for grp in ([pins, stages, [first], hstages] + ([pipe.arena_h] if pipe is not None else []))
+            for pb in grp]
     threading.Thread(target=_release_pinned, args=(held,), daemon=True).start()
     held = None
     d_ins = d_text = pipe = None
