@@ -95,29 +95,33 @@ class _Pinned:
         return self.b.array
 
 
-_libc = C.CDLL(None)
-_libc.malloc.restype = C.c_void_p
-_libc.malloc.argtypes = [C.c_size_t]
-_libc.free.argtypes = [C.c_void_p]
+_libc = C.CDLL(None, use_errno=True)
+_libc.mmap.restype = C.c_void_p
+_libc.mmap.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_int, C.c_long]
+_libc.munmap.argtypes = [C.c_void_p, C.c_size_t]
+_libc.madvise.argtypes = [C.c_void_p, C.c_size_t, C.c_int]
 
 
 class _Pageable:
-    """Pageable staging from libc malloc: freed through a foreign call, so the
-    multi-GB munmap runs without the GIL (a NumPy array's free holds it, and
-    the staging released on a background thread stalled the step's own thread
-    for ~0.5 s at the end of the config-2 ingest)."""
+    """Pageable staging mapped through libc (anonymous, transparent huge pages
+    advised, as NumPy does for large arrays) and unmapped through a foreign
+    call, so the multi-GB munmap runs without the GIL (a NumPy array's free
+    holds it: the staging released on a background thread stalled the step's
+    own thread for ~0.5 s at the end of the config-2 ingest)."""
 
     def __init__(self, nbytes):
-        self.nbytes = int(nbytes)
-        self.ptr = _libc.malloc(max(self.nbytes, 1))
-        if not self.ptr:
+        self.nbytes = max(int(nbytes), 1)
+        p = _libc.mmap(None, self.nbytes, 3, 0x22, -1, 0)      # PROT_READ|WRITE, MAP_PRIVATE|ANONYMOUS
+        if p is None or p == C.c_void_p(-1).value:
             raise MemoryError(f"staging of {self.nbytes} bytes")
+        _libc.madvise(p, self.nbytes, 14)                      # MADV_HUGEPAGE (advice only)
+        self.ptr = p
         self.array = np.ctypeslib.as_array((C.c_uint8 * self.nbytes).from_address(self.ptr))
 
     def free(self):
         if self.ptr:
             self.array = None
-            _libc.free(self.ptr)
+            _libc.munmap(self.ptr, self.nbytes)
             self.ptr = None
 
     def __del__(self):
@@ -778,9 +782,11 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
     # takes a fraction of a second -- done on a thread of its own, off the step's path
     held = [pb for grp in ([pins, stages, [first], hstages] + ([pipe.arena_h] if pipe is not None else []))
             for pb in grp]
+    # device buffers first (their release and the host unmaps contend for the
+    # address space), then the host staging on its own thread
+    d_ins = d_text = pipe = None
     threading.Thread(target=_release_pinned, args=(held,), daemon=True).start()
     held = None
-    d_ins = d_text = pipe = None
     if TRACE:
         import sys
         print(f"[ingest] input/text buffers freed at {time.perf_counter() - t_start:.3f} s", file=sys.stderr,
