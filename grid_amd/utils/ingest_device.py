@@ -227,7 +227,10 @@ def _chunks(files, tlen):
     return cfile, cstart, cfirst, tot
 
 
-def _release_pinned(held):
+def _release_pinned(held, dbufs=()):
+    for db in dbufs:                   # device buffers first (see the caller)
+        if db is not None:
+            db.free()
     for pb in held:
         if pb.b is not None:
             pb.b.free()
@@ -782,11 +785,14 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
     # takes a fraction of a second -- done on a thread of its own, off the step's path
     held = [pb for grp in ([pins, stages, [first], hstages] + ([pipe.arena_h] if pipe is not None else []))
             for pb in grp]
-    # device buffers first (their release and the host unmaps contend for the
-    # address space), then the host staging on its own thread
-    d_ins = d_text = pipe = None
-    threading.Thread(target=_release_pinned, args=(held,), daemon=True).start()
-    held = None
+    # the batches' device buffers (tens of GB: their release takes ~0.5 s) and
+    # then the host staging, on a thread of their own, off the step's path
+    dbufs = [d_ins[0], d_ins[1], d_text]
+    d_ins = d_text = d_in = pipe = None
+    th = threading.Thread(target=_release_pinned, args=(held, dbufs), daemon=True)
+    th.start()
+    _abi.RELEASES.append((th, dev.ctx))
+    held = dbufs = None
     if TRACE:
         import sys
         print(f"[ingest] input/text buffers freed at {time.perf_counter() - t_start:.3f} s", file=sys.stderr,
@@ -798,6 +804,9 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
     valid, cpos = dev.alloc(nK, np.int32), dev.alloc(nK, np.int64)
     present, nvalid = dev.alloc(max(nfiles, 1), np.uint64), dev.alloc(max(nfiles, 1), np.uint64)
     m = C.c_int64()
+    if TRACE:
+        import sys
+        print(f"[ingest] finish buffers at {time.perf_counter() - t_start:.3f} s", file=sys.stderr, flush=True)
     d_rows = dev.upload(rows if rows.size else np.zeros(1, np.int32))
     call("grid_md_finish", dev.ctx, Q.ptr, nK, nK, nfiles, d_rows.ptr, len(rows), float(min_depth),
          float(max_depth), mean.ptr, valid.ptr, cpos.ptr, present.ptr, nvalid.ptr, C.byref(m))
