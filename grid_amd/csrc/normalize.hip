@@ -1531,7 +1531,7 @@ __device__ __forceinline__ void z7_body(Q16 s16, int64_t n, int64_t ld, const in
   }
   const int64_t s0 = (by * 256 + threadIdx.x) * 4;
   if (s0 >= r) return;
-  if (zblk) {   // timing probe (tools build): step-4 output blocked [col block][row][1024]
+  if (zblk & 1) {   // timing probe (tools build): step-4 output blocked [col block][row][1024]
     zq += by * (n - 1) * 1024;
     ld_zq = 1024;
   }
@@ -1575,12 +1575,17 @@ __device__ __forceinline__ void z7_body(Q16 s16, int64_t n, int64_t ld, const in
   const int64_t base = W16 ? (js[0] & ~7ll) : (js[0] & ~3ll);
   const int nwin = W16 ? (base + 16 <= ld ? 16 : 8) : (base + 12 <= ld ? 12 : base + 8 <= ld ? 8 : 4);
   int d[4];
-  bool inwin = true;
+  bool inwin = true, need_hi = false;
 #pragma unroll
   for (int c = 0; c < 4; c++) {
     d[c] = (int)(js[c] - base);
     inwin = inwin && (c >= w || d[c] < nwin);
+    need_hi = need_hi || (c < w && d[c] >= 8);
   }
+  // W16: the upper 16 B of the window only for a lane whose columns reach past
+  // its first 8 codes (about half of them at 90 % selected); the others would
+  // select nothing from it.  zblk bit 1 (tools build): always load it (A/B)
+  const bool ld_hi = nwin >= 16 && (need_hi || (zblk & 2));
   // byte-permute selectors of code c: the 8-B piece it is not in selects zero
   // bytes (0x0c), so code = perm(va) | perm(vb) | perm(vc), branch-free
   uint32_t pa[4], pb[4], pc[4], pd[4];
@@ -1613,9 +1618,9 @@ __device__ __forceinline__ void z7_body(Q16 s16, int64_t n, int64_t ld, const in
       typedef unsigned v4u __attribute__((ext_vector_type(4)));
       const v4u lo = NT & 1 ? __builtin_nontemporal_load(reinterpret_cast<const v4u *>(p))
                             : *reinterpret_cast<const v4u *>(p);
-      const v4u hi = nwin >= 16 ? (NT & 1 ? __builtin_nontemporal_load(reinterpret_cast<const v4u *>(p + 8))
-                                          : *reinterpret_cast<const v4u *>(p + 8))
-                                : v4u{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+      const v4u hi = ld_hi ? (NT & 1 ? __builtin_nontemporal_load(reinterpret_cast<const v4u *>(p + 8))
+                                     : *reinterpret_cast<const v4u *>(p + 8))
+                           : v4u{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
       va[u] = lo.xy; vb[u] = lo.zw; vc[u] = hi.xy; vd[u] = hi.zw;
     } else {
       vd[u] = v2u{0u, 0u};
@@ -2398,8 +2403,9 @@ static int zquant_impl(grid_ctx *ctx, const int32_t *d_q, const Q16 &s16, int64_
       const int64_t nrg7 = ceil_div(n, ZR), ncb7 = ceil_div(ceil_div(r, 4), 256);
 #ifdef GRID_PROBES
       const char *zbe = getenv("GRID_Z7_ZBLK");     // wrong escape positions: timing only
-      const int zblk = zbe ? atoi(zbe) : 0;
-      REQUIRE(!zblk || ld_zq >= ncb7 * 1024, "GRID_Z7_ZBLK needs ld_zq >= %lld", (long long)(ncb7 * 1024));
+      const char *hae = getenv("GRID_Z7_HIALL");    // 1: every lane loads its window's upper 16 B (A/B)
+      const int zblk = (zbe && atoi(zbe) ? 1 : 0) | (hae && atoi(hae) ? 2 : 0);
+      REQUIRE(!(zblk & 1) || ld_zq >= ncb7 * 1024, "GRID_Z7_ZBLK needs ld_zq >= %lld", (long long)(ncb7 * 1024));
 #else
       const int zblk = 0;
 #endif
