@@ -299,12 +299,30 @@ class Device:
     def sync(self):
         call("grid_sync", self.ctx)
 
+    def cached(self, name, nbytes) -> "DevBuf":
+        """A uint8 device buffer of at least ``nbytes`` kept on this context
+        under ``name`` for reuse by later calls (the device ingest's input and
+        text buffers, tens of GB: releasing them took ~0.4 s of the step's
+        time, hipFree holding the device); freed by close() or when a larger
+        one replaces it."""
+        cache = self.__dict__.setdefault("_cache", {})
+        b = cache.get(name)
+        if b is None or b.nbytes < nbytes:
+            if b is not None:
+                b.free()
+                cache[name] = b = None
+            b = cache[name] = self.alloc(int(nbytes), np.uint8)
+        return b
+
     def close(self):
         if getattr(self, "ctx", None):
             # background releases of this context's buffers (ingest_device) finish first
             for t in [t for t, ctx in RELEASES if ctx == self.ctx]:
                 t.join()
             RELEASES[:] = [(t, ctx) for t, ctx in RELEASES if ctx != self.ctx and t.is_alive()]
+            for b in self.__dict__.pop("_cache", {}).values():
+                if b is not None:
+                    b.free()
             load().grid_ctx_destroy(self.ctx)
             self.ctx = None
 

@@ -229,10 +229,7 @@ def _chunks(files, tlen):
     return cfile, cstart, cfirst, tot
 
 
-def _release_pinned(held, dbufs=()):
-    for db in dbufs:                   # device buffers first (see the caller)
-        if db is not None:
-            db.free()
+def _release_pinned(held):
     for pb in held:
         if pb.b is not None:
             pb.b.free()
@@ -648,12 +645,12 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
                 if pipe is not None:
                     pipe.drain()
                 d_ins[bi % 2] = None
-                d_ins[bi % 2] = dev.alloc(in_need if bi else int(off[-1]) + 256, np.uint8)
+                d_ins[bi % 2] = dev.cached(f"ingest_in{bi % 2}", in_need if bi else int(off[-1]) + 256)
             if d_text is None or d_text.nbytes < toff[-1] + 256:
                 if pipe is not None:
                     pipe.drain()
                 d_text = None
-                d_text = dev.alloc(int(min(toff[-1] + 256 + toff[-1] // 8, 2 * BATCH_TEXT + 256)), np.uint8)
+                d_text = dev.cached("ingest_text", int(min(toff[-1] + 256 + toff[-1] // 8, 2 * BATCH_TEXT + 256)))
             d_in = d_ins[bi % 2]
             todo = [k for k in range(nb) if gz[k] and sizes[fs[k]] > 0]
             bgzf = {k: members[k] is not None for k in todo}
@@ -787,14 +784,13 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
     # takes a fraction of a second -- done on a thread of its own, off the step's path
     held = [pb for grp in ([pins, stages, [first], hstages] + ([pipe.arena_h] if pipe is not None else []))
             for pb in grp]
-    # the batches' device buffers (tens of GB: their release takes ~0.5 s) and
-    # then the host staging, on a thread of their own, off the step's path
-    dbufs = [d_ins[0], d_ins[1], d_text]
+    # the batches' device buffers stay cached on the context (Device.cached);
+    # the host staging is released on a thread of its own, off the step's path
     d_ins = d_text = d_in = pipe = None
-    th = threading.Thread(target=_release_pinned, args=(held, dbufs), daemon=True)
+    th = threading.Thread(target=_release_pinned, args=(held,), daemon=True)
     th.start()
     _abi.RELEASES.append((th, dev.ctx))
-    held = dbufs = None
+    held = None
     if TRACE:
         import sys
         print(f"[ingest] input/text buffers freed at {time.perf_counter() - t_start:.3f} s", file=sys.stderr,
