@@ -165,7 +165,6 @@ class GridNativeError(RuntimeError):
 
 
 _lib = None
-RELEASES = []     # (thread, ctx): buffers of ctx being released off the caller's path (Device.close joins)
 
 
 def load():
@@ -316,10 +315,6 @@ class Device:
 
     def close(self):
         if getattr(self, "ctx", None):
-            # background releases of this context's buffers (ingest_device) finish first
-            for t in [t for t, ctx in RELEASES if ctx == self.ctx]:
-                t.join()
-            RELEASES[:] = [(t, ctx) for t, ctx in RELEASES if ctx != self.ctx and t.is_alive()]
             for b in self.__dict__.pop("_cache", {}).values():
                 if b is not None:
                     b.free()

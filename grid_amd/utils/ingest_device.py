@@ -39,7 +39,6 @@ from __future__ import annotations
 
 import ctypes as C
 import os
-import threading
 import time
 from collections.abc import Sequence
 from concurrent.futures import ThreadPoolExecutor
@@ -229,11 +228,18 @@ def _chunks(files, tlen):
     return cfile, cstart, cfirst, tot
 
 
-def _release_pinned(held):
-    for pb in held:
-        if pb.b is not None:
-            pb.b.free()
-            pb.b = None
+# The host staging of the device ingest, kept for the process (reused by later
+# ingests): releasing tens of GB of staging the HIP runtime has copied from
+# (page-locked, or pageable pages it has seen) holds the runtime for 0.4-0.8 s,
+# and every HIP call of the step after the ingest waited for it (r04y, r04ac).
+_STAGING = {}
+
+
+def _staging(name, bound, pinned=False):
+    b = _STAGING.get(name)
+    if b is None:
+        b = _STAGING[name] = _Pinned(bound, pinned=pinned)
+    return b
 
 
 class _Async:
@@ -259,7 +265,7 @@ class _Async:
         self.h2d = [_abi.Event(), _abi.Event()]
         self.done = [_abi.Event(), _abi.Event()]
         self.issued = [False, False]
-        self.arena_h = [_Pinned(64 << 20, pinned=False), _Pinned(64 << 20, pinned=False)]
+        self.arena_h = [_staging("arena0", 64 << 20), _staging("arena1", 64 << 20)]
         self.arena_d = [None, None]
         self.scr = [None, None]                 # per parity: member table, chunk counts/lines, file status
         self.out = []                           # per batch: (fs, owner, unit status, unit length, flags, kept, okb)
@@ -464,16 +470,16 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
     if cur:
         batches.append(cur)
     in_need = 256 + max((sum(_align(max(sizes[f], 1)) for f in b) for b in batches), default=0)
-    pins = [_Pinned(BATCH_IN + 512, pinned=False), _Pinned(BATCH_IN + 512, pinned=False)]
-    first = _Pinned(FIRST_BATCH_IN + 512, pinned=False)    # the (small) first batch: K, quickly
-    stages = [_Pinned(STAGE + 512), _Pinned(STAGE + 512)]
+    pins = [_staging("in0", BATCH_IN + 512), _staging("in1", BATCH_IN + 512)]
+    first = _staging("first", FIRST_BATCH_IN + 512)        # the (small) first batch: K, quickly
+    stages = [_staging("text0", STAGE + 512, pinned=True), _staging("text1", STAGE + 512, pinned=True)]
     nthreads = max(1, min(int(threads or 1), 32))
     pool = ThreadPoolExecutor(nthreads)
     rpool = ThreadPoolExecutor(1)         # the next batch's read (its files on `pool`)
     copier = ThreadPoolExecutor(1)        # H2D of CPU-inflated text, on its own stream
     waiter = ThreadPoolExecutor(1)        # notes when the GPU's inflate ends
     hctl = ThreadPoolExecutor(1)          # pipelined batches: the host share's inflate (its files on `pool`)
-    hstages = [_Pinned(8 << 30, pinned=False), _Pinned(8 << 30, pinned=False)]
+    hstages = [_staging("host0", 8 << 30), _staging("host1", 8 << 30)]
     cdev = _abi.Device(dev.index)          # its own non-blocking stream
     split = _Split(nthreads)
 
@@ -782,15 +788,9 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
               file=sys.stderr, flush=True)
     # the staging buffers: GBs of page-locked memory whose release (unpinning)
     # takes a fraction of a second -- done on a thread of its own, off the step's path
-    held = [pb for grp in ([pins, stages, [first], hstages] + ([pipe.arena_h] if pipe is not None else []))
-            for pb in grp]
-    # the batches' device buffers stay cached on the context (Device.cached);
-    # the host staging is released on a thread of its own, off the step's path
+    # the batches' device buffers stay cached on the context (Device.cached),
+    # the host staging in _STAGING
     d_ins = d_text = d_in = pipe = None
-    th = threading.Thread(target=_release_pinned, args=(held,), daemon=True)
-    th.start()
-    _abi.RELEASES.append((th, dev.ctx))
-    held = None
     if TRACE:
         import sys
         print(f"[ingest] input/text buffers freed at {time.perf_counter() - t_start:.3f} s", file=sys.stderr,
