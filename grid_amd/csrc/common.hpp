@@ -30,6 +30,11 @@ struct grid_ctx {
   void *aux = nullptr;         // small device workspace: Gram tile list + round counters
   int32_t *aux_tiles_host = nullptr;   // host copy of the uploaded tile list (re-upload check)
   int aux_tiles_n = 0;
+  // buffers a call keeps on the context for the next one (the device writer's
+  // GBs of device and page-locked memory: their release at the end of a call
+  // held the runtime for a fraction of a second); freed by grid_ctx_destroy
+  void *keep = nullptr;
+  void (*keep_free)(void *) = nullptr;
 };
 // K-blocked bf16 panel of the k-NN Gram: [kpad / KBW][np][KBW] (a 16-row
 // half K-step of k_gram8's ring is then 1 KiB contiguous: whole 128-B lines)

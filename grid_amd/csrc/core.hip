@@ -72,6 +72,7 @@ int grid_ctx_destroy(grid_ctx *ctx) {
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
   if (ctx->aux) (void)hipFree(ctx->aux);
+  if (ctx->keep && ctx->keep_free) ctx->keep_free(ctx->keep);
   delete[] ctx->aux_tiles_host;
   for (auto &e : ctx->ev) (void)hipEventDestroy(e);
   if (ctx->own) (void)hipStreamDestroy(ctx->own);

@@ -647,6 +647,18 @@ struct HBuf {
   }
 };
 
+// The device writer's buffers, kept on the context between calls.
+struct WriterBufs {
+  DBuf<int64_t> d_blen, d_boff, d_rowoff, d_prelen, d_preoff, d_sstart, d_sbase, d_moff, d_msize, d_mrow, d_mlen,
+      d_mbits, d_mstart, d_mseg0;
+  DBuf<int32_t> d_slen;
+  DBuf<uint32_t> d_sbits, d_crc, d_hdr, d_tab, d_out, d_scrc;
+  DBuf<char> d_pre, d_text;
+  DBuf<CodeDev> d_code;
+  DBuf<unsigned long long> d_hist;
+  HBuf hb[2];
+};
+
 #define HIPCHK_E(x)                                                                   \
   do {                                                                                \
     hipError_t e_ = (x);                                                              \
@@ -743,14 +755,23 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
   crc_tables(crctab.data());
   const X2N x2n = make_x2n();
   const CrcOps cops = make_crc_ops(x2n);
-  DBuf<int64_t> d_blen, d_boff, d_rowoff, d_prelen, d_preoff, d_sstart, d_sbase, d_moff, d_msize, d_mrow, d_mlen,
-      d_mbits, d_mstart, d_mseg0;
-  DBuf<int32_t> d_slen;
-  DBuf<uint32_t> d_sbits, d_crc, d_hdr, d_tab, d_out, d_scrc;
-  DBuf<char> d_pre, d_text;
-  DBuf<CodeDev> d_code;
-  DBuf<unsigned long long> d_hist;
-  HBuf hb[2];
+  // the buffers stay on the context for the next call (grid_ctx::keep)
+  if (!ctx->keep) {
+    ctx->keep = new WriterBufs;
+    ctx->keep_free = [](void *p) { delete static_cast<WriterBufs *>(p); };
+  }
+  WriterBufs &wbuf = *static_cast<WriterBufs *>(ctx->keep);
+  auto &d_blen = wbuf.d_blen, &d_boff = wbuf.d_boff, &d_rowoff = wbuf.d_rowoff, &d_prelen = wbuf.d_prelen,
+       &d_preoff = wbuf.d_preoff, &d_sstart = wbuf.d_sstart, &d_sbase = wbuf.d_sbase, &d_moff = wbuf.d_moff,
+       &d_msize = wbuf.d_msize, &d_mrow = wbuf.d_mrow, &d_mlen = wbuf.d_mlen, &d_mbits = wbuf.d_mbits,
+       &d_mstart = wbuf.d_mstart, &d_mseg0 = wbuf.d_mseg0;
+  auto &d_slen = wbuf.d_slen;
+  auto &d_sbits = wbuf.d_sbits, &d_crc = wbuf.d_crc, &d_hdr = wbuf.d_hdr, &d_tab = wbuf.d_tab, &d_out = wbuf.d_out,
+       &d_scrc = wbuf.d_scrc;
+  auto &d_pre = wbuf.d_pre, &d_text = wbuf.d_text;
+  auto &d_code = wbuf.d_code;
+  auto &d_hist = wbuf.d_hist;
+  auto &hb = wbuf.hb;
   int rc = GRID_OK;
   bool io_ok = true;
   // writer thread: member 0 first, then the batches in order

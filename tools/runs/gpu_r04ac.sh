@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r04ac
 mkdir -p $O
 timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread -p no:cacheprovider \
-  tests/test_gpu_ingest.py tests/test_gpu_e2e.py > $O/pytest.log 2>&1 || { tail -n 40 $O/pytest.log; exit 1; }
+  tests/test_gpu_ingest.py tests/test_gpu_e2e.py tests/test_gpu_gzwrite.py > $O/pytest.log 2>&1 || { tail -n 40 $O/pytest.log; exit 1; }
 tail -n 1 $O/pytest.log
 for r in 1 2; do
   keep=--reuse; [ $r = 2 ] && keep=""
