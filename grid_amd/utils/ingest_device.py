@@ -59,9 +59,9 @@ XSTREAM_WAIT = True             # dev's stream waits for the copy stream (False 
 AFTER_HOST_TEXT = None          # test seam: called (dev, d_text, toff, files) once host text is in HBM
 # pipelined BGZF batches: the fraction of each batch's files the host threads
 # inflate beside the GPU (every k-th file; 0 = the GPU inflates all).  With 16
-# host threads beside the MI355X's 37 GB/s: 0.2 -> config-2 ingest 10.7 -> 10.3 s
-# (r04y; 0.25: the threads, which also read the files, fall behind)
-HOST_FRAC = float(os.environ.get("GRID_INGEST_HOST_FRAC", "0.2"))
+# host threads beside the MI355X's 37 GB/s, config-2 ingest (r04y, kept
+# staging): 0.15 9.9 s, 0.2 9.5 s, 0.25 9.1-9.25 s, 0.33 9.3-9.6 s
+HOST_FRAC = float(os.environ.get("GRID_INGEST_HOST_FRAC", "0.25"))
 
 
 class DeviceIngestUnsupported(Exception):
