@@ -786,8 +786,10 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
   // pwrite of [p, p + len) at file offset o by up to 4 threads (page-cache
   // copies: one thread moves ~5 GB/s); on the direct descriptor the pieces
   // split at FA multiples
+  const char *wwe = GRID_AB_KNOB("GRID_WRITER_W");   // writer threads per batch (A/B)
+  const size_t WMAX = wwe && atoi(wwe) > 0 ? (size_t)atoi(wwe) : 4;
   auto pwrite_all = [&](int f, const char *p, size_t len, int64_t o, size_t unit) {
-    const int W = (int)std::max<size_t>(1, std::min<size_t>(4, len >> 26));
+    const int W = (int)std::max<size_t>(1, std::min<size_t>(WMAX, len >> 26));
     std::vector<std::thread> ws;
     std::vector<char> ok((size_t)W, 1);
     for (int t = 0; t < W; t++)
