@@ -378,3 +378,25 @@ def test_device_ingest_chunk_table():
         assert tot == len(exp)
         assert [(int(a), int(b)) for a, b in zip(cfile[:tot], cstart[:tot])] == exp
         assert cfirst.tolist() == [0] + list(np.cumsum([-(-int(tlen[f]) // d.CH) for f in files]))
+
+
+def test_staging_is_kept_and_grows():
+    """The device ingest's host staging (ingest_device._staging): one buffer
+    per name for the process, reused while large enough, replaced by a larger
+    one when a request outgrows it; the pageable form is an anonymous mapping
+    released through a foreign call (no GIL held while it unmaps)."""
+    from grid_amd.utils import ingest_device as idv
+    name = "test_staging_cpu"
+    idv._STAGING.pop(name, None)
+    s = idv._staging(name, 1 << 20)
+    a = s.get(4096)
+    a[:4] = [1, 2, 3, 4]
+    assert idv._staging(name, 1 << 20) is s
+    b = s.get(1000)                       # fits: the same memory
+    assert b.ctypes.data == a.ctypes.data and list(b[:4]) == [1, 2, 3, 4]
+    c = s.get(3 << 20)                    # larger than the buffer: a new one
+    assert c.nbytes >= 3 << 20
+    c[-1] = 7
+    s.b.free()
+    s.b = None
+    idv._STAGING.pop(name, None)
