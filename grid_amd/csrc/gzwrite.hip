@@ -19,7 +19,7 @@
 //      segment's absolute output bit); k_encode: each segment packs its codes
 //      into an LDS word image and stores it, atomically only on the two edge
 //      words it may share with a neighbour;
-//   4. k_seg_crc / k_seg_fold: CRC-32 of every 4 KiB text segment (a wave
+//   4. k_seg_crc / k_seg_fold_wave: CRC-32 of every 4 KiB text segment (a wave
 //      each: 64-byte lane slices, slicing-by-4 tables in LDS, a tree of the
 //      fixed GF(2) shift operators x^(8 len) mod P -- zlib's crc32_combine
 //      algorithm, restated), then the segments folded per member;
@@ -509,7 +509,7 @@ __device__ __forceinline__ void glb_byte(uint32_t *out, uint64_t byte, uint32_t 
 // [64 l, 64 l + 64) (four 16-B loads, slicing-by-4 in LDS), then a 6-level
 // tree of the fixed operators gives the segment's CRC in lane 0; a segment
 // shorter than 4 KiB (a member's or a range's last) is folded by lane 0 with
-// the general operator.  Then one thread per member folds its segments.
+// the general operator.  Then one wave per member folds its segments.
 constexpr int CSEG = 4096;
 struct CrcOps {
   uint32_t m[7][32];     // M_(64 * 2^k), k = 0..6
@@ -567,18 +567,38 @@ __global__ __launch_bounds__(256) void k_seg_crc(const uint8_t *__restrict__ tex
   }
 }
 
-// one thread per group (member / range): its segments [g0[i], g0[i + 1]) in order
-__global__ void k_seg_fold(const uint32_t *__restrict__ scrc, const int32_t *__restrict__ slen,
-                           const int64_t *__restrict__ g0, int64_t ng, CrcOps ops, X2N x2n,
-                           uint32_t *__restrict__ crc) {
-  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= ng) return;
+// One wave per group: lane l folds a contiguous run of ceil(n / 64) of the
+// group's n segments in order (each step: the 4 KiB operator, or the general
+// one for a short last segment), then the 64 runs are joined by
+// a tree, CRC(A || B) = M_|B| crc(A) ^ crc(B) with |B| summed alongside (the
+// general operator x^(8 |B|) mod P).  A range of 50 MB (12 k segments) took
+// one thread ~7 ms serially (the device ingest's guard, r04aj).
+__global__ __launch_bounds__(256) void k_seg_fold_wave(const uint32_t *__restrict__ scrc,
+                                                       const int32_t *__restrict__ slen,
+                                                       const int64_t *__restrict__ g0, int64_t ng, CrcOps ops,
+                                                       X2N x2n, uint32_t *__restrict__ crc) {
+  const int lane = threadIdx.x & 63;
+  const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= ng) return;                       // whole waves only
+  const int64_t a = g0[g], n = g0[g + 1] - a, run = (n + 63) / 64;
+  const int64_t s0 = a + (int64_t)lane * run, s1 = min(a + n, s0 + run);
   uint32_t acc = 0;
-  for (int64_t s = g0[g]; s < g0[g + 1]; s++) {
+  uint64_t len = 0;
+  for (int64_t s = s0; s < s1; s++) {
     const int L = slen[s];
     acc = (L == CSEG ? gf2_mul(ops.m[6], acc) : multmodp(x8n((uint64_t)L, x2n), acc)) ^ scrc[s];
+    len += (uint64_t)L;
   }
-  crc[g] = acc;
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    const uint32_t oc = __shfl_down(acc, 1 << k, 64);
+    const uint64_t ol = __shfl_down(len, 1 << k, 64);
+    if ((lane & ((2 << k) - 1)) == 0) {
+      acc = multmodp(x8n(ol, x2n), acc) ^ oc;
+      len += ol;
+    }
+  }
+  if (lane == 0) crc[g] = acc;
 }
 
 // gzip framing of member m at byte moff[m]: header with the GR index, the
@@ -1006,7 +1026,7 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
                          d_sstart.p, d_slen.p, ns, d_tab.p, cops, x2n, d_scrc.p);
       STEP(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_seg_fold, dim3((unsigned)((nm + 63) / 64)), dim3(64), 0, st, d_scrc.p, d_slen.p,
+    hipLaunchKernelGGL(k_seg_fold_wave, dim3((unsigned)((nm + 3) / 4)), dim3(256), 0, st, d_scrc.p, d_slen.p,
                        d_mseg0.p, nm, cops, x2n, d_crc.p);
     STEP(hipGetLastError());
     h_sbits.resize((size_t)ns);
@@ -1085,7 +1105,7 @@ int grid_text_crc32(grid_ctx *ctx, const uint8_t *d_base, const int64_t *h_off, 
                     uint32_t *h_crc) {
   REQUIRE(ctx && n >= 0 && (n == 0 || (d_base && h_off && h_len && h_crc)), "bad args");
   if (n == 0) return GRID_OK;
-  // 4 KiB segments of every range (k_seg_crc), folded per range (k_seg_fold)
+  // 4 KiB segments of every range (k_seg_crc), folded per range (k_seg_fold_wave)
   std::vector<int64_t> ss, g0(n + 1);
   std::vector<int32_t> sl;
   for (int64_t i = 0; i < n; i++) {
@@ -1123,8 +1143,8 @@ int grid_text_crc32(grid_ctx *ctx, const uint8_t *d_base, const int64_t *h_off, 
                        d_tab.p, cops, x2n, d_sc.p);
     LAUNCHCHK();
   }
-  hipLaunchKernelGGL(k_seg_fold, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, d_sc.p, d_l.p, d_g0.p, n, cops,
-                     x2n, d_c.p);
+  hipLaunchKernelGGL(k_seg_fold_wave, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, d_sc.p, d_l.p, d_g0.p, n,
+                     cops, x2n, d_c.p);
   LAUNCHCHK();
   HIPCHK(hipMemcpyAsync(h_crc, d_c.p, n * 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
