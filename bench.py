@@ -273,14 +273,21 @@ def launch_ranks(gpus):
     return subprocess.call(cmd, env=env)
 
 
-def plan_memory(n, ml, world, budget):
+def plan_memory(n, ml, world, budget, shard="bin", piece_bytes=0):
     """Resident (one chunk) when the whole shard fits the HBM budget, else the
     widest 8192-multiple chunk that does.  Returns (chunk or None, bytes)."""
     np_ = -(-max(n, 1) // 256) * 256
-    # Gram + (multi-GPU) the segment send / receive buffers: (2W+1)/(4W) and
-    # 1/W of that of np^2 int64 (fused.Steps47._step5_segments)
-    seg = (2 * world + 1) / (4.0 * world) * (1 + 1.0 / world) if world > 1 else 0.0
-    fixed = np_ * np_ * 8 * (1 + seg) + n * (-(-ml // 8192)) * 24 + ml * 64
+    if shard == "cohort" and world > 1:
+        # no whole Gram: the two row segments (B (2W+1) B int64, B a multiple
+        # of 256) and two panel-piece buffers (fused.Steps47, split="cohort")
+        B = -(-(-(-np_ // (2 * world))) // 256) * 256
+        fixed = B * (2 * world + 1) * B * 8 + 2 * piece_bytes
+    else:
+        # Gram + (multi-GPU) the segment send / receive buffers: (2W+1)/(4W) and
+        # 1/W of that of np^2 int64 (fused.Steps47._step5_segments)
+        seg = (2 * world + 1) / (4.0 * world) * (1 + 1.0 / world) if world > 1 else 0.0
+        fixed = np_ * np_ * 8 * (1 + seg)
+    fixed += n * (-(-ml // 8192)) * 24 + ml * 64
     per_col_resident = n * 4 + n * 2 + np_ * 2            # q int32 + z int16 + bf16 panel
     if fixed + per_col_resident * ml <= budget:
         return None, fixed + per_col_resident * ml
@@ -293,7 +300,9 @@ def plan_memory(n, ml, world, budget):
 
 def run_workload(args, n, m, steps, warmup, world, rank, local, dist, comm, dev, note, profile_pass=True):
     """One workload's timed steps (steps 4-7 of an n x m cohort over `world`
-    ranks): the bench line's fields for it."""
+    ranks): the bench line's fields for it.  With --sim-world W the process
+    is rank --sim-rank of a simulated W-rank run on one GPU (fused.SimComm):
+    `world` / `rank` are then the simulated ones, the clock this process's."""
     import torch
 
     from grid_amd import _abi
@@ -303,10 +312,11 @@ def run_workload(args, n, m, steps, warmup, world, rank, local, dist, comm, dev,
     ml = c1 - c0
     talloc = TorchAlloc(local)
     ops = HipOps(dev)
+    piece_bytes = int(args.piece_mb * 2 ** 20)
     if args.chunk and (n, m) == (args.samples, args.bins):
         chunk, _ = args.chunk, None
     else:
-        chunk, _ = plan_memory(n, ml, world, args.hbm_budget_gb * 1e9)
+        chunk, _ = plan_memory(n, ml, world, args.hbm_budget_gb * 1e9, args.shard, piece_bytes)
     streamed = chunk is not None and chunk < ml
     depth_format = args.depth_format
     if depth_format == "auto":
@@ -341,7 +351,7 @@ def run_workload(args, n, m, steps, warmup, world, rank, local, dist, comm, dev,
             lane.append((HipOps(pdev), pstream))
     st = Steps47(ops, talloc, n, m, c0, ml, k=args.k, n_nbr=300, top_frac=0.1, zmax=2.0, sigma2_max=1000.0,
                  frac_r=1.0, min_nbr=1, n_iters=args.n_iters, comm=comm, phase_lane=lane,
-                 chunk=chunk if streamed else None, keep_z=not streamed)
+                 chunk=chunk if streamed else None, keep_z=not streamed, split=args.shard, piece_bytes=piece_bytes)
     st.set_reads(reads)
     st.set_phasing_graph(off, nbr, w)
 
@@ -358,6 +368,8 @@ def run_workload(args, n, m, steps, warmup, world, rank, local, dist, comm, dev,
     t0 = time.perf_counter()
     gms, glaunch = 0.0, 0
     gram_pairs = []
+    if hasattr(comm, "bytes_in"):
+        comm.bytes_in.clear()
     for s in range(steps):
         st.run(q, ldq, time_gram=True)
         gram_pairs += st.gram_evs
@@ -366,6 +378,7 @@ def run_workload(args, n, m, steps, warmup, world, rank, local, dist, comm, dev,
     st.finish()                                 # the last step's (deferred) phasing, inside the clock
     torch.cuda.synchronize()
     note("timed steps done")
+    sim_bytes = dict(comm.bytes_in) if hasattr(comm, "bytes_in") else None     # the timed steps' only
     if dist:
         dist.barrier()
     t1 = time.perf_counter()
@@ -391,10 +404,17 @@ def run_workload(args, n, m, steps, warmup, world, rank, local, dist, comm, dev,
         if hits and shape_ok and world == 1 and not streamed:
             traffic, tsrc = hits[0]["traffic_bytes"], args.traffic_json
     ruse = st.ruse_loc
-    flops = 2.0 * n * n * ruse                          # 2 N^2 R_use per step (this rank)
-    nt, ni = st.np_ // 128, st.np_ // 256               # k_gram8: 256x128 tiles (I, j >= 2I)
-    ntiles = sum(nt - 2 * i for i in range(ni))
-    executed = 2.0 * ntiles * 256 * 128 * sum(-(-u // 64) * 64 for u in st.chunk_used)
+    cohort = st.split == "cohort"
+    if cohort:
+        # this rank's share of 2 N^2 R_use over all ranks' columns, and the
+        # MFMA work its segment launches executed (fused.Steps47._gram_piece)
+        flops = 2.0 * n * n * st.ruse_tot / world
+        executed = st.exec_flops
+    else:
+        flops = 2.0 * n * n * ruse                      # 2 N^2 R_use per step (this rank)
+        nt, ni = st.np_ // 128, st.np_ // 256           # k_gram8: 256x128 tiles (I, j >= 2I)
+        ntiles = sum(nt - 2 * i for i in range(ni))
+        executed = 2.0 * ntiles * 256 * 128 * sum(-(-u // 64) * 64 for u in st.chunk_used)
     gsec = gms * 1e-3
     streamed_note = (f", bin-streamed in {st.nch} chunks of {chunk} bins regenerated on the device every pass "
                      f"(inside the timed region), step-4 output written per chunk") if streamed else ""
@@ -416,7 +436,9 @@ def run_workload(args, n, m, steps, warmup, world, rank, local, dist, comm, dev,
         "config": {"workload": f"{cfgname}: {n} samples x {m} bins, k={args.k}, n_iters={args.n_iters}, "
                                f"{world} GPU(s){streamed_note}",
                    "samples": n, "bins": m, "k": args.k, "n_iters": args.n_iters,
-                   "parallelism": f"bin-sharded x{world}", "depth_format": depth_format,
+                   "parallelism": (f"{args.shard}-sharded x{world}" + (f" (rank {rank} of a simulated {world}-rank run "
+                                   f"on one GPU)" if args.sim_world else "")), "shard": args.shard,
+                   "depth_format": depth_format,
                    "streamed": streamed, "chunk_bins": chunk if streamed else None, "chunks": st.nch,
                    "selected_regions": st.r_loc if world == 1 else None, "R_use_rank0": ruse,
                    "dipcn_valid": valid, "phasing_levels": st.nlev},
@@ -430,10 +452,16 @@ def run_workload(args, n, m, steps, warmup, world, rank, local, dist, comm, dev,
                      "gram_ms": gms, "gram_launches_per_step": glaunch,
                      "executed_mfma_tflops": executed / gsec / 1e12,
                      "executed_frac": executed / gsec / 1e12 / PEAK_BF16_TFLOPS,
-                     "flops_def": "2*N^2*R_use per step on this rank (SURVEY 8d), over the summed HIP-event time "
-                                  "of its Gram launches; executed = the 256x128 upper-triangle tiles k_gram8 "
-                                  "computes (the symmetric half is not executed)"},
+                     "flops_def": ("2*N^2*R_use per step on this rank (SURVEY 8d), over the summed HIP-event time "
+                                   "of its Gram launches; executed = the 256x128 upper-triangle tiles k_gram8 "
+                                   "computes (the symmetric half is not executed)") if not cohort else
+                                  ("cohort split: this rank's 1/W share of 2*N^2*R_use (all ranks' columns) over the "
+                                   "summed HIP-event time of its segment Gram launches (grid_knn_gram_kb_rows, one "
+                                   "pair per gathered panel piece); executed = the segment tiles it computes")},
     }
+    if sim_bytes is not None:
+        # simulated rank: what the real collectives would bring into this rank per step
+        out["sim_collective_bytes_in_per_step"] = {k: v / steps for k, v in sim_bytes.items()}
     timing = {"stages": stages, "elapsed": elapsed}
     # release the workload's device memory before another one
     del st, q
@@ -474,6 +502,17 @@ def main():
     ap.add_argument("--config3-warmup", type=int, default=1)
     ap.add_argument("--traffic-json", default=TRAFFIC_JSON,
                     help="rocprofv3 PMC summary (tools/pmc_traffic.py) of this same command, for roofline.traffic")
+    ap.add_argument("--shard", choices=["bin", "cohort"], default="bin",
+                    help="multi-rank split of step 5's all-pairs Gram: bin = every rank sums the whole upper triangle "
+                         "over its bins, one reduce-scatter of int64 segments; cohort = the Gram's rows sharded, the "
+                         "quantised panel all-gathered in pieces overlapped with the segment Gram (step 4 stays "
+                         "bin-sharded either way)")
+    ap.add_argument("--piece-mb", type=float, default=2048.0,
+                    help="cohort split: bytes of one gathered panel piece (all ranks), two buffers")
+    ap.add_argument("--sim-world", type=int, default=0,
+                    help="per-rank timing on ONE GPU: run rank --sim-rank of a simulated W-rank job (fused.SimComm: "
+                         "collectives do their local copies only; xGMI time not included)")
+    ap.add_argument("--sim-rank", type=int, default=0)
     ap.add_argument("--depth-format", choices=["auto", "int32", "q16"], default="auto",
                     help="depth matrix in HBM: the compact uint16 hundredths + escape table (q16: half the bytes of "
                          "the step-4 passes, same int32 values after decoding) or int32 hundredths; auto = q16 when "
@@ -524,6 +563,19 @@ def main():
             print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
     n, m = args.samples, args.bins
+    if args.sim_world:
+        if world != 1 or not 0 <= args.sim_rank < args.sim_world:
+            raise SystemExit("bench: --sim-world runs one process (no --gpus) with 0 <= --sim-rank < --sim-world")
+        from grid_amd.fused import SimComm
+        comm = SimComm(args.sim_world, args.sim_rank)
+        out, timing = run_workload(args, n, m, args.steps, args.warmup, args.sim_world, args.sim_rank, local, None,
+                                   comm, dev, note)
+        out["n_gpus"] = 1
+        out["value"] = None          # not a job throughput: one rank's work of a W-rank step
+        out["rank_ms_per_step"] = out["ms_per_step"]
+        out["build"] = _abi.build_info()
+        print(json.dumps(out), file=result_out, flush=True)
+        return
     out, timing = run_workload(args, n, m, args.steps, args.warmup, world, rank, local, dist, comm, dev, note)
     # the metric's own shape (BASELINE config 3: 50k x 3M, streamed on one
     # GPU): one more timed measurement in the same run, beside the line's

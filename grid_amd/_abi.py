@@ -40,6 +40,7 @@ _SIGS = {
     "grid_ctx_own_stream": [_vp],
     "grid_sync": [_vp],
     "grid_ctx_cu_count": [_vp, C.POINTER(_i32)],
+    "grid_mem_info": [_vp, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)],
     "grid_dev_alloc": [_vp, C.c_size_t, C.POINTER(_vp)],
     "grid_dev_free": [_vp, _vp],
     "grid_host_alloc": [C.c_size_t, C.POINTER(_vp)],
@@ -81,6 +82,8 @@ _SIGS = {
     "grid_knn_gram_kb": [_vp, _vp, _i64, _i64, _i32, _vp],
     "grid_knn_topk": [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _vp, _vp, _vp],
     "grid_knn_mirror": [_vp, _vp, _i64],
+    "grid_knn_gram_kb_rows": [_vp, _vp, _i64, _i64, _i32, _i64, _i64, _vp, _i64],
+    "grid_knn_mirror_ld": [_vp, _vp, _i64, _i64],
     "grid_knn_diag": [_vp, _vp, _i64, _i64, _vp],
     "grid_knn_topk_rows": [_vp, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp],
     "grid_knn_topk_d2": [_vp, _vp, _i64, _f64, _i64, _i64, _i64, _i64, _vp, _vp, _vp],
@@ -312,6 +315,27 @@ class Device:
                 cache[name] = b = None
             b = cache[name] = self.alloc(int(nbytes), np.uint8)
         return b
+
+    def release_cached(self, prefix=""):
+        """Free the buffers cached under names starting with ``prefix``;
+        returns the bytes freed."""
+        cache = self.__dict__.get("_cache", {})
+        freed = 0
+        for name in [k for k in cache if k.startswith(prefix)]:
+            b = cache.pop(name)
+            if b is not None:
+                freed += b.nbytes
+                b.free()
+        return freed
+
+    def cached_bytes(self):
+        return sum(b.nbytes for b in self.__dict__.get("_cache", {}).values() if b is not None)
+
+    def mem_info(self):
+        """(free, total) HBM bytes of this device (hipMemGetInfo)."""
+        f, t = C.c_size_t(), C.c_size_t()
+        call("grid_mem_info", self.ctx, C.byref(f), C.byref(t))
+        return f.value, t.value
 
     def close(self):
         if getattr(self, "ctx", None):

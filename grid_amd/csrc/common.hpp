@@ -18,6 +18,15 @@
 
 #include "grid_abi.h"
 
+// One uploaded Gram tile list (launch_gram8): key = (np, first, last row tile)
+constexpr int GRID_TILE_SLOTS = 4;
+struct GridTileSlot {
+  int64_t key = -1;
+  int n = 0;
+  int32_t *host = nullptr;
+  uint64_t used = 0;
+};
+
 struct grid_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -27,9 +36,9 @@ struct grid_ctx {
   void *pinned = nullptr;      // small pinned host buffer for scalars
   hipEvent_t ev[8] = {};
   int ncu = 0;                 // compute units (persistent-kernel grids)
-  void *aux = nullptr;         // small device workspace: Gram tile list + round counters
-  int32_t *aux_tiles_host = nullptr;   // host copy of the uploaded tile list (re-upload check)
-  int aux_tiles_n = 0;
+  void *aux = nullptr;         // small device workspace: Gram tile lists + round counters
+  GridTileSlot tiles[GRID_TILE_SLOTS];   // the uploaded tile lists (host copies, re-upload check)
+  uint64_t tiles_clock = 0;
   // buffers a call keeps on the context for the next one (the device writer's
   // GBs of device and page-locked memory: their release at the end of a call
   // held the runtime for a fraction of a second); freed by grid_ctx_destroy
@@ -39,7 +48,7 @@ struct grid_ctx {
 // K-blocked bf16 panel of the k-NN Gram: [kpad / KBW][np][KBW] (a 16-row
 // half K-step of k_gram8's ring is then 1 KiB contiguous: whole 128-B lines)
 constexpr int KBW = 32;
-constexpr size_t GRID_AUX_BYTES = 4 << 20;   // Gram tile list (<= 512 Ki tiles) + round counters
+constexpr size_t GRID_AUX_BYTES = 4 << 20;   // Gram tile lists (4 slots of <= 128 Ki tiles) + round counters
 
 void grid_set_error(const char *fmt, ...);
 int grid_scratch(grid_ctx *ctx, size_t bytes, void **p);

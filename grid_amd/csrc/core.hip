@@ -73,7 +73,7 @@ int grid_ctx_destroy(grid_ctx *ctx) {
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
   if (ctx->aux) (void)hipFree(ctx->aux);
   if (ctx->keep && ctx->keep_free) ctx->keep_free(ctx->keep);
-  delete[] ctx->aux_tiles_host;
+  for (auto &ts : ctx->tiles) delete[] ts.host;
   for (auto &e : ctx->ev) (void)hipEventDestroy(e);
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
   delete ctx;
@@ -95,6 +95,13 @@ int grid_ctx_own_stream(grid_ctx *ctx) {
 int grid_ctx_cu_count(grid_ctx *ctx, int32_t *n) {
   REQUIRE(ctx && n, "bad args");
   *n = ctx->ncu;
+  return GRID_OK;
+}
+
+int grid_mem_info(grid_ctx *ctx, size_t *free_bytes, size_t *total_bytes) {
+  REQUIRE(ctx && free_bytes && total_bytes, "bad args");
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipMemGetInfo(free_bytes, total_bytes));
   return GRID_OK;
 }
 

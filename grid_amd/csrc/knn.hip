@@ -1805,31 +1805,53 @@ __global__ __launch_bounds__(256) void k_dist(const T *__restrict__ z, int64_t l
 
 extern "C" {
 
-// Launch k_gram8 (persistent, XCD-paced): the tile table lives in ctx->aux.
+// Launch k_gram8 (persistent, XCD-paced) over the upper-triangle 256x128
+// tiles (I, j >= 2I) with I in [ti0, ti1) -- all of them for the whole Gram,
+// one row range for the cohort split's segments (grid_knn_gram_kb_rows);
+// tile element (row, col) is added into d_gram[row * ldg + col].  The tile
+// lists live in ctx->aux, one per (np, ti0, ti1) in GRID_TILE_SLOTS slots, so
+// launches that alternate between row ranges re-use their uploaded lists
+// instead of re-uploading them (a host sync) every time.
 static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t nsteps, int64_t ld,
-                        int64_t q2, int64_t sps_max, bool blocked, int mode, int64_t *d_gram) {
-  const int nt = (int)(np_ / BM), ni = (int)(np_ / BM3);
+                        int64_t q2, int64_t sps_max, bool blocked, int mode, int64_t *d_gram, int ti0, int ti1,
+                        int64_t ldg) {
+  const int nt = (int)(np_ / BM);
   int nt6 = 0;
-  for (int i = 0; i < ni; i++) nt6 += nt - 2 * i;
-  REQUIRE((size_t)nt6 * 4 <= GRID_AUX_BYTES / 2, "too many Gram tiles (np %lld)", (long long)np_);
-  if (ctx->aux_tiles_n != nt6 || !ctx->aux_tiles_host) {
-    delete[] ctx->aux_tiles_host;
-    ctx->aux_tiles_host = new int32_t[nt6];
-    // tile_blocked6 order, enumerated incrementally (one pass over the groups)
+  for (int i = ti0; i < ti1; i++) nt6 += nt - 2 * i;
+  REQUIRE(nt6 > 0, "empty Gram row range");
+  constexpr size_t SLOT_BYTES = GRID_AUX_BYTES / 2 / GRID_TILE_SLOTS;
+  REQUIRE((size_t)nt6 * 4 <= SLOT_BYTES, "too many Gram tiles (np %lld)", (long long)np_);
+  const int64_t key = (np_ << 24) | ((int64_t)ti0 << 12) | ti1;
+  int slot = -1, lru = 0;
+  for (int s = 0; s < GRID_TILE_SLOTS; s++) {
+    if (ctx->tiles[s].key == key && ctx->tiles[s].n == nt6 && ctx->tiles[s].host) slot = s;
+    if (ctx->tiles[s].used < ctx->tiles[lru].used) lru = s;
+  }
+  if (slot < 0) {
+    slot = lru;
+    GridTileSlot &ts = ctx->tiles[slot];
+    delete[] ts.host;
+    ts.host = new int32_t[nt6];
+    // tile_blocked6 order (groups of GI6 row tiles x GJ6 column tiles),
+    // enumerated incrementally from the range's first row tile
     int t = 0;
-    for (int bi = 0; bi * GI6 < ni; bi++) {
-      const int i0 = bi * GI6, i1 = std::min(ni, i0 + GI6);
+    for (int i0 = ti0; i0 < ti1; i0 += GI6) {
+      const int i1 = std::min(ti1, i0 + GI6);
       for (int bj = (2 * i0) / GJ6; bj * GJ6 < nt; bj++) {
         const int j0 = bj * GJ6, j1 = std::min(nt, j0 + GJ6);
         for (int i = i0; i < i1; i++)
-          for (int j = std::max(j0, 2 * i); j < j1; j++) ctx->aux_tiles_host[t++] = (i << 16) | j;
+          for (int j = std::max(j0, 2 * i); j < j1; j++) ts.host[t++] = (i << 16) | j;
       }
     }
     REQUIRE(t == nt6, "tile enumeration");
-    HIPCHK(hipMemcpyAsync(ctx->aux, ctx->aux_tiles_host, (size_t)nt6 * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync((char *)ctx->aux + slot * SLOT_BYTES, ts.host, (size_t)nt6 * 4, hipMemcpyHostToDevice,
+                          ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
-    ctx->aux_tiles_n = nt6;
+    ts.key = key;
+    ts.n = nt6;
   }
+  ctx->tiles[slot].used = ++ctx->tiles_clock;
+  const int32_t *d_tiles = (const int32_t *)((char *)ctx->aux + slot * SLOT_BYTES);
   unsigned *rounds = (unsigned *)((char *)ctx->aux + GRID_AUX_BYTES / 2);
   HIPCHK(hipMemsetAsync(rounds, 0, (128 + 8 * 16) * 4, ctx->stream));   // round and unit counters
   int per = ctx->ncu >= 8 ? ctx->ncu / 8 : 1;
@@ -1937,7 +1959,7 @@ static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_
       xoff.x[x] = tot;
       tot += ngx > 0 ? ((ngx - 1) * per + lastsz) * bkc : 0;
     }
-    if (mode == 0 && !q16 && part_cap > 0 && tot * (int64_t)(BM3 * BN3 * 4) <= part_cap) {
+    if (mode == 0 && !q16 && part_cap > 0 && ldg == np_ && ti0 == 0 && tot * (int64_t)(BM3 * BN3 * 4) <= part_cap) {
       void *sp = nullptr;
       int rc = grid_scratch(ctx, (size_t)tot * BM3 * BN3 * 4, &sp);
       if (rc) return rc;
@@ -1945,13 +1967,13 @@ static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_
     }
   }
   hipLaunchKernelGGL(kern, dim3((unsigned)(8 * per)), dim3(512), 0, ctx->stream, d_zb, ld,
-                     (const int32_t *)ctx->aux, nt6, (int)bkc, (int)bkx, nsteps, lag, spin, np_,
+                     d_tiles, nt6, (int)bkc, (int)bkx, nsteps, lag, spin, ldg,
                      (unsigned long long *)d_gram, rounds, dyn, d_part, xoff);
   LAUNCHCHK();
   if (d_part) {
     hipLaunchKernelGGL(k_gram_part_reduce, dim3((unsigned)(BM3 * BN3 / 256), (unsigned)nt6), dim3(256), 0,
-                       ctx->stream, d_part, xoff, per, (int)bkc, (int)bkx, nsteps, nt6, (const int32_t *)ctx->aux,
-                       np_, d_gram);
+                       ctx->stream, d_part, xoff, per, (int)bkc, (int)bkx, nsteps, nt6, d_tiles,
+                       ldg, d_gram);
     LAUNCHCHK();
   }
   return GRID_OK;
@@ -1989,7 +2011,7 @@ int grid_knn_gram(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t kpad
   const int variant = gram_variant();
   if (variant >= 21 && np_ % BM3 == 0)
     return launch_gram8(ctx, d_zb, np_, nsteps, ld, q2, sps_max, false, variant == 22 ? 5 : variant == 23 ? 6
-                                                                                : variant == 24 ? 1 : 0, d_gram);
+                        : variant == 24 ? 1 : 0, d_gram, 0, (int)(np_ / BM3), np_);
 #ifdef GRID_PROBES
   if (variant >= 6 && np_ % BM3 == 0) {
     // 256x128 tiles; 4-step fp32 chunks stay exact: 4 * 64 * qmax^2 < 2^24 for qmax <= 256
@@ -2042,7 +2064,29 @@ int grid_knn_gram_kb(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t k
   const int variant = gram_variant();
   const int mode = variant == 22 ? 5 : variant == 23 ? 6 : variant == 24 ? 1 : variant == 25 ? 7
                  : variant == 26 ? 8 : 0;
-  return launch_gram8(ctx, d_zb, np_, kpad / BK, np_ * BK, q2, sps_max, true, mode, d_gram);
+  return launch_gram8(ctx, d_zb, np_, kpad / BK, np_ * BK, q2, sps_max, true, mode, d_gram, 0, (int)(np_ / BM3),
+                      np_);
+}
+
+int grid_knn_gram_kb_rows(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t kpad, int32_t qmax, int64_t row0,
+                          int64_t nrows, int64_t *d_out, int64_t ld) {
+  REQUIRE(ctx && d_zb && d_out, "bad args");
+  REQUIRE(np_ > 0 && np_ % BM3 == 0, "np (%lld) must be a positive multiple of %d", (long long)np_, BM3);
+  REQUIRE(kpad >= 0 && kpad % BK == 0, "kpad must be a multiple of %d", BK);
+  REQUIRE(row0 >= 0 && nrows > 0 && row0 % BM3 == 0 && nrows % BM3 == 0 && row0 + nrows <= np_,
+          "rows [%lld, %lld) must be whole 256-row tiles within np %lld", (long long)row0, (long long)(row0 + nrows),
+          (long long)np_);
+  REQUIRE(ld >= np_ - row0, "ld (%lld) below the segment width %lld", (long long)ld, (long long)(np_ - row0));
+  REQUIRE(((uintptr_t)d_zb % 16) == 0 && ((uintptr_t)d_out % 8) == 0, "misaligned buffers");
+  REQUIRE(qmax >= 0 && qmax <= 256, "qmax must be in [0, 256]");
+  if (kpad == 0) return GRID_OK;
+  const int64_t q2 = (int64_t)(qmax > 0 ? qmax : 1) * (qmax > 0 ? qmax : 1);
+  const int64_t sps_max = ((1ll << 31) - 1) / (q2 * BK);
+  // the kernel adds tile element (row, col) at base + row * ld + col: the
+  // base sits row0 * (ld + 1) elements before d_out (never dereferenced there)
+  int64_t *base = (int64_t *)((uintptr_t)d_out - (uintptr_t)(row0 * (ld + 1)) * sizeof(int64_t));
+  return launch_gram8(ctx, d_zb, np_, kpad / BK, np_ * BK, q2, sps_max, true, 0, base, (int)(row0 / BM3),
+                      (int)((row0 + nrows) / BM3), ld);
 }
 
 int grid_knn_mirror(grid_ctx *ctx, int64_t *d_gram, int64_t np_) {
@@ -2052,6 +2096,17 @@ int grid_knn_mirror(grid_ctx *ctx, int64_t *d_gram, int64_t np_) {
   if (pairs == 0) return GRID_OK;
   REQUIRE(pairs < (1ll << 31), "np too large");
   hipLaunchKernelGGL(k_mirror, dim3((unsigned)pairs), dim3(256), 0, ctx->stream, d_gram, np_);
+  LAUNCHCHK();
+  return GRID_OK;
+}
+
+int grid_knn_mirror_ld(grid_ctx *ctx, int64_t *d, int64_t n, int64_t ld) {
+  REQUIRE(ctx && d && n >= 0 && n % 64 == 0 && ld >= n, "n (%lld) must be a multiple of 64 and <= ld",
+          (long long)n);
+  const int64_t nb = n / 64, pairs = nb * (nb - 1) / 2;
+  if (pairs == 0) return GRID_OK;
+  REQUIRE(pairs < (1ll << 31), "n too large");
+  hipLaunchKernelGGL(k_mirror, dim3((unsigned)pairs), dim3(256), 0, ctx->stream, d, ld);
   LAUNCHCHK();
   return GRID_OK;
 }

@@ -159,6 +159,93 @@ class TorchComm:
         self.dist.reduce_scatter_tensor(out, t.contiguous())
         return out
 
+    def all_gather_into(self, out, t, async_op=False):
+        """out's first world x t.numel() elements = every rank's t in rank order, as
+        raw bytes (int32 words: RCCL has no 16-bit integer type).  Over RCCL
+        with async_op the collective runs on the communicator's stream after
+        the work queued so far on the current one; the returned handle's
+        wait() orders the current stream after it (the cohort split's panel
+        pieces: the next piece moves while the Gram of this one runs)."""
+        import torch
+        src = t.reshape(-1).view(torch.int32)
+        dst = out.reshape(-1).view(torch.int32)[: self.world * src.numel()]
+        if self.host or not t.is_cuda:
+            h = src.cpu() if t.is_cuda else src
+            parts = [torch.empty_like(h) for _ in range(self.world)]
+            self.dist.all_gather(parts, h)
+            dst.copy_(torch.cat(parts).to(dst.device))
+            return None
+        return self.dist.all_gather_into_tensor(dst, src, async_op=async_op)
+
+
+class SimComm:
+    """One rank's share of a W-rank run on ONE GPU (per-rank timing,
+    ``bench.py --sim-world W --sim-rank r``): every collective does the
+    local memory work of the real one -- an all-gather writes W copies of
+    this rank's part, a reduce-scatter copies this rank's block -- without
+    the other ranks, so the step's device time is rank r's compute and local
+    copies; xGMI time is not in it.  ``bytes_in`` counts what the real
+    collectives would bring into this rank (per step when reset per step).
+    The values are not those of a real run (other ranks' parts are this
+    rank's), so results are meaningless; only the work is the same."""
+
+    def __init__(self, world, rank):
+        self.world, self.rank, self.host = world, rank, False
+        self.bytes_in = {}
+
+    def _count(self, kind, nbytes):
+        self.bytes_in[kind] = self.bytes_in.get(kind, 0) + int(nbytes)
+
+    def all_gather(self, t):
+        import torch
+        t = t.contiguous()
+        self._count("all_gather", (self.world - 1) * t.numel() * t.element_size())
+        return torch.stack([t] * self.world)
+
+    def all_reduce_sum(self, t):
+        self._count("all_reduce", 2 * (self.world - 1) / self.world * t.numel() * t.element_size())
+        return t
+
+    def reduce_scatter_sum(self, out, t):
+        t = t.contiguous()
+        self._count("reduce_scatter", (self.world - 1) * out.numel() * out.element_size())
+        out.view(-1).copy_(t.view(self.world, -1)[self.rank])
+        return out
+
+    def all_gather_into(self, out, t, async_op=False):
+        """The W copies; with async_op on a side stream ordered after the work
+        queued so far (as RCCL's stream is), the handle's wait() orders the
+        current stream after them -- so the copies overlap the next Gram as
+        the real collective would."""
+        n = t.numel()
+        self._count("all_gather_panel", (self.world - 1) * n * t.element_size())
+        dst = out.reshape(-1)[: self.world * n].view(self.world, n)
+        if not (async_op and t.is_cuda):
+            dst.copy_(t.reshape(1, n).expand(self.world, n))
+            return None
+        import torch
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream()
+        ev = torch.cuda.Event()
+        ev.record()
+        self._side.wait_event(ev)
+        with torch.cuda.stream(self._side):
+            dst.copy_(t.reshape(1, n).expand(self.world, n))
+        done = torch.cuda.Event()
+        done.record(self._side)
+        return _StreamWait(done)
+
+
+class _StreamWait:
+    """A collective handle: wait() orders the current stream after an event."""
+
+    def __init__(self, ev):
+        self.ev = ev
+
+    def wait(self):
+        import torch
+        torch.cuda.current_stream().wait_event(self.ev)
+
 
 class HipOps:
     """The chain's compute steps as libgridhip.so kernels (include/grid_abi.h)."""
@@ -277,6 +364,14 @@ class HipOps:
     def mirror(self, gram, np_):
         call("grid_knn_mirror", self.ctx, ptr(gram), np_)
 
+    def gram_rows(self, zb, np_, kpad, qmax, row0, nrows, out, ld):
+        """Cohort split: rows [row0, row0+nrows) x columns [row0, np) of the
+        K-blocked panel's Gram, added into out (stride ld, origin (row0, row0))."""
+        call("grid_knn_gram_kb_rows", self.ctx, ptr(zb), np_, kpad, qmax, row0, nrows, ptr(out), ld)
+
+    def mirror_ld(self, buf, n, ld):
+        call("grid_knn_mirror_ld", self.ctx, ptr(buf), n, ld)
+
     def diag(self, gram, np_, n, norms):
         call("grid_knn_diag", self.ctx, ptr(gram), np_, n, ptr(norms))
 
@@ -367,7 +462,7 @@ class Steps47:
 
     def __init__(self, ops, alloc, n, m_total, col0, m_local, *, k=10, n_nbr=300, top_frac=0.1, zmax=2.0,
                  sigma2_max=1000.0, frac_r=1.0, min_nbr=1, n_iters=100, comm=None, phase_lane=None, zq16=True,
-                 chunk=None, keep_z=True, on_z_chunk=None):
+                 chunk=None, keep_z=True, on_z_chunk=None, split="bin", piece_bytes=1 << 31):
         """``phase_lane``: optional (ops, torch.cuda.Stream) pair on which step
         7 runs.  Phasing is one workgroup for ~4 ms, so on its own stream it
         overlaps other work instead of idling the other 255 CUs.  It is
@@ -378,7 +473,19 @@ class Steps47:
         per-rank steps of the multi-GPU runs).  It then overlaps pass i+1's
         top-k / dipCN and pass i+2's statistics and quantisation.  dipCN
         writes alternate buffers; ``finish()`` issues the last pass's phasing
-        (call it before reading ``hap`` / ``imp`` or stopping a clock)."""
+        (call it before reading ``hap`` / ``imp`` or stopping a clock).
+
+        ``split`` (multi-rank runs): how step 5's all-pairs Gram is shared.
+        "bin": every rank sums the whole upper triangle over its own bins and
+        ONE reduce-scatter of int64 segments completes it.  "cohort" (north
+        star's cohort axis, the reference's all-pairs search
+        find_neighbors.py:204-213 with the Gram's rows sharded): step 4 stays
+        bin-sharded (column statistics local and exact), then the quantised
+        bf16 panel moves in pieces of at most ``piece_bytes`` per rank-set by
+        an all-gather overlapped with the Gram of the previous piece, and
+        every rank computes its own two row segments over ALL bins -- no
+        Gram reduce-scatter.  Both give the same segments, bit for bit
+        (integer sums), and share the candidate merge."""
         self.ops, self.A, self.comm = ops, alloc, comm
         # one lane, or two: the phasing of _dips[b] then runs on lane b, so the
         # last two passes' phasings (finish()) overlap instead of queueing
@@ -388,6 +495,9 @@ class Steps47:
         self._ev_phase = {}
         self.rank = comm.rank if comm else 0
         self.world = comm.world if comm else 1
+        if split not in ("bin", "cohort"):
+            raise ValueError(f"split must be 'bin' or 'cohort', not {split!r}")
+        self.split = split if comm is not None else "bin"
         self.n, self.m, self.col0, self.ml = n, m_total, col0, m_local
         assert col0 % BLOCK == 0
         self.k, self.n_nbr, self.top_frac = k, n_nbr, top_frac
@@ -406,6 +516,11 @@ class Steps47:
         self.bsum = a.empty((n1, max(self.nblk_l, 1)), F8)
         self.bcnt = a.empty((n1, max(self.nblk_l, 1)), I4)
         cw = max(b - a_ for a_, b in self.chunks)             # widest chunk
+        # every rank's chunk count and widest chunk (the cohort split's panel
+        # exchange runs the same number of rounds on every rank)
+        rchunks = [chunk_ranges(c1 - c0, chunk) for c0, c1 in widths]
+        self.nch_x = max(len(rc) for rc in rchunks)
+        cw_x = max(max(b - a_ for a_, b in rc) for rc in rchunks)
         if self.nch > 1:
             nbc = -(-cw // BLOCK)
             self.bsum_c, self.bcnt_c = a.empty(n1 * nbc, F8), a.empty(n1 * nbc, I4)
@@ -441,17 +556,22 @@ class Steps47:
             self.esc_idx, self.esc_val = a.empty(cap, I8), a.empty(cap, I4)
         self.np_ = pad_to(n1, 256)
         # multi-GPU step 5 (comm given): the Gram's 2W row blocks of B rows; rank
-        # r reduces only the upper-triangle segments of blocks r and 2W-1-r
-        # (grid_knn_seg_topk), about half of the full rows, equal per rank
+        # r holds only the upper-triangle segments of blocks r and 2W-1-r
+        # (grid_knn_seg_topk), about half of the full rows, equal per rank.  The
+        # cohort split computes them with the Gram kernel's 256-row tiles, so
+        # there B is a multiple of 256
         self.B = -(-self.np_ // (2 * self.world))
+        if self.split == "cohort":
+            self.B = pad_to(self.B, 256)
         self.npw = 2 * self.world * self.B
         self.np_rs = self.npw if comm is not None else self.np_
-        self.kpad = pad_to(cw, 64)
+        self.kpad = pad_to(cw_x if self.split == "cohort" else cw, 64)
         # step-5 input panel (bf16), K-blocked [kpad/32][np][32]: one K-step of a
         # row panel is contiguous for the Gram kernel's DMA
         self.zb = a.empty((self.kpad // _abi.KBW, self.np_, _abi.KBW), U2)
         self.zb.zero_()                                  # pad rows stay zero
-        self.gram = a.empty((self.np_rs, self.np_), I8)   # row stride np; rows >= np stay zero
+        # row stride np; rows >= np stay zero (the cohort split has no whole Gram)
+        self.gram = a.empty((self.np_rs, self.np_), I8) if self.split == "bin" else None
         self.norms = a.empty(self.np_, I8)
         self.norms.zero_()
         kk = max(k, 1)
@@ -461,8 +581,17 @@ class Steps47:
             W, B = self.world, self.B
             self.my_blocks = (self.rank, 2 * W - 1 - self.rank)
             self.seg_len = B * (2 * W + 1) * B                 # int64 cells of one rank's two segments
-            self.seg_send = a.empty(W * self.seg_len, I8)
             self.seg_recv = a.empty(self.seg_len, I8)
+            if self.split == "bin":
+                self.seg_send = a.empty(W * self.seg_len, I8)
+            else:
+                # panel pieces: P K-blocks of every rank (P even: the Gram takes
+                # whole 64-column K-steps), two buffers (gather p+1 || Gram p)
+                per_blk = W * self.np_ * _abi.KBW * 2
+                nkb = max(self.kpad // _abi.KBW, 2)
+                self.piece = max(2, min(nkb, int(piece_bytes // per_blk)) // 2 * 2)
+                self.gbuf = [a.empty((W * self.piece, self.np_, _abi.KBW), U2) for _ in range(2)]
+                self.norms_l = a.empty((2, B), I8)
             K1 = _abi.SEG_K1
             self.rowc_l = a.empty((2, B, K1), I8)               # packed keys (uint64 bits)
             self.colc_l = a.empty((2, self.npw, K1), I8)
@@ -555,7 +684,7 @@ class Steps47:
 
     def _sum_int(self, v):
         import torch
-        t = torch.tensor([v], dtype=torch.int64, device=self.gram.device)
+        t = torch.tensor([v], dtype=torch.int64, device=self.norms.device)
         self.comm.all_reduce_sum(t)
         return int(t.item())
 
@@ -676,13 +805,26 @@ class Steps47:
         self.r_tot = int(h[_abi.SEL_RTOT])
         self.ruse_loc = int(h[_abi.SEL_RUSE])
         sb, kb = self._chunk_bounds(r_loc)
+        if self.split == "cohort":
+            self._cohort_plan(kb)
         self._mark("select_sort")
         # ---- pass D: z (step-4 output) + clipped bf16 panel per chunk, the
-        # exact Gram accumulated over chunks (MFMA) ----
-        self.gram.zero_()
+        # exact Gram accumulated over chunks (MFMA); the cohort split instead
+        # all-gathers each chunk's panel in pieces and adds every piece's
+        # product into this rank's two row segments (the same number of
+        # exchange rounds on every rank: a rank out of chunks sends zeros) ----
+        if self.gram is not None:
+            self.gram.zero_()
+        else:
+            self.seg_recv.zero_()
         self.nesc, self.zq_is16 = 0, self.zq16 is not None
         self.chunk_used = []
-        for ci in order:
+        self._gslot = 0
+        self.exec_flops = 0.0                    # cohort split: MFMA work its Gram launches executed
+        for ci in range(self.nch_x if self.split == "cohort" else self.nch):
+            if ci >= self.nch:
+                self._cohort_gram(ci, 0)
+                continue
             a, b = self.chunks[ci]
             s0, s1 = sb[ci], sb[ci + 1]
             used = kb[ci + 1] - kb[ci]
@@ -699,16 +841,19 @@ class Steps47:
             self.cur = {"ci": ci, "a": a, "b": b, "s0": s0, "s1": s1, "q": qc, "ld": ldc, "sel": sel_c,
                         "colmap": cm_c, "k0": kb[ci], "used": used}
             self._zquant(q, qc, ldc, a, b, s0, s1, sel_c, cm_c)
-            if used == 0 or n == 0:
-                continue
             kpad_c = pad_to(used, 64)
-            if kpad_c > used:
+            if used and n and kpad_c > used:
                 # columns colmap did not write this chunk (all in its last K-block)
                 b0 = used // _abi.KBW
                 if used % _abi.KBW:
                     self.zb[b0, :n, used % _abi.KBW:].zero_()
                     b0 += 1
                 self.zb[b0:kpad_c // _abi.KBW, :n].zero_()
+            if self.split == "cohort":
+                self._cohort_gram(ci, used)
+                continue
+            if used == 0 or n == 0:
+                continue
             if self.gram_evs is not None:
                 import torch
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -722,12 +867,16 @@ class Steps47:
         if not profile:
             self._issue_pending()
         # ---- step 5: full rows (mirror), reduce-scatter by row blocks, top-k ----
-        o.mirror(self.gram, self.np_)
-        o.diag(self.gram, self.np_, n, self.norms)
-        if self.comm is not None:
+        if self.split == "cohort":
+            self._step5_cohort()
+        elif self.comm is not None:
+            o.mirror(self.gram, self.np_)
+            o.diag(self.gram, self.np_, n, self.norms)
             self.comm.all_reduce_sum(self.norms)
             self._step5_segments()
         else:
+            o.mirror(self.gram, self.np_)
+            o.diag(self.gram, self.np_, n, self.norms)
             o.topk_rows(self.gram, self.np_, self.norms, n, self.k, 0, n, self.idx_l, self.d2_l, self.cnt_l)
         idx, self.d2, cnt = self.idx_l, self.d2_l, self.cnt_l
         self._mark("topk")
@@ -810,6 +959,94 @@ class Steps47:
                 off += B * nc
         self.comm.reduce_scatter_sum(self.seg_recv, self.seg_send)
         self._mark("reduce_scatter")
+        self._seg_candidates()
+
+    def _cohort_plan(self, kb):
+        """The cohort split's exchange rounds: per chunk index, the most
+        K-blocks any rank fills (one small all-gather of every rank's used
+        panel columns per chunk; the chunk bounds are known after pass C)."""
+        torch = self.A.torch
+        used = [kb[c + 1] - kb[c] for c in range(self.nch)] + [0] * (self.nch_x - self.nch)
+        g = self.comm.all_gather(torch.tensor(used, dtype=torch.int64, device=self.zb.device)).cpu()
+        g = g.view(self.world, self.nch_x)
+        self.xkb = [pad_to(int(g[:, c].max()), 64) // _abi.KBW for c in range(self.nch_x)]
+        self.ruse_tot = int(g.sum())
+
+    def _cohort_gram(self, ci, used):
+        """Chunk ci's panel across all ranks, piece by piece: the all-gather of
+        piece p+1 is issued before the Gram of piece p, so the two overlap
+        (RCCL runs on its own stream).  K-blocks this rank did not fill in the
+        round's range are zeroed first (exact zeros in the integer sums)."""
+        nkb = self.xkb[ci]
+        if nkb == 0:
+            return
+        own = pad_to(used, 64) // _abi.KBW if used and self.n else 0
+        if own < nkb:
+            self.zb[own:nkb].zero_()
+        pend = None
+        for p0 in range(0, nkb, self.piece):
+            pp = min(self.piece, nkb - p0)
+            buf = self.gbuf[self._gslot]
+            self._gslot ^= 1
+            h = self.comm.all_gather_into(buf, self.zb[p0:p0 + pp], async_op=True)
+            if pend is not None:
+                self._gram_piece(*pend)
+            pend = (buf, pp, h)
+        self._gram_piece(*pend)
+
+    def _gram_piece(self, buf, pp, h):
+        """Both row segments of this rank over one gathered piece: W ranks' pp
+        K-blocks each, a K-blocked panel of W * pp blocks (buf's first ones)."""
+        if h is not None:
+            h.wait()
+        W, B, np_ = self.world, self.B, self.np_
+        if self.gram_evs is not None:
+            import torch
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        off = 0
+        for b in self.my_blocks:
+            nc = (2 * W - b) * B
+            if b * B < np_:
+                nr = min(B, np_ - b * B)
+                self.ops.gram_rows(buf, np_, W * pp * _abi.KBW, self.qmax, b * B, nr,
+                                   self.seg_recv[off:off + B * nc], nc)
+                # MFMA work executed: the range's 256x128 tiles (j >= 2I) over W pp K-blocks
+                ti0, nt = b * B // 256, np_ // 128
+                tiles = sum(nt - 2 * i for i in range(ti0, ti0 + nr // 256))
+                self.exec_flops += 2.0 * tiles * 256 * 128 * W * pp * _abi.KBW
+            off += B * nc
+        if self.gram_evs is not None:
+            ev[1].record()
+            self.gram_evs.append(ev)
+
+    def _step5_cohort(self):
+        """The cohort split's segments are complete on their rank: mirror their
+        diagonal blocks, take the norms G_jj of their rows, all-gather the
+        norms (2B int64 per rank), then the shared candidate path."""
+        o, W, B, np_ = self.ops, self.world, self.B, self.np_
+        self.norms_l.zero_()
+        off = 0
+        for slot, b in enumerate(self.my_blocks):
+            nc = (2 * W - b) * B
+            if b * B < np_:
+                seg, nr = self.seg_recv[off:off + B * nc], min(B, np_ - b * B)
+                o.mirror_ld(seg, nr, nc)
+                o.diag(seg, nc, nr, self.norms_l[slot])
+            off += B * nc
+        torch = self.A.torch
+        ng = self.comm.all_gather(self.norms_l)                 # [W][2][B]
+        sel_q = torch.tensor([q for q, _ in self.blk_src], device=ng.device)
+        sel_s = torch.tensor([s_ for _, s_ in self.blk_src], device=ng.device)
+        self.norms.copy_(ng[sel_q, sel_s].reshape(-1)[:np_])
+        self._mark("gram_rows")
+        self._seg_candidates()
+
+    def _seg_candidates(self):
+        """Row and column candidates of this rank's two (complete) segments,
+        their all-gather, and the exact merge into every row's neighbours."""
+        o, n, W, B, npw = self.ops, self.n, self.world, self.B, self.npw
+        torch = self.A.torch
         off = 0
         for slot, b in enumerate(self.my_blocks):
             nc = (2 * W - b) * B

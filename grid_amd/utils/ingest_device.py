@@ -118,15 +118,21 @@ class _Pageable:
         _libc.madvise(p, self.nbytes, 14)                      # MADV_HUGEPAGE (advice only)
         self.ptr = p
         self.array = np.ctypeslib.as_array((C.c_uint8 * self.nbytes).from_address(self.ptr))
+        # its own reference: at interpreter exit the module's globals may be
+        # gone before this object's __del__ runs
+        self._munmap = _libc.munmap
 
     def free(self):
         if self.ptr:
             self.array = None
-            _libc.munmap(self.ptr, self.nbytes)
+            self._munmap(self.ptr, self.nbytes)
             self.ptr = None
 
     def __del__(self):
-        self.free()
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 def _opts(dev, prefix, window, excluded, keep):
@@ -228,10 +234,13 @@ def _chunks(files, tlen):
     return cfile, cstart, cfirst, tot
 
 
-# The host staging of the device ingest, kept for the process (reused by later
-# ingests): releasing tens of GB of staging the HIP runtime has copied from
-# (page-locked, or pageable pages it has seen) holds the runtime for 0.4-0.8 s,
-# and every HIP call of the step after the ingest waited for it (r04y, r04ac).
+# The host staging of the device ingest, kept between the batches and the
+# ingests of one run: releasing tens of GB of staging the HIP runtime has
+# copied from (page-locked, or pageable pages it has seen) holds the runtime for
+# 0.4-0.8 s, and every HIP call of the step after the ingest waited for it (r04y,
+# r04ac).  release_staging() frees it: at the end of a pipeline run or of a
+# standalone step 4, and when the ingest hands over to the host parser
+# (grid_amd/device.py release_ingest_buffers).
 _STAGING = {}
 
 
@@ -240,6 +249,22 @@ def _staging(name, bound, pinned=False):
     if b is None:
         b = _STAGING[name] = _Pinned(bound, pinned=pinned)
     return b
+
+
+def staging_bytes():
+    return sum(p.b.nbytes for p in _STAGING.values() if p.b is not None)
+
+
+def release_staging():
+    """Free the kept host staging; returns the bytes released."""
+    freed = 0
+    for p in list(_STAGING.values()):
+        if p.b is not None:
+            freed += p.b.nbytes
+            p.b.free()
+            p.b = None
+    _STAGING.clear()
+    return freed
 
 
 class _Async:
@@ -786,10 +811,11 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
         import sys
         print(f"[ingest] batches done (threads joined, copy context closed) at {time.perf_counter() - t_start:.3f} s",
               file=sys.stderr, flush=True)
-    # the staging buffers: GBs of page-locked memory whose release (unpinning)
-    # takes a fraction of a second -- done on a thread of its own, off the step's path
-    # the batches' device buffers stay cached on the context (Device.cached),
-    # the host staging in _STAGING
+    # the batches' device buffers stay cached on the context (Device.cached,
+    # names "ingest_*") and the host staging in _STAGING until
+    # device.release_ingest_buffers() -- the end of the run or of a standalone
+    # step 4 -- since their release holds the HIP runtime for a fraction of a
+    # second; here only this function's references go
     d_ins = d_text = d_in = pipe = None
     if TRACE:
         import sys

@@ -71,6 +71,9 @@ int grid_ctx_set_stream(grid_ctx *ctx, void *hip_stream);
 int grid_ctx_own_stream(grid_ctx *ctx);
 /* Compute units of the context's device (persistent grids, batch sizing). */
 int grid_ctx_cu_count(grid_ctx *ctx, int32_t *n);
+/* hipMemGetInfo of the context's device: free and total HBM bytes (buffer
+ * lifetime checks: the step-4 ingest releases its device buffers). */
+int grid_mem_info(grid_ctx *ctx, size_t *free_bytes, size_t *total_bytes);
 int grid_sync(grid_ctx *ctx);
 int grid_dev_alloc(grid_ctx *ctx, size_t bytes, void **d_ptr);
 int grid_dev_free(grid_ctx *ctx, void *d_ptr);
@@ -308,10 +311,24 @@ int grid_knn_gram(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t kpad
  * layout: one K-step of a row panel is contiguous); np % 256 == 0. */
 int grid_knn_gram_kb(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t kpad, int32_t qmax,
                      int64_t *d_gram);
+/* Cohort split of step 5 (the reference's all-pairs search,
+ * find_neighbors.py:204-213, with the Gram's ROWS sharded over ranks): rows
+ * [row0, row0 + nrows) x columns [row0, np) of G = Zb Zb^T on the K-blocked
+ * panel of grid_knn_gram_kb -- the upper-triangle 256x128 tiles whose rows lie
+ * in the range (row0, nrows multiples of 256) -- ADDED as int64 into
+ * d_out[(i - row0) * ld + (j - row0)], ld >= np - row0.  Called once per
+ * panel piece (the pieces' K ranges are disjoint; integer sums, so any order
+ * is exact).  Entries below the diagonal outside the 256-row diagonal tiles
+ * are not written (grid_knn_mirror_ld completes them). */
+int grid_knn_gram_kb_rows(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t kpad, int32_t qmax,
+                          int64_t row0, int64_t nrows, int64_t *d_out, int64_t ld);
 /* Lower triangle from the upper: every 64x64 block (a, b), a > b, of the
  * [np][np] Gram becomes the transpose of block (b, a), so row i is contiguous
  * (np % 64 == 0).  Idempotent. */
 int grid_knn_mirror(grid_ctx *ctx, int64_t *d_gram, int64_t np_);
+/* The same on the leading n x n block of a row-major buffer of stride ld
+ * (n % 64 == 0, ld >= n): the diagonal block of a cohort-split segment. */
+int grid_knn_mirror_ld(grid_ctx *ctx, int64_t *d, int64_t n, int64_t ld);
 /* d_norms[j] = G_jj (= ||z_j||^2) for j < n. */
 int grid_knn_diag(grid_ctx *ctx, const int64_t *d_gram, int64_t np_, int64_t n, int64_t *d_norms);
 /* Row top-k on complete Gram rows: d_rows[r*ld + j] = G(row0 + r, j) for

@@ -205,14 +205,34 @@ class NumpyOps:
         t = np.arange(np_) // 128
         _np(gram)[:np_, :np_] += np.where(t[:, None] <= t[None, :], g, 0)
 
+    def gram_rows(self, zb, np_, kpad, qmax, row0, nrows, out, ld):
+        """Cohort split (grid_knn_gram_kb_rows): the upper-triangle 256x128
+        tiles of rows [row0, row0+nrows), added at out[(i-row0)*ld + j-row0]."""
+        assert row0 % 256 == 0 and nrows % 256 == 0 and row0 + nrows <= np_ and ld >= np_ - row0
+        zr = _np(zb).reshape(-1)[: (kpad // KBW) * np_ * KBW].reshape(kpad // KBW, np_, KBW)
+        zr = zr.transpose(1, 0, 2).reshape(np_, kpad)
+        z = (zr.view(np.uint16).astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+        g = (z[row0:row0 + nrows] @ z[row0:].T).astype(np.int64)
+        ti = (np.arange(row0, row0 + nrows) // 256)[:, None]
+        tj = (np.arange(row0, np_) // 128)[None, :]
+        o = _np(out).reshape(-1)[: nrows * ld].reshape(nrows, ld)
+        o[:, : np_ - row0] += np.where(tj >= 2 * ti, g, 0)
+
     def mirror(self, gram, np_):
         g = _np(gram)[:np_, :np_]
         b = np.arange(np_) // 64
         low = b[:, None] > b[None, :]
         g[low] = g.T[low]
 
+    def mirror_ld(self, buf, n, ld):
+        g = _np(buf).reshape(-1)[: n * ld].reshape(n, ld)[:, :n]
+        b = np.arange(n) // 64
+        low = b[:, None] > b[None, :]
+        g[low] = g.T[low]
+
     def diag(self, gram, np_, n, norms):
-        _np(norms)[:n] = np.diag(_np(gram)[:n, :n])
+        """norms[j] = gram[j * np_ + j] (np_ = the row stride)."""
+        _np(norms).reshape(-1)[:n] = _np(gram).reshape(-1)[np.arange(n) * (np_ + 1)]
 
     # multi-GPU step 5 (grid_knn_seg_topk / grid_knn_seg_merge): packed keys
     # (d2 << 20 | index) as uint64 bits in int64 buffers, K1 = 16 per list

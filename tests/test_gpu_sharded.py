@@ -36,7 +36,7 @@ def cohort():
     return q, reads, offs, np.array(nbr, dtype=np.int32), np.ones(len(nbr))
 
 
-def run_chain(rank, world, comm, lane):
+def run_chain(rank, world, comm, lane, split="bin", piece_bytes=1 << 31):
     from grid_amd import _abi
     from grid_amd.fused import HipOps, Steps47, TorchAlloc, shard_range
     q, reads, off, nbr, w = cohort()
@@ -54,7 +54,7 @@ def run_chain(rank, world, comm, lane):
             pl.append((HipOps(pdev), ps))
         pl = pl[0] if lane == 1 else pl
     st = Steps47(HipOps(dev), TorchAlloc(0), N, M, c0, c1 - c0, k=K, n_nbr=4, n_iters=ITERS, comm=comm,
-                 phase_lane=pl)
+                 phase_lane=pl, split=split, piece_bytes=piece_bytes)
     st.set_reads(reads)
     st.set_phasing_graph(off, nbr, w)
     st.run(qs, c1 - c0)
@@ -70,11 +70,12 @@ def run_chain(rank, world, comm, lane):
     }
 
 
-def _worker(rank, world, port, out_path):
+def _worker(rank, world, port, out_path, split="bin", piece_bytes=1 << 31):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from grid_amd.fused import TorchComm
-    res = run_chain(rank, world, TorchComm(dist), lane=2 if world % 2 == 0 else 1)
+    res = run_chain(rank, world, TorchComm(dist), lane=2 if world % 2 == 0 else 1, split=split,
+                    piece_bytes=piece_bytes)
     np.savez(f"{out_path}.{rank}.npz", **{k: np.asarray(v) for k, v in res.items()})
     dist.barrier()
     dist.destroy_process_group()
@@ -93,12 +94,29 @@ def single():
     return run_chain(0, 1, None, lane=False)
 
 
-@pytest.mark.parametrize("world", [2, 3, 4, 8])
-def test_gpu_sharded_equals_single(single, world, tmp_path):
+def _run(world, tmp_path, split="bin", piece_bytes=1 << 31):
     port = _free_port()
     out = str(tmp_path / "res")
-    mp.start_processes(_worker, args=(world, port, out), nprocs=world, join=True, start_method="spawn")
-    parts = [dict(np.load(f"{out}.{r}.npz")) for r in range(world)]
+    mp.start_processes(_worker, args=(world, port, out, split, piece_bytes), nprocs=world, join=True,
+                       start_method="spawn")
+    return [dict(np.load(f"{out}.{r}.npz")) for r in range(world)]
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+def test_gpu_sharded_equals_single(single, world, tmp_path):
+    _check(_run(world, tmp_path), single)
+
+
+# the cohort split: np = 512 in 256-row blocks, so at
+# world 2 ranks hold blocks (0, 3), (1, 2), at 4 and 8 ranks >= 1 have padding
+# blocks; small pieces: several all-gathers per pass, a short last piece
+@pytest.mark.parametrize("world,piece", [(2, 1 << 31), (2, 2 * 512 * 64 * 22), (4, 4 * 512 * 64 * 10),
+                                         (8, 1 << 31)])
+def test_gpu_cohort_split_equals_single(single, world, piece, tmp_path):
+    _check(_run(world, tmp_path, split="cohort", piece_bytes=piece), single)
+
+
+def _check(parts, single):
     for key in ("rm", "idx", "d2", "dip", "hap", "imp"):
         for p in parts:
             assert np.array_equal(p[key], single[key], equal_nan=True), key

@@ -43,7 +43,7 @@ def cohort(n=N, m=M):
     return q, reads, offs, np.array(nbr, dtype=np.int32), np.ones(len(nbr))
 
 
-def run_chain(rank, world, comm, chunk=None, source="resident", shape=(N, M)):
+def run_chain(rank, world, comm, chunk=None, source="resident", shape=(N, M), split="bin", piece_bytes=1 << 31):
     from grid_amd.fused import HostSource, Steps47, TorchAlloc, shard_range
     from tests.cpu_ops import NumpyOps
     N, M = shape
@@ -51,7 +51,7 @@ def run_chain(rank, world, comm, chunk=None, source="resident", shape=(N, M)):
     c0, c1 = shard_range(M, rank, world)
     qs = torch.from_numpy(np.ascontiguousarray(q[:, c0:c1]))
     st = Steps47(NumpyOps(), TorchAlloc("cpu"), N, M, c0, c1 - c0, k=K, n_nbr=3, n_iters=ITERS, comm=comm,
-                 chunk=chunk)
+                 chunk=chunk, split=split, piece_bytes=piece_bytes)
     st.set_reads(reads)
     st.set_phasing_graph(off, nbr, w)
     st.run(HostSource(qs.numpy()) if source == "host" else qs, c1 - c0)
@@ -65,12 +65,12 @@ def run_chain(rank, world, comm, chunk=None, source="resident", shape=(N, M)):
     }
 
 
-def _worker(rank, world, port, out_path, chunk, shape=(N, M)):
+def _worker(rank, world, port, out_path, chunk, shape=(N, M), split="bin", piece_bytes=1 << 31):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(1)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from grid_amd.fused import TorchComm
-    res = run_chain(rank, world, TorchComm(dist), chunk=chunk, shape=shape)
+    res = run_chain(rank, world, TorchComm(dist), chunk=chunk, shape=shape, split=split, piece_bytes=piece_bytes)
     np.savez(f"{out_path}.{rank}.npz", **{k: np.asarray(v) for k, v in res.items()})
     dist.barrier()
     dist.destroy_process_group()
@@ -116,10 +116,10 @@ def single_wide():
     return run_chain(0, 1, None, shape=WIDE)
 
 
-def _run_world(world, chunk, shape, tmp_path):
+def _run_world(world, chunk, shape, tmp_path, split="bin", piece_bytes=1 << 31):
     port = _free_port()
     out = str(tmp_path / "res")
-    mp.start_processes(_worker, args=(world, port, out, chunk, shape), nprocs=world, join=True,
+    mp.start_processes(_worker, args=(world, port, out, chunk, shape, split, piece_bytes), nprocs=world, join=True,
                        start_method="spawn")
     return [dict(np.load(f"{out}.{r}.npz")) for r in range(world)]
 
@@ -137,6 +137,21 @@ def test_sharded_world_4_5_8_equals_single(single_wide, world, chunk, tmp_path):
     from grid_amd.fused import shard_range
     assert all(shard_range(WIDE[1], r, world)[1] > shard_range(WIDE[1], r, world)[0] for r in range(world))
     _check_parts(_run_world(world, chunk, WIDE, tmp_path), single_wide)
+
+
+# cohort split: the Gram's rows sharded, the panel
+# all-gathered in pieces.  piece_bytes small enough for several pieces per
+# chunk (odd piece counts, a short last piece) at N = 20 (np 256, 1 block of
+# 256 rows: ranks > 0 hold only padding blocks) and at N = 300 (np 512)
+@pytest.mark.parametrize("world,chunk,piece", [(2, None, 1 << 31), (2, 8192, 40 * 256 * 64), (3, None, 6 * 256 * 64)])
+def test_cohort_split_equals_single(single, world, chunk, piece, tmp_path):
+    _check_parts(_run_world(world, chunk, (N, M), tmp_path, split="cohort", piece_bytes=piece), single)
+
+
+@pytest.mark.parametrize("world,chunk,piece", [(4, None, 4 * 512 * 64 * 30), (8, None, 1 << 31),
+                                               (8, 8192, 8 * 512 * 64 * 50)])
+def test_cohort_split_world_2_4_8_equals_single(single_wide, world, chunk, piece, tmp_path):
+    _check_parts(_run_world(world, chunk, WIDE, tmp_path, split="cohort", piece_bytes=piece), single_wide)
 
 
 def test_wide_single_rank_matches_oracle_neighbours(single_wide):
@@ -170,3 +185,20 @@ def _check_parts(parts, single):
     assert np.array_equal(np.concatenate([p["zq"] for p in parts], axis=1), single["zq"])
     assert sum(int(p["ruse"]) for p in parts) == int(single["ruse"])
     assert all(float(p["scale"]) == single["scale"] for p in parts)
+
+
+@pytest.mark.parametrize("split", ["bin", "cohort"])
+def test_simulated_rank_runs(split):
+    """bench.py --sim-world W --sim-rank r (per-rank timing on one GPU): rank
+    r's share of a W-rank step runs through fused.SimComm, whose collectives
+    do only their local copies, and counts the bytes the real ones would
+    bring in (the results are meaningless by design: other ranks' parts are
+    this rank's)."""
+    from grid_amd.fused import SimComm
+    comm = SimComm(4, 1)
+    res = run_chain(1, 4, comm, shape=WIDE, split=split, piece_bytes=4 * 512 * 64 * 8)
+    assert res["idx"].shape == (WIDE[0], K)
+    kinds = set(comm.bytes_in)
+    assert {"all_gather", "all_reduce"} <= kinds
+    assert ("all_gather_panel" in kinds) == (split == "cohort")
+    assert ("reduce_scatter" in kinds) == (split == "bin")
