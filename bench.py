@@ -224,7 +224,8 @@ def from_files_config2(args, note):
     ph = r["phases_s"]
     stages = {k: round(v, 3) for k, v in ph.items() if k.startswith("step")}
     return {"value": r["samples_per_s_from_files"], "unit": "samples/s", "steps_4_7_s": r["steps_4_7_s"],
-            "samples": 3202, "bins": 3_000_000, "stages_s": stages,
+            "samples": 3202, "bins": 3_000_000, "threads": args.files_threads, "stages_s": stages,
+            "release_ingest_buffers_after_step7_s": ph.get("release_ingest_buffers_after_step7"),
             "cohort_generation_s": round(ph.get("generate_cohort", 0.0), 1), "cohort_bytes": r.get("cohort_bytes"),
             "outputs_bytes": r.get("outputs"), "outputs_xxh3_64": r.get("outputs_xxh3_64"),
             "peak_rss_gb": max(r.get("peak_rss_gb_after", {0: 0}).values()),

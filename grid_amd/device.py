@@ -6,11 +6,46 @@ multi-process launcher.  There is no CPU fallback.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 from ._abi import Device
 
 _dev = {}
+_defer = 0
+
+
+def release_ingest_buffers(*devs):
+    """Free what the device ingest keeps between its batches and ingests: the
+    device input / text buffers cached on the step contexts (get_device) and
+    on ``devs`` (Device.cached, names "ingest_*"), and the host staging
+    (ingest_device._STAGING).  Returns (device bytes, host bytes) released."""
+    from .utils import ingest_device
+    ds = {id(d): d for d in list(_dev.values()) + list(devs) if getattr(d, "ctx", None)}
+    dbytes = sum(d.release_cached("ingest_") for d in ds.values())
+    return dbytes, ingest_device.release_staging()
+
+
+def step4_done():
+    """End of step 4: its ingest buffers go now, unless a pipeline run (or a
+    benchmark) holds them to the end (``deferred_release``) -- their release
+    holds the HIP runtime for a fraction of a second."""
+    if not _defer:
+        release_ingest_buffers()
+
+
+@contextlib.contextmanager
+def deferred_release():
+    """Keep the ingest buffers until the outermost such block ends (the end of
+    ``run_wgs_pipeline``), then release them."""
+    global _defer
+    _defer += 1
+    try:
+        yield
+    finally:
+        _defer -= 1
+        if not _defer:
+            release_ingest_buffers()
 
 
 def get_device(config=None) -> Device:

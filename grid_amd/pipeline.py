@@ -17,6 +17,14 @@ def _oos(console, what):
 
 
 def run_wgs_pipeline(console=False, config=None, **args):
+    from .device import deferred_release
+    # step 4's ingest buffers are kept to the end of the run, then released
+    # (their release holds the HIP runtime for a fraction of a second)
+    with deferred_release():
+        _run(console, config)
+
+
+def _run(console, config):
     if not config:
         raise log(console, "Config file is required for running the WGS pipeline.", style="danger")
     try:

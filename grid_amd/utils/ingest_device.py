@@ -62,6 +62,24 @@ AFTER_HOST_TEXT = None          # test seam: called (dev, d_text, toff, files) o
 # host threads beside the MI355X's 37 GB/s, config-2 ingest (r04y, kept
 # staging): 0.15 9.9 s, 0.2 9.5 s, 0.25 9.1-9.25 s, 0.33 9.3-9.6 s
 HOST_FRAC = float(os.environ.get("GRID_INGEST_HOST_FRAC", "0.25"))
+# the host share is sized from the config's `threads` (the
+# reference defaults to 1 thread, its example config uses 4): the host files
+# take as long as the GPU's when f / (t H) = (1 - f) / G, so f = t H / (G + t H)
+# with H one thread's inflate rate beside the GPU and G the GPU's; 0.25 at 16
+# threads (the r04ae optimum) gives H ~ 0.77 GB/s at G ~ 37 GB/s.  Below one file
+# in 20 the share does not pay for its copies and CRC check: none
+HOST_RATE_PER_THREAD = 0.77e9
+GPU_INFLATE_RATE = 37e9
+# file reads and member tables: a pool of their own, independent of `threads`
+READ_THREADS = int(os.environ.get("GRID_INGEST_READ_THREADS", "8"))
+
+
+def host_frac(threads):
+    """Fraction of a pipelined batch's BGZF files the host threads inflate."""
+    t = max(1, int(threads))
+    f = t * HOST_RATE_PER_THREAD / (GPU_INFLATE_RATE + t * HOST_RATE_PER_THREAD)
+    f = min(f, HOST_FRAC)
+    return f if f >= 0.05 else 0.0
 
 
 class DeviceIngestUnsupported(Exception):
@@ -499,8 +517,10 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
     first = _staging("first", FIRST_BATCH_IN + 512)        # the (small) first batch: K, quickly
     stages = [_staging("text0", STAGE + 512, pinned=True), _staging("text1", STAGE + 512, pinned=True)]
     nthreads = max(1, min(int(threads or 1), 32))
-    pool = ThreadPoolExecutor(nthreads)
-    rpool = ThreadPoolExecutor(1)         # the next batch's read (its files on `pool`)
+    pool = ThreadPoolExecutor(nthreads)   # host inflate (the host share, non-BGZF files)
+    iopool = ThreadPoolExecutor(max(1, READ_THREADS))   # file reads + member tables
+    rpool = ThreadPoolExecutor(1)         # the next batch's read (its files on `iopool`)
+    hfrac = host_frac(nthreads)
     copier = ThreadPoolExecutor(1)        # H2D of CPU-inflated text, on its own stream
     waiter = ThreadPoolExecutor(1)        # notes when the GPU's inflate ends
     hctl = ThreadPoolExecutor(1)          # pipelined batches: the host share's inflate (its files on `pool`)
@@ -528,7 +548,7 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
                 return (0, 0), None
             v = buf[off[k]:off[k] + sizes[f]]
             return _abi.gz_text_size(v), _abi.gz_members(v)
-        info = list(pool.map(one, range(len(fs))))
+        info = list(iopool.map(one, range(len(fs))))
         return buf, off, [i[0] for i in info], [i[1] for i in info]
 
     def inflate(buf, off, fs, caps_, gz, members, toff, d_in, d_text, plan):
@@ -692,10 +712,10 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
                 if pipe is None:
                     pipe = _Async(dev, cdev, opts, K, nK, kidx, ref_nlines, Q)
                 hshare = None
-                if HOST_FRAC > 0 and len(todo) > 1:
+                if hfrac > 0 and len(todo) > 1:
                     # every step-th file to the host threads (they start now, beside the
                     # GPU's work on the previous batch and this batch's copies)
-                    step = max(2, int(round(1.0 / HOST_FRAC)))
+                    step = max(2, int(round(1.0 / hfrac)))
                     hfiles = todo[step - 1::step]
                     so, pos = {}, 0
                     for k in hfiles:
@@ -738,9 +758,13 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
             call("grid_md_count", dev.ctx, d_text.ptr, d_toff.ptr, d_tl.ptr, nch, d_cfile.ptr, d_cstart.ptr,
                  d_cfirst.ptr, len(okb), cnl.ptr, cline0.ptr, bflags.ptr, None)
             if K is None:
-                # the reference key list: the first file that inflated with text
-                r = okb[0]
-                c0, c1 = int(cfirst[0]), int(cfirst[1])
+                # the reference key list: the first batch's file with the most
+                # text (a short or truncated file sorted first
+                # no longer sends the cohort to the host parser; K must hold
+                # every later file's keys, which the largest file does)
+                ri = int(np.argmax(tlen[okb]))
+                r = okb[ri]
+                c0, c1 = int(cfirst[ri]), int(cfirst[ri + 1])
                 rc_file = np.zeros(c1 - c0, np.int32) + r
                 cl = cline0.numpy()[c0:c1]
                 nl = cnl.numpy()[c0:c1]
@@ -802,6 +826,7 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
         if pipe is not None:
             pipe.close()
         rpool.shutdown(wait=True)
+        iopool.shutdown(wait=True)
         pool.shutdown(wait=True)
         copier.shutdown(wait=True)
         waiter.shutdown(wait=True)

@@ -19,7 +19,7 @@ from pathlib import Path
 import numpy as np
 
 from .. import _abi, engine
-from ..device import get_device
+from ..device import get_device, release_ingest_buffers, step4_done
 from . import handoff, ingest_device
 from .mosdepth import remove_intermediate_files
 from .utils import get_samples, log, progress_bar, setup_output_file
@@ -317,11 +317,13 @@ def ingest(individuals, mosdepth_dir, chromosome, start, end, excluded, min_dept
         except ingest_device.DeviceIngestUnsupported as e:
             msg = f"device mosdepth parser: {e}; using the host parser"
             log(console, msg, style="warning") if console else print(msg)
+            release_ingest_buffers(dev)        # the host parser and step 4 get the HBM back
         except _abi.GridNativeError as e:
             # e.g. the device buffers do not fit (a smaller GPU, ranks sharing
-            # one): the device path's buffers are released with its frame
+            # one): what the device path allocated and cached goes now
             msg = f"device mosdepth ingest failed ({e}); using the host parser"
             log(console, msg, style="warning") if console else print(msg)
+            release_ingest_buffers(dev)
     if ints:
         try:
             return ingest_native(individuals, mosdepth_dir, chromosome, start, end, excluded, min_depth,
@@ -522,6 +524,7 @@ def normalize_mosdepth(config, console):
         ratios = np.where(sel_means > 0, 100.0 * sel_vars / sel_means, np.nan)
     handoff.publish(output_path, ids, engine.round_decimals(dev, raw, 2), engine.round_decimals(dev, ratios, 3),
                     zq, (n, r))
+    step4_done()            # the ingest's cached buffers (kept to the end of a pipeline run)
     log(console, f"Mosdepth normalization complete. Results written to {output_path}", style="success")
     if remove_intermediate:
         remove_intermediate_files(mosdepth_dir, console, include_region_bed_gz=True)

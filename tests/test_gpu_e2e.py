@@ -140,3 +140,35 @@ def test_step5_handoff_and_reparse_agree(tmp_path):
     os.utime(norm, ns=(st.st_atime_ns, st.st_mtime_ns + 1_000_000_000))
     find_neighbors(c, None)                                   # stale entry: parse the file
     assert _content(os.path.join(out, nb)) == _content(os.path.join(exp, nb))
+
+
+def test_step4_releases_the_ingest_buffers(tmp_path):
+    """a standalone step 4 returns the device ingest's
+    cached input / text buffers and its host staging; HBM in use afterwards
+    (hipMemGetInfo through the ABI) is the pre-step level plus at most the
+    hand-off matrix step 5 takes (n x r int32) and allocator slack.  Inside a
+    pipeline run (deferred_release) they are kept to the end of the run."""
+    import gc
+
+    from grid_amd.device import deferred_release, get_device
+    from grid_amd.utils import handoff, ingest_device
+    from grid_amd.utils.normalize_mosdepth import normalize_mosdepth
+    c, _ = _stage("g1b", tmp_path, device_ingest=True)
+    dev = get_device(c)
+    handoff.clear()
+    gc.collect()
+    dev.sync()
+    free0, _ = dev.mem_info()
+    normalize_mosdepth(c, None)
+    gc.collect()
+    dev.sync()
+    free1, _ = dev.mem_info()
+    assert dev.cached_bytes() == 0 and ingest_device.staging_bytes() == 0
+    ent = next(iter(handoff._entries.values()))
+    n, r = ent[-1]
+    assert free0 - free1 <= n * r * 4 + (64 << 20), (free0, free1, n, r)
+    with deferred_release():
+        normalize_mosdepth(c, None)
+        assert dev.cached_bytes() > 0              # kept to the end of the run
+    assert dev.cached_bytes() == 0 and ingest_device.staging_bytes() == 0
+    handoff.clear()

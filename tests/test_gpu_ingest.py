@@ -58,10 +58,11 @@ def split(request, monkeypatch):
 
 def _dev_vs_host(dev, d, samples, chrom=None, start=None, end=None, excluded=None, lo=20, hi=100):
     # the file order is the caller's sample order, not the directory's glob
-    # order: the device path takes the first file that inflates as its key
+    # order: the device path takes the first batch's largest file as its key
     # list, and a later file with a key outside it hands the cohort to the host
-    # parser (test_subset_reference_file_hands_over) -- the r03af failure was
-    # exactly that, a shorter file first in one box's directory order
+    # parser (test_short_file_first_stays_on_the_device) -- the r03af failure was
+    # a shorter file first in one box's directory order, when the first file
+    # that inflated was the key list
     m = nm.map_mosdepth_files_to_samples(d, samples)
     inds = {s: m[s] for s in samples if s in m}
     ex = excluded or {}
@@ -136,28 +137,46 @@ def test_subsets_bgzf_empty_corrupt_and_zero_depth(dev, tmp_path, split, monkeyp
     assert len(a[0]) == 8
 
 
-def test_subset_reference_file_hands_over(dev, tmp_path):
-    """The cause of the r03af failure, shown deterministically: when the first
-    file that inflates (the device path's key list K) holds only a subset of
-    the bins, a later file's record has a key outside K, and the device path
-    hands the cohort over (DeviceIngestUnsupported); ingest() then returns the
-    host parser's result.  Which file is first follows the directory's glob
-    order (map_mosdepth_files_to_samples, reference normalize_mosdepth.py:162),
-    so the earlier test met this case only on some boxes."""
+def test_short_file_first_stays_on_the_device(dev, tmp_path):
+    """The r03af case: a file holding only a subset of the
+    bins, or a truncated file, sorted first.  The device path's key list K is
+    the first batch's LARGEST file, so the cohort stays on the device and
+    equals the host parser's matrix (the earlier rule -- the first file that
+    inflated -- handed the whole cohort to the ~5x slower host parser).  Which
+    file is first follows the directory's glob order
+    (map_mosdepth_files_to_samples, reference normalize_mosdepth.py:162)."""
     rng = np.random.default_rng(2)
     base = _rand_lines(rng, 3000)
     files = {"A_short": base[:2500], "B_full": base, "C_full": list(base)}
     d = _cohort(tmp_path, files, members=1)
+    good = (d / "B_full.regions.bed.gz").read_bytes()
+    (d / "A_trunc.regions.bed.gz").write_bytes(good[: len(good) // 3])      # truncated: dropped
+    for order in (["A_short", "B_full", "C_full"], ["A_trunc", "A_short", "B_full", "C_full"],
+                  ["B_full", "A_short", "C_full"]):
+        a = _dev_vs_host(dev, d, order)
+        assert "A_short" in a[0] and "A_trunc" not in a[0]
+
+
+def test_no_file_of_the_first_batch_holds_every_key_hands_over(dev, tmp_path):
+    """When even the first batch's largest file lacks a key another file has,
+    that file's record falls outside K and the device path hands the cohort
+    over (DeviceIngestUnsupported); ingest() then returns the host parser's
+    result, and the device ingest's cached buffers and staging are released."""
+    from grid_amd.device import release_ingest_buffers
+    rng = np.random.default_rng(4)
+    base = _rand_lines(rng, 3000)
+    files = {"A_head": base[:2500], "B_tail": base[400:]}       # B larger; A holds keys B lacks
+    d = _cohort(tmp_path, files, members=1)
     m = nm.map_mosdepth_files_to_samples(d, list(files))
-    inds = {k: m[k] for k in ("A_short", "B_full", "C_full")}
+    inds = {k: m[k] for k in files}
     with pytest.raises(ingest_device.DeviceIngestUnsupported, match="a key outside K"):
         nm._ingest_dev(dev, inds, d, None, None, None, {}, 20, 100, 2)
+    release_ingest_buffers(dev)
     got = nm.ingest(inds, d, None, None, None, {}, 20, 100, 2, dev=dev)
     exp = nm.ingest_native(inds, d, None, None, None, {}, 20, 100, 2)
     assert got[0] == exp[0] and got[1] == exp[1]
     assert np.array_equal(np.asarray(got[2]), np.asarray(exp[2]))
-    # the full file first: the device path itself
-    _dev_vs_host(dev, d, ["B_full", "A_short", "C_full"])
+    assert dev.cached_bytes() == 0 and ingest_device.staging_bytes() == 0
 
 
 def test_outside_the_common_case_hands_over(dev, tmp_path):
@@ -169,7 +188,8 @@ def test_outside_the_common_case_hands_over(dev, tmp_path):
     cases = {
         "unsorted": ([base[5]] + base[:5] + base[6:], base),
         "dup": (base, base[:100] + [base[50]] + base[100:]),
-        "extra_key": (base[:-1], base),
+        # each file holds a key the other lacks: outside K whichever is larger
+        "extra_key": (base[:-2] + [base[-1]], base[:-1]),
         "exotic": (base, base[:10] + ["chr1\t9999000\t9999100\t3e1\n"] + base[10:]),
     }
     for name, (la, lb) in cases.items():
@@ -177,7 +197,7 @@ def test_outside_the_common_case_hands_over(dev, tmp_path):
         root.mkdir()
         d = _cohort(root, {"A": la, "B": lb})
         m = nm.map_mosdepth_files_to_samples(d, ["A", "B"])
-        inds = {k: m[k] for k in ("A", "B")}          # A first: A's keys are the key list K
+        inds = {k: m[k] for k in ("A", "B")}
         with pytest.raises(ingest_device.DeviceIngestUnsupported):
             nm._ingest_dev(dev, inds, d, None, None, None, {}, 20, 100, 2)
         got = nm.ingest(inds, d, None, None, None, {}, 20, 100, 2, dev=dev)
@@ -264,7 +284,7 @@ def test_pipelined_batches_equal_the_host_parser(dev, tmp_path, monkeypatch, hos
     that fails to inflate is dropped like a GPU one)."""
     # batches of a few files (one file each when host_frac is 0: many batches)
     monkeypatch.setattr(ingest_device, "BATCH_IN", (120 if host_frac else 40) << 10)
-    monkeypatch.setattr(ingest_device, "HOST_FRAC", host_frac)
+    monkeypatch.setattr(ingest_device, "host_frac", lambda threads: host_frac)
     rng = np.random.default_rng(21)
     base = _rand_lines(rng, 3000)
     files = {}
@@ -308,7 +328,7 @@ def test_pipelined_host_share_guard(dev, tmp_path, monkeypatch):
     the device path hands the cohort over (DeviceIngestUnsupported); clean, the
     same cohort gives the host parser's result on the device path."""
     monkeypatch.setattr(ingest_device, "BATCH_IN", 120 << 10)
-    monkeypatch.setattr(ingest_device, "HOST_FRAC", 0.5)
+    monkeypatch.setattr(ingest_device, "host_frac", lambda threads: 0.5)
     rng = np.random.default_rng(23)
     base = _rand_lines(rng, 3000)
     d = tmp_path / "md"
