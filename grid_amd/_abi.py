@@ -181,14 +181,21 @@ def load():
         raise GridNativeError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
                               "or `make -C grid_amd/csrc`")
     lib = C.CDLL(str(LIB_PATH), mode=C.RTLD_GLOBAL)
-    for name, args in _SIGS.items():
-        f = getattr(lib, name)
-        f.argtypes = args
-        f.restype = C.c_int
-    lib.grid_last_error.argtypes = []
-    lib.grid_last_error.restype = C.c_char_p
-    info = _build_info(lib)
-    want = source_sha256()
+    try:
+        for name, args in _SIGS.items():
+            f = getattr(lib, name)
+            f.argtypes = args
+            f.restype = C.c_int
+        lib.grid_last_error.argtypes = []
+        lib.grid_last_error.restype = C.c_char_p
+        info = _build_info(lib)
+    except AttributeError as e:
+        raise GridNativeError(f"{LIB_PATH} lacks an entry point this package binds ({e}): rebuild with "
+                              "`make -C grid_amd/csrc`") from None
+    # the file list the library hashed (its build info), so the two sides
+    # cannot drift apart when a source is added to the Makefile
+    files = info.get("src_files")
+    want = source_sha256(files.split() if files else None)
     if want is not None and info.get("src_sha256") != want:
         raise GridNativeError(f"{LIB_PATH} was built from other sources (library {info.get('src_sha256')}, "
                               f"tree {want}): rebuild with `make -C grid_amd/csrc`")
@@ -203,11 +210,16 @@ _HASHED = sorted(["core.hip", "normalize.hip", "knn.hip", "dipcn_phase.hip", "sy
                   "common.hpp", "synth_model.hpp", "inflate_core.hpp", "fastgz.hpp"])
 
 
-def source_sha256():
-    """sha256 of the native sources as the Makefile hashes them (None when the
-    tree holds no sources, e.g. an installed copy)."""
+def source_sha256(names=None):
+    """sha256 of the native sources as the Makefile hashes them: ``names``
+    relative to grid_amd/csrc in the Makefile's order (the library's build
+    info carries them), else the list below (None when the tree holds no
+    sources, e.g. an installed copy)."""
     import hashlib
-    files = [_CSRC / f for f in _HASHED] + [_HERE.parent / "include" / "grid_abi.h"]
+    if names is not None:
+        files = [_CSRC / f for f in names]
+    else:
+        files = [_CSRC / f for f in _HASHED] + [_HERE.parent / "include" / "grid_abi.h"]
     if not all(f.exists() for f in files):
         return None
     h = hashlib.sha256()

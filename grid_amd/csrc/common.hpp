@@ -42,8 +42,12 @@ struct grid_ctx {
   // buffers a call keeps on the context for the next one (the device writer's
   // GBs of device and page-locked memory: their release at the end of a call
   // held the runtime for a fraction of a second); freed by grid_ctx_destroy
+  // keep_tag names the owner (the address of a tag object of the call that
+  // stored it): a call finding another owner's buffers frees them first, so
+  // no call ever casts the slot to the wrong type
   void *keep = nullptr;
   void (*keep_free)(void *) = nullptr;
+  const void *keep_tag = nullptr;
 };
 // K-blocked bf16 panel of the k-NN Gram: [kpad / KBW][np][KBW] (a 16-row
 // half K-step of k_gram8's ring is then 1 KiB contiguous: whole 128-B lines)

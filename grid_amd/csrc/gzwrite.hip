@@ -775,10 +775,17 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
   crc_tables(crctab.data());
   const X2N x2n = make_x2n();
   const CrcOps cops = make_crc_ops(x2n);
-  // the buffers stay on the context for the next call (grid_ctx::keep)
+  // the buffers stay on the context for the next call (grid_ctx::keep, owned
+  // by this writer: another owner's object in the slot is freed first)
+  static const char kWriterTag = 0;
+  if (ctx->keep && ctx->keep_tag != &kWriterTag) {
+    if (ctx->keep_free) ctx->keep_free(ctx->keep);
+    ctx->keep = nullptr;
+  }
   if (!ctx->keep) {
     ctx->keep = new WriterBufs;
     ctx->keep_free = [](void *p) { delete static_cast<WriterBufs *>(p); };
+    ctx->keep_tag = &kWriterTag;
   }
   WriterBufs &wbuf = *static_cast<WriterBufs *>(ctx->keep);
   auto &d_blen = wbuf.d_blen, &d_boff = wbuf.d_boff, &d_rowoff = wbuf.d_rowoff, &d_prelen = wbuf.d_prelen,

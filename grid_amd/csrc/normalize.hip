@@ -691,8 +691,13 @@ __device__ __forceinline__ void unpack_raw(const uint32_t (&w)[CUN], int32_t (&v
 
 // PF: software-pipelined row groups (the next group's loads issued before
 // this group is summed; the summation order is unchanged).
-template <int VW, bool S16, int CUN = CU, bool NTL = false, bool PF = false>
-__global__ __launch_bounds__(256) void k_col_means(const int32_t *__restrict__ q, Q16 s16, int64_t n, int64_t m,
+// WPE: waves per SIMD the register budget is held to.  A thread walks all n
+// rows of its columns, so a launch runs in ROUNDS of resident waves: the
+// compact pipelined kernel took 68 VGPRs (7 waves per SIMD, 7,168 on the chip),
+// and config 2's 23,438 waves ran 3.27 rounds -- a fourth round a quarter full;
+// at 61 VGPRs (8 per SIMD, no spill) they run 2.86, i.e. 3 rounds.
+template <int VW, bool S16, int CUN = CU, bool NTL = false, bool PF = false, int WPE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_col_means(const int32_t *__restrict__ q, Q16 s16, int64_t n, int64_t m,
                                                    int64_t ld, const double *__restrict__ rm,
                                                    const double *__restrict__ rinv, const uint8_t *__restrict__ rbad,
                                                    double *__restrict__ mu) {
@@ -790,8 +795,8 @@ __global__ __launch_bounds__(256) void k_col_means(const int32_t *__restrict__ q
   for (int c = 0; c < VW; c++) mu[j0 + c] = acc[c] / (double)cnt[c];   // 0/0 -> NaN (numpy)
 }
 
-template <int VW, bool S16, int CUN = CU, bool NTL = false, bool PF = false>
-__global__ __launch_bounds__(256) void k_col_vars(const int32_t *__restrict__ q, Q16 s16, int64_t n, int64_t m,
+template <int VW, bool S16, int CUN = CU, bool NTL = false, bool PF = false, int WPE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_col_vars(const int32_t *__restrict__ q, Q16 s16, int64_t n, int64_t m,
                                                   int64_t ld, const double *__restrict__ rm,
                                                   const double *__restrict__ rinv, const uint8_t *__restrict__ rbad,
                                                   const double *__restrict__ mu, double *__restrict__ var,
@@ -2275,7 +2280,7 @@ static int col_stats_impl(grid_ctx *ctx, bool vars, const int32_t *d_q, const Q1
   const dim3 grid((unsigned)ceil_div(ceil_div(m, vw), 256));
   if (!vars) {
     auto kern = s16.q ? (vw == 8 ? (nt ? k_col_means<8, true, CU, true> : k_col_means<8, true>) : vw == 4 ? k_col_means<4, true>
-                         : vw == 2 ? (pf ? (cu16 ? k_col_means<2, true, 16, true, true> : k_col_means<2, true, CU, true, true>)
+                         : vw == 2 ? (pf ? (cu16 ? k_col_means<2, true, 16, true, true> : k_col_means<2, true, CU, true, true, 8>)
                                       : cu16 ? k_col_means<2, true, 16, true>
                                       : nt ? k_col_means<2, true, CU, true> : k_col_means<2, true>)
                                    : pf ? (cu16 ? k_col_means<1, true, 16, true, true> : k_col_means<1, true, CU, true, true>)
@@ -2285,7 +2290,7 @@ static int col_stats_impl(grid_ctx *ctx, bool vars, const int32_t *d_q, const Q1
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, ctx->stream, d_q, s16, n, m, ld, d_rm, rinv, rbad, d_out);
   } else {
     auto kern = s16.q ? (vw == 8 ? (nt ? k_col_vars<8, true, CU, true> : k_col_vars<8, true>) : vw == 4 ? k_col_vars<4, true>
-                         : vw == 2 ? (pf ? (cu16 ? k_col_vars<2, true, 16, true, true> : k_col_vars<2, true, CU, true, true>)
+                         : vw == 2 ? (pf ? (cu16 ? k_col_vars<2, true, 16, true, true> : k_col_vars<2, true, CU, true, true, 8>)
                                       : cu16 ? k_col_vars<2, true, 16, true>
                                       : nt ? k_col_vars<2, true, CU, true> : k_col_vars<2, true>)
                                    : pf ? (cu16 ? k_col_vars<1, true, 16, true, true> : k_col_vars<1, true, CU, true, true>)

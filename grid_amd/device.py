@@ -26,12 +26,19 @@ def release_ingest_buffers(*devs):
     return dbytes, ingest_device.release_staging()
 
 
-def step4_done():
+def step4_done(dev=None):
     """End of step 4: its ingest buffers go now, unless a pipeline run (or a
     benchmark) holds them to the end (``deferred_release``) -- their release
-    holds the HIP runtime for a fraction of a second."""
+    holds the HIP runtime for a fraction of a second -- and even
+    then when less than a quarter of the device's HBM is free (a smaller GPU:
+    step 5's Gram needs it more than the next run needs the buffers)."""
     if not _defer:
-        release_ingest_buffers()
+        release_ingest_buffers(*([dev] if dev is not None else []))
+        return
+    if dev is not None:
+        free, total = dev.mem_info()
+        if free < total // 4:
+            release_ingest_buffers(dev)
 
 
 @contextlib.contextmanager

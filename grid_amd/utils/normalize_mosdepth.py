@@ -524,7 +524,7 @@ def normalize_mosdepth(config, console):
         ratios = np.where(sel_means > 0, 100.0 * sel_vars / sel_means, np.nan)
     handoff.publish(output_path, ids, engine.round_decimals(dev, raw, 2), engine.round_decimals(dev, ratios, 3),
                     zq, (n, r))
-    step4_done()            # the ingest's cached buffers (kept to the end of a pipeline run)
+    step4_done(dev)         # the ingest's cached buffers (kept to the end of a pipeline run)
     log(console, f"Mosdepth normalization complete. Results written to {output_path}", style="success")
     if remove_intermediate:
         remove_intermediate_files(mosdepth_dir, console, include_region_bed_gz=True)

@@ -512,7 +512,9 @@ int grid_write_normalized_gz(const char *path, int64_t n, int64_t r, const char 
  * header member (level) on the host; only compressed bytes cross PCIe.
  * batch_bytes: text formatted per device batch (<= 0: 2 GiB).  Same member
  * layout and 'GR' index as grid_write_normalized_gz; the decompressed text is
- * identical. */
+ * identical.  Its device and page-locked buffers stay on ctx between calls
+ * (freed by grid_ctx_destroy), so the writer is not re-entrant per context:
+ * one call at a time on a given ctx (contexts are per thread anyway). */
 int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int64_t r, const char *ids_nl,
                                  const double *raw, const double *sel_means, const double *sel_ratios,
                                  const int32_t *d_zq, int64_t ld_zq, int32_t level, int32_t threads,

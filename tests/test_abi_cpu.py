@@ -124,8 +124,12 @@ def test_library_provenance_matches_the_tree(monkeypatch):
     from grid_amd import _abi
     info = _abi.build_info()
     assert info["src_sha256"] == _abi.source_sha256()
+    # the library names the files it hashed: the loader hashes those
+    names = info["src_files"].split()
+    assert info["src_sha256"] == _abi.source_sha256(names)
+    assert sorted(n for n in names if not n.startswith("..")) == _abi._HASHED
     assert info["arch"] == "gfx950" and info["built_utc"]
     monkeypatch.setattr(_abi, "_lib", None)
-    monkeypatch.setattr(_abi, "source_sha256", lambda: "0" * 64)
+    monkeypatch.setattr(_abi, "source_sha256", lambda names=None: "0" * 64)
     with pytest.raises(_abi.GridNativeError, match="other sources"):
         _abi.load()

@@ -304,7 +304,15 @@ def test_pipelined_batches_equal_the_host_parser(dev, tmp_path, monkeypatch, hos
     (d / "X002.regions.bed.gz").write_bytes(good[: len(good) // 2])     # truncated: dropped
     (d / "X003.regions.bed.gz").write_bytes(b"")                        # empty: no lines
     (d / "X004.regions.bed.gz").write_bytes(b"not gzip")                # dropped
-    samples = sorted(files)[:3] + ["X001", "X002"] + sorted(files)[3:] + ["X003", "X004"]
+    # a BGZF member whose ISIZE understates its text (it inflates past it,
+    # GZ_ESPACE): a corrupt member, dropped on every path, as the
+    # host parser drops it (the reference's gzip raises on the length check)
+    bz = bytearray(_bgzf("".join(files["S005"]).encode()))
+    end = int.from_bytes(bz[16:18], "little") + 1                       # BSIZE + 1: the first member's end
+    isz = int.from_bytes(bz[end - 4:end], "little")
+    bz[end - 4:end] = (isz - 1).to_bytes(4, "little")
+    (d / "X005.regions.bed.gz").write_bytes(bytes(bz))
+    samples = sorted(files)[:3] + ["X001", "X002"] + sorted(files)[3:] + ["X003", "X004", "X005"]
     calls = []
     orig = ingest_device._Async.batch
 
