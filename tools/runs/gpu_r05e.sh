@@ -29,3 +29,6 @@ for sh in bin cohort; do
     || { tail -n 30 $O/sim_cfg3_$sh.err; exit 1; }
   python -c "import json;d=json.load(open('$O/sim_cfg3_w8_r0_$sh.json'));print('cfg3 $sh', d['ms_per_step'], d['stages_ms'], d['roofline']['gram_ms'], d.get('sim_collective_bytes_in_per_step'))"
 done
+# zquant7 store-shape microbenchmark (tools/micro/zqstore.hip, built on the CPU side)
+timeout -k 10 120 tools/micro/zqstore > $O/zqstore.jsonl 2>&1 || { cat $O/zqstore.jsonl; exit 1; }
+cat $O/zqstore.jsonl
