@@ -20,6 +20,23 @@ def _np(t):
     return t.numpy()
 
 
+def _hundredths(z):
+    """f"{v:.2f}" of every cell as int64 hundredths (NaN -> MISSING, a
+    negative value printing as "-0.00" -> NEG0).  rint(v * 100) is the
+    correctly rounded decimal unless the exact product lies within an ulp of a
+    half (|v * 100| < 2^31 here, an ulp < 2^-21): those cells -- and only
+    those -- are printed by Python's formatter."""
+    with np.errstate(invalid="ignore"):
+        t = z * 100.0
+        k = np.rint(t)
+        near = np.abs(np.abs(t - np.trunc(t)) - 0.5) < 1e-6
+    out = np.where(np.isnan(z), MISSING, k).astype(np.int64)
+    for i, s in zip(*np.nonzero(near & ~np.isnan(z))):
+        out[i, s] = int(f"{z[i, s]:.2f}".replace(".", ""))
+    out[(out == 0) & np.signbit(z) & ~np.isnan(z)] = NEG0
+    return out
+
+
 class NumpyOps:
     @staticmethod
     def _mat(q, n, m, ld):
@@ -174,16 +191,7 @@ class NumpyOps:
         with np.errstate(all="ignore"):
             y = np.where(qa == MISSING, np.nan, (qa / 100.0) / np.where(rr == 0, np.nan, rr)[:, None])
             z = ((y - mj[None, :]) / np.sqrt(mj)[None, :]) * scale
-        out = np.empty((n, r), dtype=np.int64)
-        for i in range(n):
-            for s in range(r):
-                v = z[i, s]
-                if np.isnan(v):
-                    out[i, s] = MISSING
-                else:
-                    t = f"{v:.2f}"
-                    k = int(t.replace(".", ""))
-                    out[i, s] = NEG0 if (k == 0 and t.startswith("-")) else k
+        out = _hundredths(z)
         zqa = _np(zq).reshape(-1)                # row stride ld_zq (flat views allowed)
         zqa[(np.arange(n)[:, None] * ld_zq + np.arange(r)[None, :]).reshape(-1)] = out.reshape(-1)
         cm = _np(colmap)[:r]
