@@ -612,6 +612,20 @@ def main():
             out["cpu_baseline"]["sweep"] = sweep
     if rank == 0 and world == 1 and not args.no_files_config2 and (n, m) == (3202, 3_000_000):
         out["from_files_config2"] = from_files_config2(args, note)
+    if rank == 0 and "cpu_baseline" in out:
+        # which CPU number each ratio divides by (say it on the line)
+        cb = out["cpu_baseline"]
+        sp = {"device_chain_vs_math_slice": out["value"] / cb["value"],
+              "basis_device_chain_vs_math_slice": "value (device chain, inputs in HBM) / cpu_baseline.value (the "
+                                                  "oracle's math on a bounded slice of the same cohort, scaled)"}
+        sw, ff = cb.get("sweep"), out.get("from_files_config2", {})
+        if sw and ff.get("value"):
+            sp["from_files_vs_reference_from_files"] = ff["value"] / sw["config2_samples_per_s"]
+            sp["basis_from_files_vs_reference_from_files"] = (
+                "from_files_config2.value (grid wgs steps 4-7 from mosdepth files, every output written) / "
+                "cpu_baseline.sweep.config2_samples_per_s (the oracle from files, per-stage fits of the measured sweep "
+                "extrapolated to config 2)")
+        out["speedup_vs_cpu_baseline"] = sp
     if rank == 0:
         out["build"] = _abi.build_info()          # the library's source sha256 = this tree's (checked at load)
         print(json.dumps(out), file=result_out, flush=True)
