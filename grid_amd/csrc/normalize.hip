@@ -696,7 +696,11 @@ __device__ __forceinline__ void unpack_raw(const uint32_t (&w)[CUN], int32_t (&v
 // compact pipelined kernel took 68 VGPRs (7 waves per SIMD, 7,168 on the chip),
 // and config 2's 23,438 waves ran 3.27 rounds -- a fourth round a quarter full;
 // at 61 VGPRs (8 per SIMD, no spill) they run 2.86, i.e. 3 rounds.
-template <int VW, bool S16, int CUN = CU, bool NTL = false, bool PF = false, int WPE = 1>
+// PFD (compact pipelined path): row groups in flight ahead of the one being
+// summed -- 1 by default; a launch of less than one round of resident waves
+// (the per-rank shards of a multi-GPU run: 2,930 waves at 3,202 x 375,000)
+// takes 3, since each wave's serial walk over the rows is then latency-bound.
+template <int VW, bool S16, int CUN = CU, bool NTL = false, bool PF = false, int WPE = 1, int PFD = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_col_means(const int32_t *__restrict__ q, Q16 s16, int64_t n, int64_t m,
                                                    int64_t ld, const double *__restrict__ rm,
                                                    const double *__restrict__ rinv, const uint8_t *__restrict__ rbad,
@@ -750,17 +754,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   const int64_t ng = n / CUN;
   int64_t i = 0;
   if constexpr (PF && S16 && VW <= 2) {
-    // the next group's codes in flight while this group is summed (same order),
-    // held as the raw 4-byte words (2 codes each): 8 registers per group, so the
-    // pipelined loop keeps the occupancy of the plain one
-    uint32_t wa[CUN], wb[CUN];
-    if (ng > 0) ld_raw<VW, CUN, NTL>(s16, 0, ld, j0, wa);
-    for (int64_t g = 0; g < ng; g += 2) {
-      if (g + 1 < ng) ld_raw<VW, CUN, NTL>(s16, (g + 1) * CUN, ld, j0, wb);
-      { int32_t v[CUN][VW]; unpack_raw<VW, CUN>(wa, v); do_grp(v, g * CUN); }
-      if (g + 1 >= ng) break;
-      if (g + 2 < ng) ld_raw<VW, CUN, NTL>(s16, (g + 2) * CUN, ld, j0, wa);
-      { int32_t v[CUN][VW]; unpack_raw<VW, CUN>(wb, v); do_grp(v, (g + 1) * CUN); }
+    // the next PFD groups' codes in flight while this group is summed (same
+    // order), held as the raw 4-byte words (2 codes each): 8 registers per
+    // group, so the pipelined loop (PFD 1) keeps the occupancy of the plain one
+    constexpr int NB = PFD + 1;
+    uint32_t w[NB][CUN];
+#pragma unroll
+    for (int b = 0; b < PFD; b++)
+      if (b < ng) ld_raw<VW, CUN, NTL>(s16, b * CUN, ld, j0, w[b]);
+    for (int64_t g = 0; g < ng; g += NB) {
+#pragma unroll
+      for (int b = 0; b < NB; b++) {
+        const int64_t gg = g + b;
+        if (gg >= ng) break;
+        if (gg + PFD < ng) ld_raw<VW, CUN, NTL>(s16, (gg + PFD) * CUN, ld, j0, w[(b + PFD) % NB]);
+        int32_t v[CUN][VW];
+        unpack_raw<VW, CUN>(w[b], v);
+        do_grp(v, gg * CUN);
+      }
     }
     i = ng * CUN;
   } else if constexpr (PF) {
@@ -795,7 +806,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   for (int c = 0; c < VW; c++) mu[j0 + c] = acc[c] / (double)cnt[c];   // 0/0 -> NaN (numpy)
 }
 
-template <int VW, bool S16, int CUN = CU, bool NTL = false, bool PF = false, int WPE = 1>
+template <int VW, bool S16, int CUN = CU, bool NTL = false, bool PF = false, int WPE = 1, int PFD = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_col_vars(const int32_t *__restrict__ q, Q16 s16, int64_t n, int64_t m,
                                                   int64_t ld, const double *__restrict__ rm,
                                                   const double *__restrict__ rinv, const uint8_t *__restrict__ rbad,
@@ -860,14 +871,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   const int64_t ng = n / CUN;
   int64_t i = 0;
   if constexpr (PF && S16 && VW <= 2) {
-    uint32_t wa[CUN], wb[CUN];
-    if (ng > 0) ld_raw<VW, CUN, NTL>(s16, 0, ld, j0, wa);
-    for (int64_t g = 0; g < ng; g += 2) {
-      if (g + 1 < ng) ld_raw<VW, CUN, NTL>(s16, (g + 1) * CUN, ld, j0, wb);
-      { int32_t v[CUN][VW]; unpack_raw<VW, CUN>(wa, v); do_grp(v, g * CUN); }
-      if (g + 1 >= ng) break;
-      if (g + 2 < ng) ld_raw<VW, CUN, NTL>(s16, (g + 2) * CUN, ld, j0, wa);
-      { int32_t v[CUN][VW]; unpack_raw<VW, CUN>(wb, v); do_grp(v, (g + 1) * CUN); }
+    constexpr int NB = PFD + 1;                // as k_col_means
+    uint32_t w[NB][CUN];
+#pragma unroll
+    for (int b = 0; b < PFD; b++)
+      if (b < ng) ld_raw<VW, CUN, NTL>(s16, b * CUN, ld, j0, w[b]);
+    for (int64_t g = 0; g < ng; g += NB) {
+#pragma unroll
+      for (int b = 0; b < NB; b++) {
+        const int64_t gg = g + b;
+        if (gg >= ng) break;
+        if (gg + PFD < ng) ld_raw<VW, CUN, NTL>(s16, (gg + PFD) * CUN, ld, j0, w[(b + PFD) % NB]);
+        int32_t v[CUN][VW];
+        unpack_raw<VW, CUN>(w[b], v);
+        do_grp(v, gg * CUN);
+      }
     }
     i = ng * CUN;
   } else if constexpr (PF) {
@@ -2278,9 +2296,14 @@ static int col_stats_impl(grid_ctx *ctx, bool vars, const int32_t *d_q, const Q1
   const int vw = s16.q ? (vw16 == 8 && (ld % 8 != 0 || (uintptr_t)s16.q % 16 != 0) ? 4 : vw16)
                        : vec4_ok(d_q, ld) ? (want == 4 ? 4 : want == 1 ? 1 : 2) : 1;
   const dim3 grid((unsigned)ceil_div(ceil_div(m, vw), 256));
+  // less than one round of resident waves (8 per SIMD): the deep-prefetch form
+  const bool deep = s16.q && vw == 2 && pf && !cu16 &&
+                    ceil_div(ceil_div(m, vw), 64) < (int64_t)(ctx->ncu > 0 ? ctx->ncu : 256) * 4 * 8;
   if (!vars) {
     auto kern = s16.q ? (vw == 8 ? (nt ? k_col_means<8, true, CU, true> : k_col_means<8, true>) : vw == 4 ? k_col_means<4, true>
-                         : vw == 2 ? (pf ? (cu16 ? k_col_means<2, true, 16, true, true> : k_col_means<2, true, CU, true, true, 8>)
+                         : vw == 2 ? (pf ? (cu16 ? k_col_means<2, true, 16, true, true>
+                                           : deep ? k_col_means<2, true, CU, true, true, 4, 3>
+                                                  : k_col_means<2, true, CU, true, true, 8>)
                                       : cu16 ? k_col_means<2, true, 16, true>
                                       : nt ? k_col_means<2, true, CU, true> : k_col_means<2, true>)
                                    : pf ? (cu16 ? k_col_means<1, true, 16, true, true> : k_col_means<1, true, CU, true, true>)
@@ -2290,7 +2313,9 @@ static int col_stats_impl(grid_ctx *ctx, bool vars, const int32_t *d_q, const Q1
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, ctx->stream, d_q, s16, n, m, ld, d_rm, rinv, rbad, d_out);
   } else {
     auto kern = s16.q ? (vw == 8 ? (nt ? k_col_vars<8, true, CU, true> : k_col_vars<8, true>) : vw == 4 ? k_col_vars<4, true>
-                         : vw == 2 ? (pf ? (cu16 ? k_col_vars<2, true, 16, true, true> : k_col_vars<2, true, CU, true, true, 8>)
+                         : vw == 2 ? (pf ? (cu16 ? k_col_vars<2, true, 16, true, true>
+                                           : deep ? k_col_vars<2, true, CU, true, true, 4, 3>
+                                                  : k_col_vars<2, true, CU, true, true, 8>)
                                       : cu16 ? k_col_vars<2, true, 16, true>
                                       : nt ? k_col_vars<2, true, CU, true> : k_col_vars<2, true>)
                                    : pf ? (cu16 ? k_col_vars<1, true, 16, true, true> : k_col_vars<1, true, CU, true, true>)
