@@ -10,15 +10,17 @@
 //   1. k_fmt_len / k_fmt_rows: the "%.2f" cells of the int32 hundredths that
 //      step 4 left in HBM, laid out row after row (prefix "ID \t scale \t" and
 //      the newline come from the host), staged per 2048-cell block in LDS;
-//   2. one length-limited canonical Huffman code per file (package-merge on
-//      the histogram of the first batch, every byte value encodable), written
-//      as ONE dynamic-Huffman deflate block per member: literals only (on
-//      this text an LZ77 match of 3-4 bytes costs as many bits as the
-//      literals it replaces), ~13 % larger than libdeflate level 1;
-//   3. k_seg_bits: code bits per 4 KiB text segment (host scan -> each
-//      segment's absolute output bit); k_encode: each segment packs its codes
-//      into an LDS word image and stores it, atomically only on the two edge
-//      words it may share with a neighbour;
+//   2. k_lz_parse: LZ77 tokens of every 4 KiB text segment, parsed on its own
+//      against the 2 KiB of its member before it (below: hashed 4-byte
+//      matches, greedy with one lazy step, the token chain walked by all
+//      threads from guessed entry points), one descriptor per text byte;
+//   3. one pair of length-limited canonical Huffman codes per file
+//      (package-merge on the token histogram of the first batch, every byte,
+//      length and distance encodable), written as ONE dynamic-Huffman deflate
+//      block per member; k_lz_bits: code bits per segment (host scan -> each
+//      segment's absolute output bit); k_lz_encode: each segment packs its
+//      codes into an LDS word image and stores it, atomically only on the two
+//      edge words it may share with a neighbour;
 //   4. k_seg_crc / k_seg_fold_wave: CRC-32 of every 4 KiB text segment (a wave
 //      each: 64-byte lane slices, slicing-by-4 tables in LDS, a tree of the
 //      fixed GF(2) shift operators x^(8 len) mod P -- zlib's crc32_combine
@@ -187,6 +189,75 @@ void build_code(const uint64_t *hist256, Code &c) {
   w.put(2, 2);              // BTYPE = 10: dynamic Huffman
   w.put(0, 5);              // HLIT: 257 codes
   w.put(1, 5);              // HDIST: 2 codes
+  w.put((uint32_t)(hclen - 4), 4);
+  for (int i = 0; i < hclen; i++) w.put(cl[ord[i]], 3);
+  for (uint8_t v : seq) w.put(cc[v], cl[v]);
+  c.hdr_bits = (int)w.bits();
+  w.flush();
+  c.hdr.assign((w.buf.size() + 3) / 4 + 1, 0u);
+  for (size_t i = 0; i < w.buf.size(); i++) c.hdr[i / 4] |= (uint32_t)w.buf[i] << (8 * (i % 4));
+}
+
+// ---- LZ77 symbols (RFC 1951 3.2.5) ---------------------------------------------
+// Length 3..258 -> lit/len symbol 257..285 and its extra bits; distance
+// 1..32768 -> symbol 0..29 and its extra bits.  Closed forms of the RFC's
+// tables (the base of a symbol with e extra bits is (4 + low two bits) << e).
+__host__ __device__ __forceinline__ int ilog2u(uint32_t v) { return 31 - __builtin_clz(v); }
+__host__ __device__ __forceinline__ void len_sym(int len, int &sym, int &ne, int &ev) {
+  if (len == 258) { sym = 285; ne = 0; ev = 0; return; }
+  const int l = len - 3;
+  if (l < 8) { sym = 257 + l; ne = 0; ev = 0; return; }
+  const int e = ilog2u((uint32_t)l) - 2;
+  const int lo = (l >> e) & 3;
+  sym = 257 + 4 * (e + 1) + lo;
+  ne = e;
+  ev = l - ((4 + lo) << e);
+}
+__host__ __device__ __forceinline__ void dist_sym(int d, int &sym, int &ne, int &ev) {
+  const uint32_t x = (uint32_t)(d - 1);
+  if (x < 4) { sym = (int)x; ne = 0; ev = 0; return; }
+  const int k = ilog2u(x);                 // x in [2^k, 2^(k+1)), k >= 2
+  const int hi = (int)((x >> (k - 1)) & 1);
+  sym = 2 * k + hi;
+  ne = k - 1;
+  ev = (int)(x - ((uint32_t)(2 + hi) << (k - 1)));
+}
+
+// The LZ77 code of a file: 286 lit/len and 30 distance lengths from the first
+// batch's token histogram (+1 each: every byte, length and distance stays
+// encodable in later batches), and the dynamic block header (HLIT 286, HDIST
+// 30, the code-length code) as a bit string.
+struct CodeLZ {
+  uint8_t len[286], dlen[30];
+  uint16_t rcode[286], drcode[30];
+  std::vector<uint32_t> hdr;
+  int hdr_bits = 0;
+};
+
+void build_code_lz(const uint64_t *hll, const uint64_t *hd, CodeLZ &c) {
+  uint64_t f[286], fd[30];
+  for (int i = 0; i < 286; i++) f[i] = hll[i] + 1;
+  for (int i = 0; i < 30; i++) fd[i] = hd[i] + 1;
+  limited_lengths(f, 286, 15, c.len);
+  canonical_codes(c.len, 286, c.rcode);
+  limited_lengths(fd, 30, 15, c.dlen);
+  canonical_codes(c.dlen, 30, c.drcode);
+  std::vector<uint8_t> seq(c.len, c.len + 286);
+  seq.insert(seq.end(), c.dlen, c.dlen + 30);
+  uint64_t cf[19] = {0};
+  for (uint8_t v : seq) cf[v]++;
+  uint8_t cl[19];
+  uint16_t cc[19];
+  limited_lengths(cf, 19, 7, cl);
+  canonical_codes(cl, 19, cc);
+  static const int ord[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+  int hclen = 19;
+  while (hclen > 4 && cl[ord[hclen - 1]] == 0) hclen--;
+  BitW w;
+  w.put(1, 1);              // BFINAL
+  w.put(2, 2);              // BTYPE = 10: dynamic Huffman
+  w.put(286 - 257, 5);      // HLIT
+  w.put(30 - 1, 5);         // HDIST
   w.put((uint32_t)(hclen - 4), 4);
   for (int i = 0; i < hclen; i++) w.put(cl[ord[i]], 3);
   for (uint8_t v : seq) w.put(cc[v], cl[v]);
@@ -373,49 +444,241 @@ __global__ __launch_bounds__(256) void k_fmt_rows(const int32_t *__restrict__ zq
   if (b == nblk - 1 && tid == 0) dst[total] = '\n';
 }
 
-// Byte histogram of text[0, n) (the code of the file).
-__global__ __launch_bounds__(256) void k_hist(const uint8_t *__restrict__ text, int64_t n,
-                                              unsigned long long *__restrict__ hist) {
-  __shared__ unsigned int s_h[256];
+// ---- device: LZ77 parse ------------------------------------------------------------
+// Each 4 KiB segment is parsed on its own (one workgroup), so the segments of a
+// batch parse in parallel and the encoder can place every segment's bits once
+// their lengths are known.  A segment's matches reach back into the LZW bytes
+// of its member before it (the decoder has them) and end inside the segment.
+//   1. match finding: the window and the segment go to LDS; positions are
+//      taken 256 at a time (one per thread) in text order: each segment
+//      position looks up the two latest earlier positions of its 4-byte hash
+//      (a 2-way table filled by the previous rounds: a round does not see its
+//      own positions) and keeps the longer match (>= 4 bytes, the nearer one on
+//      a tie), compared 4 bytes at a time; then the round's positions enter
+//      the table (atomicMax keeps the latest, the displaced one moves to the
+//      second way);
+//   2. the parse: greedy with one step of lazy evaluation (a match at j is
+//      replaced by a literal when position j + 1 has a longer one), i.e. a
+//      token length at every position; the token chain from position 0 is
+//      walked by 256 threads at once, 16 positions each, from guessed entry
+//      points that are corrected until they agree (below);
+//   3. one descriptor per segment position: 0 (inside a token), 1 + byte (a
+//      literal) or dist << 9 | len (a match, len >= 4).
+// On config-2 text this parse gives ~0.34 bytes per text byte against ~0.43 for
+// literals alone (libdeflate level 1: 0.33; tools/lz_model.c).
+constexpr int LZW = 2048;                  // window bytes before a segment
+constexpr int LZ_HB = 11;                  // hash bits
+constexpr int LZ_MIN = 4, LZ_MAX = 258;
+constexpr int LZ_TW = (3 + LZW + SEG) / 4 + 4;   // text words in LDS (+ zero pad)
+
+__device__ __forceinline__ uint32_t lz_w4(const uint32_t *w, int i) {
+  // the 4 text bytes at LDS byte index i (little-endian)
+  return __builtin_amdgcn_alignbyte(w[(i >> 2) + 1], w[i >> 2], (uint32_t)(i & 3));
+}
+__device__ __forceinline__ int lz_match(const uint32_t *w, int i, int c, int lim) {
+  int l = 0;
+  while (l < lim) {
+    const uint32_t x = lz_w4(w, i + l) ^ lz_w4(w, c + l);
+    if (x) { l += (int)(__builtin_ctz(x) >> 3); break; }
+    l += 4;
+  }
+  return min(l, lim);
+}
+
+// text: the batch; sstart/slen: the segments; swin: window bytes before each
+// segment (<= LZW, inside its member); desc: SEG descriptors per segment.
+__global__ __launch_bounds__(256) void k_lz_parse(const uint8_t *__restrict__ text, const int64_t *__restrict__ sstart,
+                                                  const int32_t *__restrict__ slen, const int32_t *__restrict__ swin,
+                                                  uint32_t *__restrict__ desc) {
+  __shared__ uint32_t s_txt[LZ_TW];
+  __shared__ int32_t s_tab[2][1 << LZ_HB];        // later: the doubling arrays
+  __shared__ uint32_t s_m[SEG];                    // per position: dist << 9 | len (len < 4: no match)
   const int tid = threadIdx.x;
-  s_h[tid] = 0;
+  const int64_t s = blockIdx.x;
+  const int L = slen[s], win = swin[s];
+  const int64_t ws = sstart[s] - win;
+  const int64_t base = ws & ~(int64_t)3;
+  const int o = (int)(ws - base), so = o + win, end = so + L;
+  const int nw = (end + 3) >> 2;
+  const uint32_t *g = reinterpret_cast<const uint32_t *>(text + base);
+  for (int e = tid; e < LZ_TW; e += 256) s_txt[e] = e < nw ? g[e] : 0u;
+  for (int e = tid; e < (2 << LZ_HB); e += 256) (&s_tab[0][0])[e] = -1;
   __syncthreads();
-  for (int64_t e = (int64_t)blockIdx.x * 256 + tid; e < n; e += (int64_t)gridDim.x * 256) atomicAdd(&s_h[text[e]], 1u);
+  if (end - o > 0) {
+    // zero the bytes past the segment in its last word (the match compare reads them)
+    if (tid == 0 && (end & 3)) s_txt[end >> 2] &= (1u << (8 * (end & 3))) - 1u;
+  }
   __syncthreads();
-  if (s_h[tid]) atomicAdd(&hist[tid], (unsigned long long)s_h[tid]);
+  const int last = end - LZ_MIN;                   // last position with 4 bytes
+  for (int c0 = o; c0 <= last; c0 += 256) {
+    const int i = c0 + tid;
+    const bool ok = i <= last;
+    uint32_t h = 0;
+    if (ok) {
+      h = (lz_w4(s_txt, i) * 2654435761u) >> (32 - LZ_HB);
+      if (i >= so) {
+        const int lim = min(LZ_MAX, end - i);
+        const int c1 = s_tab[0][h], c2 = s_tab[1][h];
+        int bl = 0, bd = 0;
+        if (c1 >= 0) { bl = lz_match(s_txt, i, c1, lim); bd = i - c1; }
+        if (c2 >= 0) {
+          const int l2 = lz_match(s_txt, i, c2, lim);
+          if (l2 > bl) { bl = l2; bd = i - c2; }
+        }
+        s_m[i - so] = bl >= LZ_MIN ? ((uint32_t)bd << 9) | (uint32_t)bl : 0u;
+      }
+    } else if (i >= so && i < end) {
+      s_m[i - so] = 0u;                            // fewer than 4 bytes left
+    }
+    __syncthreads();
+    if (ok) {
+      const int old = atomicMax(&s_tab[0][h], i);
+      atomicMax(&s_tab[1][h], min(old, i));
+    }
+    __syncthreads();
+  }
+  // positions of a segment shorter than 4 bytes never entered the loop
+  for (int j = tid; j < L; j += 256)
+    if (so + j > last) s_m[j] = 0u;
+  __syncthreads();
+  // the parse: token lengths (1 = literal) in the table space, now free
+  uint16_t *tl = reinterpret_cast<uint16_t *>(&s_tab[0][0]);            // [SEG]
+  int32_t *s_x = reinterpret_cast<int32_t *>(tl + SEG);                 // [256] exits
+  for (int j = tid; j < L; j += 256) {
+    const int m = (int)(s_m[j] & 511u);
+    // lazy: a match is dropped for a literal when the next position matches longer
+    tl[j] = (uint16_t)((m < LZ_MIN || (j + 1 < L && (int)(s_m[j + 1] & 511u) > m)) ? 1 : m);
+  }
+  __syncthreads();
+  // Thread t owns positions [lo, lo + LZ_S): its entry e is the first token
+  // position >= lo, and e(t + 1) = its exit x(t), the first token position
+  // >= lo + LZ_S of the walk from e(t).  Guess e = lo, walk, pass the exits on
+  // and walk again until no entry changes: e(0) = 0 is exact, so round k has
+  // the first k entries right; greedy parses from nearby starts merge within
+  // a few tokens, so two or three rounds settle a segment.
+  constexpr int LZ_S = SEG / 256;
+  const int lo = tid * LZ_S, hi = min(lo + LZ_S, L);
+  int e = lo;
+  for (;;) {
+    int x = e;
+    while (x < hi) x += tl[x];
+    s_x[tid] = x;
+    __syncthreads();
+    const int ne = tid ? s_x[tid - 1] : 0;
+    const bool changed = ne != e;
+    e = ne;
+    if (!__syncthreads_or(changed)) break;
+  }
+  uint32_t *d = desc + s * SEG;
+  int nxt = e;
+  for (int j = lo; j < hi; j++) {
+    uint32_t v = 0;
+    if (j == nxt) {
+      const int t = tl[j];
+      nxt += t;
+      v = t == 1 ? 1u + ((s_txt[(so + j) >> 2] >> (8 * ((so + j) & 3))) & 0xffu) : s_m[j];
+    }
+    d[j] = v;
+  }
 }
 
 // ---- device: entropy coding ------------------------------------------------------
 struct CodeDev {
-  uint8_t len[256];
-  uint16_t rcode[256];
+  uint8_t len[286], dlen[30];
+  uint16_t rcode[286], drcode[30];
 };
 
-// Code bits of each 4 KiB segment s = [sstart[s], sstart[s] + slen[s]).
-__global__ __launch_bounds__(256) void k_seg_bits(const uint8_t *__restrict__ text, const int64_t *__restrict__ sstart,
-                                                  const int32_t *__restrict__ slen, const CodeDev *__restrict__ cd,
-                                                  uint32_t *__restrict__ sbits) {
-  __shared__ uint8_t s_len[256];
+// Histogram of the tokens of segments [0, ns): lit/len symbols and distances.
+__global__ __launch_bounds__(256) void k_lz_hist(const uint32_t *__restrict__ desc, const int32_t *__restrict__ slen,
+                                                 int64_t ns, unsigned long long *__restrict__ hist /* [286 + 30] */) {
+  __shared__ unsigned int s_h[316];
+  const int tid = threadIdx.x;
+  for (int e = tid; e < 316; e += 256) s_h[e] = 0;
+  __syncthreads();
+  for (int64_t s = blockIdx.x; s < ns; s += gridDim.x) {
+    const int L = slen[s];
+    for (int j = tid; j < L; j += 256) {
+      const uint32_t v = desc[s * SEG + j];
+      if (!v) continue;
+      if (v <= 256) {
+        atomicAdd(&s_h[v - 1], 1u);
+      } else {
+        int sym, ne, ev;
+        len_sym((int)(v & 511u), sym, ne, ev);
+        atomicAdd(&s_h[sym], 1u);
+        dist_sym((int)(v >> 9), sym, ne, ev);
+        atomicAdd(&s_h[286 + sym], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < 316; e += 256)
+    if (s_h[e]) atomicAdd(&hist[e], (unsigned long long)s_h[e]);
+}
+
+// The code bits of token v (<= 48: lit/len code, length extra, distance code,
+// distance extra) as up to four (value, nbits) pieces; returns the count.
+__device__ __forceinline__ int lz_pieces(uint32_t v, const uint8_t *len, const uint16_t *rc, const uint8_t *dlen,
+                                         const uint16_t *drc, uint32_t (&pv)[4], int (&pn)[4]) {
+  if (v <= 256) {
+    pv[0] = rc[v - 1];
+    pn[0] = len[v - 1];
+    return 1;
+  }
+  int sym, ne, ev;
+  len_sym((int)(v & 511u), sym, ne, ev);
+  pv[0] = rc[sym];
+  pn[0] = len[sym];
+  pv[1] = (uint32_t)ev;
+  pn[1] = ne;
+  dist_sym((int)(v >> 9), sym, ne, ev);
+  pv[2] = drc[sym];
+  pn[2] = dlen[sym];
+  pv[3] = (uint32_t)ev;
+  pn[3] = ne;
+  return 4;
+}
+
+struct LzCodeLds {
+  uint8_t len[286], dlen[30];
+  uint16_t rc[286], drc[30];
+  __device__ void load(const CodeDev *cd, int tid) {
+    for (int e = tid; e < 286; e += 256) { len[e] = cd->len[e]; rc[e] = cd->rcode[e]; }
+    if (tid < 30) { dlen[tid] = cd->dlen[tid]; drc[tid] = cd->drcode[tid]; }
+  }
+};
+
+// Code bits of each segment.
+__global__ __launch_bounds__(256) void k_lz_bits(const uint32_t *__restrict__ desc, const int32_t *__restrict__ slen,
+                                                 const CodeDev *__restrict__ cd, uint32_t *__restrict__ sbits) {
+  __shared__ LzCodeLds c;
   __shared__ uint32_t s_w[4];
   const int tid = threadIdx.x;
-  s_len[tid] = cd->len[tid];
+  c.load(cd, tid);
   __syncthreads();
   const int64_t s = blockIdx.x;
-  const uint8_t *p = text + sstart[s];
   const int L = slen[s];
+  const uint32_t *d = desc + s * SEG;
   uint32_t bits = 0;
   const int o = tid * 16;
+#pragma unroll 4
+  for (int u = 0; u < 16; u++) {
+    if (o + u >= L) break;
+    const uint32_t v = d[o + u];
+    if (!v) continue;
+    uint32_t pv[4];
+    int pn[4];
+    const int np = lz_pieces(v, c.len, c.rc, c.dlen, c.drc, pv, pn);
+    for (int k = 0; k < np; k++) bits += (uint32_t)pn[k];
+  }
 #pragma unroll
-  for (int u = 0; u < 16; u++)
-    if (o + u < L) bits += s_len[p[o + u]];
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) bits += __shfl_xor(bits, d, 64);
+  for (int dd = 32; dd > 0; dd >>= 1) bits += __shfl_xor(bits, dd, 64);
   if ((tid & 63) == 0) s_w[tid >> 6] = bits;
   __syncthreads();
   if (tid == 0) sbits[s] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
 }
 
-constexpr int SEG_WORDS = (SEG * 15) / 32 + 3;
+constexpr int SEG_WORDS = (SEG * 15) / 32 + 3;     // a token's bits never exceed 15 per text byte
 
 __device__ __forceinline__ void lds_put(uint32_t *w, uint32_t bitpos, uint32_t v32, int nbits) {
   // nbits <= 32 bits of v32 at bit position bitpos of the LDS word image
@@ -424,39 +687,41 @@ __device__ __forceinline__ void lds_put(uint32_t *w, uint32_t bitpos, uint32_t v
   if (sh && sh + nbits > 32) atomicOr(&w[wi + 1], v32 >> (32 - sh));
 }
 
-// Segment s: its codes packed at absolute output bit sbase[s] (LSB-first
-// deflate order in little-endian words).  Interior words are stored, the two
-// edge words (shared with the neighbouring segment or the member's header /
-// end-of-block bits) OR-ed atomically into the zeroed output.
-__global__ __launch_bounds__(256) void k_encode(const uint8_t *__restrict__ text, const int64_t *__restrict__ sstart,
-                                                const int32_t *__restrict__ slen, const int64_t *__restrict__ sbase,
-                                                const uint32_t *__restrict__ sbits, const CodeDev *__restrict__ cd,
-                                                uint32_t *__restrict__ out) {
-  __shared__ uint8_t s_len[256];
-  __shared__ uint16_t s_code[256];
+// Segment s: its tokens' codes packed at absolute output bit sbase[s]
+// (LSB-first deflate order in little-endian words).  Interior words are
+// stored, the two edge words (shared with the neighbouring segment or the
+// member's header / end-of-block bits) OR-ed atomically into the zeroed output.
+__global__ __launch_bounds__(256) void k_lz_encode(const uint32_t *__restrict__ desc, const int32_t *__restrict__ slen,
+                                                   const int64_t *__restrict__ sbase, const uint32_t *__restrict__ sbits,
+                                                   const CodeDev *__restrict__ cd, uint32_t *__restrict__ out) {
+  __shared__ LzCodeLds c;
   __shared__ uint32_t s_img[SEG_WORDS];
   __shared__ uint32_t s_wsum[4];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  s_len[tid] = cd->len[tid];
-  s_code[tid] = cd->rcode[tid];
+  c.load(cd, tid);
   for (int e = tid; e < SEG_WORDS; e += 256) s_img[e] = 0;
   __syncthreads();
   const int64_t s = blockIdx.x;
-  const uint8_t *p = text + sstart[s];
   const int L = slen[s];
+  const uint32_t *d = desc + s * SEG;
   const int o = tid * 16;
-  uint8_t c[16];
+  uint32_t v[16];
   uint32_t bits = 0;
 #pragma unroll
   for (int u = 0; u < 16; u++) {
-    c[u] = o + u < L ? p[o + u] : 0;
-    if (o + u < L) bits += s_len[c[u]];
+    v[u] = o + u < L ? d[o + u] : 0u;
+    if (v[u]) {
+      uint32_t pv[4];
+      int pn[4];
+      const int np = lz_pieces(v[u], c.len, c.rc, c.dlen, c.drc, pv, pn);
+      for (int k = 0; k < np; k++) bits += (uint32_t)pn[k];
+    }
   }
   uint32_t x = bits;
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d, 64);
-    if (lane >= d) x += y;
+  for (int dd = 1; dd < 64; dd <<= 1) {
+    const uint32_t y = __shfl_up(x, dd, 64);
+    if (lane >= dd) x += y;
   }
   if (lane == 63) s_wsum[wv] = x;
   __syncthreads();
@@ -466,11 +731,14 @@ __global__ __launch_bounds__(256) void k_encode(const uint8_t *__restrict__ text
   uint32_t pos = (uint32_t)(abs0 & 31) + pre;       // bit position in the LDS image
   uint64_t acc = 0;
   int na = 0;
-#pragma unroll
   for (int u = 0; u < 16; u++) {
-    if (o + u < L) {
-      acc |= (uint64_t)s_code[c[u]] << na;
-      na += s_len[c[u]];
+    if (!v[u]) continue;
+    uint32_t pv[4];
+    int pn[4];
+    const int np = lz_pieces(v[u], c.len, c.rc, c.dlen, c.drc, pv, pn);
+    for (int k = 0; k < np; k++) {
+      acc |= (uint64_t)pv[k] << na;
+      na += pn[k];
       if (na >= 32) {
         lds_put(s_img, pos, (uint32_t)acc, 32);
         pos += 32;
@@ -490,6 +758,7 @@ __global__ __launch_bounds__(256) void k_encode(const uint8_t *__restrict__ text
     else out[w] = val;
   }
 }
+
 
 __device__ __forceinline__ void glb_put(uint32_t *out, uint64_t bitpos, uint32_t v32, int nbits) {
   const uint64_t wi = bitpos >> 5;
@@ -671,8 +940,8 @@ struct HBuf {
 struct WriterBufs {
   DBuf<int64_t> d_blen, d_boff, d_rowoff, d_prelen, d_preoff, d_sstart, d_sbase, d_moff, d_msize, d_mrow, d_mlen,
       d_mbits, d_mstart, d_mseg0;
-  DBuf<int32_t> d_slen;
-  DBuf<uint32_t> d_sbits, d_crc, d_hdr, d_tab, d_out, d_scrc;
+  DBuf<int32_t> d_slen, d_swin;
+  DBuf<uint32_t> d_sbits, d_crc, d_hdr, d_tab, d_out, d_scrc, d_desc;
   DBuf<char> d_pre, d_text;
   DBuf<CodeDev> d_code;
   DBuf<unsigned long long> d_hist;
@@ -792,9 +1061,9 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
        &d_preoff = wbuf.d_preoff, &d_sstart = wbuf.d_sstart, &d_sbase = wbuf.d_sbase, &d_moff = wbuf.d_moff,
        &d_msize = wbuf.d_msize, &d_mrow = wbuf.d_mrow, &d_mlen = wbuf.d_mlen, &d_mbits = wbuf.d_mbits,
        &d_mstart = wbuf.d_mstart, &d_mseg0 = wbuf.d_mseg0;
-  auto &d_slen = wbuf.d_slen;
+  auto &d_slen = wbuf.d_slen, &d_swin = wbuf.d_swin;
   auto &d_sbits = wbuf.d_sbits, &d_crc = wbuf.d_crc, &d_hdr = wbuf.d_hdr, &d_tab = wbuf.d_tab, &d_out = wbuf.d_out,
-       &d_scrc = wbuf.d_scrc;
+       &d_scrc = wbuf.d_scrc, &d_desc = wbuf.d_desc;
   auto &d_pre = wbuf.d_pre, &d_text = wbuf.d_text;
   auto &d_code = wbuf.d_code;
   auto &d_hist = wbuf.d_hist;
@@ -916,11 +1185,11 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
     STEP(d_tab.need(1024));
     STEP(hipMemcpyAsync(d_tab.p, crctab.data(), 4096, hipMemcpyHostToDevice, st));
   }
-  Code code;
+  CodeLZ code;
   bool have_code = false;
   std::vector<int64_t> h_blen, h_rowoff, h_prelen, h_preoff, h_sstart, h_sbase, h_moff, h_msize, h_mrow, h_mlen,
       h_mbits, h_mstart;
-  std::vector<int32_t> h_slen;
+  std::vector<int32_t> h_slen, h_swin;
   std::vector<uint32_t> h_sbits;
   int64_t i0 = 0;
   int cur = 0;
@@ -971,25 +1240,6 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
                          st, d_zq, ld_zq, r, i0, nblk, y0, d_boff.p, d_pre.p, d_preoff.p, d_rowoff.p, d_text.p);
       STEP(hipGetLastError());
     }
-    if (!have_code) {            // the file's code: histogram of the first batch
-      STEP(d_hist.need(256));
-      STEP(hipMemsetAsync(d_hist.p, 0, 256 * 8, st));
-      const int64_t hb_n = std::min<int64_t>(tlen, 1ll << 30);
-      hipLaunchKernelGGL(k_hist, dim3(1024), dim3(256), 0, st, (const uint8_t *)d_text.p, hb_n, d_hist.p);
-      STEP(hipGetLastError());
-      uint64_t hh[256];
-      STEP(hipMemcpyAsync(hh, d_hist.p, 256 * 8, hipMemcpyDeviceToHost, st));
-      STEP(hipStreamSynchronize(st));
-      build_code(hh, code);
-      CodeDev cdh;
-      memcpy(cdh.len, code.len, 256);
-      memcpy(cdh.rcode, code.rcode, 512);
-      STEP(d_code.need(1));
-      STEP(hipMemcpyAsync(d_code.p, &cdh, sizeof cdh, hipMemcpyHostToDevice, st));
-      STEP(d_hdr.need(code.hdr.size()));
-      STEP(hipMemcpyAsync(d_hdr.p, code.hdr.data(), code.hdr.size() * 4, hipMemcpyHostToDevice, st));
-      have_code = true;
-    }
     // members and their 4 KiB segments
     const int64_t nm = (nr + rpc - 1) / rpc;
     h_mstart.resize((size_t)nm);
@@ -997,6 +1247,7 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
     h_mrow.resize((size_t)nm);
     h_sstart.clear();
     h_slen.clear();
+    h_swin.clear();
     std::vector<int64_t> mseg0((size_t)nm + 1, 0);
     for (int64_t m = 0; m < nm; m++) {
       const int64_t a = m * rpc, b = std::min(nr, a + rpc);
@@ -1006,6 +1257,7 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
       for (int64_t e = 0; e < h_mlen[m]; e += SEG) {
         h_sstart.push_back(h_mstart[m] + e);
         h_slen.push_back((int32_t)std::min<int64_t>(SEG, h_mlen[m] - e));
+        h_swin.push_back((int32_t)std::min<int64_t>(LZW, e));   // the member's bytes before the segment
       }
       mseg0[m + 1] = (int64_t)h_sstart.size();
     }
@@ -1020,9 +1272,40 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
     STEP(hipMemcpyAsync(d_slen.p, h_slen.data(), ns * 4, hipMemcpyHostToDevice, st));
     STEP(hipMemcpyAsync(d_mstart.p, h_mstart.data(), nm * 8, hipMemcpyHostToDevice, st));
     STEP(hipMemcpyAsync(d_mlen.p, h_mlen.data(), nm * 8, hipMemcpyHostToDevice, st));
+    STEP(d_swin.need((size_t)ns));
+    STEP(d_desc.need((size_t)ns * SEG));
+    STEP(hipMemcpyAsync(d_swin.p, h_swin.data(), ns * 4, hipMemcpyHostToDevice, st));
     if (ns > 0) {
-      hipLaunchKernelGGL(k_seg_bits, dim3((unsigned)ns), dim3(256), 0, st, (const uint8_t *)d_text.p, d_sstart.p,
-                         d_slen.p, d_code.p, d_sbits.p);
+      hipLaunchKernelGGL(k_lz_parse, dim3((unsigned)ns), dim3(256), 0, st, (const uint8_t *)d_text.p, d_sstart.p,
+                         d_slen.p, d_swin.p, d_desc.p);
+      STEP(hipGetLastError());
+    }
+    if (!have_code) {            // the file's code: token histogram of the first batch
+      STEP(d_hist.need(316));
+      STEP(hipMemsetAsync(d_hist.p, 0, 316 * 8, st));
+      if (ns > 0) {
+        hipLaunchKernelGGL(k_lz_hist, dim3((unsigned)std::min<int64_t>(ns, 2048)), dim3(256), 0, st, d_desc.p, d_slen.p,
+                           ns, d_hist.p);
+        STEP(hipGetLastError());
+      }
+      uint64_t hh[316];
+      STEP(hipMemcpyAsync(hh, d_hist.p, 316 * 8, hipMemcpyDeviceToHost, st));
+      STEP(hipStreamSynchronize(st));
+      build_code_lz(hh, hh + 286, code);
+      CodeDev cdh;
+      memcpy(cdh.len, code.len, sizeof cdh.len);
+      memcpy(cdh.dlen, code.dlen, sizeof cdh.dlen);
+      memcpy(cdh.rcode, code.rcode, sizeof cdh.rcode);
+      memcpy(cdh.drcode, code.drcode, sizeof cdh.drcode);
+      STEP(d_code.need(1));
+      STEP(hipMemcpyAsync(d_code.p, &cdh, sizeof cdh, hipMemcpyHostToDevice, st));
+      STEP(d_hdr.need(code.hdr.size()));
+      STEP(hipMemcpyAsync(d_hdr.p, code.hdr.data(), code.hdr.size() * 4, hipMemcpyHostToDevice, st));
+      STEP(hipStreamSynchronize(st));        // cdh and the header leave the host now
+      have_code = true;
+    }
+    if (ns > 0) {
+      hipLaunchKernelGGL(k_lz_bits, dim3((unsigned)ns), dim3(256), 0, st, d_desc.p, d_slen.p, d_code.p, d_sbits.p);
       STEP(hipGetLastError());
     }
     STEP(d_scrc.need((size_t)std::max<int64_t>(ns, 1)));
@@ -1073,8 +1356,8 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
     STEP(hipMemcpyAsync(d_mrow.p, h_mrow.data(), nm * 8, hipMemcpyHostToDevice, st));
     STEP(hipMemcpyAsync(d_mbits.p, h_mbits.data(), nm * 8, hipMemcpyHostToDevice, st));
     if (ns > 0) {
-      hipLaunchKernelGGL(k_encode, dim3((unsigned)ns), dim3(256), 0, st, (const uint8_t *)d_text.p, d_sstart.p,
-                         d_slen.p, d_sbase.p, d_sbits.p, d_code.p, d_out.p);
+      hipLaunchKernelGGL(k_lz_encode, dim3((unsigned)ns), dim3(256), 0, st, d_desc.p, d_slen.p, d_sbase.p, d_sbits.p,
+                         d_code.p, d_out.p);
       STEP(hipGetLastError());
     }
     hipLaunchKernelGGL(k_frame, dim3((unsigned)((nm + 63) / 64)), dim3(64), 0, st, d_out.p, d_moff.p, d_msize.p,

@@ -39,6 +39,8 @@ ap.add_argument("--ingest", choices=["device", "host"], default="device",
 ap.add_argument("--device-ingest", action="store_true", help=argparse.SUPPRESS)   # older spelling of --ingest device
 ap.add_argument("--reuse", action="store_true", help="keep the cohort in --data for a later run (implies --keep)")
 ap.add_argument("--generate-only", action="store_true", help="write the cohort and inputs into --data, then exit")
+ap.add_argument("--verify-normalized", action="store_true",
+                help="after the timed steps, read the step-4 file back and digest the parsed matrix")
 a = ap.parse_args()
 
 
@@ -156,6 +158,22 @@ with deferred_release():
 res["phases_s"]["release_ingest_buffers_after_step7"] = time.perf_counter() - t_rel
 
 res["outputs"] = {f: os.path.getsize(os.path.join(a.out, f)) for f in sorted(os.listdir(a.out))}
+if a.verify_normalized:
+    # outside the timed steps: the step-4 file read back by the library's reader
+    # (every member inflated and its CRC-32 -- computed on the device from the
+    # text before compression -- checked), and a digest of the parsed matrix
+    # that runs with other writers can be compared on
+    from grid_amd import _abi  # noqa: E402
+    import numpy as np  # noqa: E402
+    t = time.perf_counter()
+    nf = [f for f in os.listdir(a.out) if f.startswith("normalized")][0]
+    rid, rsc, rmu, rrat, rzq = _abi.read_normalized_gz(os.path.join(a.out, nf), threads=16)
+    t_read = time.perf_counter() - t
+    import xxhash  # noqa: E402
+    res["normalized_readback"] = {"file": nf, "seconds": t_read, "rows": int(rzq.shape[0]), "cols": int(rzq.shape[1]),
+                                  "ids_ok": rid == ids, "zq_xxh3_64": xxhash.xxh3_64(np.ascontiguousarray(rzq)).hexdigest()}
+    del rzq
+    note(f"normalized file read back in {t_read:.1f} s")
 try:                                    # content digests (outside the timed steps): runs compare byte for byte
     import xxhash
 

@@ -1,0 +1,21 @@
+#!/bin/bash
+# round 5: LZ77 writer iteration -- parity (device = host text), then size / time and the kernel trace on a
+# 200-row config-2-like matrix
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/${RUN:-r05r}
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider \
+  tests/test_gpu_gzwrite.py > $O/pytest.log 2>&1 || { tail -n 40 $O/pytest.log; exit 1; }
+tail -n 1 $O/pytest.log
+timeout -k 10 300 python -u tools/bench_gzwrite_dev.py --n 200 > $O/gzw.json 2> $O/gzw.err || { tail -n 30 $O/gzw.err; exit 1; }
+cat $O/gzw.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -- python3 tools/bench_gzwrite_dev.py --n 200 --reps 1 \
+  > $O/gzw_prof.json 2> $O/gzw_prof.err || { tail -n 30 $O/gzw_prof.err; exit 1; }
+find $O/prof -name "*kernel_stats.csv" -exec cp {} $O/gzw_kernel_stats.csv \;
+python3 -c "
+import csv
+for r in csv.DictReader(open('$O/gzw_kernel_stats.csv')):
+  print(r['Name'][22:40], r['Calls'], round(float(r['AverageNs'])/1e6,3))
+"
