@@ -155,49 +155,6 @@ struct BitW {
   }
 };
 
-// The literal-only code of a file: 257 lit/len lengths (EOB = 256), the block
-// header (BFINAL 1, BTYPE dynamic, HLIT 257 codes, HDIST 2 codes of length 1
-// -- complete, as zlib's own deflate emits for match-free blocks -- HCLEN and
-// the code-length code) as a bit string.
-struct Code {
-  uint8_t len[257];
-  uint16_t rcode[257];
-  std::vector<uint32_t> hdr;   // header bits, LSB-first in 32-bit words
-  int hdr_bits = 0;
-};
-
-void build_code(const uint64_t *hist256, Code &c) {
-  uint64_t f[257];
-  for (int i = 0; i < 256; i++) f[i] = hist256[i] + 1;     // every byte encodable (IDs, anything)
-  f[256] = 1;
-  limited_lengths(f, 257, 15, c.len);
-  canonical_codes(c.len, 257, c.rcode);
-  std::vector<uint8_t> seq(c.len, c.len + 257);
-  seq.push_back(1);
-  seq.push_back(1);                                         // two distance codes of length 1
-  uint64_t cf[19] = {0};
-  for (uint8_t v : seq) cf[v]++;
-  uint8_t cl[19];
-  uint16_t cc[19];
-  limited_lengths(cf, 19, 7, cl);
-  canonical_codes(cl, 19, cc);
-  static const int ord[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
-  int hclen = 19;
-  while (hclen > 4 && cl[ord[hclen - 1]] == 0) hclen--;
-  BitW w;
-  w.put(1, 1);              // BFINAL
-  w.put(2, 2);              // BTYPE = 10: dynamic Huffman
-  w.put(0, 5);              // HLIT: 257 codes
-  w.put(1, 5);              // HDIST: 2 codes
-  w.put((uint32_t)(hclen - 4), 4);
-  for (int i = 0; i < hclen; i++) w.put(cl[ord[i]], 3);
-  for (uint8_t v : seq) w.put(cc[v], cl[v]);
-  c.hdr_bits = (int)w.bits();
-  w.flush();
-  c.hdr.assign((w.buf.size() + 3) / 4 + 1, 0u);
-  for (size_t i = 0; i < w.buf.size(); i++) c.hdr[i / 4] |= (uint32_t)w.buf[i] << (8 * (i % 4));
-}
-
 // ---- LZ77 symbols (RFC 1951 3.2.5) ---------------------------------------------
 // Length 3..258 -> lit/len symbol 257..285 and its extra bits; distance
 // 1..32768 -> symbol 0..29 and its extra bits.  Closed forms of the RFC's
@@ -582,6 +539,53 @@ __global__ __launch_bounds__(256) void k_lz_parse(const uint8_t *__restrict__ te
   }
 }
 
+// Host restatement of k_lz_parse for one member's text t[0, n) (the host form
+// of the member coding, grid_gz_huffman_member; tests): the same segments,
+// windows, hash, rounds of 256 positions (a round's table updates are the
+// two-way top-2 that the device's atomicMax pair leaves), match choice, lazy
+// rule and token chain, so it gives the device's descriptors.
+void lz_tokens_host(const uint8_t *t, int64_t n, std::vector<uint32_t> &desc) {
+  desc.assign((size_t)n, 0u);
+  std::vector<int32_t> t1(1u << LZ_HB), t2(1u << LZ_HB);
+  std::vector<uint32_t> sm(SEG);
+  std::vector<uint16_t> tl(SEG);
+  std::vector<std::pair<uint32_t, int32_t>> ins;
+  for (int64_t s0 = 0; s0 < n; s0 += SEG) {
+    const int L = (int)std::min<int64_t>(SEG, n - s0), win = (int)std::min<int64_t>(LZW, s0);
+    const uint8_t *b = t + s0 - win;                 // local coordinates: window then segment
+    const int so = win, end = win + L, last = end - LZ_MIN;
+    std::fill(t1.begin(), t1.end(), -1);
+    std::fill(t2.begin(), t2.end(), -1);
+    std::fill(sm.begin(), sm.end(), 0u);
+    auto w4 = [&](int i) { uint32_t v; memcpy(&v, b + i, 4); return v; };
+    for (int c0 = 0; c0 <= last; c0 += 256) {
+      ins.clear();
+      for (int i = c0; i < c0 + 256 && i <= last; i++) {
+        const uint32_t h = (w4(i) * 2654435761u) >> (32 - LZ_HB);
+        ins.push_back({h, i});
+        if (i < so) continue;
+        const int lim = std::min(LZ_MAX, end - i);
+        auto mlen = [&](int c) { int l = 0; while (l < lim && b[c + l] == b[i + l]) l++; return l; };
+        int bl = 0, bd = 0;
+        if (t1[h] >= 0) { bl = mlen(t1[h]); bd = i - t1[h]; }
+        if (t2[h] >= 0) { const int l2 = mlen(t2[h]); if (l2 > bl) { bl = l2; bd = i - t2[h]; } }
+        sm[i - so] = bl >= LZ_MIN ? ((uint32_t)bd << 9) | (uint32_t)bl : 0u;
+      }
+      for (auto &e : ins) {                          // top two of {t1, t2} and the round's positions
+        const int32_t p = e.second;
+        int32_t &a = t1[e.first], &c = t2[e.first];
+        if (p > a) { c = a; a = p; } else if (p > c) { c = p; }
+      }
+    }
+    for (int j = 0; j < L; j++) {
+      const int m = (int)(sm[j] & 511u);
+      tl[j] = (uint16_t)((m < LZ_MIN || (j + 1 < L && (int)(sm[j + 1] & 511u) > m)) ? 1 : m);
+    }
+    for (int j = 0; j < L; j += tl[j])
+      desc[(size_t)(s0 + j)] = tl[j] == 1 ? 1u + t[s0 + j] : sm[j];
+  }
+}
+
 // ---- device: entropy coding ------------------------------------------------------
 struct CodeDev {
   uint8_t len[286], dlen[30];
@@ -963,13 +967,33 @@ extern "C" {
 
 int grid_gz_huffman_member(const uint8_t *text, int64_t n, uint8_t *out, int64_t cap, int64_t *out_len) {
   REQUIRE(n >= 0 && (text || !n) && out && out_len && cap >= 0, "grid_gz_huffman_member: bad args");
-  uint64_t hist[256] = {0};
-  for (int64_t e = 0; e < n; e++) hist[text[e]]++;
-  Code c;
-  build_code(hist, c);
+  std::vector<uint32_t> desc;
+  lz_tokens_host(text, n, desc);
+  uint64_t hist[316] = {0};
+  for (uint32_t v : desc) {
+    if (!v) continue;
+    if (v <= 256) { hist[v - 1]++; continue; }
+    int sym, ne, ev;
+    len_sym((int)(v & 511u), sym, ne, ev);
+    hist[sym]++;
+    dist_sym((int)(v >> 9), sym, ne, ev);
+    hist[286 + sym]++;
+  }
+  CodeLZ c;
+  build_code_lz(hist, hist + 286, c);
   BitW w;
   for (int k = 0; k < c.hdr_bits; k++) w.put((c.hdr[k >> 5] >> (k & 31)) & 1, 1);
-  for (int64_t e = 0; e < n; e++) w.put(c.rcode[text[e]], c.len[text[e]]);
+  for (uint32_t v : desc) {
+    if (!v) continue;
+    if (v <= 256) { w.put(c.rcode[v - 1], c.len[v - 1]); continue; }
+    int sym, ne, ev;
+    len_sym((int)(v & 511u), sym, ne, ev);
+    w.put(c.rcode[sym], c.len[sym]);
+    w.put((uint32_t)ev, ne);
+    dist_sym((int)(v >> 9), sym, ne, ev);
+    w.put(c.drcode[sym], c.dlen[sym]);
+    w.put((uint32_t)ev, ne);
+  }
   w.put(c.rcode[256], c.len[256]);
   w.flush();
   uint32_t t[1024];

@@ -506,9 +506,10 @@ int grid_write_normalized_gz(const char *path, int64_t n, int64_t r, const char 
                              const double *raw, const double *sel_means, const double *sel_ratios,
                              const int32_t *zq, int64_t ld_zq, int32_t level, int32_t threads);
 /* The same file from step 4's int32 hundredths still in HBM (d_zq [n][ld_zq],
- * GRID_ZQ_* sentinels): the row members are formatted, CRC'd and Huffman-coded
- * on the device (one literal-only dynamic-Huffman deflate block per member,
- * one canonical code per file from the first batch's byte histogram), the
+ * GRID_ZQ_* sentinels): the row members are formatted, CRC'd, LZ77-parsed
+ * (per 4 KiB segment against 2 KiB of the member before it) and Huffman-coded
+ * on the device (one dynamic-Huffman deflate block per member, one pair of
+ * canonical codes per file from the first batch's token histogram), the
  * header member (level) on the host; only compressed bytes cross PCIe.
  * batch_bytes: text formatted per device batch (<= 0: 2 GiB).  Same member
  * layout and 'GR' index as grid_write_normalized_gz; the decompressed text is
@@ -520,9 +521,9 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
                                  const int32_t *d_zq, int64_t ld_zq, int32_t level, int32_t threads,
                                  int64_t batch_bytes);
 /* Host form of that member coding (tests, small inputs): text[0, n) as one
- * plain gzip member whose single dynamic-Huffman block codes literals only,
- * with the code built from text's own histogram.  *out_len = bytes needed
- * (GRID_EINVAL when above cap). */
+ * plain gzip member, the device parse's LZ77 tokens (restated on the host) in
+ * one dynamic-Huffman block whose codes come from text's own token
+ * histogram.  *out_len = bytes needed (GRID_EINVAL when above cap). */
 int grid_gz_huffman_member(const uint8_t *text, int64_t n, uint8_t *out, int64_t cap, int64_t *out_len);
 /* Reader: parse into a handle (*n_out rows, *r_out columns); z values as
  * integer hundredths (GRID_MISSING for "NA").  GRID_EUNSUPPORTED if the text

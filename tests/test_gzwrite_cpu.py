@@ -1,7 +1,9 @@
 """Host checks of the device writer's member coding (grid_gz_huffman_member:
-the same package-merge code, canonical codes, block header and CRC-32 as
-gzwrite.hip's device kernels): every member must inflate, with zlib and with
-the library's own reader, to exactly its text."""
+the host restatement of k_lz_parse's LZ77 tokens -- same segments, windows,
+hash rounds, lazy rule and token chain -- and the same package-merge codes,
+canonical codes, block header, symbol tables and CRC-32 as gzwrite.hip's
+device kernels): every member must inflate, with zlib and with the library's
+own reader, to exactly its text."""
 import ctypes as C
 import gzip
 import os
@@ -49,14 +51,35 @@ def test_huffman_member_roundtrip(case):
 
 
 def test_huffman_member_is_smallish_on_z_text():
-    """Order-0 Huffman on "%.2f" text: within 20 % of zlib level 1."""
+    """LZ77 + Huffman on "%.2f" text: smaller than zlib level 1 (order-0
+    Huffman alone, the round-4 writer, was ~1.2x it)."""
     text = _z_text(np.random.default_rng(3), 200000)
-    assert len(_member(text)) < 1.2 * len(zlib.compress(text, 1))
+    assert len(_member(text)) < 0.95 * len(zlib.compress(text, 1))
+
+
+@pytest.mark.parametrize("case", ["runs", "period", "window_edge"])
+def test_lz77_member_matches(case):
+    """Matches at the parse's limits: 258-byte matches back to back,
+    overlapping copies (distance < length), repeats exactly at the 2 KiB
+    window and 4 KiB segment edges; zlib must inflate each to its text."""
+    rng = np.random.default_rng(5)
+    if case == "runs":
+        text = b"0.00\t" * 50000 + b"x" + b"\t-1.25" * 30000
+    elif case == "period":
+        text = (b"ab" * 3 + b"c") * 20000
+    else:
+        blk = rng.integers(48, 58, 2048, dtype=np.uint8).tobytes()
+        text = blk + blk + rng.integers(48, 58, 6000, dtype=np.uint8).tobytes() + blk * 5
+    m = _member(text)
+    assert zlib.decompress(m, 31) == text
+    if case != "window_edge":
+        assert len(m) < len(text) // 50
 
 
 def test_reader_takes_huffman_members(tmp_path):
-    """A normalised file whose row members are literal-only Huffman blocks
-    (what the device writer emits) reads back through grid_read_normalized_gz."""
+    """A normalised file whose row members are single LZ77 + dynamic-Huffman
+    blocks (what the device writer emits) reads back through
+    grid_read_normalized_gz."""
     rng = np.random.default_rng(11)
     n, r = 5, 300
     zq = rng.integers(-500, 500, (n, r)).astype(np.int32)
