@@ -77,17 +77,21 @@ struct DevP {
   uint32_t *ftab;                // LDS: F_LEN literal/length entries, then F_DIST distance entries
   uint8_t *ring;                 // LDS
   uint8_t *out;                  // global
-  int64_t cap;
-  int64_t pos, flushed, mstart;
+  // output positions and the fast loop's input window in 32 bits (a wave's
+  // stream is < 2^31 bytes either way, checked at the start): the decode is
+  // bound by the CU's one scalar unit (r05w: 98 % of cycles issue a scalar
+  // instruction), and 64-bit compares and adds take two to four of them
+  int32_t cap;
+  int32_t pos, flushed, mstart;
   grid_gz_member *mem;
   int nmem, mcap, lane;
   uint32_t win;                  // core input window: lane k = bytes wbase + 4k .. + 3
   int64_t wbase;
   uint32_t fcur, fnxt;           // fast_codes' windows: bytes fbase .. +256, +256 .. +512
-  int64_t fbase;
+  int32_t fbase;
 
   __device__ __forceinline__ uint32_t load_word(int64_t b) const {
-    const int64_t o = b + 4 * lane;
+    const int64_t o = b + 4 * lane;   // (the core's window: int64 b; the fast loop's: int32)
     uint32_t w = 0;
     if (o + 4 <= n_in) {
       w = *reinterpret_cast<const uint32_t *>(src + o);
@@ -158,7 +162,7 @@ struct DevP {
     }
   }
   __device__ __forceinline__ void flush_tail() {
-    for (int64_t k = flushed + lane; k < pos; k += 64) out[k] = ring[k & RMASK];
+    for (int k = flushed + lane; k < pos; k += 64) out[k] = ring[k & RMASK];
     flushed = pos;
   }
   __device__ __forceinline__ bool put(uint8_t b) {
@@ -174,7 +178,7 @@ struct DevP {
   // precedes pos: (k + 0.5) / dist is >= 0.5 / 258 from any integer, far
   // more than the reciprocal's error, so the quotient below is exact
   __device__ __forceinline__ void copy_bytes(uint32_t dist, uint32_t len) {
-    const int64_t s0 = pos - dist;
+    const int s0 = pos - (int)dist;
     if (dist > (uint32_t)NEAR) {       // FAR (rare): no overlap (dist > len); source in HBM
       // this wave's flush stores must have reached L2, and the loads go to L2
       // (agent scope): an L1 line of the neighbouring member's wave may hold
@@ -205,7 +209,7 @@ struct DevP {
     pos += len;
   }
   __device__ __forceinline__ int copy(uint32_t dist, int len) {
-    if ((int64_t)dist > pos - mstart) return icore::E_DATA;
+    if (dist > (uint32_t)(pos - mstart)) return icore::E_DATA;
     if (pos + len > cap) return icore::E_SPACE;
     copy_bytes(dist, (uint32_t)len);
     if (pos - flushed >= FLUSH) flush_full();
@@ -293,7 +297,7 @@ struct DevP {
       lit = 0;
       nl = 0;
     }
-    if ((int64_t)dist > pos - mstart) { inf.err = icore::E_DATA; ret = -1; return false; }
+    if (dist > (uint32_t)(pos - mstart)) { inf.err = icore::E_DATA; ret = -1; return false; }
     copy_bytes(dist, len);
     if (pos - flushed >= FLUSH) flush_full();
     return pos + 296 <= cap;
@@ -309,20 +313,21 @@ struct DevP {
   template <class I>
   __device__ int fast_codes(I &inf) {
     if (pos + 296 > cap) return 0;
-    if (inf.ip - fbase < 0 || inf.ip - fbase >= 256) {
-      fbase = inf.ip & ~(int64_t)255;
+    int ip = (int)inf.ip;
+    if (ip - fbase < 0 || ip - fbase >= 256) {
+      fbase = ip & ~255;
       fcur = load_word(fbase);
       fnxt = load_word(fbase + 256);
     }
     uint64_t bb = inf.bb, lit = 0;
     int bc = inf.bc, nl = 0, ret = 0;
-    int64_t ip = inf.ip;
+    const int nin = (int)n_in;
     // one loop, one exit (`go`): the literal path goes straight back to the
     // top, everything else is rarer
     bool go = true;
     while (go) {
       if (bc < 48) {                    // 8 more bytes, of which (63 - bc) / 8 are kept
-        if (ip + 16 > n_in) {
+        if (ip + 16 > nin) {
           go = false;
           continue;
         }
@@ -331,7 +336,7 @@ struct DevP {
           fcur = fnxt;
           fnxt = load_word(fbase + 256);
         }
-        const int r = (int)(ip - fbase), i = r >> 2, sh = (r & 3) * 8;
+        const int r = ip - fbase, i = r >> 2, sh = (r & 3) * 8;
         const uint64_t lo = (uint64_t)fword(i) | ((uint64_t)fword(i + 1) << 32);
         const uint64_t v = sh ? (lo >> sh) | ((uint64_t)fword(i + 2) << (64 - sh)) : lo;
         bb |= v << bc;
@@ -407,10 +412,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GRID_INFLATE
   p.n_in = in_len[f] + skew;
   p.tab = s_tab;
   p.ftab = s_ftab;
-  p.fbase = -((int64_t)1 << 40);
+  p.fbase = -(1 << 30);                         // no window yet
   p.ring = s_ring;
   p.out = out + out_off[f];
-  p.cap = out_cap[f];
+  // 32-bit positions (DevP): a stream or an output of 2^31 bytes or more is
+  // left to the host path (status E_SPACE, as for any output that overflows)
+  const bool fits = in_len[f] + skew + 512 < ((int64_t)1 << 31);
+  p.cap = (int32_t)min(out_cap[f], (int64_t)0x7fffff00);
   p.pos = p.flushed = p.mstart = 0;
   p.mem = mem + (int64_t)f * mcap;
   p.nmem = 0;
@@ -420,7 +428,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GRID_INFLATE
   p.wbase = -1;
   icore::Inflater<DevP> inf(p);
   inf.ip = skew;
-  const int rc = in_len[f] > 0 ? inf.gunzip() : (int)icore::E_HEADER;
+  const int rc = !fits ? (int)icore::E_SPACE : in_len[f] > 0 ? inf.gunzip() : (int)icore::E_HEADER;
   p.flush_full();
   p.flush_tail();
   if (threadIdx.x == 0) {
