@@ -69,7 +69,7 @@ HOST_FRAC = float(os.environ.get("GRID_INGEST_HOST_FRAC", "0.25"))
 # threads (the r04ae optimum) gives H ~ 0.77 GB/s at G ~ 37 GB/s.  Below one file
 # in 20 the share does not pay for its copies and CRC check: none
 HOST_RATE_PER_THREAD = 0.77e9
-GPU_INFLATE_RATE = 37e9
+GPU_INFLATE_RATE = 39e9          # r05x: BGZF members, 32-bit decode state
 # file reads and member tables: a pool of their own, independent of `threads`
 READ_THREADS = int(os.environ.get("GRID_INGEST_READ_THREADS", "8"))
 

@@ -4,7 +4,7 @@
 # the 7-wave build, interleaved
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r05x
+O=gpurun_out/${RUN:-r05x}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider \
