@@ -13,10 +13,9 @@
 // windows held in one VGPR each (lane k holds bytes 4k..4k+3).  The bit-level
 // decoder is inflate_core.hpp (headers, tables, stored blocks, the last
 // symbols of a stream); a block's codes run in fast_codes below: 64-bit bit
-// buffer refilled 8 bytes at a time from two windows (the next one loaded
-// ahead), one u32 table entry per literal/length or distance code that
-// carries the base and extra-bit count, literals written to the ring 8 at a
-// time, copies without a division.
+// buffer refilled 8 bytes at a time from a 256-B window held one word per
+// lane, one u32 table entry per literal/length or distance code that carries
+// the base and extra-bit count, copies without a division.
 //
 // k_gz_crc: one workgroup per file checks every member's CRC-32 and size
 // (gzip's trailer): lanes compute the raw CRC register of 256 byte ranges
@@ -87,7 +86,7 @@ struct DevP {
   int nmem, mcap, lane;
   uint32_t win;                  // core input window: lane k = bytes wbase + 4k .. + 3
   int64_t wbase;
-  uint32_t fcur, fnxt;           // fast_codes' windows: bytes fbase .. +256, +256 .. +512
+  uint32_t fcur;                 // fast_codes' input window: bytes fbase .. +256 (lane k: 4k..4k+3)
   int32_t fbase;
 
   __device__ __forceinline__ uint32_t load_word(int64_t b) const {
@@ -215,22 +214,31 @@ struct DevP {
     if (pos - flushed >= FLUSH) flush_full();
     return 0;
   }
-  __device__ __forceinline__ void put_lits(uint64_t lit, int n) {   // n bytes at pos
-    if (lane < n) ring[(pos + lane) & RMASK] = (uint8_t)(lit >> (8 * lane));
-    __builtin_amdgcn_wave_barrier();
-    pos += n;
-  }
-  __device__ __forceinline__ uint32_t fword(int i) const {   // word i of fcur|fnxt, i < 128
-    return (uint32_t)(i < 64 ? __builtin_amdgcn_readlane((int)fcur, i) : __builtin_amdgcn_readlane((int)fnxt, i - 64));
-  }
 
-  // everything but a fast literal, for fast_codes: false = leave the loop
-  // (ret: 1 end of block, -1 error, 0 out of room)
+
+
+  // A block's codes while >= 16 input bytes and >= 296 bytes of output room
+  // remain.  Returns 1 after the end-of-block code, -1 on an error (err set),
+  // 0 when the core's per-symbol loop must finish the block.  The decode
+  // state is wave-uniform and the CU's one scalar unit bounds the kernel
+  // (r05w: 98 % of cycles issue a scalar instruction), so the loop is flat:
+  // one test per exit, a literal goes to the ring at once (every lane stores
+  // the same byte: no exec mask), the input window is one 256-B VGPR reloaded
+  // in place (a wave decodes ~100 us per window: the load's latency is
+  // nothing), and the 64-bit funnel of the refill has no branch.  Every
+  // iteration starts with >= 48 bits in bb, enough for the longest symbol
+  // pair (15 + 5 length bits, 15 + 13 distance bits).
   template <class I>
-  __device__ __forceinline__ bool nonlit(I &inf, uint32_t e, uint64_t &bb, int &bc, uint64_t &lit, int &nl,
-                                         int &ret) {
+  __device__ int fast_codes(I &inf) {
+    const int room = cap - 296;
+    if (pos > room) return 0;
+    int ip = (int)inf.ip;
+    const int nin = (int)n_in;
+    uint64_t bb = inf.bb;
+    int bc = inf.bc, ret = 0, flush_at = flushed + FLUSH;
     auto slow = [&](int co, int so) -> int {   // puff's canonical walk (-1: no such code)
       int code = 0, first = 0, index = 0;
+#pragma unroll 1
       for (int l = 1; l < 16; l++) {
         code |= (int)(bb & 1);
         bb >>= 1;
@@ -244,124 +252,87 @@ struct DevP {
       }
       return -1;
     };
-    const uint32_t kind = (e >> 4) & 15;
-    uint32_t len;
-    if (kind == K_LEN) {
-      const int l = e & 15, x = (e >> 8) & 7;
-      len = (e >> 16) + (uint32_t)((bb >> l) & ((1u << x) - 1));
-      bb >>= l + x;
-      bc -= l + x;
-    } else if (kind == K_EOB) {
-      const int l = e & 15;
-      bb >>= l;
-      bc -= l;
-      ret = 1;
-      return false;
-    } else {                            // a code longer than LFAST bits, or 286/287
-      const int sym = slow(icore::T_LCNT, icore::T_LSYM);
-      if (sym < 0 || sym > 285) { inf.err = icore::E_DATA; ret = -1; return false; }
-      if (sym == 256) { ret = 1; return false; }
-      if (sym < 256) {
-        lit |= (uint64_t)sym << (8 * nl);
-        if (++nl == 8) {
-          put_lits(lit, 8);
-          lit = 0;
-          nl = 0;
-          if (pos - flushed >= FLUSH) flush_full();
-          return pos + 296 <= cap;
-        }
-        return true;
-      }
-      const int x = icore::kLenExtra[sym - 257];
-      len = icore::kLenBase[sym - 257] + (uint32_t)(bb & ((1u << x) - 1));
-      bb >>= x;
-      bc -= x;
-    }
-    const uint32_t d = ftab_rd(F_LEN + (int)(bb & (F_DIST - 1)));
-    uint32_t dist;
-    if (((d >> 4) & 15) == K_DIST) {
-      const int l = d & 15, x = (d >> 8) & 15;
-      dist = (d >> 17) + (uint32_t)((bb >> l) & ((1u << x) - 1));
-      bb >>= l + x;
-      bc -= l + x;
-    } else {
-      const int ds = slow(icore::T_DCNT, icore::T_DSYM);
-      if (ds < 0 || ds >= 30) { inf.err = icore::E_DATA; ret = -1; return false; }
-      const int x = icore::kDistExtra[ds];
-      dist = icore::kDistBase[ds] + (uint32_t)(bb & ((1u << x) - 1));
-      bb >>= x;
-      bc -= x;
-    }
-    if (nl) {
-      put_lits(lit, nl);
-      lit = 0;
-      nl = 0;
-    }
-    if (dist > (uint32_t)(pos - mstart)) { inf.err = icore::E_DATA; ret = -1; return false; }
-    copy_bytes(dist, len);
-    if (pos - flushed >= FLUSH) flush_full();
-    return pos + 296 <= cap;
-  }
-
-  // A block's codes while >= 16 input bytes and >= 296 bytes of output room
-  // remain.  Returns 1 after the end-of-block code, -1 on an error (err set),
-  // 0 when the core's per-symbol loop must finish the block.  Literals wait
-  // in `lit` (8 at most) and reach the ring together; pos excludes them.
-  // Self-contained (no call into the core: its state would crowd the scalar
-  // registers of this loop): every iteration starts with >= 48 bits in bb,
-  // enough for the longest symbol (15 + 5 length bits, 15 + 13 distance).
-  template <class I>
-  __device__ int fast_codes(I &inf) {
-    if (pos + 296 > cap) return 0;
-    int ip = (int)inf.ip;
-    if (ip - fbase < 0 || ip - fbase >= 256) {
-      fbase = ip & ~255;
-      fcur = load_word(fbase);
-      fnxt = load_word(fbase + 256);
-    }
-    uint64_t bb = inf.bb, lit = 0;
-    int bc = inf.bc, nl = 0, ret = 0;
-    const int nin = (int)n_in;
-    // one loop, one exit (`go`): the literal path goes straight back to the
-    // top, everything else is rarer
-    bool go = true;
-    while (go) {
+    for (;;) {
       if (bc < 48) {                    // 8 more bytes, of which (63 - bc) / 8 are kept
-        if (ip + 16 > nin) {
-          go = false;
-          continue;
+        if (ip + 16 > nin) break;
+        int r = ip - fbase;
+        if ((unsigned)r > 244u) {       // words i..i+2 must lie in the window
+          fbase = ip & ~3;
+          fcur = load_word(fbase);
+          r = ip - fbase;
         }
-        if (ip - fbase >= 256) {         // ip moved < 256 since the last refill
-          fbase += 256;
-          fcur = fnxt;
-          fnxt = load_word(fbase + 256);
-        }
-        const int r = ip - fbase, i = r >> 2, sh = (r & 3) * 8;
-        const uint64_t lo = (uint64_t)fword(i) | ((uint64_t)fword(i + 1) << 32);
-        const uint64_t v = sh ? (lo >> sh) | ((uint64_t)fword(i + 2) << (64 - sh)) : lo;
+        const int i = r >> 2, sh = (r & 3) * 8;
+        const uint64_t lo = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)fcur, i) |
+                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)fcur, i + 1) << 32);
+        const uint64_t w2 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)fcur, i + 2);
+        const uint64_t v = (lo >> sh) | ((w2 << 1) << (63 - sh));   // sh = 0: the second term is 0
         bb |= v << bc;
         const int take = (63 - bc) >> 3;
         ip += take;
         bc += take * 8;
       }
       const uint32_t e = ftab_rd((int)(bb & (F_LEN - 1)));
-      if (((e >> 4) & 15) == K_LIT) {
+      const uint32_t kind = (e >> 4) & 15;
+      uint32_t len;
+      if (kind == K_LIT) {
         const int l = e & 15;
         bb >>= l;
         bc -= l;
-        lit |= (uint64_t)(e >> 16) << (8 * nl);
-        if (++nl == 8) {
-          put_lits(lit, 8);
-          lit = 0;
-          nl = 0;
-          if (pos - flushed >= FLUSH) flush_full();
-          go = pos + 296 <= cap;
-        }
+        ring[pos & RMASK] = (uint8_t)(e >> 16);
+        __builtin_amdgcn_wave_barrier();
+        pos++;
+        if (pos >= flush_at) { flush_full(); flush_at = flushed + FLUSH; }
+        if (pos > room) break;
         continue;
       }
-      go = nonlit(inf, e, bb, bc, lit, nl, ret);
+      if (kind == K_LEN) {
+        const int l = e & 15, x = (e >> 8) & 7;
+        len = (e >> 16) + ((uint32_t)(bb >> l) & ((1u << x) - 1));
+        bb >>= l + x;
+        bc -= l + x;
+      } else if (kind == K_EOB) {
+        const int l = e & 15;
+        bb >>= l;
+        bc -= l;
+        ret = 1;
+        break;
+      } else {                          // a code longer than LFAST bits, or 286/287
+        const int sym = slow(icore::T_LCNT, icore::T_LSYM);
+        if (sym < 0 || sym > 285) { inf.err = icore::E_DATA; ret = -1; break; }
+        if (sym == 256) { ret = 1; break; }
+        if (sym < 256) {
+          ring[pos & RMASK] = (uint8_t)sym;
+          __builtin_amdgcn_wave_barrier();
+          pos++;
+          if (pos >= flush_at) { flush_full(); flush_at = flushed + FLUSH; }
+          if (pos > room) break;
+          continue;
+        }
+        const int x = icore::kLenExtra[sym - 257];
+        len = icore::kLenBase[sym - 257] + (uint32_t)(bb & ((1u << x) - 1));
+        bb >>= x;
+        bc -= x;
+      }
+      const uint32_t d = ftab_rd(F_LEN + (int)(bb & (F_DIST - 1)));
+      uint32_t dist;
+      if (((d >> 4) & 15) == K_DIST) {
+        const int l = d & 15, x = (d >> 8) & 15;
+        dist = (d >> 17) + (uint32_t)((bb >> l) & ((1u << x) - 1));
+        bb >>= l + x;
+        bc -= l + x;
+      } else {
+        const int ds = slow(icore::T_DCNT, icore::T_DSYM);
+        if (ds < 0 || ds >= 30) { inf.err = icore::E_DATA; ret = -1; break; }
+        const int x = icore::kDistExtra[ds];
+        dist = icore::kDistBase[ds] + (uint32_t)(bb & ((1u << x) - 1));
+        bb >>= x;
+        bc -= x;
+      }
+      if (dist > (uint32_t)(pos - mstart)) { inf.err = icore::E_DATA; ret = -1; break; }
+      copy_bytes(dist, len);
+      if (pos >= flush_at) { flush_full(); flush_at = flushed + FLUSH; }
+      if (pos > room) break;
     }
-    if (nl) put_lits(lit, nl);
     inf.bb = bb;
     inf.bc = bc;
     inf.ip = ip;
