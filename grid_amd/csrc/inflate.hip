@@ -221,27 +221,34 @@ struct DevP {
   // remain.  Returns 1 after the end-of-block code, -1 on an error (err set),
   // 0 when the core's per-symbol loop must finish the block.  The decode
   // state is wave-uniform and the CU's one scalar unit bounds the kernel
-  // (r05w: 98 % of cycles issue a scalar instruction), so the loop is flat:
+  // (r05w: 98 % of cycles issue a scalar instruction; the vector units ~7 %
+  // busy), so the loop splits its work between the two: the bit buffer lives
+  // in a VGPR pair (uniform, but the vector ALU shifts it, extracts the extra
+  // bits and forms the table addresses), and only what steers control or
+  // addresses the ring comes back to scalar registers (readfirstlane).  Flat:
   // one test per exit, a literal goes to the ring at once (every lane stores
-  // the same byte: no exec mask), the input window is one 256-B VGPR reloaded
-  // in place (a wave decodes ~100 us per window: the load's latency is
-  // nothing), and the 64-bit funnel of the refill has no branch.  Every
-  // iteration starts with >= 48 bits in bb, enough for the longest symbol
-  // pair (15 + 5 length bits, 15 + 13 distance bits).
+  // the same byte: no exec mask), the input window is one 256-B VGPR
+  // reloaded in place (a wave decodes ~100 us per window: the load's latency
+  // is nothing).  Every iteration starts with >= 48 bits in the buffer,
+  // enough for the longest symbol pair (15 + 5 length bits, 15 + 13 distance).
   template <class I>
   __device__ int fast_codes(I &inf) {
     const int room = cap - 296;
     if (pos > room) return 0;
     int ip = (int)inf.ip;
     const int nin = (int)n_in;
-    uint64_t bb = inf.bb;
+    uint64_t vb;                        // the bit buffer, in VGPRs
+    asm volatile("v_mov_b64 %0, %1" : "=v"(vb) : "s"(inf.bb));
     int bc = inf.bc, ret = 0, flush_at = flushed + FLUSH;
+    auto low = [&](int sh) -> uint32_t {   // bits [sh, sh + 32) of the buffer (sh < 32)
+      return __builtin_amdgcn_alignbit((uint32_t)(vb >> 32), (uint32_t)vb, (uint32_t)sh);
+    };
     auto slow = [&](int co, int so) -> int {   // puff's canonical walk (-1: no such code)
       int code = 0, first = 0, index = 0;
 #pragma unroll 1
       for (int l = 1; l < 16; l++) {
-        code |= (int)(bb & 1);
-        bb >>= 1;
+        code |= __builtin_amdgcn_readfirstlane((int)((uint32_t)vb & 1u));
+        vb >>= 1;
         bc--;
         const int count = rd(co + l);
         if (code - count < first) return rd(so + index + (code - first));
@@ -251,6 +258,12 @@ struct DevP {
         code <<= 1;
       }
       return -1;
+    };
+    auto extra = [&](int n) -> uint32_t {  // the next n <= 13 bits, consumed
+      const uint32_t v = __builtin_amdgcn_ubfe((uint32_t)vb, 0u, (uint32_t)n);
+      vb >>= n;
+      bc -= n;
+      return v;
     };
     for (;;) {
       if (bc < 48) {                    // 8 more bytes, of which (63 - bc) / 8 are kept
@@ -262,21 +275,26 @@ struct DevP {
           r = ip - fbase;
         }
         const int i = r >> 2, sh = (r & 3) * 8;
-        const uint64_t lo = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)fcur, i) |
-                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)fcur, i + 1) << 32);
-        const uint64_t w2 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)fcur, i + 2);
-        const uint64_t v = (lo >> sh) | ((w2 << 1) << (63 - sh));   // sh = 0: the second term is 0
-        bb |= v << bc;
+        const uint32_t w0 = (uint32_t)__builtin_amdgcn_readlane((int)fcur, i);
+        const uint32_t w1 = (uint32_t)__builtin_amdgcn_readlane((int)fcur, i + 1);
+        const uint32_t w2 = (uint32_t)__builtin_amdgcn_readlane((int)fcur, i + 2);
+        // the 8 input bytes from byte sh of w0 (vector funnel shifts)
+        uint64_t v;
+        asm volatile("v_mov_b64 %0, %1" : "=v"(v) : "s"(((uint64_t)w1 << 32) | w0));
+        const uint32_t vlo = __builtin_amdgcn_alignbit((uint32_t)(v >> 32), (uint32_t)v, (uint32_t)sh);
+        const uint32_t vhi = __builtin_amdgcn_alignbit(w2, (uint32_t)(v >> 32), (uint32_t)sh);
+        vb |= (((uint64_t)vhi << 32) | vlo) << bc;
         const int take = (63 - bc) >> 3;
         ip += take;
         bc += take * 8;
       }
-      const uint32_t e = ftab_rd((int)(bb & (F_LEN - 1)));
-      const uint32_t kind = (e >> 4) & 15;
+      const uint32_t e =
+          (uint32_t)__builtin_amdgcn_readfirstlane((int)ftab[(uint32_t)vb & (uint32_t)(F_LEN - 1)]);
+      const uint32_t kind = e & 0xf0u;
       uint32_t len;
-      if (kind == K_LIT) {
+      if (kind == (K_LIT << 4)) {
         const int l = e & 15;
-        bb >>= l;
+        vb >>= l;
         bc -= l;
         ring[pos & RMASK] = (uint8_t)(e >> 16);
         __builtin_amdgcn_wave_barrier();
@@ -285,14 +303,15 @@ struct DevP {
         if (pos > room) break;
         continue;
       }
-      if (kind == K_LEN) {
+      if (kind == (K_LEN << 4)) {
         const int l = e & 15, x = (e >> 8) & 7;
-        len = (e >> 16) + ((uint32_t)(bb >> l) & ((1u << x) - 1));
-        bb >>= l + x;
+        const uint32_t xb = __builtin_amdgcn_ubfe(low(l), 0u, (uint32_t)x);
+        len = (uint32_t)__builtin_amdgcn_readfirstlane((int)((e >> 16) + xb));
+        vb >>= l + x;
         bc -= l + x;
-      } else if (kind == K_EOB) {
+      } else if (kind == (K_EOB << 4)) {
         const int l = e & 15;
-        bb >>= l;
+        vb >>= l;
         bc -= l;
         ret = 1;
         break;
@@ -309,31 +328,30 @@ struct DevP {
           continue;
         }
         const int x = icore::kLenExtra[sym - 257];
-        len = icore::kLenBase[sym - 257] + (uint32_t)(bb & ((1u << x) - 1));
-        bb >>= x;
-        bc -= x;
+        len = icore::kLenBase[sym - 257] + (uint32_t)__builtin_amdgcn_readfirstlane((int)extra(x));
       }
-      const uint32_t d = ftab_rd(F_LEN + (int)(bb & (F_DIST - 1)));
+      const uint32_t d = (uint32_t)__builtin_amdgcn_readfirstlane(
+          (int)ftab[F_LEN + ((uint32_t)vb & (uint32_t)(F_DIST - 1))]);
       uint32_t dist;
-      if (((d >> 4) & 15) == K_DIST) {
+      if ((d & 0xf0u) == (K_DIST << 4)) {
         const int l = d & 15, x = (d >> 8) & 15;
-        dist = (d >> 17) + (uint32_t)((bb >> l) & ((1u << x) - 1));
-        bb >>= l + x;
+        const uint32_t xb = __builtin_amdgcn_ubfe(low(l), 0u, (uint32_t)x);
+        dist = (uint32_t)__builtin_amdgcn_readfirstlane((int)((d >> 17) + xb));
+        vb >>= l + x;
         bc -= l + x;
       } else {
         const int ds = slow(icore::T_DCNT, icore::T_DSYM);
         if (ds < 0 || ds >= 30) { inf.err = icore::E_DATA; ret = -1; break; }
         const int x = icore::kDistExtra[ds];
-        dist = icore::kDistBase[ds] + (uint32_t)(bb & ((1u << x) - 1));
-        bb >>= x;
-        bc -= x;
+        dist = icore::kDistBase[ds] + (uint32_t)__builtin_amdgcn_readfirstlane((int)extra(x));
       }
       if (dist > (uint32_t)(pos - mstart)) { inf.err = icore::E_DATA; ret = -1; break; }
       copy_bytes(dist, len);
       if (pos >= flush_at) { flush_full(); flush_at = flushed + FLUSH; }
       if (pos > room) break;
     }
-    inf.bb = bb;
+    inf.bb = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(vb >> 32)) << 32) |
+             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)vb);
     inf.bc = bc;
     inf.ip = ip;
     return ret;

@@ -3,7 +3,7 @@
 # member inflate (bench_inflate --bgzf --units), one PMC pass, beside the plain timing
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r05w
+O=gpurun_out/${RUN:-r05w}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 300 python -u tools/bench_inflate.py --bgzf --units --files 128 --json $O/inflate.json > $O/inflate.log 2>&1 \
