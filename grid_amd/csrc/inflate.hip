@@ -197,13 +197,23 @@ struct DevP {
       return;
     }
     const float rdist = __builtin_amdgcn_rcpf((float)dist);
-    for (uint32_t k0 = 0; k0 < len; k0 += 64) {
-      const uint32_t k = k0 + lane;
-      if (k < len) {
-        const uint32_t j = dist >= len ? k : k - dist * (uint32_t)(((float)k + 0.5f) * rdist);
-        ring[(pos + k) & RMASK] = ring[(s0 + j) & RMASK];
-      }
+    // the first 64 bytes: every lane moves one, unmasked -- lanes k >= len
+    // write bytes pos + k that a later symbol overwrites before anything reads
+    // them (their ring slots, 1985-2048 bytes back, are flushed and beyond
+    // NEAR), and for k < len <= dist the quotient below is 0 (j = k)
+    {
+      const uint32_t k = (uint32_t)lane;
+      const uint32_t j = k - dist * (uint32_t)(((float)k + 0.5f) * rdist);
+      ring[(pos + (int)k) & RMASK] = ring[(s0 + (int)j) & RMASK];
     }
+    if (len > 64)
+      for (uint32_t k0 = 64; k0 < len; k0 += 64) {
+        const uint32_t k = k0 + lane;
+        if (k < len) {
+          const uint32_t j = dist >= len ? k : k - dist * (uint32_t)(((float)k + 0.5f) * rdist);
+          ring[(pos + (int)k) & RMASK] = ring[(s0 + (int)j) & RMASK];
+        }
+      }
     __builtin_amdgcn_wave_barrier();
     pos += len;
   }
@@ -265,6 +275,19 @@ struct DevP {
       bc -= n;
       return v;
     };
+    // one limit per symbol: the next flush or the end of the output room
+    int lim = min(flush_at, room + 1);
+    // a near copy's distance beyond the member's output reads only ring
+    // bytes, so it is tested on the vector unit and reported at the exit
+    uint32_t verr = 0;
+    auto limit = [&]() -> bool {        // false: out of room
+      if (pos >= flush_at) {
+        flush_full();
+        flush_at = flushed + FLUSH;
+      }
+      lim = min(flush_at, room + 1);
+      return pos <= room;
+    };
     for (;;) {
       if (bc < 48) {                    // 8 more bytes, of which (63 - bc) / 8 are kept
         if (ip + 16 > nin) break;
@@ -288,27 +311,28 @@ struct DevP {
         ip += take;
         bc += take * 8;
       }
-      const uint32_t e =
-          (uint32_t)__builtin_amdgcn_readfirstlane((int)ftab[(uint32_t)vb & (uint32_t)(F_LEN - 1)]);
+      // the entry stays in a VGPR (its fields are cut on the vector unit);
+      // a scalar copy steers
+      const uint32_t ev = ftab[(uint32_t)vb & (uint32_t)(F_LEN - 1)];
+      const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane((int)ev);
       const uint32_t kind = e & 0xf0u;
       uint32_t len;
-      if (kind == (K_LIT << 4)) {
-        const int l = e & 15;
-        vb >>= l;
-        bc -= l;
-        ring[pos & RMASK] = (uint8_t)(e >> 16);
+      if (kind == (K_LEN << 4)) {
+        const uint32_t lv = ev & 15u, xv = (ev >> 8) & 7u, lxv = lv + xv;
+        const uint32_t xb = __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit((uint32_t)(vb >> 32), (uint32_t)vb, lv),
+                                                  0u, xv);
+        len = (uint32_t)__builtin_amdgcn_readfirstlane((int)((ev >> 16) + xb));
+        vb >>= lxv;
+        bc -= __builtin_amdgcn_readfirstlane((int)lxv);
+      } else if (kind == (K_LIT << 4)) {
+        const uint32_t lv = ev & 15u;
+        vb >>= lv;
+        bc -= __builtin_amdgcn_readfirstlane((int)lv);
+        ring[pos & RMASK] = (uint8_t)(ev >> 16);
         __builtin_amdgcn_wave_barrier();
         pos++;
-        if (pos >= flush_at) { flush_full(); flush_at = flushed + FLUSH; }
-        if (pos > room) break;
+        if (pos >= lim && !limit()) break;
         continue;
-      }
-      if (kind == (K_LEN << 4)) {
-        const int l = e & 15, x = (e >> 8) & 7;
-        const uint32_t xb = __builtin_amdgcn_ubfe(low(l), 0u, (uint32_t)x);
-        len = (uint32_t)__builtin_amdgcn_readfirstlane((int)((e >> 16) + xb));
-        vb >>= l + x;
-        bc -= l + x;
       } else if (kind == (K_EOB << 4)) {
         const int l = e & 15;
         vb >>= l;
@@ -323,33 +347,39 @@ struct DevP {
           ring[pos & RMASK] = (uint8_t)sym;
           __builtin_amdgcn_wave_barrier();
           pos++;
-          if (pos >= flush_at) { flush_full(); flush_at = flushed + FLUSH; }
-          if (pos > room) break;
+          if (pos >= lim && !limit()) break;
           continue;
         }
         const int x = icore::kLenExtra[sym - 257];
         len = icore::kLenBase[sym - 257] + (uint32_t)__builtin_amdgcn_readfirstlane((int)extra(x));
       }
-      const uint32_t d = (uint32_t)__builtin_amdgcn_readfirstlane(
-          (int)ftab[F_LEN + ((uint32_t)vb & (uint32_t)(F_DIST - 1))]);
-      uint32_t dist;
+      const uint32_t dv = ftab[F_LEN + ((uint32_t)vb & (uint32_t)(F_DIST - 1))];
+      const uint32_t d = (uint32_t)__builtin_amdgcn_readfirstlane((int)dv);
+      uint32_t dist, distv;
       if ((d & 0xf0u) == (K_DIST << 4)) {
-        const int l = d & 15, x = (d >> 8) & 15;
-        const uint32_t xb = __builtin_amdgcn_ubfe(low(l), 0u, (uint32_t)x);
-        dist = (uint32_t)__builtin_amdgcn_readfirstlane((int)((d >> 17) + xb));
-        vb >>= l + x;
-        bc -= l + x;
+        const uint32_t lv = dv & 15u, xv = (dv >> 8) & 15u, lxv = lv + xv;
+        const uint32_t xb = __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit((uint32_t)(vb >> 32), (uint32_t)vb, lv),
+                                                  0u, xv);
+        distv = (dv >> 17) + xb;
+        dist = (uint32_t)__builtin_amdgcn_readfirstlane((int)distv);
+        vb >>= lxv;
+        bc -= __builtin_amdgcn_readfirstlane((int)lxv);
       } else {
         const int ds = slow(icore::T_DCNT, icore::T_DSYM);
         if (ds < 0 || ds >= 30) { inf.err = icore::E_DATA; ret = -1; break; }
         const int x = icore::kDistExtra[ds];
         dist = icore::kDistBase[ds] + (uint32_t)__builtin_amdgcn_readfirstlane((int)extra(x));
+        distv = dist;
       }
-      if (dist > (uint32_t)(pos - mstart)) { inf.err = icore::E_DATA; ret = -1; break; }
+      if (dist > (uint32_t)NEAR) {      // a far copy reads HBM: test it here
+        if (dist > (uint32_t)(pos - mstart)) { inf.err = icore::E_DATA; ret = -1; break; }
+      } else {
+        verr |= distv > (uint32_t)(pos - mstart) ? 1u : 0u;
+      }
       copy_bytes(dist, len);
-      if (pos >= flush_at) { flush_full(); flush_at = flushed + FLUSH; }
-      if (pos > room) break;
+      if (pos >= lim && !limit()) break;
     }
+    if (ret >= 0 && __builtin_amdgcn_readfirstlane((int)verr)) { inf.err = icore::E_DATA; ret = -1; }
     inf.bb = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(vb >> 32)) << 32) |
              (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)vb);
     inf.bc = bc;
