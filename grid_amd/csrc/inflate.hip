@@ -288,28 +288,34 @@ struct DevP {
       lim = min(flush_at, room + 1);
       return pos <= room;
     };
+    // the input position as an offset r into the window at fbase; one test
+    // per refill: r > rmax means the window must move, or the input is
+    // within 16 bytes of its end (the core finishes the block)
+    int r = ip - fbase, rmax = min(244, nin - 16 - fbase);
     for (;;) {
-      if (bc < 48) {                    // 8 more bytes, of which (63 - bc) / 8 are kept
-        if (ip + 16 > nin) break;
-        int r = ip - fbase;
-        if ((unsigned)r > 244u) {       // words i..i+2 must lie in the window
+      if (bc < 48) {                    // 8 more bytes, of which 7 - bc / 8 are kept (libdeflate's refill)
+        if (r > rmax || r < 0) {
+          ip = fbase + r;
+          if (ip + 16 > nin) break;
           fbase = ip & ~3;
           fcur = load_word(fbase);
           r = ip - fbase;
+          rmax = min(244, nin - 16 - fbase);
         }
-        const int i = r >> 2, sh = (r & 3) * 8;
-        const uint32_t w0 = (uint32_t)__builtin_amdgcn_readlane((int)fcur, i);
-        const uint32_t w1 = (uint32_t)__builtin_amdgcn_readlane((int)fcur, i + 1);
-        const uint32_t w2 = (uint32_t)__builtin_amdgcn_readlane((int)fcur, i + 2);
-        // the 8 input bytes from byte sh of w0 (vector funnel shifts)
-        uint64_t v;
-        asm volatile("v_mov_b64 %0, %1" : "=v"(v) : "s"(((uint64_t)w1 << 32) | w0));
-        const uint32_t vlo = __builtin_amdgcn_alignbit((uint32_t)(v >> 32), (uint32_t)v, (uint32_t)sh);
-        const uint32_t vhi = __builtin_amdgcn_alignbit(w2, (uint32_t)(v >> 32), (uint32_t)sh);
+        // words i..i+2 of the window broadcast by the LDS crossbar, the 8
+        // bytes from byte r & 3 of word i funnelled out: vector work
+        uint32_t rv;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(rv) : "s"(r));
+        const int a = (int)(rv & ~3u);
+        const uint32_t w0 = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)fcur);
+        const uint32_t w1 = (uint32_t)__builtin_amdgcn_ds_bpermute(a + 4, (int)fcur);
+        const uint32_t w2 = (uint32_t)__builtin_amdgcn_ds_bpermute(a + 8, (int)fcur);
+        const uint32_t shv = (rv & 3u) * 8u;
+        const uint32_t vlo = __builtin_amdgcn_alignbit(w1, w0, shv);
+        const uint32_t vhi = __builtin_amdgcn_alignbit(w2, w1, shv);
         vb |= (((uint64_t)vhi << 32) | vlo) << bc;
-        const int take = (63 - bc) >> 3;
-        ip += take;
-        bc += take * 8;
+        r += 7 - (bc >> 3);
+        bc |= 56;
       }
       // the entry stays in a VGPR (its fields are cut on the vector unit);
       // a scalar copy steers
@@ -380,6 +386,7 @@ struct DevP {
       if (pos >= lim && !limit()) break;
     }
     if (ret >= 0 && __builtin_amdgcn_readfirstlane((int)verr)) { inf.err = icore::E_DATA; ret = -1; }
+    ip = fbase + r;
     inf.bb = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(vb >> 32)) << 32) |
              (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)vb);
     inf.bc = bc;
