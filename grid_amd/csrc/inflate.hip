@@ -51,7 +51,9 @@ __constant__ uint32_t c_crc_pow[48][32];   // columns of M^(2^k), M = one zero b
 //   [31:17] distance base, [16:12] symbol, [11:8] extra bits, [7:4] kind,
 //   [3:0] code length
 // kind 0 = a symbol the fast loop does not take (286, 287, distance 30, 31)
-constexpr uint32_t K_LIT = 1, K_LEN = 2, K_EOB = 3, K_DIST = 1;
+// K_LEN is the only kind with bit 5 of the entry set (the fast loop's one-bit
+// test for its commonest symbol: a match length); K_DIST has bit 4
+constexpr uint32_t K_LIT = 1, K_LEN = 2, K_EOB = 4, K_DIST = 1;
 constexpr int F_LEN = 1 << icore::LFAST, F_DIST = 1 << icore::DFAST;
 
 __device__ __forceinline__ uint32_t fast_entry(int ft, uint32_t sym, uint32_t l) {
@@ -323,7 +325,7 @@ struct DevP {
       const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane((int)ev);
       const uint32_t kind = e & 0xf0u;
       uint32_t len;
-      if (kind == (K_LEN << 4)) {
+      if (__builtin_expect((e & (K_LEN << 4)) != 0, 1)) {
         const uint32_t lv = ev & 15u, xv = (ev >> 8) & 7u, lxv = lv + xv;
         const uint32_t xb = __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit((uint32_t)(vb >> 32), (uint32_t)vb, lv),
                                                   0u, xv);
@@ -362,7 +364,7 @@ struct DevP {
       const uint32_t dv = ftab[F_LEN + ((uint32_t)vb & (uint32_t)(F_DIST - 1))];
       const uint32_t d = (uint32_t)__builtin_amdgcn_readfirstlane((int)dv);
       uint32_t dist, distv;
-      if ((d & 0xf0u) == (K_DIST << 4)) {
+      if (__builtin_expect((d & (K_DIST << 4)) != 0, 1)) {
         const uint32_t lv = dv & 15u, xv = (dv >> 8) & 15u, lxv = lv + xv;
         const uint32_t xb = __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit((uint32_t)(vb >> 32), (uint32_t)vb, lv),
                                                   0u, xv);
