@@ -66,10 +66,14 @@ HOST_FRAC = float(os.environ.get("GRID_INGEST_HOST_FRAC", "0.25"))
 # reference defaults to 1 thread, its example config uses 4): the host files
 # take as long as the GPU's when f / (t H) = (1 - f) / G, so f = t H / (G + t H)
 # with H one thread's inflate rate beside the GPU and G the GPU's; 0.25 at 16
-# threads (the r04ae optimum) gives H ~ 0.77 GB/s at G ~ 37 GB/s.  Below one file
-# in 20 the share does not pay for its copies and CRC check: none
+# threads (the r04ae optimum) gives H ~ 0.77 GB/s at G ~ 37 GB/s.  Round 5's
+# inflate runs at G ~ 63 GB/s (r05ag), where the model's 16 % at 16 threads
+# measured slower than none (config 2 ingest 6.34 vs 6.04 s, r05ah: the host
+# reads, copies and checks its files beside the batch and they no longer hide
+# under the GPU's part); below one file in 5 the share is not used
 HOST_RATE_PER_THREAD = 0.77e9
-GPU_INFLATE_RATE = 39e9          # r05x: BGZF members, 32-bit decode state
+GPU_INFLATE_RATE = 63e9          # r05ag: BGZF members (tools/bench_inflate.py --bgzf --units)
+HOST_FRAC_MIN = 0.2
 # file reads and member tables: a pool of their own, independent of `threads`
 READ_THREADS = int(os.environ.get("GRID_INGEST_READ_THREADS", "8"))
 
@@ -79,7 +83,7 @@ def host_frac(threads):
     t = max(1, int(threads))
     f = t * HOST_RATE_PER_THREAD / (GPU_INFLATE_RATE + t * HOST_RATE_PER_THREAD)
     f = min(f, HOST_FRAC)
-    return f if f >= 0.05 else 0.0
+    return f if f >= HOST_FRAC_MIN else 0.0
 
 
 class DeviceIngestUnsupported(Exception):
