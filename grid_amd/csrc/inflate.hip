@@ -198,17 +198,21 @@ struct DevP {
       pos += len;
       return;
     }
-    const float rdist = __builtin_amdgcn_rcpf((float)dist);
     // the first 64 bytes: every lane moves one, unmasked -- lanes k >= len
     // write bytes pos + k that a later symbol overwrites before anything reads
     // them (their ring slots, 1985-2048 bytes back, are flushed and beyond
-    // NEAR), and for k < len <= dist the quotient below is 0 (j = k)
-    {
+    // NEAR).  Without overlap (the common case) byte k comes from s0 + k: no
+    // division on the common path
+    if (dist >= len) {
+      ring[(pos + lane) & RMASK] = ring[(s0 + lane) & RMASK];
+    } else {
+      const float rdist = __builtin_amdgcn_rcpf((float)dist);
       const uint32_t k = (uint32_t)lane;
       const uint32_t j = k - dist * (uint32_t)(((float)k + 0.5f) * rdist);
       ring[(pos + (int)k) & RMASK] = ring[(s0 + (int)j) & RMASK];
     }
-    if (len > 64)
+    if (len > 64) {
+      const float rdist = __builtin_amdgcn_rcpf((float)dist);
       for (uint32_t k0 = 64; k0 < len; k0 += 64) {
         const uint32_t k = k0 + lane;
         if (k < len) {
@@ -216,6 +220,7 @@ struct DevP {
           ring[(pos + (int)k) & RMASK] = ring[(s0 + (int)j) & RMASK];
         }
       }
+    }
     __builtin_amdgcn_wave_barrier();
     pos += len;
   }
