@@ -43,7 +43,8 @@ struct MdOpts {
   const int64_t *mkb;       // sorted unique 1 kb keys per chromosome
 };
 
-__device__ __forceinline__ bool md_masked(const MdOpts &o, const uint8_t *c, int clen, int64_t s, int64_t e) {
+template <class P>
+__device__ __forceinline__ bool md_masked(const MdOpts &o, P c, int clen, int64_t s, int64_t e) {
   if (o.nmask == 0) return false;
   // the normalised chromosome name: the field itself if it starts with "chr",
   // else "chr" + field (norm_chrom, normalize_mosdepth.py:210-215)
@@ -130,7 +131,8 @@ __global__ void k_md_scan(const int32_t *__restrict__ cfirst, const int32_t *__r
 }
 
 // canonical "CHROM\tSTART\tEND\tDEPTH" (ingest.cpp canonical_line)
-__device__ __forceinline__ bool md_line(const uint8_t *p, int len, int &clen, int64_t &s, int64_t &e, int64_t &q) {
+template <class P>
+__device__ __forceinline__ bool md_line(P p, int len, int &clen, int64_t &s, int64_t &e, int64_t &q) {
   int i = 0;
   while (i < len && (unsigned)(p[i] - 0x21) < 0x5e) i++;
   if (i == 0 || i == len || p[i] != '\t') return false;
@@ -185,6 +187,19 @@ __device__ __forceinline__ uint32_t nl_mask16(const uint4 v) {
   return m;
 }
 
+// The chunk in LDS with 4 bytes of padding after every 64-byte block (block
+// t + 1 holds segment t; the 16-byte halo sits in block 0): a thread's
+// segment, and the lines it parses, start 68 bytes after its neighbour's, so
+// the 64 lanes of a wave reading "their" byte k hit 64 different banks (an
+// unpadded 64-byte stride put 16 lanes on every bank: every LDS read of the
+// parse 16-way serialised)
+__device__ __forceinline__ int md_phys(int i) { return i + 4 * ((i + 48) >> 6); }
+struct PadText {
+  const uint8_t *t;
+  int i0;
+  __device__ __forceinline__ uint8_t operator[](int k) const { return t[md_phys(i0 + k)]; }
+};
+
 // MODE 0 (reference file): kept[i] = 1 and keys[i] = (s, e) for every line i
 // that passes the prefix, window and mask tests, whatever its depth (a bin
 // the reference sample did not cover can be covered by another sample; a key
@@ -197,7 +212,7 @@ __device__ __forceinline__ uint32_t nl_mask16(const uint4 v) {
 // from the newline bit masks of its 16 words; line numbers come from a block
 // scan of the per-segment newline counts.
 template <int MODE>
-__global__ __launch_bounds__(PTH) void k_md_parse(const uint8_t *__restrict__ text, const int64_t *__restrict__ toff,
+__global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(5))) void k_md_parse(const uint8_t *__restrict__ text, const int64_t *__restrict__ toff,
                                                   const int64_t *__restrict__ tlen,
                                                   const int32_t *__restrict__ cfile,
                                                   const int64_t *__restrict__ cstart,
@@ -214,7 +229,8 @@ __global__ __launch_bounds__(PTH) void k_md_parse(const uint8_t *__restrict__ te
                                                   unsigned long long *__restrict__ kept,
                                                   const int32_t *__restrict__ fst) {
   constexpr int HALO = 16, SPAN = HALO + CH + MAXLINE + 16;   // bytes a-16 .. a+CH+MAXLINE (+16 slack)
-  __shared__ __attribute__((aligned(16))) uint8_t s_t[SPAN];
+  static_assert(HALO == 16 && SEG == 64, "md_phys: block t + 1 = segment t");
+  __shared__ __attribute__((aligned(16))) uint8_t s_t[SPAN + 4 * (SPAN / 64 + 2)];
   __shared__ int s_wsum[PTH / 64];
   const int c = blockIdx.x, f = cfile[c], tid = threadIdx.x;
   if (fst && fst[f]) return;            // a file that did not inflate: dropped
@@ -245,7 +261,12 @@ __global__ __launch_bounds__(PTH) void k_md_parse(const uint8_t *__restrict__ te
           for (int j = 0; j < 16; j++) q[j] = p + j < hi ? t[p + j] : 0;
           v[k] = *reinterpret_cast<const uint4 *>(q);
         }
-        reinterpret_cast<uint4 *>(s_t)[w] = v[k];
+        // 16 bytes at chunk byte 16 w: the four words stay inside one padded block
+        uint32_t *d = reinterpret_cast<uint32_t *>(s_t + md_phys(16 * w));
+        d[0] = v[k].x;
+        d[1] = v[k].y;
+        d[2] = v[k].z;
+        d[3] = v[k].w;
       }
     }
   }
@@ -253,9 +274,9 @@ __global__ __launch_bounds__(PTH) void k_md_parse(const uint8_t *__restrict__ te
   // my segment [s0, s1): its newline masks and count
   const int64_t s0 = a + (int64_t)tid * SEG, s1 = min(b, s0 + SEG);
   const int nw = s1 > s0 ? (int)((s1 - s0 + 15) / 16) : 0;
-  const uint4 *seg = reinterpret_cast<const uint4 *>(s_t + HALO + tid * SEG);
+  const uint32_t *seg = reinterpret_cast<const uint32_t *>(s_t + md_phys(HALO + tid * SEG));
   auto mask = [&](int k) {              // newlines of word k, inside the segment only
-    uint32_t mk = nl_mask16(seg[k]);
+    uint32_t mk = nl_mask16(make_uint4(seg[4 * k], seg[4 * k + 1], seg[4 * k + 2], seg[4 * k + 3]));
     const int64_t rest = s1 - (s0 + 16 * k);
     if (rest < 16) mk &= (1u << rest) - 1u;
     return mk;
@@ -278,7 +299,7 @@ __global__ __launch_bounds__(PTH) void k_md_parse(const uint8_t *__restrict__ te
   unsigned long long nkept = 0;
   // one line: [x, x + len), its line number idx
   auto line = [&](int64_t x, int len, int64_t idx) {
-    const uint8_t *p = s_t + HALO + (x - a);
+    const PadText p{s_t, (int)(HALO + (x - a))};
     if (o.npre != 0) {
       if (len < o.npre) return;
       for (int k = 0; k < o.npre; k++)
@@ -322,7 +343,7 @@ __global__ __launch_bounds__(PTH) void k_md_parse(const uint8_t *__restrict__ te
   if (s1 > s0) {
     // lines starting in [s0, s1): at s0 if it follows a newline (or starts
     // the file), then after every newline of the segment but its last byte
-    int64_t cur = (s0 == 0 || s_t[HALO + (s0 - a) - 1] == '\n') ? s0 : -1;
+    int64_t cur = (s0 == 0 || s_t[md_phys((int)(HALO + (s0 - a) - 1))] == '\n') ? s0 : -1;
     int64_t idx = idx0;
     for (int k = 0; k < nw; k++) {
       uint32_t mk = mask(k);
@@ -339,7 +360,7 @@ __global__ __launch_bounds__(PTH) void k_md_parse(const uint8_t *__restrict__ te
       }
     }
     if (cur >= 0) {                     // the last line started here ends in a later segment
-      const uint8_t *p = s_t + HALO + (cur - a);
+      const PadText p{s_t, (int)(HALO + (cur - a))};
       const int64_t lim = min(L, cur + MAXLINE + 1) - cur;
       int len = 0;
       while (len < lim && p[len] != '\n') len++;
