@@ -1236,7 +1236,7 @@ __global__ __launch_bounds__(512, 1) void k_gram8(const uint16_t *__restrict__ z
                                                   int64_t nsteps, int lag, int spin_ticks,
                                                   int64_t np_, unsigned long long *__restrict__ gram,
                                                   unsigned *__restrict__ rounds, int dyn,
-                                                  int32_t *__restrict__ part, GramXoff xoff) {
+                                                  int32_t *__restrict__ part, GramXoff xoff, int gs) {
   __shared__ __attribute__((aligned(1024))) char smem[3 * SLOT3];
   __shared__ int64_t s_unit;
   const int nwg = gridDim.x;
@@ -1246,13 +1246,14 @@ __global__ __launch_bounds__(512, 1) void k_gram8(const uint16_t *__restrict__ z
   const int kr = xcd % kx, gx = 8 / kx, xg = xcd / kx;
   const int64_t xs0 = nsteps * kr / kx, xs1 = nsteps * (kr + 1) / kx;
   const int64_t xlen = xs1 - xs0;
-  // this XCD's tile groups: g = xg, xg + gx, ...; only the last group overall
-  // can be partial, so every group but this XCD's last holds per * kc units
-  const int64_t ngroups = ((int64_t)ntiles + per - 1) / per;
+  // this XCD's tile groups of gs tiles (gs = per unless a small cohort deals
+  // one group to every XCD): g = xg, xg + gx, ...; only the last group overall
+  // can be partial, so every group but this XCD's last holds gs * kc units
+  const int64_t ngroups = ((int64_t)ntiles + gs - 1) / gs;
   const int64_t ngx = ngroups > xg ? (ngroups - xg + gx - 1) / gx : 0;
   const int64_t glast = xg + (ngx - 1) * gx;
-  const int64_t lastsz = ngx > 0 ? min((int64_t)per, (int64_t)ntiles - glast * per) : 0;
-  const int64_t units = ngx > 0 ? ((ngx - 1) * per + lastsz) * kc : 0;
+  const int64_t lastsz = ngx > 0 ? min((int64_t)gs, (int64_t)ntiles - glast * gs) : 0;
+  const int64_t units = ngx > 0 ? ((ngx - 1) * gs + lastsz) * kc : 0;
   // dyn: the XCD's workgroups take units in order from a counter instead of
   // unit r * per + l in round r, so a workgroup that starts late (its CU still
   // running the phasing lane's kernel) takes fewer units instead of holding
@@ -1269,10 +1270,10 @@ __global__ __launch_bounds__(512, 1) void k_gram8(const uint16_t *__restrict__ z
     if (u >= units) break;
     const int64_t ru = u / per;                     // the unit's round (pacing)
     // unit -> (group, chunk, tile)
-    const int64_t gl = u / ((int64_t)per * kc);
-    const int64_t gbase = (xg + gl * gx) * per;
-    const int gsz = (int)min((int64_t)per, (int64_t)ntiles - gbase);
-    const int64_t v = u - gl * (int64_t)per * kc;
+    const int64_t gl = u / ((int64_t)gs * kc);
+    const int64_t gbase = (xg + gl * gx) * gs;
+    const int gsz = (int)min((int64_t)gs, (int64_t)ntiles - gbase);
+    const int64_t v = u - gl * (int64_t)gs * kc;
     const int c = (int)(v / gsz);
     const int t = (int)(gbase + v % gsz);
     const int32_t tv = tiles[t];
@@ -1335,7 +1336,7 @@ __global__ __launch_bounds__(512, 1) void k_gram8(const uint16_t *__restrict__ z
 template __global__ void k_gram8<9, true, 1, 3>(const uint16_t *__restrict__, int64_t, const int32_t *__restrict__,
                                                 int, int, int, int64_t, int, int, int64_t,
                                                 unsigned long long *__restrict__, unsigned *__restrict__, int,
-                                                int32_t *__restrict__, GramXoff);
+                                                int32_t *__restrict__, GramXoff, int);
 #endif
 
 // ---- symmetric completion and row access ------------------------------------
@@ -1859,7 +1860,13 @@ static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_
   // feed rate per CU changes with the number of CUs streaming at once
   const char *pere = GRID_AB_KNOB("GRID_GRAM_PER");
   if (pere && atoi(pere) >= 1 && atoi(pere) < per) per = atoi(pere);
-  const int64_t ngroups = ceil_div(nt6, per);
+  // tiles per group (tools A/B GRID_GRAM_GS, default per): fewer than per deals
+  // a small cohort's tiles to more groups, so that every XCD can take whole
+  // groups over the full K range (kx = 1) and all XCDs stream the same K-steps
+  int gs = per;
+  const char *gse = GRID_AB_KNOB("GRID_GRAM_GS");
+  if (gse && atoi(gse) >= 1 && atoi(gse) < per) gs = atoi(gse);
+  const int64_t ngroups = ceil_div(nt6, gs);
   // (kx, kc): cost = the longest XCD's sequential work per workgroup in
   // K-step units: rounds x (steps per unit + UF), where UF prices a unit's
   // prologue and its int64-atomic flush (256 KiB per workgroup at ~5 GB/s per
@@ -1880,8 +1887,8 @@ static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_
         const int64_t ngx = ngroups > xg ? (ngroups - xg + gx - 1) / gx : 0;
         if (ngx == 0) continue;
         const int64_t glast = xg + (ngx - 1) * gx;
-        const int64_t lastsz = std::min((int64_t)per, (int64_t)nt6 - glast * per);
-        const int64_t units = ((ngx - 1) * per + lastsz) * kc;
+        const int64_t lastsz = std::min((int64_t)gs, (int64_t)nt6 - glast * gs);
+        const int64_t units = ((ngx - 1) * gs + lastsz) * kc;
         worst = std::max(worst, ceil_div(units, per));
       }
       const double cost = (double)worst * ((double)ceil_div(xlen, kc) + UF);
@@ -1955,11 +1962,11 @@ static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_
       const int xg = x / (int)bkx;
       const int64_t ngx = ngroups > xg ? (ngroups - xg + gx - 1) / gx : 0;
       const int64_t glast = xg + (ngx - 1) * gx;
-      const int64_t lastsz = ngx > 0 ? std::min((int64_t)per, (int64_t)nt6 - glast * per) : 0;
+      const int64_t lastsz = ngx > 0 ? std::min((int64_t)gs, (int64_t)nt6 - glast * gs) : 0;
       xoff.x[x] = tot;
-      tot += ngx > 0 ? ((ngx - 1) * per + lastsz) * bkc : 0;
+      tot += ngx > 0 ? ((ngx - 1) * gs + lastsz) * bkc : 0;
     }
-    if (mode == 0 && !q16 && part_cap > 0 && ldg == np_ && ti0 == 0 && tot * (int64_t)(BM3 * BN3 * 4) <= part_cap) {
+    if (mode == 0 && !q16 && gs == per && part_cap > 0 && ldg == np_ && ti0 == 0 && tot * (int64_t)(BM3 * BN3 * 4) <= part_cap) {
       void *sp = nullptr;
       int rc = grid_scratch(ctx, (size_t)tot * BM3 * BN3 * 4, &sp);
       if (rc) return rc;
@@ -1968,7 +1975,7 @@ static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_
   }
   hipLaunchKernelGGL(kern, dim3((unsigned)(8 * per)), dim3(512), 0, ctx->stream, d_zb, ld,
                      d_tiles, nt6, (int)bkc, (int)bkx, nsteps, lag, spin, ldg,
-                     (unsigned long long *)d_gram, rounds, dyn, d_part, xoff);
+                     (unsigned long long *)d_gram, rounds, dyn, d_part, xoff, gs);
   LAUNCHCHK();
   if (d_part) {
     hipLaunchKernelGGL(k_gram_part_reduce, dim3((unsigned)(BM3 * BN3 / 256), (unsigned)nt6), dim3(256), 0,

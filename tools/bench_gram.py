@@ -49,7 +49,7 @@ for rep in range(a.reps):
     for vv in a.variants.split(","):
         # "kb21:LAG=2:KC=9" -> variant kb21 with GRID_GRAM_LAG=2, GRID_GRAM_KC=9 (performance knobs)
         v, *knobs = vv.split(":")
-        for kv in ("LAG", "SPIN", "KC", "KX", "QL", "UF", "DYN", "PART_MB", "Q16", "PER"):
+        for kv in ("LAG", "SPIN", "KC", "KX", "QL", "UF", "DYN", "PART_MB", "Q16", "PER", "GS"):
             os.environ.pop("GRID_GRAM_" + kv, None)
         for kv in knobs:
             key, val = kv.split("=")
