@@ -39,7 +39,7 @@ PEAK_BF16_TFLOPS = 2516.6     # 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz (dense
 PEAK_HBM_GBS = 8000.0
 # HBM bytes per Gram launch from the rocprofv3 FETCH_SIZE / WRITE_SIZE passes
 # of this same command (tools/gpu_round.sh -> tools/pmc_traffic.py)
-TRAFFIC_JSON = "profiles/r05ap_pmc_traffic.json"
+TRAFFIC_JSON = "profiles/r05az_pmc_traffic.json"
 # the oracle from files over N x M, per-stage fits (tools/cpu_sweep.py,
 # run on a GPU box's host cores); reported beside the live bounded sample
 CPU_SWEEP_JSON = "profiles/r04k_cpu_sweep.json"
