@@ -1,26 +1,29 @@
 #!/usr/bin/env python3
 """Benchmark: GRiD steps 4-7 end to end on MI355X (BASELINE.json metric).
 
-One "step" = one pass of the device chain of steps 4-7 (grid_amd/fused.py)
-over a synthetic cohort, k = 10 neighbours, n_iters = 100.  value =
-samples / s (whole job).
+The headline: ONE step = one whole
+`grid wgs` run FROM FILES -- run_wgs_pipeline over BASELINE config 2 (3,202
+mosdepth BGZF regions.bed.gz files x 3,000,000 bins, k = 10, n_iters = 100):
+ingest, normalisation, the normalised gz file written, neighbours, dipCN,
+haploid calls, every output file written.  value = samples / s of those runs
+(whole job).  The cohort is generated before the clock (tools/gen_cohort, the
+bench's depth model as mosdepth text) in --files-dir.  With --gpus N the N
+ranks run the distributed drop-in (grid_amd/utils/dist_step4.py: files
+sliced over the ranks, all-to-all to column shards, RCCL collectives,
+offset-placed writer); steps 6-7 on rank 0.
 
-  * default: BASELINE config 2, 3,202 samples x 3,000,000 bins (hg38 @ 1 kb),
-    the depth matrix generated in HBM before timing (resident, 38 GB);
-  * --samples 50000 (config 3) / --bins 30000000 (config 4): the matrix does
-    not fit (600 GB / 6 TB int32), so the bin axis is STREAMED: every pass
-    regenerates its 8192-aligned chunk on the device (grid_amd.fused.
-    SynthSource), inside the timed region, and the step-4 output is written
-    chunk by chunk (fused mode).
+Beside it, in the same line:
+  * device_chain: the device-resident chain of steps 4-7 (grid_amd/fused.py)
+    on the same shape, the depth matrix generated in HBM before timing --
+    its Gram is the line's roofline (the metric's "k-NN distance vs peak");
+  * config3_1gpu (N = 1): the metric's own 50k x 3M shape, bin-streamed;
+  * cpu_baseline: the oracle on a bounded slice, and the committed sweep.
 
 Multi-GPU: one rank per GPU over RCCL.  ``--gpus N`` without an external
 launcher starts ``torch.distributed.run`` with N ranks as a child process
-before anything touches the GPU.  The cohort is bin-sharded in 8192-aligned
-ranges (strong scaling); the data-path collectives are the all-gathers of
-row-block partials and ratios and ONE reduce-scatter of the int64 Gram by
-row blocks.
+before anything touches the GPU.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--samples N] [--bins M]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--headline files|chain]
 """
 from __future__ import annotations
 
@@ -186,53 +189,220 @@ def cpu_baseline_from_files(n_target, m_target, k, n_iters):
                       "(single-threaded Python/NumPy, as the reference runs with threads=1)"}
 
 
-def from_files_config2(args, note):
-    """SURVEY 8(d)'s second number: BASELINE config 2 end to end FROM FILES --
-    `grid wgs` steps 4-7 through the drop-in step API (tools/e2e_files.py, a
-    child process: mosdepth BGZF regions.bed.gz files -> normalised gz text ->
-    neighbours -> dipCN -> haploid calls, every output file written) on a
-    synthetic 3,202-sample x 3 M-bin cohort written to /dev/shm before the
-    clock (tools/gen_cohort, the bench's depth model as mosdepth text).  The
-    record carries the per-step wall times and content digests of the output
-    files (runs compare byte for byte)."""
-    import shutil
-    import tempfile
+FILES_DIRNAME = "grid_bench_cfg2"
+
+
+def prepare_files_cohort(data, out, n, m, gen_threads=16, threads=16, bgzf=True, note=print):
+    """The from-files cohort in ``data``: ``n`` mosdepth regions.bed.gz files
+    of ``m`` 1 kb bins (tools/gen_cohort: the bench's depth model as "%.2f"
+    text, BGZF like mosdepth, libdeflate level 1), samples.txt, an empty
+    repeat mask, the IBS hap-neighbour file (synth_reads_and_ibs), counts.tsv
+    in ``out`` and config.yaml (`grid wgs` steps 4-7, k = 10, n_iters = 100).
+    Runs before anything touches the GPU (a child process).  Returns
+    (config path, generation seconds, cohort bytes)."""
+    import gzip
+    import yaml
+    t0 = time.perf_counter()
     root = os.path.dirname(os.path.abspath(__file__))
-    data = os.path.join(args.files_dir, "grid_bench_cfg2")
-    out = os.path.join(tempfile.gettempdir(), "grid_bench_cfg2_out")
-    js = os.path.join(tempfile.gettempdir(), f"grid_bench_cfg2_{os.getpid()}.json")
+    mos = os.path.join(data, "mosdepth")
+    os.makedirs(mos, exist_ok=True)
+    os.makedirs(out, exist_ok=True)
+    gen = os.path.join(root, "tools", "gen_cohort")
+    if not os.path.exists(gen) or os.path.getmtime(gen) < os.path.getmtime(gen + ".cpp"):
+        subprocess.run(["g++", "-O3", "-std=c++17", "-pthread", "-o", gen, gen + ".cpp", "-lz", "-ldl"], check=True)
+    have = len([f for f in os.listdir(mos) if f.endswith(".regions.bed.gz")])
+    if have != n:
+        note(f"generating {n} x {m} mosdepth files in {mos}")
+        subprocess.run([gen, mos, str(n), str(m), "20260821", str(gen_threads), "0"] + (["bgzf"] if bgzf else []),
+                       check=True, stdout=sys.stderr)
+    ids = [f"S{i:05d}" for i in range(n)]
+    reads, off, nbr, w = synth_reads_and_ibs(n)
+    with open(os.path.join(data, "samples.txt"), "w") as f:
+        f.write("\n".join(ids) + "\n")
+    with open(os.path.join(out, "counts.tsv"), "w") as f:
+        f.write("Sample\tchr1:1-3000000000\n")
+        f.writelines(f"{ids[i]}\t{int(reads[i])}\n" for i in range(n))
+    with gzip.open(os.path.join(data, "ibs.tsv.gz"), "wt", compresslevel=1) as f:
+        f.write("ID\thap\tnbrInd\tcMlen\tcMedge\tIDnbr\thapNbr\n")
+        for h in range(2 * n):
+            for t in range(off[h], off[h + 1]):
+                j = int(nbr[t])
+                f.write(f"{ids[h // 2]}\t{h % 2 + 1}\t{t - off[h]}\t5.0\t0\t{ids[j // 2]}\t{j % 2 + 1}\n")
+    open(os.path.join(data, "mask.bed"), "w").close()
+    cfg = {
+        "samples_file": os.path.join(data, "samples.txt"), "output_dir": out, "threads": threads,
+        "chrom": "chr1", "output_file_type": "tsv", "index": {"run": False},
+        "count_reads": {"run": False, "output_file_prefix": "counts"},
+        "mosdepth": {"run": False, "work_dir": mos, "remove_intermediate": False,
+                     "normalize": {"run": True, "min_depth": 20, "max_depth": 100, "top_frac": 0.1,
+                                   "device_ingest": True, "output_file_prefix": "normalized",
+                                   "repeat_mask_file": os.path.join(data, "mask.bed")},
+                     "neighbors": {"run": True, "output_file_prefix": "neighbors", "num_neighbors": 10, "zmax": 2.0,
+                                   "sigma2_max": 1000}},
+        "compute_diploid_genotypes": {"run": True, "output_file_prefix": "dipcn", "n_nbr": 10},
+        "compute_haploid_genotypes": {"run": True, "output_file_prefix": "haploid", "method": "ibs",
+                                      "min_neighbors": 1, "max_neighbors": 10, "n_iters": 100,
+                                      "ibs_output": os.path.join(data, "ibs.tsv.gz")},
+    }
+    path = os.path.join(data, "config.yaml")
+    with open(path, "w") as f:
+        yaml.safe_dump(cfg, f)
+    nbytes = sum(os.path.getsize(os.path.join(mos, f)) for f in os.listdir(mos))
+    return path, time.perf_counter() - t0, nbytes
+
+
+def files_paths(args):
+    import tempfile
+    data = os.path.join(args.files_dir, FILES_DIRNAME)
+    out = os.path.join(tempfile.gettempdir(), FILES_DIRNAME + "_out")
+    return data, out
+
+
+def files_prepare(args, rank, local, world, note):
+    """Rank 0 writes the cohort (before the GPU is touched); the other ranks
+    of this job wait for its marker (the job's master port in it, so a
+    marker left by another job is not taken).  Returns (config path,
+    generation s, bytes) or a dict {"skipped": why}."""
+    import shutil
+    data, out = files_paths(args)
+    marker = os.path.join(data, "READY")
+    token = f"{os.environ.get('MASTER_PORT', 'solo')}:{args.samples}x{args.bins}"
+    if rank == 0:
+        try:
+            free = shutil.disk_usage(args.files_dir).free
+        except OSError as e:
+            why = f"{args.files_dir}: {e}"
+            free = 0
+        else:
+            why = f"{args.files_dir} has {free / 1e9:.0f} GB free; the BGZF cohort needs ~{args.samples * args.bins * 8e-9:.0f} GB"
+        if os.path.exists(marker):
+            os.remove(marker)
+        need = args.samples * args.bins * 8 + (20 << 30)
+        if free < need and not os.path.isdir(os.path.join(data, "mosdepth")):
+            res = {"skipped": why}
+        else:
+            note("from files: generating the BGZF cohort (outside the clock)")
+            try:
+                res = prepare_files_cohort(data, out, args.samples, args.bins, gen_threads=16,
+                                           threads=args.files_threads, note=note)
+            except (OSError, subprocess.CalledProcessError) as e:
+                res = {"skipped": f"cohort generation: {e}"}
+        if world > 1:
+            os.makedirs(data, exist_ok=True)
+            with open(marker + ".tmp", "w") as f:
+                f.write(token + "\n" + json.dumps(res if isinstance(res, dict) else list(res)))
+            os.replace(marker + ".tmp", marker)
+        return res
+    t0 = time.time()
+    while time.time() - t0 < args.files_timeout:
+        try:
+            with open(marker) as f:
+                head, body = f.read().split("\n", 1)
+            if head == token:
+                res = json.loads(body)
+                return res if isinstance(res, dict) else tuple(res)
+        except (OSError, ValueError):
+            pass
+        time.sleep(0.5)
+    return {"skipped": "timed out waiting for rank 0's cohort"}
+
+
+def files_leg(args, prep, steps, warmup, world, rank, dist, note):
+    """The headline: ``steps`` timed runs of run_wgs_pipeline (the drop-in
+    `grid wgs`, steps 4-7 from the mosdepth files to every output file) after
+    ``warmup`` untimed ones, every rank (the distributed drop-in at N > 1),
+    bracketed by a barrier and a device synchronisation on both sides; the
+    max over ranks.  The ingest buffers stay cached from run to run
+    (keep_buffers: a service's steady state), so no run pays their release.
+    Per-step wall times of the four step functions (and, at one rank, the
+    ingest / text write inside step 4) are averaged over the timed runs."""
+    import functools
+    import torch
+    from grid_amd import pipeline
+    from grid_amd.utils import compute_dipcn as cd
+    from grid_amd.utils import find_neighbors as fn
+    from grid_amd.utils import hi_inference as hi
+    from grid_amd.utils import normalize_mosdepth as nm
+    cfg_path, gen_s, nbytes = prep
+    phases = {}
+    wrapped = []
+
+    def timed(mod, name, key):
+        fun = getattr(mod, name)
+
+        @functools.wraps(fun)
+        def wrap(*a, **kw):
+            t = time.perf_counter()
+            try:
+                return fun(*a, **kw)
+            finally:
+                phases[key] = phases.get(key, 0.0) + time.perf_counter() - t
+        setattr(mod, name, wrap)
+        wrapped.append((mod, name, fun))
+
+    timed(nm, "normalize_mosdepth", "step4_total")
+    timed(fn, "find_neighbors", "step5_total")
+    timed(cd, "compute_diploid_genotypes", "step6_total")
+    timed(hi, "hi_inference", "step7_total")
+    if world == 1:
+        timed(nm, "ingest", "step4_ingest")
+        timed(nm, "_write_normalized_q", "step4_write_text")
+    else:
+        from grid_amd.utils import dist_step4
+        timed(dist_step4.HipBackend, "ingest", "step4_ingest_rank")
+        timed(dist_step4.HipBackend, "parts_rows", "step4_code_rows_rank")
+        timed(dist_step4, "_write_parts", "step4_write_rank")
     try:
-        free = shutil.disk_usage(args.files_dir).free
-    except OSError as e:
-        return {"skipped": f"{args.files_dir}: {e}"}
-    if free < 100e9:
-        return {"skipped": f"{args.files_dir} has {free / 1e9:.0f} GB free; the BGZF cohort needs ~76 GB"}
-    cmd = [sys.executable, "-u", os.path.join(root, "tools", "e2e_files.py"), "--bgzf", "--samples", "3202",
-           "--bins", "3000000", "--data", data, "--out", out, "--json", js, "--threads", str(args.files_threads)]
-    note("from files, config 2: generating the BGZF cohort (outside the clock), then grid wgs steps 4-7")
-    try:
-        rc = subprocess.run(cmd, stdout=subprocess.DEVNULL, timeout=args.files_timeout).returncode
-    except subprocess.TimeoutExpired:
-        rc = "timeout"
+        for w_ in range(warmup):
+            pipeline.run_wgs_pipeline(console=None, config=cfg_path, keep_buffers=True)
+            note(f"from files: warmup {w_} done")
+        phases.clear()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for s_ in range(steps):
+            pipeline.run_wgs_pipeline(console=None, config=cfg_path, keep_buffers=True)
+            note(f"from files: step {s_} done")
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        t1 = time.perf_counter()
     finally:
-        shutil.rmtree(data, ignore_errors=True)
-        shutil.rmtree(out, ignore_errors=True)
-    if rc != 0 or not os.path.exists(js):
-        return {"skipped": f"tools/e2e_files.py exited with {rc}"}
-    r = json.load(open(js))
-    os.remove(js)
-    ph = r["phases_s"]
-    stages = {k: round(v, 3) for k, v in ph.items() if k.startswith("step")}
-    return {"value": r["samples_per_s_from_files"], "unit": "samples/s", "steps_4_7_s": r["steps_4_7_s"],
-            "samples": 3202, "bins": 3_000_000, "threads": args.files_threads, "stages_s": stages,
-            "release_ingest_buffers_after_step7_s": ph.get("release_ingest_buffers_after_step7"),
-            "cohort_generation_s": round(ph.get("generate_cohort", 0.0), 1), "cohort_bytes": r.get("cohort_bytes"),
-            "outputs_bytes": r.get("outputs"), "outputs_xxh3_64": r.get("outputs_xxh3_64"),
-            "peak_rss_gb": max(r.get("peak_rss_gb_after", {0: 0}).values()),
-            "workload": "BASELINE config 2 from files: 3202 mosdepth BGZF regions.bed.gz (3 M x 1 kb bins, '%.2f' "
-                        "depths) -> `grid wgs` steps 4-7 (drop-in step API, device ingest, every output file written "
-                        "to " + os.path.dirname(out) + "); cohort generated before the clock in " + args.files_dir,
-            "timed": "wall clock of the four step functions in one process (tools/e2e_files.py)"}
+        for mod, name, fun in wrapped:
+            setattr(mod, name, fun)
+    el = torch.tensor([t1 - t0], dtype=torch.float64, device="cuda")
+    if dist:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    data, out = files_paths(args)
+    outputs = {f: os.path.getsize(os.path.join(out, f)) for f in sorted(os.listdir(out))} if rank == 0 else None
+    digests = None
+    if rank == 0:
+        try:
+            import xxhash
+            import gzip
+            digests = {}
+            for f in sorted(os.listdir(out)):
+                pth = os.path.join(out, f)
+                if f.startswith("normalized"):
+                    continue                 # 16 GB: its size above (its bytes differ with N: per-rank codes)
+                h = xxhash.xxh3_64()
+                with (gzip.open(pth, "rb") if f.endswith(".gz") else open(pth, "rb")) as fh:
+                    h.update(fh.read())
+                digests[f] = h.hexdigest()
+        except ImportError:
+            pass
+    stages = {k: round(v / steps, 4) for k, v in sorted(phases.items())}
+    stage_sum = sum(v for k, v in stages.items() if k.endswith("_total"))
+    return {
+        "value": args.samples * steps / elapsed, "ms_per_step": 1000.0 * elapsed / steps, "elapsed": elapsed,
+        "stages_s": stages, "stages_total_s": round(stage_sum, 4),
+        "stages_vs_step": round(stage_sum / (elapsed / steps), 4),
+        "cohort_generation_s": round(gen_s, 1), "cohort_bytes": nbytes, "outputs_bytes": outputs,
+        "outputs_xxh3_64_text": digests, "threads": args.files_threads,
+    }
 
 
 def cpu_sweep_fit():
@@ -488,12 +658,16 @@ def main():
     ap.add_argument("--cpu-samples", type=int, default=4096)
     ap.add_argument("--cpu-bins", type=int, default=16384)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-files-baseline", action="store_true",
-                    help="skip the from-files oracle run at config 1 (~1 min of host time)")
+    ap.add_argument("--files-baseline", action="store_true",
+                    help="also time the oracle from files at config 1 (~30 s of host time; the committed sweep is "
+                         "reported either way)")
+    ap.add_argument("--no-files-baseline", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-overlap", action="store_true", help="run step 7 inline on the main stream")
-    ap.add_argument("--no-files-config2", action="store_true",
-                    help="N=1: skip the from-files config-2 record (BGZF cohort generated in --files-dir, ~1 min, "
-                         "then grid wgs steps 4-7 timed)")
+    ap.add_argument("--headline", choices=["auto", "files", "chain"], default="auto",
+                    help="the line's value: files = K whole `grid wgs` runs from the mosdepth files (the default at "
+                         "BASELINE config 2), chain = K passes of the device chain over a cohort generated in HBM")
+    ap.add_argument("--no-files-config2", action="store_true", help="= --headline chain")
+    ap.add_argument("--keep-files", action="store_true", help="keep the generated cohort and outputs afterwards")
     ap.add_argument("--files-dir", default="/dev/shm")
     ap.add_argument("--files-threads", type=int, default=16)
     ap.add_argument("--files-timeout", type=float, default=360.0)
@@ -534,11 +708,25 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
 
+    def note(msg):
+        if rank == 0:
+            print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+    n, m = args.samples, args.bins
+    headline = args.headline
+    if args.no_files_config2 or args.sim_world:
+        headline = "chain"
+    if headline == "auto":
+        headline = "files" if (n, m) == (3202, 3_000_000) else "chain"
+    # the from-files cohort is written before anything touches the GPU (a child process)
+    prep = files_prepare(args, rank, local, world, note) if headline == "files" else None
+
     import torch
     # GRID_BENCH_SHARE_GPU=1 (rehearsal only): ranks share the visible GPUs
     # round-robin, with GRID_DIST_BACKEND=gloo since RCCL needs one GPU per rank
     if os.environ.get("GRID_BENCH_SHARE_GPU") == "1":
         local = local % torch.cuda.device_count()
+        os.environ["GRID_SHARE_GPU"] = "1"          # the drop-in's get_device likewise
     torch.cuda.set_device(local)
     dist = None
     comm = None
@@ -556,15 +744,9 @@ def main():
 
     from grid_amd import _abi
 
-    dev = _abi.Device(local)
-    dev.set_stream(torch.cuda.current_stream())
-
-    def note(msg):
-        if rank == 0:
-            print(f"[bench] {msg}", file=sys.stderr, flush=True)
-
-    n, m = args.samples, args.bins
     if args.sim_world:
+        dev = _abi.Device(local)
+        dev.set_stream(torch.cuda.current_stream())
         if world != 1 or not 0 <= args.sim_rank < args.sim_world:
             raise SystemExit("bench: --sim-world runs one process (no --gpus) with 0 <= --sim-rank < --sim-world")
         from grid_amd.fused import SimComm
@@ -577,7 +759,52 @@ def main():
         out["build"] = _abi.build_info()
         print(json.dumps(out), file=result_out, flush=True)
         return
-    out, timing = run_workload(args, n, m, args.steps, args.warmup, world, rank, local, dist, comm, dev, note)
+
+    # ---- the headline: `grid wgs` from files, K whole runs ----
+    files = None
+    if headline == "files":
+        if isinstance(prep, dict):
+            files = prep                                   # {"skipped": why}
+            note(f"from files skipped: {prep['skipped']}")
+        else:
+            note(f"from files: {n} x {m}, {world} rank(s); warmup {args.warmup}, steps {args.steps}")
+            files = files_leg(args, prep, args.steps, args.warmup, world, rank, dist, note)
+        # the pipeline's device context holds its ingest buffers: free them for the chain below
+        from grid_amd.device import release_ingest_buffers
+        release_ingest_buffers()
+        torch.cuda.empty_cache()
+
+    # ---- the device chain (inputs generated in HBM): the Gram's roofline ----
+    dev = _abi.Device(local)
+    dev.set_stream(torch.cuda.current_stream())
+    chain, timing = run_workload(args, n, m, args.steps, args.warmup, world, rank, local, dist, comm, dev, note)
+    if files is not None and "value" in files:
+        out = dict(chain)
+        out["value"] = files["value"]
+        out["ms_per_step"] = files["ms_per_step"]
+        out["data"] = ("synthetic mosdepth BGZF cohort on disk (tools/gen_cohort: the bench's 26-cluster depth model "
+                       "as '%.2f' text, 1 kb bins), generated before the clock")
+        out["config"] = {
+            "workload": (f"BASELINE config 2 FROM FILES: {n} mosdepth regions.bed.gz x {m} bins -> `grid wgs` steps "
+                         f"4-7 (run_wgs_pipeline: device ingest, normalised gz file, neighbours, dipCN, haploid calls, "
+                         f"every output written), k={args.k}, n_iters={args.n_iters}, {world} GPU(s)"
+                         + (" (distributed drop-in: files sliced over the ranks, all-to-all to 8192-aligned column "
+                            "shards, RCCL segment reduce-scatter, row-sharded writer)" if world > 1 else "")),
+            "samples": n, "bins": m, "k": args.k, "n_iters": args.n_iters,
+            "parallelism": f"files x{world} -> bins x{world} -> rows x{world}" if world > 1 else "1 GPU",
+            "threads": args.files_threads, "step": "one whole run_wgs_pipeline call (ingest buffers kept cached between "
+                                                  "runs; outputs rewritten every run)"}
+        out["from_files"] = files
+        dc = {k: chain[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup", "config", "stages_ms")}
+        dc["data"] = chain["data"]
+        dc["roofline"] = chain["roofline"]
+        out["device_chain"] = dc
+        out["roofline"] = dict(chain["roofline"], measured_in="device_chain (the same config-2 shape, inputs in HBM; "
+                                                              "the metric's k-NN distance kernel)")
+    else:
+        out = chain
+        if files is not None:
+            out["from_files"] = files
     # the metric's own shape (BASELINE config 3: 50k x 3M, streamed on one
     # GPU): one more timed measurement in the same run, beside the line's
     # workload (N = 1 only: the scaling runs keep one workload per N)
@@ -604,25 +831,23 @@ def main():
             cb3 = scale_cpu_baseline(out["cpu_baseline"]["measured"], 50_000, 3_000_000)
             c3["cpu_baseline"] = {k: cb3[k] for k in ("value", "unit", "cores", "kind", "sample")}
             c3["speedup_vs_cpu_baseline"] = c3["value"] / cb3["value"]
-        if not args.no_files_baseline:
+        if args.files_baseline:
             note("cpu baseline: the oracle from files at config 1")
             out["cpu_baseline"]["from_files"] = cpu_baseline_from_files(n, m, args.k, args.n_iters)
         sweep = cpu_sweep_fit()
         if sweep is not None:
             out["cpu_baseline"]["sweep"] = sweep
-    if rank == 0 and world == 1 and not args.no_files_config2 and (n, m) == (3202, 3_000_000):
-        out["from_files_config2"] = from_files_config2(args, note)
     if rank == 0 and "cpu_baseline" in out:
         # which CPU number each ratio divides by (say it on the line)
         cb = out["cpu_baseline"]
-        sp = {"device_chain_vs_math_slice": out["value"] / cb["value"],
-              "basis_device_chain_vs_math_slice": "value (device chain, inputs in HBM) / cpu_baseline.value (the "
+        sp = {"device_chain_vs_math_slice": chain["value"] / cb["value"],
+              "basis_device_chain_vs_math_slice": "device_chain.value (inputs in HBM) / cpu_baseline.value (the "
                                                   "oracle's math on a bounded slice of the same cohort, scaled)"}
-        sw, ff = cb.get("sweep"), out.get("from_files_config2", {})
+        sw, ff = cb.get("sweep"), out.get("from_files", {})
         if sw and ff.get("value"):
             sp["from_files_vs_reference_from_files"] = ff["value"] / sw["config2_samples_per_s"]
             sp["basis_from_files_vs_reference_from_files"] = (
-                "from_files_config2.value (grid wgs steps 4-7 from mosdepth files, every output written) / "
+                "value (grid wgs steps 4-7 from mosdepth files, every output written) / "
                 "cpu_baseline.sweep.config2_samples_per_s (the oracle from files, per-stage fits of the measured sweep "
                 "extrapolated to config 2)")
         out["speedup_vs_cpu_baseline"] = sp
@@ -631,6 +856,11 @@ def main():
         print(json.dumps(out), file=result_out, flush=True)
     if dist:
         dist.barrier()
+    if headline == "files" and rank == 0 and not args.keep_files:
+        import shutil
+        for d in files_paths(args):
+            shutil.rmtree(d, ignore_errors=True)
+    if dist:
         dist.destroy_process_group()
 
 

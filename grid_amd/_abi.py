@@ -154,6 +154,18 @@ _SIGS = {
     "grid_fill_i32": [_vp, _vp, _i64, _i32],
     "grid_md_finish": [_vp, _vp, _i64, _i64, _i64, _vp, _i32, _f64, _f64, _vp, _vp, _vp, _vp, _vp, C.POINTER(_i64)],
     "grid_md_gather": [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp],
+    # distributed `grid wgs` (grid_amd/utils/dist_step4.py)
+    "grid_md_popsum": [_vp, _vp, _i64, _i64, _vp, _i32, _vp, _vp],
+    "grid_md_popvalid": [_vp, _vp, _vp, _i64, _f64, _f64, _vp],
+    "grid_md_rowstats": [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, C.POINTER(_i64)],
+    "grid_md_pack_shards": [_vp, _vp, _i64, _i64, _vp, _vp, _vp, _i32, _vp, _i32, _vp],
+    "grid_gz_parts_new": [C.POINTER(_vp)],
+    "grid_gz_parts_header": [_vp, _i64, _i64, _vp, _vp, _i32, _i32],
+    "grid_gz_parts_rows": [_vp, _i64, _i64, _i64, C.c_char_p, _vp, _vp, _i64, _i32, _i32],
+    "grid_gz_parts_rows_dev": [_vp, _vp, _i64, _i64, _i64, C.c_char_p, _vp, _vp, _i64, _i32, _i64],
+    "grid_gz_parts_size": [_vp, C.POINTER(_i64)],
+    "grid_gz_parts_write": [_vp, C.c_char_p, _i64, _i32],
+    "grid_gz_parts_free": [_vp],
 }
 EXPORTS = tuple(_SIGS) + ("grid_last_error", "grid_build_info")
 
@@ -508,6 +520,58 @@ def write_normalized_gz_dev(dev, path, ids, raw, sel_means, sel_ratios, d_zq, n,
     call("grid_write_normalized_gz_dev", dev.ctx, str(path).encode(), n, r, ids_b, raw.ctypes.data if n else None,
          mu.ctypes.data if r else None, rt.ctypes.data if r else None, ptr(d_zq) if (n and r) else None, max(ld, r),
          level, thr, int(batch_bytes))
+
+
+class GzParts:
+    """One rank's share of a normalised file written by several ranks
+    (grid_gz_parts_*): gzip members coded into host memory, then written at
+    the rank's byte offset once the ranks have exchanged their sizes."""
+
+    def __init__(self):
+        h = _vp()
+        call("grid_gz_parts_new", C.byref(h))
+        self.h = h.value
+
+    def header(self, n_total, sel_means, sel_ratios, level=1, threads=None):
+        """Member 0: the two header lines (N = n_total)."""
+        mu = np.ascontiguousarray(sel_means, dtype=np.float64)
+        rt = np.ascontiguousarray(sel_ratios, dtype=np.float64)
+        call("grid_gz_parts_header", self.h, int(n_total), len(mu), mu.ctypes.data if len(mu) else None,
+             rt.ctypes.data if len(rt) else None, level, threads or min(16, os.cpu_count() or 1))
+
+    def rows(self, ids, raw, zq, row0, level=1, threads=None):
+        """Row members of host int32 hundredths zq [n][r] (rows row0 + i)."""
+        zq = np.ascontiguousarray(zq, dtype=np.int32)
+        n, r = zq.shape
+        raw = np.ascontiguousarray(raw, dtype=np.float64)
+        call("grid_gz_parts_rows", self.h, n, int(row0), r, "\n".join(ids).encode(), raw.ctypes.data if n else None,
+             zq.ctypes.data if zq.size else None, max(r, 0), level, threads or min(16, os.cpu_count() or 1))
+
+    def rows_dev(self, dev, ids, raw, d_zq, n, r, ld, row0, batch_bytes=0):
+        """Row members of int32 hundredths in HBM (d_zq [n][ld]), coded on the
+        device as write_normalized_gz_dev codes them."""
+        raw = np.ascontiguousarray(raw, dtype=np.float64)
+        call("grid_gz_parts_rows_dev", dev.ctx, self.h, n, int(row0), r, "\n".join(ids).encode(),
+             raw.ctypes.data if n else None, ptr(d_zq) if (n and r) else None, max(ld, r), 1, int(batch_bytes))
+
+    def size(self):
+        s = _i64()
+        call("grid_gz_parts_size", self.h, C.byref(s))
+        return s.value
+
+    def write(self, path, offset, threads=4):
+        call("grid_gz_parts_write", self.h, str(path).encode(), int(offset), threads)
+
+    def free(self):
+        if self.h:
+            load().grid_gz_parts_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 def read_normalized_gz(path, threads=None):

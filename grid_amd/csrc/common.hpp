@@ -18,12 +18,17 @@
 
 #include "grid_abi.h"
 
-// One uploaded Gram tile list (launch_gram8): key = (np, first, last row tile)
+// One uploaded Gram tile list (launch_gram8), keyed by (np, first row tile,
+// end row tile); its device copy is the slot's own buffer, grown on demand
+// (no cap on np from a fixed workspace)
 constexpr int GRID_TILE_SLOTS = 4;
 struct GridTileSlot {
-  int64_t key = -1;
+  int64_t np = -1;
+  int ti0 = -1, ti1 = -1;
   int n = 0;
   int32_t *host = nullptr;
+  int32_t *dev = nullptr;
+  size_t cap = 0;                 // int32 entries of dev
   uint64_t used = 0;
 };
 
@@ -52,7 +57,7 @@ struct grid_ctx {
 // K-blocked bf16 panel of the k-NN Gram: [kpad / KBW][np][KBW] (a 16-row
 // half K-step of k_gram8's ring is then 1 KiB contiguous: whole 128-B lines)
 constexpr int KBW = 32;
-constexpr size_t GRID_AUX_BYTES = 4 << 20;   // Gram tile lists (4 slots of <= 128 Ki tiles) + round counters
+constexpr size_t GRID_AUX_BYTES = 4 << 20;   // the Gram's round and unit counters (from byte GRID_AUX_BYTES / 2)
 
 void grid_set_error(const char *fmt, ...);
 int grid_scratch(grid_ctx *ctx, size_t bytes, void **p);

@@ -73,7 +73,10 @@ int grid_ctx_destroy(grid_ctx *ctx) {
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
   if (ctx->aux) (void)hipFree(ctx->aux);
   if (ctx->keep && ctx->keep_free) ctx->keep_free(ctx->keep);
-  for (auto &ts : ctx->tiles) delete[] ts.host;
+  for (auto &ts : ctx->tiles) {
+    delete[] ts.host;
+    if (ts.dev) (void)hipFree(ts.dev);
+  }
   for (auto &e : ctx->ev) (void)hipEventDestroy(e);
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
   delete ctx;

@@ -53,6 +53,8 @@
 bool grid_textio_header_member(int64_t n, int64_t r, const double *sel_means, const double *sel_ratios, int level,
                                std::string &out, int threads);
 void grid_textio_row_prefix(const char *id_b, const char *id_e, double raw, std::string &out);
+// textio.cpp: the next piece of a distributed writer's output (grid_gz_parts_*), n bytes
+char *grid_textio_parts_reserve(grid_gz_parts *h, size_t n);
 
 namespace {
 
@@ -1012,13 +1014,34 @@ int grid_gz_huffman_member(const uint8_t *text, int64_t n, uint8_t *out, int64_t
   return GRID_OK;
 }
 
-int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int64_t r, const char *ids_nl,
-                                 const double *raw, const double *sel_means, const double *sel_ratios,
-                                 const int32_t *d_zq, int64_t ld_zq, int32_t level, int32_t threads,
-                                 int64_t batch_bytes) {
-  REQUIRE(ctx && path && n >= 0 && r >= 0 && ld_zq >= r && level >= 0 && level <= 9, "bad args");
-  REQUIRE(!n || (ids_nl && raw && (!r || d_zq)), "bad args");
-  REQUIRE(!r || (sel_means && sel_ratios), "bad args");
+}  // extern "C"
+
+namespace {
+
+// The device writer's buffers, owned by ctx->keep (another owner's object in
+// the slot is freed first).
+WriterBufs &writer_bufs(grid_ctx *ctx) {
+  static const char kWriterTag = 0;
+  if (ctx->keep && ctx->keep_tag != &kWriterTag) {
+    if (ctx->keep_free) ctx->keep_free(ctx->keep);
+    ctx->keep = nullptr;
+  }
+  if (!ctx->keep) {
+    ctx->keep = new WriterBufs;
+    ctx->keep_free = [](void *p) { delete static_cast<WriterBufs *>(p); };
+    ctx->keep_tag = &kWriterTag;
+  }
+  return *static_cast<WriterBufs *>(ctx->keep);
+}
+
+// The row members of rows [0, n) of d_zq (rows row0 + i in the 'GR' index),
+// formatted, CRC'd, LZ77-parsed and coded on the device in batches of about
+// batch_bytes of text; emit(d_out, obytes) receives each batch's members (in
+// device memory, on ctx's stream, queued) in order and returns GRID_OK or an
+// error code, which ends the call.
+template <class Emit>
+int encode_rows_dev(grid_ctx *ctx, int64_t n, int64_t row0, int64_t r, const char *ids_nl, const double *raw,
+                    const int32_t *d_zq, int64_t ld_zq, int64_t batch_bytes, Emit &&emit) {
   if (batch_bytes <= 0) batch_bytes = 2ll << 30;
   // row prefixes "ID \t scale \t" (host: n strings)
   std::vector<int64_t> preoff((size_t)n + 1, 0);
@@ -1036,29 +1059,6 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
       p = q ? q + 1 : e;
     }
   }
-  // member 0 (header lines) on a host thread meanwhile
-  std::string hdr_member;
-  bool hdr_ok = false;
-  const int T = std::max(1, (int)threads);
-  std::thread hdr_thr([&] { hdr_ok = grid_textio_header_member(n, r, sel_means, sel_ratios, level, hdr_member, T); });
-  const int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
-  if (fd < 0) {
-    hdr_thr.join();
-    grid_set_error("cannot open %s for writing", path);
-    return GRID_EINVAL;
-  }
-  // The batches go to the file through a second descriptor opened O_DIRECT
-  // where the file system allows it: 4 KiB-aligned ranges straight from the
-  // pinned buffers, no page-cache copy and no dirty-page throttling (the
-  // overlay disk of the MI355X boxes: 4.6 GB/s through the page cache with a
-  // final sync, 5.5 GB/s direct, profiles/r04l_disk.txt).  Each batch is
-  // copied to host memory FA bytes into its buffer, FA = its file offset mod
-  // 4 KiB, so the buffer starts on a 4 KiB file boundary once the previous
-  // batch's unaligned tail (the carry, < 4 KiB) is put in front of it; the
-  // last carry goes through the ordinary descriptor.  Without O_DIRECT every
-  // batch is written whole through the ordinary descriptor.
-  constexpr size_t FA = 4096;
-  std::atomic<int> fdd{open(path, O_WRONLY | O_DIRECT)};
   hipStream_t st = ctx->stream;
   const int64_t nblk = std::max<int64_t>(1, (r + CPB - 1) / CPB);
   // rows per member (the host writer's rule: ~8 MB of text per member)
@@ -1068,19 +1068,7 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
   crc_tables(crctab.data());
   const X2N x2n = make_x2n();
   const CrcOps cops = make_crc_ops(x2n);
-  // the buffers stay on the context for the next call (grid_ctx::keep, owned
-  // by this writer: another owner's object in the slot is freed first)
-  static const char kWriterTag = 0;
-  if (ctx->keep && ctx->keep_tag != &kWriterTag) {
-    if (ctx->keep_free) ctx->keep_free(ctx->keep);
-    ctx->keep = nullptr;
-  }
-  if (!ctx->keep) {
-    ctx->keep = new WriterBufs;
-    ctx->keep_free = [](void *p) { delete static_cast<WriterBufs *>(p); };
-    ctx->keep_tag = &kWriterTag;
-  }
-  WriterBufs &wbuf = *static_cast<WriterBufs *>(ctx->keep);
+  WriterBufs &wbuf = writer_bufs(ctx);
   auto &d_blen = wbuf.d_blen, &d_boff = wbuf.d_boff, &d_rowoff = wbuf.d_rowoff, &d_prelen = wbuf.d_prelen,
        &d_preoff = wbuf.d_preoff, &d_sstart = wbuf.d_sstart, &d_sbase = wbuf.d_sbase, &d_moff = wbuf.d_moff,
        &d_msize = wbuf.d_msize, &d_mrow = wbuf.d_mrow, &d_mlen = wbuf.d_mlen, &d_mbits = wbuf.d_mbits,
@@ -1091,116 +1079,12 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
   auto &d_pre = wbuf.d_pre, &d_text = wbuf.d_text;
   auto &d_code = wbuf.d_code;
   auto &d_hist = wbuf.d_hist;
-  auto &hb = wbuf.hb;
-  int rc = GRID_OK;
-  bool io_ok = true;
-  // writer thread: member 0 first, then the batches in order
-  std::mutex mu;
-  std::condition_variable cv;
-  std::deque<std::pair<int, size_t>> q;      // (pinned buffer, bytes after its front gap); -1 = end
-  int busy[2] = {0, 0};
-  size_t gap[2] = {0, 0};                    // bytes in front of a buffer's batch: its file offset mod FA
-  int64_t hdr_size = -1;                     // known once the writer thread has the header member
-  // pwrite of [p, p + len) at file offset o by up to 4 threads (page-cache
-  // copies: one thread moves ~5 GB/s)
-  // pwrite of [p, p + len) at file offset o by up to 4 threads (page-cache
-  // copies: one thread moves ~5 GB/s); on the direct descriptor the pieces
-  // split at FA multiples
-  const char *wwe = GRID_AB_KNOB("GRID_WRITER_W");   // writer threads per batch (A/B)
-  const size_t WMAX = wwe && atoi(wwe) > 0 ? (size_t)atoi(wwe) : 4;
-  auto pwrite_all = [&](int f, const char *p, size_t len, int64_t o, size_t unit) {
-    const int W = (int)std::max<size_t>(1, std::min<size_t>(WMAX, len >> 26));
-    std::vector<std::thread> ws;
-    std::vector<char> ok((size_t)W, 1);
-    for (int t = 0; t < W; t++)
-      ws.emplace_back([&, t] {
-        size_t a = (len / unit) * t / W * unit, b = t + 1 == W ? len : (len / unit) * (t + 1) / W * unit;
-        while (a < b) {
-          const ssize_t k = pwrite(f, p + a, b - a, o + (int64_t)a);
-          if (k <= 0) { ok[(size_t)t] = 0; return; }
-          a += (size_t)k;
-        }
-      });
-    for (auto &w : ws) w.join();
-    for (char c : ok)
-      if (!c) return false;
-    return true;
-  };
-  int64_t foff = 0;                          // file bytes written (direct: up to the carry)
-  int64_t out_done = 0;                      // batch bytes handed to the writer (main thread)
-  std::string carry;                         // direct mode: the written batches' unaligned tail
-  std::thread wr([&] {
-    hdr_thr.join();
-    const size_t hs = hdr_member.size();
-    const size_t ha = fdd >= 0 ? hs / FA * FA : hs;
-    if (!hdr_ok || !pwrite_all(fd, hdr_member.data(), ha, 0, 1)) io_ok = false;
-    carry.assign(hdr_member.data() + ha, hs - ha);
-    foff = (int64_t)ha;
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      hdr_size = (int64_t)hs;
-    }
-    cv.notify_all();
-    for (;;) {
-      std::pair<int, size_t> job;
-      {
-        std::unique_lock<std::mutex> lk(mu);
-        cv.wait(lk, [&] { return !q.empty(); });
-        job = q.front();
-        q.pop_front();
-      }
-      if (job.first < 0) return;
-      char *b = (char *)hb[job.first].p;
-      const size_t g = gap[job.first];
-      if (io_ok && fdd >= 0 && carry.size() == g) {
-        memcpy(b, carry.data(), g);          // the buffer now starts at file offset foff (FA-aligned)
-        const size_t tot = g + job.second, da = tot / FA * FA;
-        if (da && !pwrite_all(fdd, b, da, foff, FA)) {
-          close(fdd.exchange(-1));           // direct I/O refused: this batch and the rest the ordinary way
-          if (!pwrite_all(fd, b, tot, foff, 1)) io_ok = false;
-          carry.clear();
-          foff += (int64_t)tot;
-        } else {
-          carry.assign(b + da, tot - da);
-          foff += (int64_t)da;
-        }
-      } else if (io_ok) {
-        // the ordinary descriptor: the carry (if direct I/O stopped), then the batch after its gap
-        if (!carry.empty() && !pwrite_all(fd, carry.data(), carry.size(), foff, 1)) io_ok = false;
-        foff += (int64_t)carry.size();
-        carry.clear();
-        if (io_ok && !pwrite_all(fd, b + g, job.second, foff, 1)) io_ok = false;
-        foff += (int64_t)job.second;
-      }
-      {
-        std::lock_guard<std::mutex> lk(mu);
-        busy[job.first] = 0;
-      }
-      cv.notify_all();
-    }
-  });
-  auto finish = [&](int code) {
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      q.push_back({-1, 0});
-    }
-    cv.notify_all();
-    wr.join();
-    if (io_ok && !carry.empty() && !pwrite_all(fd, carry.data(), carry.size(), foff, 1)) io_ok = false;
-    if (fdd >= 0 && close(fdd.exchange(-1)) != 0) io_ok = false;
-    if (close(fd) != 0) io_ok = false;
-    if (code == GRID_OK && !io_ok) {
-      grid_set_error("grid_write_normalized_gz_dev: %s failed", hdr_ok ? "write" : "header deflate");
-      return (int)GRID_EINVAL;
-    }
-    return code;
-  };
 #define STEP(x)                                                                       \
   do {                                                                                \
     hipError_t e_ = (x);                                                              \
     if (e_ != hipSuccess) {                                                           \
       grid_set_error("%s:%d %s: %s", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
-      return finish(GRID_EHIP);                                                       \
+      return (int)GRID_EHIP;                                                          \
     }                                                                                 \
   } while (0)
   if (n > 0) {
@@ -1216,7 +1100,6 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
   std::vector<int32_t> h_slen, h_swin;
   std::vector<uint32_t> h_sbits;
   int64_t i0 = 0;
-  int cur = 0;
   while (i0 < n) {
     // rows of this batch: whole members, text <= batch_bytes (estimated
     // first by the upper bound, then exact)
@@ -1277,7 +1160,7 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
       const int64_t a = m * rpc, b = std::min(nr, a + rpc);
       h_mstart[m] = h_rowoff[a];
       h_mlen[m] = h_rowoff[b] - h_rowoff[a];
-      h_mrow[m] = i0 + a;
+      h_mrow[m] = row0 + i0 + a;
       for (int64_t e = 0; e < h_mlen[m]; e += SEG) {
         h_sstart.push_back(h_mstart[m] + e);
         h_slen.push_back((int32_t)std::min<int64_t>(SEG, h_mlen[m] - e));
@@ -1388,6 +1271,163 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
                        d_mrow.p, d_mlen.p, d_mbits.p, d_crc.p, d_hdr.p, code.hdr_bits, (uint32_t)code.rcode[256],
                        eob_len, nm);
     STEP(hipGetLastError());
+    {
+      const int rc = emit((const void *)d_out.p, obytes);
+      if (rc != GRID_OK) return rc;
+    }
+    i0 = i1;
+  }
+#undef STEP
+  return GRID_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int64_t r, const char *ids_nl,
+                                 const double *raw, const double *sel_means, const double *sel_ratios,
+                                 const int32_t *d_zq, int64_t ld_zq, int32_t level, int32_t threads,
+                                 int64_t batch_bytes) {
+  REQUIRE(ctx && path && n >= 0 && r >= 0 && ld_zq >= r && level >= 0 && level <= 9, "bad args");
+  REQUIRE(!n || (ids_nl && raw && (!r || d_zq)), "bad args");
+  REQUIRE(!r || (sel_means && sel_ratios), "bad args");
+  // member 0 (header lines) on a host thread meanwhile
+  std::string hdr_member;
+  bool hdr_ok = false;
+  const int T = std::max(1, (int)threads);
+  std::thread hdr_thr([&] { hdr_ok = grid_textio_header_member(n, r, sel_means, sel_ratios, level, hdr_member, T); });
+  const int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+  if (fd < 0) {
+    hdr_thr.join();
+    grid_set_error("cannot open %s for writing", path);
+    return GRID_EINVAL;
+  }
+  // The batches go to the file through a second descriptor opened O_DIRECT
+  // where the file system allows it: 4 KiB-aligned ranges straight from the
+  // pinned buffers, no page-cache copy and no dirty-page throttling (the
+  // overlay disk of the MI355X boxes: 4.6 GB/s through the page cache with a
+  // final sync, 5.5 GB/s direct, profiles/r04l_disk.txt).  Each batch is
+  // copied to host memory FA bytes into its buffer, FA = its file offset mod
+  // 4 KiB, so the buffer starts on a 4 KiB file boundary once the previous
+  // batch's unaligned tail (the carry, < 4 KiB) is put in front of it; the
+  // last carry goes through the ordinary descriptor.  Without O_DIRECT every
+  // batch is written whole through the ordinary descriptor.
+  constexpr size_t FA = 4096;
+  std::atomic<int> fdd{open(path, O_WRONLY | O_DIRECT)};
+  auto &hb = writer_bufs(ctx).hb;
+  int rc = GRID_OK;
+  bool io_ok = true;
+  // writer thread: member 0 first, then the batches in order
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::pair<int, size_t>> q;      // (pinned buffer, bytes after its front gap); -1 = end
+  int busy[2] = {0, 0};
+  size_t gap[2] = {0, 0};                    // bytes in front of a buffer's batch: its file offset mod FA
+  int64_t hdr_size = -1;                     // known once the writer thread has the header member
+  // pwrite of [p, p + len) at file offset o by up to 4 threads (page-cache
+  // copies: one thread moves ~5 GB/s); on the direct descriptor the pieces
+  // split at FA multiples
+  const char *wwe = GRID_AB_KNOB("GRID_WRITER_W");   // writer threads per batch (A/B)
+  const size_t WMAX = wwe && atoi(wwe) > 0 ? (size_t)atoi(wwe) : 4;
+  auto pwrite_all = [&](int f, const char *p, size_t len, int64_t o, size_t unit) {
+    const int W = (int)std::max<size_t>(1, std::min<size_t>(WMAX, len >> 26));
+    std::vector<std::thread> ws;
+    std::vector<char> ok((size_t)W, 1);
+    for (int t = 0; t < W; t++)
+      ws.emplace_back([&, t] {
+        size_t a = (len / unit) * t / W * unit, b = t + 1 == W ? len : (len / unit) * (t + 1) / W * unit;
+        while (a < b) {
+          const ssize_t k = pwrite(f, p + a, b - a, o + (int64_t)a);
+          if (k <= 0) { ok[(size_t)t] = 0; return; }
+          a += (size_t)k;
+        }
+      });
+    for (auto &w : ws) w.join();
+    for (char c : ok)
+      if (!c) return false;
+    return true;
+  };
+  int64_t foff = 0;                          // file bytes written (direct: up to the carry)
+  int64_t out_done = 0;                      // batch bytes handed to the writer (main thread)
+  std::string carry;                         // direct mode: the written batches' unaligned tail
+  std::thread wr([&] {
+    hdr_thr.join();
+    const size_t hs = hdr_member.size();
+    const size_t ha = fdd >= 0 ? hs / FA * FA : hs;
+    if (!hdr_ok || !pwrite_all(fd, hdr_member.data(), ha, 0, 1)) io_ok = false;
+    carry.assign(hdr_member.data() + ha, hs - ha);
+    foff = (int64_t)ha;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      hdr_size = (int64_t)hs;
+    }
+    cv.notify_all();
+    for (;;) {
+      std::pair<int, size_t> job;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return !q.empty(); });
+        job = q.front();
+        q.pop_front();
+      }
+      if (job.first < 0) return;
+      char *b = (char *)hb[job.first].p;
+      const size_t g = gap[job.first];
+      if (io_ok && fdd >= 0 && carry.size() == g) {
+        memcpy(b, carry.data(), g);          // the buffer now starts at file offset foff (FA-aligned)
+        const size_t tot = g + job.second, da = tot / FA * FA;
+        if (da && !pwrite_all(fdd, b, da, foff, FA)) {
+          close(fdd.exchange(-1));           // direct I/O refused: this batch and the rest the ordinary way
+          if (!pwrite_all(fd, b, tot, foff, 1)) io_ok = false;
+          carry.clear();
+          foff += (int64_t)tot;
+        } else {
+          carry.assign(b + da, tot - da);
+          foff += (int64_t)da;
+        }
+      } else if (io_ok) {
+        // the ordinary descriptor: the carry (if direct I/O stopped), then the batch after its gap
+        if (!carry.empty() && !pwrite_all(fd, carry.data(), carry.size(), foff, 1)) io_ok = false;
+        foff += (int64_t)carry.size();
+        carry.clear();
+        if (io_ok && !pwrite_all(fd, b + g, job.second, foff, 1)) io_ok = false;
+        foff += (int64_t)job.second;
+      }
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        busy[job.first] = 0;
+      }
+      cv.notify_all();
+    }
+  });
+  auto finish = [&](int code) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      q.push_back({-1, 0});
+    }
+    cv.notify_all();
+    wr.join();
+    if (io_ok && !carry.empty() && !pwrite_all(fd, carry.data(), carry.size(), foff, 1)) io_ok = false;
+    if (fdd >= 0 && close(fdd.exchange(-1)) != 0) io_ok = false;
+    if (close(fd) != 0) io_ok = false;
+    if (code == GRID_OK && !io_ok) {
+      grid_set_error("grid_write_normalized_gz_dev: %s failed", hdr_ok ? "write" : "header deflate");
+      return (int)GRID_EINVAL;
+    }
+    return code;
+  };
+#define ESTEP(x)                                                                      \
+  do {                                                                                \
+    hipError_t e_ = (x);                                                              \
+    if (e_ != hipSuccess) {                                                           \
+      grid_set_error("%s:%d %s: %s", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      return (int)GRID_EHIP;                                                          \
+    }                                                                                 \
+  } while (0)
+  int cur = 0;
+  auto emit = [&](const void *d_out, int64_t obytes) -> int {
+    hipStream_t st = ctx->stream;
     // to pinned host memory (the writer thread must be done with this buffer),
     // gap bytes into it: the batch's file offset mod FA (the header's size is
     // needed for the first batch)
@@ -1396,9 +1436,9 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
       cv.wait(lk, [&] { return !busy[cur] && hdr_size >= 0; });
     }
     const size_t g = fdd >= 0 ? (size_t)((hdr_size + out_done) % (int64_t)FA) : 0;
-    STEP(hb[cur].need((size_t)obytes + FA));
-    STEP(hipMemcpyAsync((char *)hb[cur].p + g, d_out.p, (size_t)obytes, hipMemcpyDeviceToHost, st));
-    STEP(hipStreamSynchronize(st));
+    ESTEP(hb[cur].need((size_t)obytes + FA));
+    ESTEP(hipMemcpyAsync((char *)hb[cur].p + g, d_out, (size_t)obytes, hipMemcpyDeviceToHost, st));
+    ESTEP(hipStreamSynchronize(st));
     out_done += obytes;
     {
       std::lock_guard<std::mutex> lk(mu);
@@ -1408,12 +1448,32 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
     }
     cv.notify_all();
     cur ^= 1;
-    i0 = i1;
-  }
-#undef STEP
+    return (int)GRID_OK;
+  };
+  rc = encode_rows_dev(ctx, n, 0, r, ids_nl, raw, d_zq, ld_zq, batch_bytes, emit);
+#undef ESTEP
   return finish(rc);
 }
 
+int grid_gz_parts_rows_dev(grid_ctx *ctx, grid_gz_parts *h, int64_t n, int64_t row0, int64_t r, const char *ids_nl,
+                           const double *raw, const int32_t *d_zq, int64_t ld_zq, int32_t threads,
+                           int64_t batch_bytes) {
+  REQUIRE(ctx && h && n >= 0 && row0 >= 0 && r >= 0 && ld_zq >= r, "bad args");
+  REQUIRE(!n || (ids_nl && raw && (!r || d_zq)), "bad args");
+  (void)threads;
+  // each batch straight into its own host piece (pageable: no page-locking of
+  // GBs, no second copy)
+  auto emit = [&](const void *d_out, int64_t obytes) -> int {
+    char *dst = grid_textio_parts_reserve(h, (size_t)obytes);
+    if (hipMemcpyAsync(dst, d_out, (size_t)obytes, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+        hipStreamSynchronize(ctx->stream) != hipSuccess) {
+      grid_set_error("grid_gz_parts_rows_dev: copy of a %lld-byte batch failed", (long long)obytes);
+      return (int)GRID_EHIP;
+    }
+    return (int)GRID_OK;
+  };
+  return encode_rows_dev(ctx, n, row0, r, ids_nl, raw, d_zq, ld_zq, batch_bytes, emit);
+}
 
 int grid_text_crc32(grid_ctx *ctx, const uint8_t *d_base, const int64_t *h_off, const int64_t *h_len, int64_t n,
                     uint32_t *h_crc) {

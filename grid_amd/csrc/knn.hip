@@ -1810,9 +1810,10 @@ extern "C" {
 // tiles (I, j >= 2I) with I in [ti0, ti1) -- all of them for the whole Gram,
 // one row range for the cohort split's segments (grid_knn_gram_kb_rows);
 // tile element (row, col) is added into d_gram[row * ldg + col].  The tile
-// lists live in ctx->aux, one per (np, ti0, ti1) in GRID_TILE_SLOTS slots, so
-// launches that alternate between row ranges re-use their uploaded lists
-// instead of re-uploading them (a host sync) every time.
+// lists live in GRID_TILE_SLOTS slots keyed by (np, ti0, ti1), each in its own
+// device buffer grown to the list's size, so launches that alternate between
+// row ranges re-use their uploaded lists instead of re-uploading them (a host
+// sync) every time, and the whole triangle of any np fits.
 static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_t nsteps, int64_t ld,
                         int64_t q2, int64_t sps_max, bool blocked, int mode, int64_t *d_gram, int ti0, int ti1,
                         int64_t ldg) {
@@ -1820,18 +1821,28 @@ static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_
   int nt6 = 0;
   for (int i = ti0; i < ti1; i++) nt6 += nt - 2 * i;
   REQUIRE(nt6 > 0, "empty Gram row range");
-  constexpr size_t SLOT_BYTES = GRID_AUX_BYTES / 2 / GRID_TILE_SLOTS;
-  REQUIRE((size_t)nt6 * 4 <= SLOT_BYTES, "too many Gram tiles (np %lld)", (long long)np_);
-  const int64_t key = (np_ << 24) | ((int64_t)ti0 << 12) | ti1;
+  REQUIRE(nt < (1 << 16), "np %lld: tile coordinates exceed 16 bits", (long long)np_);
   int slot = -1, lru = 0;
   for (int s = 0; s < GRID_TILE_SLOTS; s++) {
-    if (ctx->tiles[s].key == key && ctx->tiles[s].n == nt6 && ctx->tiles[s].host) slot = s;
-    if (ctx->tiles[s].used < ctx->tiles[lru].used) lru = s;
+    const GridTileSlot &c = ctx->tiles[s];
+    if (c.np == np_ && c.ti0 == ti0 && c.ti1 == ti1 && c.n == nt6 && c.host && c.dev) slot = s;
+    if (c.used < ctx->tiles[lru].used) lru = s;
   }
   if (slot < 0) {
     slot = lru;
     GridTileSlot &ts = ctx->tiles[slot];
     delete[] ts.host;
+    ts.host = nullptr;
+    ts.np = -1;
+    if ((size_t)nt6 > ts.cap) {
+      // a launch queued on the stream may still read the slot's old list
+      HIPCHK(hipStreamSynchronize(ctx->stream));
+      if (ts.dev) HIPCHK(hipFree(ts.dev));
+      ts.dev = nullptr;
+      ts.cap = 0;
+      HIPCHK(hipMalloc((void **)&ts.dev, (size_t)nt6 * 4));
+      ts.cap = (size_t)nt6;
+    }
     ts.host = new int32_t[nt6];
     // tile_blocked6 order (groups of GI6 row tiles x GJ6 column tiles),
     // enumerated incrementally from the range's first row tile
@@ -1845,14 +1856,15 @@ static int launch_gram8(grid_ctx *ctx, const uint16_t *d_zb, int64_t np_, int64_
       }
     }
     REQUIRE(t == nt6, "tile enumeration");
-    HIPCHK(hipMemcpyAsync((char *)ctx->aux + slot * SLOT_BYTES, ts.host, (size_t)nt6 * 4, hipMemcpyHostToDevice,
-                          ctx->stream));
+    HIPCHK(hipMemcpyAsync(ts.dev, ts.host, (size_t)nt6 * 4, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
-    ts.key = key;
+    ts.np = np_;
+    ts.ti0 = ti0;
+    ts.ti1 = ti1;
     ts.n = nt6;
   }
   ctx->tiles[slot].used = ++ctx->tiles_clock;
-  const int32_t *d_tiles = (const int32_t *)((char *)ctx->aux + slot * SLOT_BYTES);
+  const int32_t *d_tiles = ctx->tiles[slot].dev;
   unsigned *rounds = (unsigned *)((char *)ctx->aux + GRID_AUX_BYTES / 2);
   HIPCHK(hipMemsetAsync(rounds, 0, (128 + 8 * 16) * 4, ctx->stream));   // round and unit counters
   int per = ctx->ncu >= 8 ? ctx->ncu / 8 : 1;

@@ -24,6 +24,8 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+
 namespace {
 
 // 16 KiB chunks, a 64-byte segment per thread: 16.7 KiB of LDS per workgroup,
@@ -428,6 +430,66 @@ __global__ __launch_bounds__(256) void k_md_popmeans(const int32_t *__restrict__
   valid[j] = c > 0 && min_d <= m && m <= max_d;
 }
 
+// distributed ingest: the population sum continued over this rank's rows (file
+// order), from the previous rank's (sum, count); the same adds as k_md_popmeans
+__global__ __launch_bounds__(256) void k_md_popsum(const int32_t *__restrict__ Q, int64_t ldq, int64_t nK,
+                                                   const int32_t *__restrict__ rows, int nrows,
+                                                   double *__restrict__ sum, int64_t *__restrict__ cnt) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nK) return;
+  double s = sum[j];
+  int64_t c = cnt[j];
+  for (int r = 0; r < nrows; r++) {
+    const int32_t q = Q[(int64_t)rows[r] * ldq + j];
+    if (q != GRID_MISSING) {
+      s = s + div100_exact(q);
+      c++;
+    }
+  }
+  sum[j] = s;
+  cnt[j] = c;
+}
+
+// the chain's totals -> valid flags, exactly as k_md_popmeans' tail
+__global__ __launch_bounds__(256) void k_md_popvalid(const double *__restrict__ sum, const int64_t *__restrict__ cnt,
+                                                     int64_t nK, double min_d, double max_d,
+                                                     int32_t *__restrict__ valid) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nK) return;
+  const int64_t c = cnt[j];
+  const double m = c > 0 ? sum[j] / (double)c : 0.0;
+  valid[j] = c > 0 && min_d <= m && m <= max_d;
+}
+
+// rows of this rank -> every rank's column shard: row i (from Q row src[i]),
+// valid column j at position c = cpos[j] in shard s (bounds[s] <= c <
+// bounds[s+1]) goes to out[nrows * bounds[s] + i * width_s + c - bounds[s]]
+constexpr int MAX_SHARDS = 256;
+__global__ __launch_bounds__(256) void k_md_pack_shards(const int32_t *__restrict__ Q, int64_t ldq, int64_t nK,
+                                                        const int32_t *__restrict__ valid,
+                                                        const int64_t *__restrict__ cpos,
+                                                        const int32_t *__restrict__ src, int64_t nrows, int64_t y0,
+                                                        const int64_t *__restrict__ bounds, int nsh,
+                                                        int32_t *__restrict__ out) {
+  __shared__ int64_t b[MAX_SHARDS + 1];
+  for (int t = threadIdx.x; t <= nsh; t += blockDim.x) b[t] = bounds[t];
+  __syncthreads();
+  const int64_t i = y0 + blockIdx.y;
+  const int32_t *qr = Q + (int64_t)src[i] * ldq;
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nK; j += (int64_t)gridDim.x * blockDim.x) {
+    if (!valid[j]) continue;
+    const int64_t c = cpos[j];
+    int lo = 0, hi = nsh - 1;               // the shard: last s with b[s] <= c
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (b[mid] <= c) lo = mid;
+      else hi = mid - 1;
+    }
+    const int64_t w = b[lo + 1] - b[lo];
+    out[nrows * b[lo] + i * w + (c - b[lo])] = qr[j];
+  }
+}
+
 // per row: entries present (all K) and present in valid columns
 __global__ __launch_bounds__(256) void k_md_rowcount(const int32_t *__restrict__ Q, int64_t ldq, int64_t nK,
                                                      const int32_t *__restrict__ valid,
@@ -627,6 +689,66 @@ int grid_md_finish(grid_ctx *ctx, const int32_t *d_Q, int64_t ldq, int64_t nK, i
   HIPCHK(hipMemcpyAsync(&lv, d_valid + nK - 1, 4, hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   *h_m = lp + lv;
+  return GRID_OK;
+}
+
+int grid_md_popsum(grid_ctx *ctx, const int32_t *d_Q, int64_t ldq, int64_t nK, const int32_t *d_rows,
+                   int32_t nrows, double *d_sum, int64_t *d_cnt) {
+  REQUIRE(ctx && nK >= 0 && nrows >= 0 && ldq >= nK && (!nrows || (d_Q && d_rows)) && (!nK || (d_sum && d_cnt)),
+          "bad args");
+  if (nK == 0 || nrows == 0) return GRID_OK;
+  hipLaunchKernelGGL(k_md_popsum, dim3((unsigned)((nK + 255) / 256)), dim3(256), 0, ctx->stream, d_Q, ldq, nK, d_rows,
+                     nrows, d_sum, d_cnt);
+  LAUNCHCHK();
+  return GRID_OK;
+}
+
+int grid_md_popvalid(grid_ctx *ctx, const double *d_sum, const int64_t *d_cnt, int64_t nK, double min_depth,
+                     double max_depth, int32_t *d_valid) {
+  REQUIRE(ctx && nK >= 0 && (!nK || (d_sum && d_cnt && d_valid)), "bad args");
+  if (nK == 0) return GRID_OK;
+  hipLaunchKernelGGL(k_md_popvalid, dim3((unsigned)((nK + 255) / 256)), dim3(256), 0, ctx->stream, d_sum, d_cnt, nK,
+                     min_depth, max_depth, d_valid);
+  LAUNCHCHK();
+  return GRID_OK;
+}
+
+int grid_md_rowstats(grid_ctx *ctx, const int32_t *d_Q, int64_t ldq, int64_t nK, int64_t nfiles,
+                     const int32_t *d_valid, int64_t *d_cpos, uint64_t *d_present, uint64_t *d_nvalid, int64_t *h_m) {
+  REQUIRE(ctx && h_m && nK >= 0 && nfiles >= 0 && nfiles <= 65535 && ldq >= nK, "bad args");
+  *h_m = 0;
+  HIPCHK(hipMemsetAsync(d_present, 0, (size_t)(nfiles > 0 ? nfiles : 1) * 8, ctx->stream));
+  HIPCHK(hipMemsetAsync(d_nvalid, 0, (size_t)(nfiles > 0 ? nfiles : 1) * 8, ctx->stream));
+  if (nK == 0) return GRID_OK;
+  int rc = excl_scan(ctx, d_valid, d_cpos, nK);
+  if (rc) return rc;
+  if (nfiles > 0) {
+    hipLaunchKernelGGL(k_md_rowcount, dim3(64, (unsigned)nfiles), dim3(256), 0, ctx->stream, d_Q, ldq, nK, d_valid,
+                       (unsigned long long *)d_present, (unsigned long long *)d_nvalid);
+    LAUNCHCHK();
+  }
+  int64_t lp = 0;
+  int32_t lv = 0;
+  HIPCHK(hipMemcpyAsync(&lp, d_cpos + nK - 1, 8, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipMemcpyAsync(&lv, d_valid + nK - 1, 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  *h_m = lp + lv;
+  return GRID_OK;
+}
+
+int grid_md_pack_shards(grid_ctx *ctx, const int32_t *d_Q, int64_t ldq, int64_t nK, const int32_t *d_valid,
+                        const int64_t *d_cpos, const int32_t *d_src_rows, int32_t nrows, const int64_t *d_bounds,
+                        int32_t nshards, int32_t *d_out) {
+  REQUIRE(ctx && nK >= 0 && nrows >= 0 && ldq >= nK && nshards >= 1 && nshards <= MAX_SHARDS && d_bounds,
+          "bad args");
+  if (nK == 0 || nrows == 0) return GRID_OK;
+  REQUIRE(d_Q && d_valid && d_cpos && d_src_rows && d_out, "bad args");
+  for (int64_t y0 = 0; y0 < nrows; y0 += 65535) {
+    hipLaunchKernelGGL(k_md_pack_shards, dim3(64, (unsigned)std::min<int64_t>(65535, nrows - y0)), dim3(256), 0,
+                       ctx->stream, d_Q, ldq, nK, d_valid, d_cpos, d_src_rows, (int64_t)nrows, y0, d_bounds, nshards,
+                       d_out);
+    LAUNCHCHK();
+  }
   return GRID_OK;
 }
 

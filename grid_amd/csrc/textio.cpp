@@ -342,16 +342,15 @@ void grid_textio_row_prefix(const char *id_b, const char *id_e, double raw, std:
   out += '\t';
 }
 
-extern "C" {
+namespace {
 
-int grid_write_normalized_gz(const char *path, int64_t n, int64_t r, const char *ids_nl, const double *raw,
-                             const double *sel_means, const double *sel_ratios, const int32_t *zq, int64_t ld_zq,
-                             int32_t level, int32_t threads) {
-  if (!path || n < 0 || r < 0 || (n && (!ids_nl || !raw || (r && !zq))) || (r && (!sel_means || !sel_ratios)) ||
-      ld_zq < r || level < 0 || level > 9) {
-    grid_set_error("grid_write_normalized_gz: bad args");
-    return GRID_EINVAL;
-  }
+// Row members [0, n) of a normalised file (rows row0 + i in the 'GR' index),
+// member 0 the header lines first when `header`; deflated by `threads`
+// threads, handed to sink(k, member) in order (k = 0 .. nchunks-1).
+template <class Sink>
+bool encode_members(int64_t n, int64_t row0, int64_t r, const char *ids_nl, const double *raw, const int32_t *zq,
+                    int64_t ld_zq, int level, int threads, bool header, int64_t n_hdr, const double *sel_means,
+                    const double *sel_ratios, Sink &&sink, bool &io_ok) {
   std::vector<const char *> idb((size_t)n), ide((size_t)n);
   {
     const char *p = ids_nl;
@@ -362,16 +361,12 @@ int grid_write_normalized_gz(const char *path, int64_t n, int64_t r, const char 
       p = q ? q + 1 : ide[i];
     }
   }
-  FILE *f = fopen(path, "wb");
-  if (!f) {
-    grid_set_error("cannot open %s for writing", path);
-    return GRID_EINVAL;
-  }
-  const int T = std::max(1, (int)threads);
-  // chunk 0: the two header lines; chunk k >= 1: rows [(k-1)*rpc, k*rpc)
+  const int T = std::max(1, threads);
+  // chunk 0: the two header lines (when `header`); then rows [(k-h)*rpc, (k-h+1)*rpc)
   const int64_t row_bytes = 24 + 6 * r;
   const int64_t rpc = std::max<int64_t>(1, (8ll << 20) / std::max<int64_t>(row_bytes, 1));
-  const int64_t nchunks = 1 + (n + rpc - 1) / rpc;
+  const int64_t h0 = header ? 1 : 0;
+  const int64_t nchunks = h0 + (n + rpc - 1) / rpc;
   std::vector<std::string> done((size_t)nchunks);
   std::vector<char> ready((size_t)nchunks, 0);
   std::atomic<int64_t> next{0};
@@ -393,12 +388,14 @@ int grid_write_normalized_gz(const char *path, int64_t n, int64_t r, const char 
       }
       const char *body = nullptr;
       size_t blen = 0;
-      if (k == 0) {
-        header_lines(n, r, sel_means, sel_ratios, text);
+      int64_t first = -1;
+      if (k < h0) {
+        header_lines(n_hdr, r, sel_means, sel_ratios, text);
         body = text.data();
         blen = text.size();
       } else {
-        const int64_t r0 = (k - 1) * rpc, r1 = std::min(n, r0 + rpc);
+        const int64_t r0 = (k - h0) * rpc, r1 = std::min(n, r0 + rpc);
+        first = row0 + r0;
         size_t need = 0;
         for (int64_t i = r0; i < r1; i++) need += (size_t)(ide[i] - idb[i]) + 400 + 14 * (size_t)r + 1;
         if (need > rowcap) {
@@ -425,7 +422,7 @@ int grid_write_normalized_gz(const char *path, int64_t n, int64_t r, const char 
         body = rowbuf.get();
         blen = (size_t)(p - rowbuf.get());
       }
-      if (!deflate_member(body, blen, level, k == 0 ? -1 : (k - 1) * rpc, gz)) failed = true;
+      if (!deflate_member(body, blen, level, first, gz)) failed = true;
       {
         std::lock_guard<std::mutex> lk(mu);
         done[k].swap(gz);
@@ -436,7 +433,7 @@ int grid_write_normalized_gz(const char *path, int64_t n, int64_t r, const char 
   };
   std::vector<std::thread> pool;
   for (int t = 0; t < T; t++) pool.emplace_back(worker);
-  bool io_ok = true;
+  io_ok = true;
   for (int64_t k = 0; k < nchunks && !failed; k++) {
     std::string buf;
     {
@@ -445,7 +442,7 @@ int grid_write_normalized_gz(const char *path, int64_t n, int64_t r, const char 
       if (failed) break;
       buf.swap(done[k]);
     }
-    if (fwrite(buf.data(), 1, buf.size(), f) != buf.size()) { io_ok = false; failed = true; }
+    if (!sink(k, buf)) { io_ok = false; failed = true; }
     {
       std::lock_guard<std::mutex> lk(mu);
       written = k + 1;
@@ -457,11 +454,165 @@ int grid_write_normalized_gz(const char *path, int64_t n, int64_t r, const char 
     cv_room.notify_all();
   }
   for (auto &t : pool) t.join();
+  return !failed;
+}
+
+// pwrite of [p, p + len) at file offset o, split over up to W threads
+bool pwrite_split(int fd, const char *p, size_t len, int64_t o, int W) {
+  W = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::max(W, 1), len >> 24));
+  std::vector<std::thread> ws;
+  std::vector<char> ok((size_t)W, 1);
+  for (int t = 0; t < W; t++)
+    ws.emplace_back([&, t] {
+      size_t a = len * (size_t)t / (size_t)W, b = len * (size_t)(t + 1) / (size_t)W;
+      while (a < b) {
+        const ssize_t k = pwrite(fd, p + a, b - a, o + (int64_t)a);
+        if (k <= 0) { ok[(size_t)t] = 0; return; }
+        a += (size_t)k;
+      }
+    });
+  for (auto &w : ws) w.join();
+  for (char c : ok)
+    if (!c) return false;
+  return true;
+}
+
+}  // namespace
+
+// The distributed writer's byte pieces (grid_gz_parts_*): gzip members in file
+// order, held in host memory until the rank's file offset is known.
+struct GzPiece {
+  std::string s;                     // a host-coded member (moved in)
+  std::unique_ptr<char[]> b;         // or a device batch copied straight into host memory
+  size_t n = 0;
+  const char *data() const { return b ? b.get() : s.data(); }
+  size_t size() const { return b ? n : s.size(); }
+};
+struct grid_gz_parts {
+  std::vector<GzPiece> pieces;
+};
+
+// for gzwrite.hip's device encoder: a host buffer of n bytes appended as the
+// next piece (uninitialised: the caller copies the batch into it)
+char *grid_textio_parts_reserve(grid_gz_parts *h, size_t n) {
+  GzPiece p;
+  p.b.reset(new char[std::max<size_t>(n, 1)]);
+  p.n = n;
+  h->pieces.push_back(std::move(p));
+  return h->pieces.back().b.get();
+}
+
+extern "C" {
+
+int grid_write_normalized_gz(const char *path, int64_t n, int64_t r, const char *ids_nl, const double *raw,
+                             const double *sel_means, const double *sel_ratios, const int32_t *zq, int64_t ld_zq,
+                             int32_t level, int32_t threads) {
+  if (!path || n < 0 || r < 0 || (n && (!ids_nl || !raw || (r && !zq))) || (r && (!sel_means || !sel_ratios)) ||
+      ld_zq < r || level < 0 || level > 9) {
+    grid_set_error("grid_write_normalized_gz: bad args");
+    return GRID_EINVAL;
+  }
+  FILE *f = fopen(path, "wb");
+  if (!f) {
+    grid_set_error("cannot open %s for writing", path);
+    return GRID_EINVAL;
+  }
+  bool io_ok = true;
+  const bool ok = encode_members(n, 0, r, ids_nl, raw, zq, ld_zq, level, threads, true, n, sel_means, sel_ratios,
+                                 [&](int64_t, std::string &buf) {
+                                   return fwrite(buf.data(), 1, buf.size(), f) == buf.size();
+                                 }, io_ok);
   if (fclose(f) != 0) io_ok = false;
-  if (failed || !io_ok) {
+  if (!ok || !io_ok) {
     grid_set_error("grid_write_normalized_gz: %s failed", io_ok ? "deflate" : "write");
     return GRID_EINVAL;
   }
+  return GRID_OK;
+}
+
+int grid_gz_parts_new(grid_gz_parts **out) {
+  if (!out) {
+    grid_set_error("grid_gz_parts_new: bad args");
+    return GRID_EINVAL;
+  }
+  *out = new grid_gz_parts();
+  return GRID_OK;
+}
+
+int grid_gz_parts_header(grid_gz_parts *h, int64_t n_total, int64_t r, const double *sel_means,
+                         const double *sel_ratios, int32_t level, int32_t threads) {
+  if (!h || n_total < 0 || r < 0 || (r && (!sel_means || !sel_ratios)) || level < 0 || level > 9) {
+    grid_set_error("grid_gz_parts_header: bad args");
+    return GRID_EINVAL;
+  }
+  GzPiece m;
+  if (!grid_textio_header_member(n_total, r, sel_means, sel_ratios, level, m.s, std::max(1, (int)threads))) {
+    grid_set_error("grid_gz_parts_header: deflate failed");
+    return GRID_EINVAL;
+  }
+  h->pieces.push_back(std::move(m));
+  return GRID_OK;
+}
+
+int grid_gz_parts_rows(grid_gz_parts *h, int64_t n, int64_t row0, int64_t r, const char *ids_nl, const double *raw,
+                       const int32_t *zq, int64_t ld_zq, int32_t level, int32_t threads) {
+  if (!h || n < 0 || row0 < 0 || r < 0 || (n && (!ids_nl || !raw || (r && !zq))) || ld_zq < r || level < 0 ||
+      level > 9) {
+    grid_set_error("grid_gz_parts_rows: bad args");
+    return GRID_EINVAL;
+  }
+  bool io_ok = true;
+  const bool ok = encode_members(n, row0, r, ids_nl, raw, zq, ld_zq, level, threads, false, 0, nullptr, nullptr,
+                                 [&](int64_t, std::string &buf) {
+                                   GzPiece pc;
+                                   pc.s.swap(buf);
+                                   h->pieces.push_back(std::move(pc));
+                                   return true;
+                                 }, io_ok);
+  if (!ok) {
+    grid_set_error("grid_gz_parts_rows: deflate failed");
+    return GRID_EINVAL;
+  }
+  return GRID_OK;
+}
+
+int grid_gz_parts_size(const grid_gz_parts *h, int64_t *bytes) {
+  if (!h || !bytes) {
+    grid_set_error("grid_gz_parts_size: bad args");
+    return GRID_EINVAL;
+  }
+  int64_t s = 0;
+  for (const auto &p : h->pieces) s += (int64_t)p.size();
+  *bytes = s;
+  return GRID_OK;
+}
+
+int grid_gz_parts_write(const grid_gz_parts *h, const char *path, int64_t offset, int32_t threads) {
+  if (!h || !path || offset < 0) {
+    grid_set_error("grid_gz_parts_write: bad args");
+    return GRID_EINVAL;
+  }
+  const int fd = open(path, O_WRONLY);
+  if (fd < 0) {
+    grid_set_error("cannot open %s for writing (the first rank creates it)", path);
+    return GRID_EINVAL;
+  }
+  bool ok = true;
+  int64_t o = offset;
+  for (const auto &p : h->pieces) {
+    if (ok && p.size()) ok = pwrite_split(fd, p.data(), p.size(), o, std::max(1, (int)threads));
+    o += (int64_t)p.size();
+  }
+  if (close(fd) != 0) ok = false;
+  if (!ok) {
+    grid_set_error("grid_gz_parts_write: write to %s failed", path);
+    return GRID_EINVAL;
+  }
+  return GRID_OK;
+}
+
+int grid_gz_parts_free(grid_gz_parts *h) {
+  delete h;
   return GRID_OK;
 }
 

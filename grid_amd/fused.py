@@ -177,6 +177,72 @@ class TorchComm:
             return None
         return self.dist.all_gather_into_tensor(dst, src, async_op=async_op)
 
+    # ---- the distributed drop-in's exchanges (grid_amd/utils/dist_step4.py)
+    def _staged(self, t):
+        return self.host and t.is_cuda
+
+    def send(self, t, dst):
+        """Point-to-point (the population-sum chain over the ranks)."""
+        self.dist.send(t.cpu() if self._staged(t) else t, dst)
+
+    def recv(self, t, src):
+        if self._staged(t):
+            h = t.cpu()
+            self.dist.recv(h, src)
+            t.copy_(h)
+        else:
+            self.dist.recv(t, src)
+        return t
+
+    def broadcast(self, t, src):
+        if self._staged(t):
+            h = t.cpu()
+            self.dist.broadcast(h, src)
+            t.copy_(h)
+        else:
+            self.dist.broadcast(t, src)
+        return t
+
+    def all_to_all(self, out, inp, out_splits, in_splits):
+        """out = concat over ranks q of rank q's block for this rank; blocks
+        of in_splits / out_splits elements (1-D tensors, any dtype: moved as
+        bytes).  RCCL over xGMI: one all-to-all, every pair on its own link."""
+        import torch
+        es = inp.element_size()
+        src = inp.reshape(-1).view(torch.uint8)
+        dst = out.reshape(-1).view(torch.uint8)
+        osp = [int(x) * es for x in out_splits]
+        isp = [int(x) * es for x in in_splits]
+        src, dst = src[: sum(isp)], dst[: sum(osp)]
+        if self._staged(inp) or self.dist.get_backend() == "gloo":
+            # gloo: per-pair sends over host memory
+            hs = src.cpu() if src.is_cuda else src
+            parts_in = list(torch.split(hs, isp))
+            parts_out = [torch.empty(k, dtype=torch.uint8) for k in osp]
+            self._a2a_p2p(parts_out, parts_in)
+            dst.copy_(torch.cat(parts_out).to(dst.device) if parts_out else dst)
+            return out
+        self.dist.all_to_all_single(dst, src, osp, isp)
+        return out
+
+    def _a2a_p2p(self, parts_out, parts_in):
+        """all-to-all as ordered pairwise exchanges (gloo has no all-to-all of
+        ragged blocks on every build)."""
+        W, r = self.world, self.rank
+        parts_out[r].copy_(parts_in[r])
+        for k in range(1, W):
+            dst, src = (r + k) % W, (r - k) % W
+            reqs = []
+            if parts_in[dst].numel():
+                reqs.append(self.dist.isend(parts_in[dst], dst))
+            if parts_out[src].numel():
+                reqs.append(self.dist.irecv(parts_out[src], src))
+            for q in reqs:
+                q.wait()
+
+    def barrier(self):
+        self.dist.barrier()
+
 
 class SimComm:
     """One rank's share of a W-rank run on ONE GPU (per-rank timing,
@@ -575,9 +641,14 @@ class Steps47:
         self.norms = a.empty(self.np_, I8)
         self.norms.zero_()
         kk = max(k, 1)
-        if comm is not None:
-            if kk + 1 > _abi.SEG_K1:
-                raise _abi.GridNativeError(f"the sharded chain needs k + 1 <= {_abi.SEG_K1}")
+        # k + 1 above the segment candidate lists' length (the drop-in's
+        # num_neighbors may be the reference's default 500): the bin split then
+        # sums the whole upper triangle over the ranks (one all-reduce of the
+        # np x np int64 Gram) and every rank selects from whole rows
+        self.full_rows = comm is not None and kk + 1 > _abi.SEG_K1
+        if self.full_rows and self.split != "bin":
+            raise _abi.GridNativeError(f"the cohort split needs k + 1 <= {_abi.SEG_K1}")
+        if comm is not None and not self.full_rows:
             W, B = self.world, self.B
             self.my_blocks = (self.rank, 2 * W - 1 - self.rank)
             self.seg_len = B * (2 * W + 1) * B                 # int64 cells of one rank's two segments
@@ -732,11 +803,15 @@ class Steps47:
         return self.qc, self.ldc
 
     # -------------------------------------------------------------------- run
-    def run(self, q, ld=None, time_gram=False, profile=False):
+    def run(self, q, ld=None, time_gram=False, profile=False, upto="step7"):
         """One pass of steps 4-7.  ``q``: the depth source of this shard (see
         the class docstring; ``ld`` = row stride of a resident matrix).
         ``time_gram``: record HIP events around every Gram launch (on the
-        stream every kernel here runs on; read with gram_ms())."""
+        stream every kernel here runs on; read with gram_ms()).  ``upto``:
+        "step4" ends after the step-4 output (no Gram), "step5" after the
+        neighbour lists (the distributed drop-in, dist_step4.py)."""
+        if upto not in ("step4", "step5", "step7"):
+            raise ValueError(f"upto must be step4, step5 or step7, not {upto!r}")
         o, n, ml = self.ops, self.n, self.ml
         self.marks = [] if profile else None
         self.gram_evs = [] if time_gram else None
@@ -849,6 +924,8 @@ class Steps47:
                     self.zb[b0, :n, used % _abi.KBW:].zero_()
                     b0 += 1
                 self.zb[b0:kpad_c // _abi.KBW, :n].zero_()
+            if upto == "step4":
+                continue
             if self.split == "cohort":
                 self._cohort_gram(ci, used)
                 continue
@@ -863,12 +940,20 @@ class Steps47:
                 ev[1].record()
                 self.gram_evs.append(ev)
         self._mark("zquant_gram")
+        if upto == "step4":
+            self._check_deferred()
+            return
         # the previous pass's deferred phasing starts once this pass's Gram is done
         if not profile:
             self._issue_pending()
         # ---- step 5: full rows (mirror), reduce-scatter by row blocks, top-k ----
         if self.split == "cohort":
             self._step5_cohort()
+        elif self.full_rows:
+            self.comm.all_reduce_sum(self.gram[: self.np_])
+            o.mirror(self.gram, self.np_)
+            o.diag(self.gram, self.np_, n, self.norms)
+            o.topk_rows(self.gram, self.np_, self.norms, n, self.k, 0, n, self.idx_l, self.d2_l, self.cnt_l)
         elif self.comm is not None:
             o.mirror(self.gram, self.np_)
             o.diag(self.gram, self.np_, n, self.norms)
@@ -880,6 +965,10 @@ class Steps47:
             o.topk_rows(self.gram, self.np_, self.norms, n, self.k, 0, n, self.idx_l, self.d2_l, self.cnt_l)
         idx, self.d2, cnt = self.idx_l, self.d2_l, self.cnt_l
         self._mark("topk")
+        if upto == "step5":
+            self.idx_out, self.cnt_out = idx, cnt
+            self._check_deferred()
+            return
         # ---- step 6: dipCN (scales as printed "%.2f", neighbour gather) ----
         lane = None if profile else self._lanes
         if lane is None:

@@ -16,11 +16,19 @@ def _oos(console, what):
     log(console, f"{what} is not part of grid_amd (steps 4-7 only); using existing outputs", style="warning")
 
 
-def run_wgs_pipeline(console=False, config=None, **args):
+def run_wgs_pipeline(console=False, config=None, keep_buffers=False, **args):
+    """Steps 4-7 as the reference's run_wgs_pipeline (:9-103).  Under
+    torch.distributed.run (WORLD_SIZE > 1) every rank runs this and steps 4-5
+    use every GPU of the job (utils/dist_step4.py); steps 6-7 run on rank 0
+    (a loci table's loci are dealt over the ranks).  ``keep_buffers``: keep
+    the device ingest's buffers cached for the process's next run instead of
+    releasing them at the end (their release holds the HIP runtime ~0.5 s)."""
     from .device import deferred_release
+    from .utils.dist_step4 import init_from_env
+    init_from_env()
     # step 4's ingest buffers are kept to the end of the run, then released
     # (their release holds the HIP runtime for a fraction of a second)
-    with deferred_release():
+    with deferred_release(release=not keep_buffers):
         _run(console, config)
 
 

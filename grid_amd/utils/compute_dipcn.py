@@ -107,6 +107,15 @@ def compute_diploid_genotypes(config, console) -> None:
         log(console, f"Config error: {e}", style="danger")
         return
 
+    from .dist_step4 import dist_comm, rank0_step
+    comm = dist_comm()
+    if comm is not None:                    # torch.distributed: rank 0 computes, the others wait
+        rank0_step(comm, lambda: _compute_one(console, counts_file, neighbors_file, n_nbr, output_file, config))
+        return
+    _compute_one(console, counts_file, neighbors_file, n_nbr, output_file, config)
+
+
+def _compute_one(console, counts_file, neighbors_file, n_nbr, output_file, config):
     reads = _read_counts(counts_file)
     neighbors, scales = load_neighbors(neighbors_file)
     with progress_bar(console, total=len(neighbors), description="Computing dipCN...") as (progress, task):

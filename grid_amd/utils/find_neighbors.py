@@ -142,6 +142,33 @@ def find_neighbors(config, console):
         return
     output_file.parent.mkdir(parents=True, exist_ok=True)
 
+    from .dist_step4 import agree, dist_comm, rank0_step
+    comm = dist_comm()
+    if comm is not None:
+        # torch.distributed: step 4 ran the search across the ranks (every rank
+        # holds the lists); rank 0 writes them.  Otherwise rank 0 runs the
+        # one-GPU step from the file while the others wait.
+        params = {"zmax": zmax, "sigma2_max": sigma2_max, "frac_r": frac_r, "n_neighbors": n_neighbors}
+        rec = handoff.take_neighbors(input_file, params)
+        if agree(comm, rec is not None):
+            def write():
+                ids, nb = rec["ids"], rec["neighbors"]
+                scales = {i: float(v) for i, v in zip(ids, rec["scales"])}
+                idx, d2, cnt = nb["idx"], nb["d2"], nb["cnt"]
+                nbrs = {ind: [(ids[int(idx[i, t])], float(d2[i, t]) / 10000.0) for t in range(cnt[i])]
+                        for i, ind in enumerate(ids)}
+                save_neighbors(nbrs, scales, output_file, zmax, nb["R_use"])
+                log(console, f"Saved neighbors to {output_file}", style="success")
+            rank0_step(comm, write)
+        else:
+            rank0_step(comm, lambda: _find_neighbors_one(config, console, input_file, output_file, zmax, sigma2_max,
+                                                         n_neighbors, frac_r))
+        return
+    _find_neighbors_one(config, console, input_file, output_file, zmax, sigma2_max, n_neighbors, frac_r)
+
+
+def _find_neighbors_one(config, console, input_file, output_file, zmax, sigma2_max, n_neighbors, frac_r):
+    """Step 5 in one process (:11-77)."""
     got = handoff.take(input_file)              # step 4 ran in this process: its matrix, no re-parse
     if got is not None:
         ids, sc, ratios, zq, _shape = got

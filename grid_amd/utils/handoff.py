@@ -47,5 +47,33 @@ def take(path):
     return ent[1:]
 
 
+def publish_neighbors(path, rec):
+    """The distributed step 4 (dist_step4.py) ran step 5's search as well:
+    record the sample ids, the "%.2f" scales and the neighbour lists (every
+    rank holds them) for ``path`` -- call on every rank once the file is
+    complete.  rec["neighbors"] is None when step 5 was not run there."""
+    _entries.pop(("nbr", os.path.realpath(path)), None)
+    _entries[("nbr", os.path.realpath(path))] = (_stamp(path), rec)
+
+
+def take_neighbors(path, params):
+    """The record published for ``path`` when the file is unchanged and its
+    search used ``params`` (zmax, sigma2_max, frac_r, n_neighbors), else None.
+    The entry is consumed."""
+    ent = _entries.pop(("nbr", os.path.realpath(path)), None)
+    if ent is None:
+        return None
+    try:
+        if _stamp(path) != ent[0]:
+            return None
+    except OSError:
+        return None
+    rec = ent[1]
+    nb = rec.get("neighbors")
+    if nb is None or nb["params"] != params:
+        return None
+    return rec
+
+
 def clear():
     _entries.clear()

@@ -428,6 +428,16 @@ def hi_inference(config, console):
         log(console, f"Config error: {e}", style="danger")
         return
 
+    from .dist_step4 import dist_comm, rank0_step
+    comm = dist_comm()
+    if comm is not None:                    # torch.distributed: rank 0 phases the locus, the others wait
+        rank0_step(comm, lambda: _hi_inference_one(config, console, hc, output_file, dip_file, method, MIN_NBR,
+                                                   MAX_NBR, N_ITERS))
+        return
+    _hi_inference_one(config, console, hc, output_file, dip_file, method, MIN_NBR, MAX_NBR, N_ITERS)
+
+
+def _hi_inference_one(config, console, hc, output_file, dip_file, method, MIN_NBR, MAX_NBR, N_ITERS):
     IDs, IRRs, IDtoInd = _read_dip_cn_file(dip_file)
     N = len(IRRs)
     log(console, f"Read diploid IRR data for {N} samples", style="success")

@@ -492,11 +492,20 @@ class _Async:
             self.scr = [None, None]
 
 
-def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, threads=16):
+def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, threads=16, ref=None,
+                  keys_only=False, finish=True):
     """paths: one per individual in file order (None = no file).  Returns
     (ok files in file order, the device state for ``gather``, records in valid
     columns per file, status per file: 0 ok, 1 failed, 3 missing); raises
-    DeviceIngestUnsupported."""
+    DeviceIngestUnsupported.
+
+    The distributed step 4 (dist_step4.py) splits this in two: rank 0 runs
+    ``keys_only`` (the first batch only: the reference key list K as host
+    arrays (K [nK][2] int64, kidx int32, ref_nlines), or None when no file
+    inflates), every rank then parses its slice of the files over that K
+    (``ref``) with ``finish=False``: (Q [nfiles][nK] int32 on the device, nK,
+    status, records kept per file) -- the population means are a chain over
+    the ranks there."""
     nfiles = len(paths)
     t_start = time.perf_counter()
     keep = []
@@ -508,7 +517,7 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
     # batches in file order
     batches, cur, cin = [], [], 0
     for f in order:
-        lim = min(FIRST_BATCH_IN, BATCH_IN) if not batches else BATCH_IN
+        lim = min(FIRST_BATCH_IN, BATCH_IN) if not batches and ref is None else BATCH_IN
         if cur and cin + _align(sizes[f]) > lim:
             batches.append(cur)
             cur, cin = [], 0
@@ -676,6 +685,14 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
 
     K = kidx = Q = None
     nK = ref_nlines = 0
+    if ref is not None:                    # the key list of another rank's reference file
+        K_h, kidx_h, ref_nlines = ref
+        nK = len(K_h)
+        K = dev.upload(np.ascontiguousarray(K_h, np.int64).reshape(max(nK, 1), 2) if nK else np.zeros((1, 2), np.int64))
+        kidx = dev.upload(np.ascontiguousarray(kidx_h, np.int32) if len(kidx_h) else np.zeros(1, np.int32))
+        ref_nlines = int(ref_nlines)
+        Q = dev.alloc((max(nfiles, 1), max(nK, 1)), np.int32)
+        call("grid_fill_i32", dev.ctx, Q.ptr, max(nfiles, 1) * max(nK, 1), _abi.MISSING)
     d_text = None
     d_ins = [None, None]
     pipe = None
@@ -790,6 +807,8 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
                 nK = h_nK.value
                 if nK == 0:
                     raise DeviceIngestUnsupported("the reference file keeps no record")
+                if keys_only:
+                    break
                 Q = dev.alloc((nfiles, nK), np.int32)
                 call("grid_fill_i32", dev.ctx, Q.ptr, nfiles * nK, _abi.MISSING)
             qrow = dev.upload(np.asarray(fs, np.int32))
@@ -850,6 +869,12 @@ def ingest_device(dev, paths, prefix, window, excluded, min_depth, max_depth, th
         import sys
         print(f"[ingest] input/text buffers freed at {time.perf_counter() - t_start:.3f} s", file=sys.stderr,
               flush=True)
+    if keys_only:
+        if K is None:
+            return None
+        return K.numpy()[:nK].copy(), kidx.numpy()[:max(ref_nlines, 0)].copy(), ref_nlines
+    if not finish:
+        return Q, nK, status, kept.numpy()[:nfiles].copy()
     if K is None:
         return [], [], None, status
     rows = np.array([f for f in range(nfiles) if status[f] == 0], np.int32)

@@ -478,16 +478,72 @@ def normalize_mosdepth(config, console):
         log(console, f"[red]Config error: {e}[/red]")
         return
 
+    from .dist_step4 import dist_comm
+    comm = dist_comm()                   # torch.distributed with > 1 rank: every GPU of the job
     output_path = Path(output_file).expanduser()
     output_path.parent.mkdir(parents=True, exist_ok=True)
-    output_path = setup_output_file(output_path, chrom, start, end)
+    if comm is None or comm.rank == 0:
+        output_path = setup_output_file(output_path, chrom, start, end)
 
     individuals = map_mosdepth_files_to_samples(mosdepth_dir, samples)
     if not individuals:
         log(console, f"✗ No mosdepth files found in {mosdepth_dir}", style="danger")
         sys.exit(1)
     excluded = load_repeat_mask(repeat_mask)
+    args = (config, console, individuals, mosdepth_dir, chrom, start, end, excluded, min_depth, max_depth, top_frac,
+            threads, output_path, remove_intermediate)
+    if comm is not None:
+        from . import dist_step4
+        if _normalize_distributed(comm, *args):
+            return
+        # a case outside the distributed path (agreed by every rank): rank 0
+        # runs the one-GPU step, the others wait for it
+        dist_step4.rank0_step(comm, lambda: _normalize_one(*args))
+        return
+    _normalize_one(*args)
 
+
+def _normalize_distributed(comm, config, console, individuals, mosdepth_dir, chrom, start, end, excluded, min_depth,
+                           max_depth, top_frac, threads, output_path, remove_intermediate):
+    """Steps 4 (+ 5's neighbour search when it is enabled) over every rank of
+    the job (dist_step4.py).  False when the ranks agreed to fall back."""
+    from . import dist_step4
+    nbr = config["mosdepth"].get("neighbors", {})
+    nbr_params = None
+    if nbr.get("run") == True:  # noqa: E712  (the pipeline's own gate)
+        nbr_params = {"zmax": nbr.get("zmax", 2.0), "sigma2_max": nbr.get("sigma2_max", 1000.0),
+                      "frac_r": nbr.get("frac_r", 1.0), "n_neighbors": nbr.get("num_neighbors", 500)}
+    if not bool(config["mosdepth"]["normalize"].get("device_ingest", True)):
+        return False
+    backend = dist_step4.make_backend(config)
+    try:
+        with backend.stream_ctx():
+            rec = dist_step4.normalize_dist(comm, backend, individuals=individuals, mosdepth_dir=mosdepth_dir,
+                                            chromosome=chrom, start=start, end=end, excluded=excluded,
+                                            min_depth=min_depth, max_depth=max_depth, top_frac=top_frac,
+                                            threads=max(1, int(threads or 1)), output_path=output_path,
+                                            nbr_params=nbr_params, console=console)
+            backend.sync()
+    except dist_step4.DistFallback:
+        release_ingest_buffers(*([backend.dev] if hasattr(backend, "dev") else []))
+        return False
+    if rec is None:
+        log(console, "No valid samples with regions found.", style="danger")
+        sys.exit(1)
+    handoff.publish_neighbors(output_path, rec)
+    if hasattr(backend, "dev"):
+        step4_done(backend.dev)
+    if comm.rank == 0:
+        log(console, f"Mosdepth normalization complete. Results written to {output_path}", style="success")
+        if remove_intermediate:
+            remove_intermediate_files(mosdepth_dir, console, include_region_bed_gz=True)
+    comm.barrier()
+    return True
+
+
+def _normalize_one(config, console, individuals, mosdepth_dir, chrom, start, end, excluded, min_depth, max_depth,
+                   top_frac, threads, output_path, remove_intermediate):
+    """Step 4 on one GPU (:23-145)."""
     dev = get_device(config)
     # mosdepth.normalize.device_ingest (default on): inflate on the GPU and the
     # host threads side by side, parse in HBM (ingest_device.py); anything

@@ -525,6 +525,29 @@ int grid_write_normalized_gz_dev(grid_ctx *ctx, const char *path, int64_t n, int
  * one dynamic-Huffman block whose codes come from text's own token
  * histogram.  *out_len = bytes needed (GRID_EINVAL when above cap). */
 int grid_gz_huffman_member(const uint8_t *text, int64_t n, uint8_t *out, int64_t cap, int64_t *out_len);
+/* The same file written by W ranks of a distributed `grid wgs` (each rank
+ * holds the z rows [row0, row0 + n) of the cohort): the rank codes its row
+ * members into host memory (a parts handle: _rows_dev from int32 hundredths
+ * in HBM, as grid_write_normalized_gz_dev codes them; _rows from host memory,
+ * as grid_write_normalized_gz does), rank 0 also member 0 (_header, N =
+ * n_total); the ranks exchange their byte counts (_size) and each writes its
+ * bytes at the exclusive prefix sum of the counts before it (_write: the file
+ * exists, created by rank 0).  Every member keeps the 'GR' {size, first row}
+ * index with GLOBAL row numbers, so the reader sees one indexed file and the
+ * text after gunzip is the reference's.  Replaces the single writer of
+ * grid/utils/normalize_mosdepth.py:502-554 under torch.distributed. */
+typedef struct grid_gz_parts grid_gz_parts;
+int grid_gz_parts_new(grid_gz_parts **out);
+int grid_gz_parts_header(grid_gz_parts *h, int64_t n_total, int64_t r, const double *sel_means,
+                         const double *sel_ratios, int32_t level, int32_t threads);
+int grid_gz_parts_rows(grid_gz_parts *h, int64_t n, int64_t row0, int64_t r, const char *ids_nl, const double *raw,
+                       const int32_t *zq, int64_t ld_zq, int32_t level, int32_t threads);
+int grid_gz_parts_rows_dev(grid_ctx *ctx, grid_gz_parts *h, int64_t n, int64_t row0, int64_t r, const char *ids_nl,
+                           const double *raw, const int32_t *d_zq, int64_t ld_zq, int32_t threads,
+                           int64_t batch_bytes);
+int grid_gz_parts_size(const grid_gz_parts *h, int64_t *bytes);
+int grid_gz_parts_write(const grid_gz_parts *h, const char *path, int64_t offset, int32_t threads);
+int grid_gz_parts_free(grid_gz_parts *h);
 /* Reader: parse into a handle (*n_out rows, *r_out columns); z values as
  * integer hundredths (GRID_MISSING for "NA").  GRID_EUNSUPPORTED if the text
  * leaves the grammar (e.g. more than 2 decimals): callers fall back to the
@@ -635,6 +658,28 @@ int grid_fill_i32(grid_ctx *ctx, int32_t *d_p, int64_t n, int32_t v);
 int grid_md_finish(grid_ctx *ctx, const int32_t *d_Q, int64_t ldq, int64_t nK, int64_t nfiles,
                    const int32_t *d_rows, int32_t nrows, double min_depth, double max_depth, double *d_mean,
                    int32_t *d_valid, int64_t *d_cpos, uint64_t *d_present, uint64_t *d_nvalid, int64_t *h_m);
+/* Distributed ingest (`grid wgs` under torch.distributed: rank r parses a
+ * contiguous slice of the files in file order into its own d_Q over the same
+ * key list K; normalize_mosdepth.py:218-301 sums the population depths in
+ * that file order).  The sum is a chain over the ranks: rank r continues
+ * (d_sum, d_cnt) from rank r-1 over its rows (grid_md_popsum: the same
+ * sequential fp64 adds as grid_md_finish's, q / 100.0 exact); the last rank's
+ * totals give the valid flags (grid_md_popvalid: mean = sum / count, the
+ * min/max window, bit for bit grid_md_finish's).  Then per rank, with the
+ * global valid flags: column positions (exclusive scan) and per-row counts
+ * (grid_md_rowstats = grid_md_finish without the means), and the rows sent to
+ * every rank's 8192-aligned column shard (grid_md_pack_shards: shard s =
+ * valid columns [d_bounds[s], d_bounds[s+1]), written as [nrows][width_s] at
+ * d_out + nrows * d_bounds[s], row i taken from d_Q row d_src_rows[i]). */
+int grid_md_popsum(grid_ctx *ctx, const int32_t *d_Q, int64_t ldq, int64_t nK, const int32_t *d_rows,
+                   int32_t nrows, double *d_sum, int64_t *d_cnt);
+int grid_md_popvalid(grid_ctx *ctx, const double *d_sum, const int64_t *d_cnt, int64_t nK, double min_depth,
+                     double max_depth, int32_t *d_valid);
+int grid_md_rowstats(grid_ctx *ctx, const int32_t *d_Q, int64_t ldq, int64_t nK, int64_t nfiles,
+                     const int32_t *d_valid, int64_t *d_cpos, uint64_t *d_present, uint64_t *d_nvalid, int64_t *h_m);
+int grid_md_pack_shards(grid_ctx *ctx, const int32_t *d_Q, int64_t ldq, int64_t nK, const int32_t *d_valid,
+                        const int64_t *d_cpos, const int32_t *d_src_rows, int32_t nrows, const int64_t *d_bounds,
+                        int32_t nshards, int32_t *d_out);
 /* the matrix: d_out[d_dst_row[f] * ldo + column] for the valid columns; their (start, end) */
 int grid_md_gather(grid_ctx *ctx, const int32_t *d_Q, int64_t ldq, int64_t nK, int64_t nfiles,
                    const int32_t *d_valid, const int64_t *d_cpos, const int32_t *d_dst_row, int32_t *d_out,
