@@ -349,9 +349,6 @@ def files_leg(args, prep, steps, warmup, world, rank, dist, note):
         timed(nm, "_write_normalized_q", "step4_write_text")
     else:
         from grid_amd.utils import dist_step4
-        timed(dist_step4.HipBackend, "ingest", "step4_ingest_rank")
-        timed(dist_step4.HipBackend, "parts_rows", "step4_code_rows_rank")
-        timed(dist_step4, "_write_parts", "step4_write_rank")
     try:
         for w_ in range(warmup):
             pipeline.run_wgs_pipeline(console=None, config=cfg_path, keep_buffers=True)
@@ -364,6 +361,9 @@ def files_leg(args, prep, steps, warmup, world, rank, dist, note):
         t0 = time.perf_counter()
         for s_ in range(steps):
             pipeline.run_wgs_pipeline(console=None, config=cfg_path, keep_buffers=True)
+            if world > 1:                  # this rank's phases of the distributed step 4 (dist_step4.py)
+                for k, v in dist_step4.LAST_PHASES.items():
+                    phases["step4_rank_" + k] = phases.get("step4_rank_" + k, 0.0) + v
             note(f"from files: step {s_} done")
         torch.cuda.synchronize()
         if dist:

@@ -52,6 +52,9 @@ from .. import _abi
 
 I4, I8, F8 = np.int32, np.int64, np.float64
 
+# wall seconds per phase of the last normalize_dist on this rank (bench.py reports rank 0's)
+LAST_PHASES: dict = {}
+
 
 class DistFallback(Exception):
     """Every rank agreed to leave the distributed path (rank 0 runs the one-GPU step)."""
@@ -286,10 +289,19 @@ def normalize_dist(comm, backend, *, individuals, mosdepth_dir, chromosome, star
     frac_r, n_neighbors) of the cohort over every rank.  Returns the
     hand-off record for step 5 (``handoff.publish_neighbors``) or raises
     DistFallback (agreed by all ranks)."""
+    import time
     from ..fused import Steps47, shard_range
     from .normalize_mosdepth import find_bed_gz_paths, norm_chrom
     from .utils import log
     torch = backend.torch
+    LAST_PHASES.clear()
+    clock = [time.perf_counter()]
+
+    def mark(name):
+        backend.sync()
+        t = time.perf_counter()
+        LAST_PHASES[name] = LAST_PHASES.get(name, 0.0) + t - clock[0]
+        clock[0] = t
     W, rank = comm.world, comm.rank
     inds = list(individuals)
     where = find_bed_gz_paths(inds, mosdepth_dir)
@@ -328,6 +340,7 @@ def normalize_dist(comm, backend, *, individuals, mosdepth_dir, chromosome, star
     comm.broadcast(kt, 0)
     ref = (Kt[:nK].cpu().numpy(), kt[:ref_nlines].cpu().numpy(), ref_nlines)
     del Kt, kt
+    mark("keys")
 
     # ---- this rank's files over K ----
     ok, Q = True, None
@@ -342,6 +355,7 @@ def normalize_dist(comm, backend, *, individuals, mosdepth_dir, chromosome, star
         raise DistFallback("ingest")
     nf = f1 - f0
     rows_local = [f for f in range(nf) if status[f] == 0]
+    mark("ingest")
 
     # ---- population sums: a chain over the ranks in file order ----
     s = backend.alloc.empty(max(nK, 1), F8)
@@ -361,6 +375,7 @@ def normalize_dist(comm, backend, *, individuals, mosdepth_dir, chromosome, star
         backend.popvalid(s, c, nK, min_depth, max_depth, valid)
     comm.broadcast(valid, W - 1)
     del s, c
+    mark("popsum_chain")
     cpos, present, nval, m = backend.rowstats(Q, nK, nf, valid)
     dup = any(int(present[f]) != int(kept[f]) for f in rows_local)
     if not agree(comm, not dup):
@@ -391,6 +406,7 @@ def normalize_dist(comm, backend, *, individuals, mosdepth_dir, chromosome, star
     c0, c1 = bounds[rank], bounds[rank + 1]
     ml = c1 - c0
     src_local = [f - f0 for f in send_files[rank]]
+    mark("rows")
     send = backend.pack(Q, nK, valid, cpos, src_local, bounds)
     backend.free(Q)
     del Q, valid, cpos
@@ -405,6 +421,7 @@ def normalize_dist(comm, backend, *, individuals, mosdepth_dir, chromosome, star
         idx = torch.from_numpy(recv_rows).to(q.device)
         q.index_copy_(0, idx, recv[: n * ml].view(n, ml))
     del recv
+    mark("to_column_shards")
 
     # ---- steps 4-5 on this rank's column shard (fused.Steps47, bin split) ----
     upto = "step4"
@@ -422,6 +439,7 @@ def normalize_dist(comm, backend, *, individuals, mosdepth_dir, chromosome, star
                  frac_r=float(nbr_params["frac_r"]) if nbr_params else 1.0, comm=comm, keep_z=True, split="bin")
     st.run(q, max(ml, 1), upto=upto)
     del q
+    mark("steps4_5")
 
     # ---- header values: the selected columns' means and "%.3f" ratios, in column order ----
     r_loc = st.r_loc
@@ -481,6 +499,7 @@ def normalize_dist(comm, backend, *, individuals, mosdepth_dir, chromosome, star
                     z32[ri, ci] = torch.from_numpy(e[:, 2].astype(I4)).to(z32.device)
 
     # ---- the file: member 0 on rank 0, then every rank's rows at its offset ----
+    mark("to_row_blocks")
     parts = _abi.GzParts()
     try:
         if rank == 0:
@@ -488,7 +507,9 @@ def normalize_dist(comm, backend, *, individuals, mosdepth_dir, chromosome, star
         if nr:
             backend.parts_rows(parts, ids[a:b], raw[a:b], z32[:nr, :r_tot] if r_tot else z32[:nr, :0], a)
         del z32
+        mark("code_rows")
         _write_parts(comm, parts, output_path)
+        mark("write")
     finally:
         parts.free()
 
