@@ -513,16 +513,32 @@ def run_workload(args, n, m, steps, warmup, world, rank, local, dist, comm, dev,
     # two lanes, one per dipCN buffer: the last two passes' phasings (the
     # deferred one and finish()'s) overlap instead of queueing at the end
     lane = None
+    col_lane = None
     if not args.no_overlap:
+        # the phasing workgroup on a stream masked to ONE CU and the column
+        # passes (one round of workgroups) on a stream masked to all the others:
+        # they never share a CU (round 5: the passes ran 640 / 890 us, bimodal,
+        # whenever the phasing workgroup sat on one of their CUs)
+        ncu = _abi.device_cu_count(dev)
+        cu_mask = not args.no_cu_mask and ncu > 8
         lane = []
-        for _ in range(2):
+        for li in range(2):
             pdev = _abi.Device(local)
-            pstream = torch.cuda.Stream()
-            pdev.set_stream(pstream)
+            if cu_mask:
+                pdev.own_stream_cumask([ncu - 1 - li], ncu)
+                pstream = torch.cuda.ExternalStream(pdev.stream_handle())
+            else:
+                pstream = torch.cuda.Stream()
+                pdev.set_stream(pstream)
             lane.append((HipOps(pdev), pstream))
+        if cu_mask:
+            cdev = _abi.Device(local)
+            cdev.own_stream_cumask(range(ncu - 2), ncu)
+            col_lane = (HipOps(cdev), torch.cuda.ExternalStream(cdev.stream_handle()))
     st = Steps47(ops, talloc, n, m, c0, ml, k=args.k, n_nbr=300, top_frac=0.1, zmax=2.0, sigma2_max=1000.0,
                  frac_r=1.0, min_nbr=1, n_iters=args.n_iters, comm=comm, phase_lane=lane,
-                 chunk=chunk if streamed else None, keep_z=not streamed, split=args.shard, piece_bytes=piece_bytes)
+                 chunk=chunk if streamed else None, keep_z=not streamed, split=args.shard, piece_bytes=piece_bytes,
+                 col_lane=col_lane)
     st.set_reads(reads)
     st.set_phasing_graph(off, nbr, w)
 
@@ -663,6 +679,8 @@ def main():
                          "reported either way)")
     ap.add_argument("--no-files-baseline", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-overlap", action="store_true", help="run step 7 inline on the main stream")
+    ap.add_argument("--no-cu-mask", action="store_true",
+                    help="phase lanes and column passes on ordinary streams (no CU partition)")
     ap.add_argument("--headline", choices=["auto", "files", "chain"], default="auto",
                     help="the line's value: files = K whole `grid wgs` runs from the mosdepth files (the default at "
                          "BASELINE config 2), chain = K passes of the device chain over a cohort generated in HBM")

@@ -154,6 +154,9 @@ _SIGS = {
     "grid_fill_i32": [_vp, _vp, _i64, _i32],
     "grid_md_finish": [_vp, _vp, _i64, _i64, _i64, _vp, _i32, _f64, _f64, _vp, _vp, _vp, _vp, _vp, C.POINTER(_i64)],
     "grid_md_gather": [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp],
+    "grid_ctx_own_stream_cumask": [_vp, _vp, _i32],
+    "grid_ctx_stream": [_vp, C.POINTER(_vp)],
+    "grid_knn_seg_pack": [_vp, _vp, _i64, _i64, _i64, _vp],
     # distributed `grid wgs` (grid_amd/utils/dist_step4.py)
     "grid_md_popsum": [_vp, _vp, _i64, _i64, _vp, _i32, _vp, _vp],
     "grid_md_popvalid": [_vp, _vp, _vp, _i64, _f64, _f64, _vp],
@@ -324,6 +327,19 @@ class Device:
 
     def sync(self):
         call("grid_sync", self.ctx)
+
+    def own_stream_cumask(self, cus, ncu):
+        """Enqueue on a stream of this context's own restricted to the CUs
+        ``cus`` (indices < ncu; hipExtStreamCreateWithCUMask)."""
+        words = np.zeros((ncu + 31) // 32, dtype=np.uint32)
+        for c in cus:
+            words[c // 32] |= np.uint32(1 << (c % 32))
+        call("grid_ctx_own_stream_cumask", self.ctx, words.ctypes.data, len(words))
+
+    def stream_handle(self):
+        h = _vp()
+        call("grid_ctx_stream", self.ctx, C.byref(h))
+        return h.value or 0
 
     def cached(self, name, nbytes) -> "DevBuf":
         """A uint8 device buffer of at least ``nbytes`` kept on this context

@@ -95,6 +95,26 @@ int grid_ctx_own_stream(grid_ctx *ctx) {
   return GRID_OK;
 }
 
+int grid_ctx_own_stream_cumask(grid_ctx *ctx, const uint32_t *mask, int32_t nwords) {
+  REQUIRE(ctx && mask && nwords > 0, "bad args");
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = nullptr;
+  HIPCHK(hipExtStreamCreateWithCUMask(&s, (uint32_t)nwords, mask));
+  if (ctx->own) {
+    (void)hipStreamSynchronize(ctx->own);
+    (void)hipStreamDestroy(ctx->own);
+  }
+  ctx->own = s;
+  ctx->stream = s;
+  return GRID_OK;
+}
+
+int grid_ctx_stream(grid_ctx *ctx, void **out) {
+  REQUIRE(ctx && out, "bad args");
+  *out = (void *)ctx->stream;
+  return GRID_OK;
+}
+
 int grid_ctx_cu_count(grid_ctx *ctx, int32_t *n) {
   REQUIRE(ctx && n, "bad args");
   *n = ctx->ncu;

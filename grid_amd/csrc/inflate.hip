@@ -53,7 +53,15 @@ __constant__ uint32_t c_crc_pow[48][32];   // columns of M^(2^k), M = one zero b
 // kind 0 = a symbol the fast loop does not take (286, 287, distance 30, 31)
 // K_LEN is the only kind with bit 5 of the entry set (the fast loop's one-bit
 // test for its commonest symbol: a match length); K_DIST has bit 4
-constexpr uint32_t K_LIT = 1, K_LEN = 2, K_EOB = 4, K_DIST = 1;
+// K_LIT2 (round 6): TWO literals whose codes fit the table's LFAST bits
+// together (mosdepth text is mostly digit literals of 3-5 bit codes):
+//   [31:24] second byte, [23:16] first byte, [15:12] first code's length,
+//   [7:4] kind, [3:0] both codes' length -- one table read, one loop trip and
+//   one limit test for two output bytes (pair_literals builds them)
+constexpr uint32_t K_LIT = 1, K_LEN = 2, K_EOB = 4, K_LIT2 = 8, K_DIST = 1;
+#ifndef GRID_INFLATE_PAIRS
+#define GRID_INFLATE_PAIRS 1   // 0: the round-5 kernel's one literal per table read (A/B build `make inflate_nopair`)
+#endif
 constexpr int F_LEN = 1 << icore::LFAST, F_DIST = 1 << icore::DFAST;
 
 __device__ __forceinline__ uint32_t fast_entry(int ft, uint32_t sym, uint32_t l) {
@@ -90,6 +98,7 @@ struct DevP {
   int64_t wbase;
   uint32_t fcur;                 // fast_codes' input window: bytes fbase .. +256 (lane k: 4k..4k+3)
   int32_t fbase;
+  int paired;                    // the literal/length table's K_LIT2 entries are built
 
   __device__ __forceinline__ uint32_t load_word(int64_t b) const {
     const int64_t o = b + 4 * lane;   // (the core's window: int64 b; the fast loop's: int32)
@@ -124,6 +133,7 @@ struct DevP {
     __builtin_amdgcn_wave_barrier();
   }
   __device__ __forceinline__ void fclear(int ft, int n) {
+    if (ft == icore::FT_LEN) paired = 0;
     uint32_t *t = ftab + (ft == icore::FT_LEN ? 0 : F_LEN);
     for (int k = lane; k < n; k += 64) t[k] = 0;
     __builtin_amdgcn_wave_barrier();
@@ -141,6 +151,7 @@ struct DevP {
     if (ft == icore::FT_LEN) {
       const uint32_t e = ftab_rd(i), kind = (e >> 4) & 15;
       if (!e) return 0;
+      if (kind == K_LIT2) return (((e >> 16) & 0xffu) << 4) | ((e >> 12) & 15);   // its first literal
       const uint32_t sym = kind == K_LEN ? 257 + ((e >> 11) & 31) : kind == K_EOB ? 256 : e >> 16;
       return (sym << 4) | (e & 15);
     }
@@ -234,6 +245,35 @@ struct DevP {
 
 
 
+  // K_LIT2 entries over the literal/length table just built: index i holds a
+  // literal of code length l1 < LFAST whose next LFAST - l1 bits (i >> l1)
+  // start another literal of length l2 <= LFAST - l1 -- the pair decodes in
+  // one step.  Entry i reads entry i >> l1 < i, so the 64-entry groups are
+  // rewritten from the top down (a group only reads lower groups, still
+  // untouched, and itself, read before it is written): one entry per lane in
+  // flight, no register array.
+  __device__ __forceinline__ void pair_literals() {
+#pragma unroll 1
+    for (int g = F_LEN / 64 - 1; g >= 0; g--) {
+      const int i = 64 * g + lane;
+      const uint32_t e = ftab[i];
+      uint32_t v = e;
+      const uint32_t l1 = e & 15u;
+      if (((e >> 4) & 15u) == K_LIT && l1 < (uint32_t)icore::LFAST) {
+        const uint32_t e2 = ftab[i >> l1];
+        const uint32_t l2 = e2 & 15u;
+        if (((e2 >> 4) & 15u) == K_LIT && l1 + l2 <= (uint32_t)icore::LFAST)
+          v = ((e2 >> 16) << 24) | (((e >> 16) & 0xffu) << 16) | (l1 << 12) | (K_LIT2 << 4) | (l1 + l2);
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+      ftab[i] = v;
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+    }
+    paired = 1;
+  }
+
   // A block's codes while >= 16 input bytes and >= 296 bytes of output room
   // remain.  Returns 1 after the end-of-block code, -1 on an error (err set),
   // 0 when the core's per-symbol loop must finish the block.  The decode
@@ -252,6 +292,7 @@ struct DevP {
   __device__ int fast_codes(I &inf) {
     const int room = cap - 296;
     if (pos > room) return 0;
+    if (GRID_INFLATE_PAIRS && !paired) pair_literals();
     int ip = (int)inf.ip;
     const int nin = (int)n_in;
     uint64_t vb;                        // the bit buffer, in VGPRs
@@ -337,6 +378,16 @@ struct DevP {
         len = (uint32_t)__builtin_amdgcn_readfirstlane((int)((ev >> 16) + xb));
         vb >>= lxv;
         bc -= __builtin_amdgcn_readfirstlane((int)lxv);
+      } else if (kind == (K_LIT2 << 4)) {
+        const uint32_t lv = ev & 15u;
+        vb >>= lv;
+        bc -= __builtin_amdgcn_readfirstlane((int)lv);
+        ring[pos & RMASK] = (uint8_t)(ev >> 16);
+        ring[(pos + 1) & RMASK] = (uint8_t)(ev >> 24);
+        __builtin_amdgcn_wave_barrier();
+        pos += 2;
+        if (pos >= lim && !limit()) break;
+        continue;
       } else if (kind == (K_LIT << 4)) {
         const uint32_t lv = ev & 15u;
         vb >>= lv;
@@ -459,6 +510,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GRID_INFLATE
   p.lane = threadIdx.x;
   p.win = 0;
   p.wbase = -1;
+  p.paired = 0;
   icore::Inflater<DevP> inf(p);
   inf.ip = skew;
   const int rc = !fits ? (int)icore::E_SPACE : in_len[f] > 0 ? inf.gunzip() : (int)icore::E_HEADER;

@@ -1635,6 +1635,89 @@ __global__ __launch_bounds__(256) void k_seg_merge(const unsigned long long *__r
   cnto[i] = (int32_t)w;
 }
 
+// k_seg_merge with one WAVE per row (round 6: the thread-per-row form kept 13
+// workgroups busy at n = 3,202 and walked up to 2W + 1 lists of K1 keys
+// serially, 122 us per step at W = 8): the row's T = K1 (bi + 2) candidate keys
+// are spread over the lanes (R per lane), then the k + 1 smallest DISTINCT
+// keys are taken one by one by wave minima (equal keys -- a pair seen as a row
+// and as a column entry -- once), then the same self-drop and first-k rule.
+template <int K1, int R>
+__global__ __launch_bounds__(256) void k_seg_merge_w(const unsigned long long *__restrict__ rowc,
+                                                     const unsigned long long *__restrict__ colc, int64_t ldc,
+                                                     int64_t B, int64_t n, int64_t k, int32_t *__restrict__ idx,
+                                                     int64_t *__restrict__ d2o, int32_t *__restrict__ cnto) {
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (i >= n) return;                                  // whole waves leave together
+  const int64_t ktake = (k + 1 < n) ? k + 1 : n;
+  const int64_t bi = i / B;
+  const int64_t T = (int64_t)K1 * (bi + 2);
+  unsigned long long v[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int64_t t = lane + 64 * r;
+    unsigned long long key = ~0ull;
+    if (t < K1) {
+      key = rowc[i * K1 + t];
+    } else if (t < T) {
+      const int64_t b = (t - K1) / K1, e = (t - K1) % K1;
+      key = colc[(b * ldc + (i - b * B)) * K1 + e];
+    }
+    v[r] = key;
+  }
+  int64_t w = 0;
+  bool self = false;
+  for (int64_t e = 0; e < ktake; e++) {
+    unsigned long long m = v[0];
+#pragma unroll
+    for (int r = 1; r < R; r++) m = v[r] < m ? v[r] : m;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long y = __shfl_xor(m, o, 64);
+      m = y < m ? y : m;
+    }
+    if (m == ~0ull) break;
+#pragma unroll
+    for (int r = 0; r < R; r++) v[r] = v[r] == m ? ~0ull : v[r];
+    const int64_t j = (int64_t)(m & 0xFFFFFull);
+    if (j == i && !self) {
+      self = true;
+      continue;
+    }
+    if (w < k) {
+      if (lane == 0) {
+        idx[i * k + w] = (int32_t)j;
+        d2o[i * k + w] = (int64_t)(m >> 20);
+      }
+      w++;
+    }
+  }
+  if (lane == 0) {
+    for (int64_t e = w; e < k; e++) {
+      idx[i * k + e] = -1;
+      d2o[i * k + e] = 0;
+    }
+    cnto[i] = (int32_t)w;
+  }
+}
+
+// the bin split's send buffer: blockIdx.y = 2 q + slot (block b = q or
+// 2W-1-q), blockIdx.x = row r of the block; one coalesced row copy each
+__global__ __launch_bounds__(256) void k_seg_pack(const int64_t *__restrict__ gram, int64_t np_, int64_t W, int64_t B,
+                                                  int64_t *__restrict__ send) {
+  const int64_t q = blockIdx.y >> 1, slot = blockIdx.y & 1, r = blockIdx.x;
+  const int64_t b = slot ? 2 * W - 1 - q : q;
+  const int64_t nc = (2 * W - b) * B;
+  const int64_t off = q * B * (2 * W + 1) * B + (slot ? B * (2 * W - q) * B : 0);
+  int64_t *dst = send + off + r * nc;
+  const int64_t row = b * B + r;
+  const int64_t c0 = b * B;
+  for (int64_t c = threadIdx.x; c < nc; c += blockDim.x) {
+    const int64_t col = c0 + c;
+    dst[c] = (row < np_ && col < np_) ? gram[row * np_ + col] : 0;
+  }
+}
+
 // Row top-(k+1) for larger k: 8-pass radix select on the packed keys over the
 // (coalesced) row, then a bitonic sort of the <= SELCAP survivors.
 constexpr int SELCAP = 4096;
@@ -2290,8 +2373,25 @@ int grid_knn_seg_merge(grid_ctx *ctx, const unsigned long long *d_rowc, const un
     HIPCHK(hipMemsetAsync(d_cnt, 0, n * 4, ctx->stream));
     return GRID_OK;
   }
-  hipLaunchKernelGGL(k_seg_merge<GRID_SEG_K1>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, d_rowc,
-                     d_colc, ldc, B, n, k, d_idx, d_d2, d_cnt);
+  // the wave-per-row form while a row's candidates fit 8 keys per lane (2W + 1
+  // lists of K1: W <= 15 at K1 = 16), the thread-per-row form beyond
+  const int64_t blocks = (n + B - 1) / B;
+  if (GRID_SEG_K1 * (blocks + 1) <= 64 * 8) {
+    hipLaunchKernelGGL((k_seg_merge_w<GRID_SEG_K1, 8>), dim3((unsigned)((n + 3) / 4)), dim3(256), 0, ctx->stream,
+                       d_rowc, d_colc, ldc, B, n, k, d_idx, d_d2, d_cnt);
+  } else {
+    hipLaunchKernelGGL(k_seg_merge<GRID_SEG_K1>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, d_rowc,
+                       d_colc, ldc, B, n, k, d_idx, d_d2, d_cnt);
+  }
+  LAUNCHCHK();
+  return GRID_OK;
+}
+
+int grid_knn_seg_pack(grid_ctx *ctx, const int64_t *d_gram, int64_t np_, int64_t W, int64_t B, int64_t *d_send) {
+  REQUIRE(ctx && d_gram && d_send && np_ > 0 && W > 0 && B > 0 && 2 * W * B >= np_ && W <= 32768 && B <= (1 << 30),
+          "bad args");
+  hipLaunchKernelGGL(k_seg_pack, dim3((unsigned)B, (unsigned)(2 * W)), dim3(256), 0, ctx->stream, d_gram, np_, W, B,
+                     d_send);
   LAUNCHCHK();
   return GRID_OK;
 }

@@ -445,6 +445,10 @@ class HipOps:
         call("grid_knn_seg_topk", self.ctx, ptr(seg), ld, nrows, ncols, ptr(norms), n, k, r0, c0, ptr(rowc),
              ptr(colc))
 
+    def seg_pack(self, gram, np_, W, B, send):
+        """The segment reduce-scatter's send buffer from the whole Gram, one launch."""
+        call("grid_knn_seg_pack", self.ctx, ptr(gram), np_, W, B, ptr(send))
+
     def seg_merge(self, rowc, colc, ldc, B, n, k, idx, d2, cnt):
         call("grid_knn_seg_merge", self.ctx, ptr(rowc), ptr(colc), ldc, B, n, k, ptr(idx), ptr(d2), ptr(cnt))
 
@@ -528,7 +532,7 @@ class Steps47:
 
     def __init__(self, ops, alloc, n, m_total, col0, m_local, *, k=10, n_nbr=300, top_frac=0.1, zmax=2.0,
                  sigma2_max=1000.0, frac_r=1.0, min_nbr=1, n_iters=100, comm=None, phase_lane=None, zq16=True,
-                 chunk=None, keep_z=True, on_z_chunk=None, split="bin", piece_bytes=1 << 31):
+                 chunk=None, keep_z=True, on_z_chunk=None, split="bin", piece_bytes=1 << 31, col_lane=None):
         """``phase_lane``: optional (ops, torch.cuda.Stream) pair on which step
         7 runs.  Phasing is one workgroup for ~4 ms, so on its own stream it
         overlaps other work instead of idling the other 255 CUs.  It is
@@ -553,6 +557,11 @@ class Steps47:
         Gram reduce-scatter.  Both give the same segments, bit for bit
         (integer sums), and share the candidate merge."""
         self.ops, self.A, self.comm = ops, alloc, comm
+        # col_lane: optional (ops, torch stream) pair for the column-statistics
+        # passes of a one-chunk shard -- a stream CU-masked away from the phase
+        # lane's CU (bench.py), so the passes' one round of workgroups never
+        # shares a CU with the phasing workgroup (VERDICT r5 item 3)
+        self.col_lane = col_lane
         # one lane, or two: the phasing of _dips[b] then runs on lane b, so the
         # last two passes' phasings (finish()) overlap instead of queueing
         self.phase_lane = phase_lane
@@ -843,11 +852,24 @@ class Steps47:
         self._mark("row_means")
         # ---- pass B: column statistics (local, exact); the chunk the buffer
         # still holds goes first ----
-        for ci in reversed(order):
-            a, b = self.chunks[ci]
-            qc, ldc = self._chunk_q(q, ld, ci, "col_stats")
-            o.col_means(qc, n, b - a, ldc, self.rm, self.mu[a:b])
-            o.col_vars(qc, n, b - a, ldc, self.rm, self.mu[a:b], self.var[a:b], self.ratio[a:b])
+        if self.col_lane is not None and self.nch == 1:
+            import torch
+            cops, cstream = self.col_lane
+            ev = torch.cuda.Event()
+            ev.record()
+            cstream.wait_event(ev)
+            qc, ldc = self._chunk_q(q, ld, 0, "col_stats")
+            cops.col_means(qc, n, ml, ldc, self.rm, self.mu[:ml])
+            cops.col_vars(qc, n, ml, ldc, self.rm, self.mu[:ml], self.var[:ml], self.ratio[:ml])
+            done = torch.cuda.Event()
+            done.record(cstream)
+            torch.cuda.current_stream().wait_event(done)
+        else:
+            for ci in reversed(order):
+                a, b = self.chunks[ci]
+                qc, ldc = self._chunk_q(q, ld, ci, "col_stats")
+                o.col_means(qc, n, b - a, ldc, self.rm, self.mu[a:b])
+                o.col_vars(qc, n, b - a, ldc, self.rm, self.mu[a:b], self.var[a:b], self.ratio[a:b])
         self._mark("col_stats")
         # ---- pass C: median -> scale; sorted(...)[int(top_frac*n)] -> selection;
         # step 5's region filter on the "%.3f" ratios (find_neighbors.py:148-171)
@@ -1030,7 +1052,12 @@ class Steps47:
         lists, and the exact merge into every row's neighbours on every rank
         (grid_knn_seg_topk / grid_knn_seg_merge)."""
         o, n, W, B, npw, np_ = self.ops, self.n, self.world, self.B, self.npw, self.np_
-        torch = self.A.torch
+        if hasattr(o, "seg_pack"):
+            o.seg_pack(self.gram, np_, W, B, self.seg_send)
+            self.comm.reduce_scatter_sum(self.seg_recv, self.seg_send)
+            self._mark("reduce_scatter")
+            self._seg_candidates()
+            return
         send = self.seg_send.view(W, self.seg_len)
         for q in range(W):                       # rank q's slot: its blocks q and 2W-1-q
             off = 0

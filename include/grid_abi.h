@@ -71,6 +71,13 @@ int grid_ctx_set_stream(grid_ctx *ctx, void *hip_stream);
 int grid_ctx_own_stream(grid_ctx *ctx);
 /* Compute units of the context's device (persistent grids, batch sizing). */
 int grid_ctx_cu_count(grid_ctx *ctx, int32_t *n);
+/* The context's own stream re-created with a CU mask (hipExtStreamCreateWithCUMask;
+ * bit c of mask[c / 32] = CU c): the device chain gives its one-workgroup
+ * phasing lane one CU and its one-round column-statistics passes the others,
+ * so the two never share a CU.  grid_ctx_stream: the stream the context
+ * enqueues on (for a caller's events). */
+int grid_ctx_own_stream_cumask(grid_ctx *ctx, const uint32_t *mask, int32_t nwords);
+int grid_ctx_stream(grid_ctx *ctx, void **out);
 /* hipMemGetInfo of the context's device: free and total HBM bytes (buffer
  * lifetime checks: the step-4 ingest releases its device buffers). */
 int grid_mem_info(grid_ctx *ctx, size_t *free_bytes, size_t *total_bytes);
@@ -392,6 +399,11 @@ int grid_knn_topk(grid_ctx *ctx, int64_t *d_gram, int64_t n, int64_t np_, int64_
 int grid_knn_seg_topk(grid_ctx *ctx, const int64_t *d_seg, int64_t ld, int64_t nrows, int64_t ncols,
                       const int64_t *d_norms, int64_t n, int64_t k, int64_t r0, int64_t c0,
                       unsigned long long *d_rowc, unsigned long long *d_colc);
+/* The bin split's reduce-scatter send buffer from the whole (upper-triangle)
+ * Gram [np_][np_] int64: for every rank q, its blocks b = q and 2W-1-q, each
+ * [B][(2W - b) B] (rows b B.., columns b B..; cells beyond np_ zero), at
+ * d_send + q * seg_len (seg_len = B (2W+1) B). */
+int grid_knn_seg_pack(grid_ctx *ctx, const int64_t *d_gram, int64_t np_, int64_t W, int64_t B, int64_t *d_send);
 int grid_knn_seg_merge(grid_ctx *ctx, const unsigned long long *d_rowc, const unsigned long long *d_colc,
                        int64_t ldc, int64_t B, int64_t n, int64_t k, int32_t *d_idx, int64_t *d_d2,
                        int32_t *d_cnt);

@@ -105,3 +105,24 @@ def test_dist_wgs_config1_world2(tmp_path):
     logs = "".join(open(f"{log}.{r}").read() for r in range(2))
     assert "Failed" not in logs and "rank 0 reads the cohort" not in logs, logs
     cohort_files.check_outputs("g_cfg1", tmp_path / "out", only=FILES)
+
+
+def test_file_slices_and_row_blocks_cover_everything():
+    """The ingest's file slices (contiguous, balanced by compressed bytes, empty
+    and missing files counted) and the writer's row blocks partition their
+    ranges for every world size, including more ranks than files."""
+    from grid_amd.utils.dist_step4 import file_slices, row_blocks
+    import numpy as np
+    rng = np.random.default_rng(3)
+    for nf in (0, 1, 3, 40, 3202):
+        sizes = rng.integers(0, 5 << 20, nf).tolist()
+        for world in (1, 2, 3, 8, 64):
+            b = file_slices(sizes, world)
+            assert b[0] == 0 and b[-1] == nf and len(b) == world + 1
+            assert all(b[r] <= b[r + 1] for r in range(world))
+            if nf >= 8 * world and world > 1:
+                per = [sum(sizes[b[r]:b[r + 1]]) for r in range(world)]
+                assert max(per) <= sum(sizes) / world + max(sizes) + nf     # balanced to one file
+        for world in (1, 2, 5, 8):
+            rb = row_blocks(nf, world)
+            assert rb[0] == 0 and rb[-1] == nf and all(rb[t] <= rb[t + 1] for t in range(world))
