@@ -515,12 +515,13 @@ def run_workload(args, n, m, steps, warmup, world, rank, local, dist, comm, dev,
     lane = None
     col_lane = None
     if not args.no_overlap:
-        # the phasing workgroup on a stream masked to ONE CU and the column
-        # passes (one round of workgroups) on a stream masked to all the others:
-        # they never share a CU (round 5: the passes ran 640 / 890 us, bimodal,
-        # whenever the phasing workgroup sat on one of their CUs)
+        # --cu-mask (A/B only): the phasing workgroup on a stream masked to ONE
+        # CU and the column passes on a stream masked to all the others, so they
+        # never share a CU.  Measured slower (r06e: 13.98 against 8.67 ms per
+        # rank; every pass on the masked streams ran 1.5-1.6x longer), so the
+        # lanes are ordinary streams by default
         ncu = _abi.device_cu_count(dev)
-        cu_mask = not args.no_cu_mask and ncu > 8
+        cu_mask = args.cu_mask and ncu > 8
         lane = []
         for li in range(2):
             pdev = _abi.Device(local)
@@ -679,8 +680,10 @@ def main():
                          "reported either way)")
     ap.add_argument("--no-files-baseline", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-overlap", action="store_true", help="run step 7 inline on the main stream")
-    ap.add_argument("--no-cu-mask", action="store_true",
-                    help="phase lanes and column passes on ordinary streams (no CU partition)")
+    ap.add_argument("--cu-mask", action="store_true",
+                    help="A/B: phase lanes on streams masked to one CU each, the column passes on a stream masked to "
+                         "the others (hipExtStreamCreateWithCUMask; measured SLOWER, r06e: 13.98 vs 8.67 ms per rank)")
+    ap.add_argument("--no-cu-mask", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--headline", choices=["auto", "files", "chain"], default="auto",
                     help="the line's value: files = K whole `grid wgs` runs from the mosdepth files (the default at "
                          "BASELINE config 2), chain = K passes of the device chain over a cohort generated in HBM")

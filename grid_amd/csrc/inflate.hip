@@ -60,7 +60,11 @@ __constant__ uint32_t c_crc_pow[48][32];   // columns of M^(2^k), M = one zero b
 //   one limit test for two output bytes (pair_literals builds them)
 constexpr uint32_t K_LIT = 1, K_LEN = 2, K_EOB = 4, K_LIT2 = 8, K_DIST = 1;
 #ifndef GRID_INFLATE_PAIRS
-#define GRID_INFLATE_PAIRS 1   // 0: the round-5 kernel's one literal per table read (A/B build `make inflate_nopair`)
+// 1: build K_LIT2 entries (A/B: `make inflate_pairs`).  Measured equal to the
+// one-literal loop (66.7 vs 66.6 GB/s of text, r06e) -- the mosdepth text's
+// literal codes rarely pair within 8 bits, and 2^9 / 2^10 tables at the lower
+// occupancy they force are slower (60.8 / 50.5 GB/s) -- so off
+#define GRID_INFLATE_PAIRS 0
 #endif
 constexpr int F_LEN = 1 << icore::LFAST, F_DIST = 1 << icore::DFAST;
 

@@ -8,8 +8,8 @@ O=gpurun_out/r06e
 mkdir -p $O
 export TMPDIR=/tmp
 L=grid_amd/_lib
-timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -p no:cacheprovider \
-  tests/test_gpu_inflate.py tests/test_gpu_sharded.py tests/test_gpu_kernels.py tests/test_gpu_cohort.py \
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider \
+  tests/test_gpu_inflate.py tests/test_gpu_sharded.py tests/test_gpu_kernels.py tests/test_gpu_cohort.py tests/test_gpu_ingest.py tests/test_gpu_e2e.py tests/test_gpu_dist_wgs.py \
   > $O/pytest.log 2>&1 || { tail -n 60 $O/pytest.log; exit 1; }
 tail -n 1 $O/pytest.log
 for v in l9 l10; do
@@ -32,3 +32,6 @@ for cm in "" "--no-cu-mask"; do
     > $O/sim_cfg2_w8_r0_bin_$tag.json 2> $O/sim_$tag.err || { tail -n 30 $O/sim_$tag.err; exit 1; }
   python3 -c "import json;d=json.load(open('$O/sim_cfg2_w8_r0_bin_$tag.json'));print('$tag', d['rank_ms_per_step'], d['stages_ms'])"
 done
+timeout -k 10 400 python3 bench.py --steps 3 --warmup 1 --config3-steps 0 --no-cpu-baseline > $O/bench_files.json \
+  2> $O/bench_files.err || { tail -n 30 $O/bench_files.err; rm -rf /dev/shm/grid_bench_cfg2 /tmp/grid_bench_cfg2_out; exit 1; }
+python3 -c "import json;d=json.load(open('$O/bench_files.json'));print('files', d['ms_per_step'], d['from_files']['stages_s'], 'chain', d['device_chain']['ms_per_step'])"
