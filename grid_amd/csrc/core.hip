@@ -650,6 +650,309 @@ __global__ void k_colmap_fix_st(const int32_t *flags, int32_t *map, int64_t n, i
   if (!flags[i]) map[i] = -1;
 }
 
+// ---- pass C, round 6: the same order statistics and compactions in about
+// half the launches (r05 kernel trace: the selection was ~55 dispatches of
+// ~5 us each between the column passes and zquant).
+//   * 11-bit digits: 6 histogram passes instead of 8 (digits [53,64) ...
+//     [9,20), then [0,9));
+//   * the first pass is one histogram for every key (no prefix yet); its total
+//     is the non-NaN count, so the count kernel and the rank kernel fold into
+//     the first pick, and the last pick writes the values (fin1 / fin2);
+//   * every pass has its own zeroed histogram (one memset), so a pick never
+//     clears bins another key's pick still reads;
+//   * a wave adds the run of lanes sharing the leading lane's digit with one
+//     LDS atomic (the first passes put nearly every value in one or two bins:
+//     35 / 18 / 25 us of LDS atomic contention in r05);
+//   * the compactions (ratio > thr -> sel + r3; kept sigma^2 -> colmap) are a
+//     block-count kernel plus an ordered scatter, instead of flags + hipcub.
+constexpr int SDB = 11, SBINS = 1 << SDB, SPASS = 6;
+__host__ __device__ constexpr int sel_lo(int p) { return p == SPASS - 1 ? 0 : 64 - SDB * (p + 1); }
+__host__ __device__ constexpr int sel_hi(int p) { return 64 - SDB * p; }
+
+__global__ __launch_bounds__(256) void k_kth_hist11(const double *__restrict__ v, int64_t n, int nk, int pass,
+                                                    const KthState *__restrict__ st, unsigned *__restrict__ ghist) {
+  __shared__ unsigned h[KTH_MAX][SBINS];
+  const int nh = pass == 0 ? 1 : nk;              // pass 0: one histogram for all keys
+  for (int t = threadIdx.x; t < nh * SBINS; t += 256) (&h[0][0])[t] = 0;
+  uint64_t pre[KTH_MAX];
+  bool own[KTH_MAX];                              // keys with an earlier key's prefix share its histogram
+#pragma unroll
+  for (int j = 0; j < KTH_MAX; j++) {
+    pre[j] = j < nk ? st[j].prefix : 0;
+    own[j] = j < nh;
+#pragma unroll
+    for (int i = 0; i < j; i++) own[j] = own[j] && pre[i] != pre[j];
+  }
+  __syncthreads();
+  const int lo = sel_lo(pass), hi = sel_hi(pass);
+  const unsigned dmask = (1u << (hi - lo)) - 1u;
+  const int lane = threadIdx.x & 63;
+  constexpr int U = 8;                            // values in flight per thread
+  for (int64_t i0 = (int64_t)blockIdx.x * 256 * U; i0 < n; i0 += (int64_t)gridDim.x * 256 * U) {
+    double d[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t i = i0 + u * 256 + threadIdx.x;
+      d[u] = i < n ? v[i] : __builtin_nan("");
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t k = dkey(d[u]);
+      const unsigned dig = (unsigned)(k >> lo) & dmask;
+#pragma unroll
+      for (int j = 0; j < KTH_MAX; j++) {
+        if (j >= nh) break;
+        bool m = own[j] && d[u] == d[u] && (hi >= 64 || ((k ^ pre[j]) >> hi) == 0);
+        // runs of lanes sharing the leading lane's digit: one atomic each.  The
+        // first pass (sign + exponent) puts nearly every value in a few bins:
+        // peel until none is left; later passes are spread: peel once (ties)
+        for (int it = 0; pass == 0 || it < 1; it++) {
+          const uint64_t act = __ballot(m);
+          if (!act) break;
+          const int ld = __builtin_ctzll(act);
+          const unsigned dl = (unsigned)__shfl((int)dig, ld, 64);
+          const uint64_t same = __ballot(m && dig == dl);
+          if (lane == ld) atomicAdd(&h[j][dl], (unsigned)__popcll(same));
+          if (dig == dl) m = false;
+        }
+        if (m) atomicAdd(&h[j][dig], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  unsigned *gh = ghist + (size_t)pass * KTH_MAX * SBINS;
+  for (int t = threadIdx.x; t < nh * SBINS; t += 256) {
+    const unsigned c = (&h[0][0])[t];
+    if (c) atomicAdd(gh + t, c);
+  }
+}
+
+// the histogram key j's pick reads: the first key with the same prefix
+__device__ __forceinline__ int kth_rep(int pass, int j, const uint64_t *pre) {
+  if (pass == 0) return 0;
+  for (int i = 0; i < j; i++)
+    if (pre[i] == pre[j]) return i;
+  return j;
+}
+
+// One wave per key j: the digit of pass `pass` holding the key's rank.  Pass 0
+// derives the ranks from the non-NaN count (mode 1: the median pair and
+// sorted(...)[int(top_frac * n)], normalize_mosdepth.py:462,495; mode 2:
+// sorted(r3)[min(int(r_tot * (1 - frac_r)), nv - 1)], find_neighbors.py:166-170),
+// the last pass writes the values (as k_sel_fin1 / k_sel_fin2).
+__global__ __launch_bounds__(64 * KTH_MAX) void k_kth_pick11(int pass, int nk, int mode, double frac,
+                                                             double sigma2_max, KthState *__restrict__ ks,
+                                                             const unsigned *__restrict__ ghist,
+                                                             int64_t *__restrict__ st) {
+  // one workgroup, a wave per key: every wave reads the pass's prefixes and
+  // ranks before any wave stores its key's next state
+  const int j = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint64_t pres[KTH_MAX];
+#pragma unroll
+  for (int i = 0; i < KTH_MAX; i++) pres[i] = i < nk && pass > 0 ? ks[i].prefix : 0ull;
+  const int64_t rank_in = pass > 0 ? ks[j].rank : 0;
+  __syncthreads();
+  const unsigned *hj = ghist + ((size_t)pass * KTH_MAX + kth_rep(pass, j, pres)) * SBINS;
+  constexpr int PER = SBINS / 64;
+  unsigned c[PER];
+  unsigned s = 0;
+#pragma unroll
+  for (int q = 0; q < PER; q++) {
+    c[q] = hj[lane * PER + q];
+    s += c[q];
+  }
+  unsigned incl = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  const int64_t nv = (int64_t)__shfl(incl, 63, 64);       // pass 0: every non-NaN value
+  int64_t rank;
+  if (pass == 0) {
+    int64_t r = 0;
+    int err = 0;
+    if (mode == 1) {
+      if (nv > 0) {
+        const int64_t a = nv % 2 ? nv / 2 : nv / 2 - 1, b = nv / 2;
+        const double x = frac * (double)nv;
+        int64_t t = (x == x && fabs(x) < 9.2e18) ? (int64_t)x : -1 - nv;     // int(): truncation toward zero
+        if (t < 0) t += nv;
+        if (t < 0 || t >= nv) {
+          err = 1;                                                          // IndexError: list index out of range
+          t = 0;
+        }
+        r = j == 0 ? a : j == 1 ? b : t;
+      }
+    } else if (nv > 0) {
+      const double x = (double)st[GRID_SEL_RTOT] * (1.0 - frac);
+      r = (x == x && fabs(x) < 9.2e18) ? (int64_t)x : nv - 1;
+      if (r > nv - 1) r = nv - 1;
+      if (r < 0) {
+        err = 2;
+        r = 0;
+      }
+    }
+    if (lane == 0) {
+      if (j == 0) st[mode == 1 ? GRID_SEL_NVALID : GRID_SEL_NV] = nv;
+      if (err) st[GRID_SEL_ERR] = err;
+    }
+    rank = r;
+  } else {
+    rank = rank_in;
+  }
+  // the lane whose bins hold the rank extends the prefix; lane 0 stores it
+  // (one writer: no same-wave store/load pair on ks[j])
+  const uint64_t pre0 = pres[j];
+  const int lo = sel_lo(pass);
+  const unsigned excl = incl - s;
+  const bool mine = (int64_t)excl <= rank && rank < (int64_t)incl;
+  int64_t r = rank - excl;
+  int q = 0;
+  while (q < PER - 1 && r >= (int64_t)c[q]) { r -= c[q]; q++; }
+  const uint64_t mb = __ballot(mine);
+  const int ml = mb ? __builtin_ctzll(mb) : 0;
+  const uint64_t pre = mb ? pre0 | ((uint64_t)(unsigned)__shfl(lane * PER + q, ml, 64) << lo) : pre0;
+  const int64_t rk = mb ? (int64_t)__shfl((int)r, ml, 64) : 0;
+  if (lane == 0) {
+    ks[j] = KthState{pre, rk};
+    if (pass == SPASS - 1) {
+      const bool any = (pass == 0 ? nv : st[mode == 1 ? GRID_SEL_NVALID : GRID_SEL_NV]) > 0;
+      const double val = any ? kth_value(pre) : 0.0;
+      if (mode == 1) {
+        st_setf(st, GRID_SEL_V0 + j, val);
+        if (j == 2) st_setf(st, GRID_SEL_THR, any ? val : __builtin_nan(""));   // NaN: nothing is >
+      } else {
+        st_setf(st, GRID_SEL_SMIN, any ? val : -__builtin_inf());
+        st_setf(st, GRID_SEL_SMAX, any ? sigma2_max : __builtin_inf());
+      }
+    }
+  }
+}
+
+// ordered compactions: block b owns elements [b * SCB, (b + 1) * SCB)
+constexpr int SCB = 4096;                       // 256 threads x 16 consecutive elements
+__device__ __forceinline__ bool sel_keep(int mode, const double *x, int64_t i, const int64_t *st) {
+  if (mode == 1) return x[i] > st_f(st, GRID_SEL_THR);
+  const double r = x[i], lo = st_f(st, GRID_SEL_SMIN), hi = st_f(st, GRID_SEL_SMAX);
+  return i < st[GRID_SEL_RLOC] && r == r && !isinf(r) && r >= lo && r <= hi;
+}
+
+__global__ __launch_bounds__(256) void k_sel_bcount(int mode, const double *__restrict__ x, int64_t n,
+                                                    const int64_t *__restrict__ st, int32_t *__restrict__ bcnt) {
+  __shared__ int ws[4];
+  const int64_t b0 = (int64_t)blockIdx.x * SCB + threadIdx.x * 16;
+  int c = 0;
+#pragma unroll 4
+  for (int t = 0; t < 16; t++) c += (b0 + t < n) && sel_keep(mode, x, b0 + t, st);
+#pragma unroll
+  for (int o = 32; o; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) bcnt[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+// mode 1: sel[] = kept indices, r3[] = "%.3f" of their ratios, NaN up to
+// len_pad, st[RLOC] = st[RTOT] = kept count (k_gt_flags_st + select + k_sel_r3);
+// mode 2: map[i] = rank among kept or -1, st[RUSE] = kept count
+// (k_keep_flags_st + scan + k_colmap_fix_st)
+__global__ __launch_bounds__(256) void k_sel_scatter(int mode, const double *__restrict__ x, int64_t n, int nb,
+                                                     const int32_t *__restrict__ bcnt, int64_t *__restrict__ st,
+                                                     int32_t *__restrict__ out, double *__restrict__ r3,
+                                                     int64_t len_pad) {
+  __shared__ int64_t s_red[2][4];
+  __shared__ int s_scan[256];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  int64_t before = 0, total = 0;
+  for (int b = tid; b < nb; b += 256) {
+    const int64_t c = bcnt[b];
+    total += c;
+    if (b < (int)blockIdx.x) before += c;
+  }
+#pragma unroll
+  for (int o = 32; o; o >>= 1) {
+    before += __shfl_xor(before, o, 64);
+    total += __shfl_xor(total, o, 64);
+  }
+  if (lane == 0) {
+    s_red[0][wv] = before;
+    s_red[1][wv] = total;
+  }
+  __syncthreads();
+  before = s_red[0][0] + s_red[0][1] + s_red[0][2] + s_red[0][3];
+  total = s_red[1][0] + s_red[1][1] + s_red[1][2] + s_red[1][3];
+  const int64_t b0 = (int64_t)blockIdx.x * SCB + tid * 16;
+  uint32_t keep = 0;
+#pragma unroll 4
+  for (int t = 0; t < 16; t++)
+    if (b0 + t < n && sel_keep(mode, x, b0 + t, st)) keep |= 1u << t;
+  s_scan[tid] = __popc(keep);
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {            // inclusive scan of the per-thread counts
+    const int v = tid >= o ? s_scan[tid - o] : 0;
+    __syncthreads();
+    s_scan[tid] += v;
+    __syncthreads();
+  }
+  int64_t pos = before + s_scan[tid] - __popc(keep);
+  for (int t = 0; t < 16; t++) {
+    const int64_t i = b0 + t;
+    if (i >= n) break;
+    if (mode == 1) {
+      if (keep >> t & 1) {
+        out[pos] = (int32_t)i;
+        const double xv = x[i];
+        double o3 = xv;
+        if (xv == xv && !isinf(xv)) {
+          const double k = round_dec_k(xv, 1000.0);
+          o3 = k / 1000.0;
+          if (k == 0.0 && signbit(xv)) o3 = -0.0;
+        }
+        if (pos < len_pad) r3[pos] = o3;
+        pos++;
+      }
+    } else {
+      out[i] = (keep >> t & 1) ? (int32_t)pos++ : -1;
+    }
+  }
+  if (mode == 1)
+    for (int64_t i = total + (int64_t)blockIdx.x * 256 + tid; i < len_pad; i += (int64_t)gridDim.x * 256)
+      r3[i] = __builtin_nan("");
+  if (blockIdx.x == 0 && tid == 0) {
+    if (mode == 1) {
+      st[GRID_SEL_RLOC] = total;
+      st[GRID_SEL_RTOT] = total;
+    } else {
+      st[GRID_SEL_RUSE] = total;
+    }
+  }
+}
+
+static bool sel_legacy() {
+  static const int v = [] {
+    const char *e = GRID_AB_KNOB("GRID_SEL_LEGACY");   // tools build: round 5's selection (A/B)
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  return v;
+}
+
+// 6 histogram passes + picks over d_v (every pass's histogram zeroed up front)
+static int kth11(grid_ctx *ctx, const double *d_v, int64_t n, int nk, int mode, double frac, double sigma2_max,
+                 KthState *ks, unsigned *gh, int64_t *d_st) {
+  HIPCHK(hipMemsetAsync(gh, 0, (size_t)SPASS * KTH_MAX * SBINS * 4, ctx->stream));
+  // two workgroups per CU at most: each flushes up to nk x 2048 counters with
+  // global atomics (r06f: 4 per CU made the flush dominate a pass; 1 per CU
+  // left too few loads in flight, r06g)
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 256 * 8), 2 * ctx->ncu));
+  for (int p = 0; p < SPASS; p++) {
+    hipLaunchKernelGGL(k_kth_hist11, dim3(blocks), dim3(256), 0, ctx->stream, d_v, n, nk, p, ks, gh);
+    hipLaunchKernelGGL(k_kth_pick11, dim3(1), dim3(64 * nk), 0, ctx->stream, p, nk, mode, frac, sigma2_max, ks, gh,
+                       d_st);
+  }
+  LAUNCHCHK();
+  return GRID_OK;
+}
+
 
 extern "C" {
 
@@ -658,6 +961,25 @@ int grid_sel_stage1(grid_ctx *ctx, const double *d_rall, int64_t rlen, const dou
   REQUIRE(ctx && d_st && rlen >= 0 && ml >= 0 && len_pad >= ml && (rlen == 0 || d_rall) &&
           (ml == 0 || (d_ratio && d_sel)) && (len_pad == 0 || d_r3), "bad args");
   REQUIRE(ml < (1ll << 31), "ml >= 2^31");
+  if (!sel_legacy()) {
+    const int nb = (int)ceil_div(ml, SCB);
+    const size_t off_h = 256, off_b = off_h + (size_t)SPASS * KTH_MAX * SBINS * 4;
+    void *s = nullptr;
+    int rc = grid_scratch(ctx, off_b + (size_t)std::max(nb, 1) * 4 + 256, &s);
+    if (rc) return rc;
+    char *base = (char *)s;
+    KthState *ks = (KthState *)base;
+    int32_t *bcnt = (int32_t *)(base + off_b);
+    HIPCHK(hipMemsetAsync(d_st, 0, GRID_SEL_STATE * 8, ctx->stream));
+    rc = kth11(ctx, d_rall, rlen, 3, 1, top_frac, 0.0, ks, (unsigned *)(base + off_h), d_st);
+    if (rc) return rc;
+    if (nb > 0)
+      hipLaunchKernelGGL(k_sel_bcount, dim3(nb), dim3(256), 0, ctx->stream, 1, d_ratio, ml, (const int64_t *)d_st, bcnt);
+    hipLaunchKernelGGL(k_sel_scatter, dim3(std::max(nb, 1)), dim3(256), 0, ctx->stream, 1, d_ratio, ml, nb,
+                       (const int32_t *)bcnt, d_st, d_sel, d_r3, len_pad);
+    LAUNCHCHK();
+    return GRID_OK;
+  }
   size_t cub = 0;
   hipcub::CountingInputIterator<int32_t> it(0);
   if (ml > 0)
@@ -702,6 +1024,25 @@ int grid_sel_stage2(grid_ctx *ctx, const double *d_r3all, int64_t r3len, const d
   REQUIRE(ctx && d_st && r3len >= 0 && ml >= 0 && (r3len == 0 || d_r3all) && (ml == 0 || (d_r3 && d_colmap)),
           "bad args");
   REQUIRE(ml < (1ll << 31), "ml >= 2^31");
+  if (!sel_legacy()) {
+    const int nb = (int)ceil_div(ml, SCB);
+    const size_t off_h = 256, off_b = off_h + (size_t)SPASS * KTH_MAX * SBINS * 4;
+    void *s = nullptr;
+    int rc = grid_scratch(ctx, off_b + (size_t)std::max(nb, 1) * 4 + 256, &s);
+    if (rc) return rc;
+    char *base = (char *)s;
+    KthState *ks = (KthState *)base;
+    int32_t *bcnt = (int32_t *)(base + off_b);
+    rc = kth11(ctx, d_r3all, r3len, 1, 2, frac_r, sigma2_max, ks, (unsigned *)(base + off_h), d_st);
+    if (rc) return rc;
+    if (nb > 0) {
+      hipLaunchKernelGGL(k_sel_bcount, dim3(nb), dim3(256), 0, ctx->stream, 2, d_r3, ml, (const int64_t *)d_st, bcnt);
+      hipLaunchKernelGGL(k_sel_scatter, dim3(nb), dim3(256), 0, ctx->stream, 2, d_r3, ml, nb,
+                         (const int32_t *)bcnt, d_st, d_colmap, (double *)nullptr, (int64_t)0);
+    }
+    LAUNCHCHK();
+    return GRID_OK;
+  }
   size_t cub = 0;
   if (ml > 0)
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, cub, (int32_t *)nullptr, d_colmap, (int)ml, ctx->stream));

@@ -783,6 +783,260 @@ __global__ __launch_bounds__(NT) void k_phase2_batch(const grid_hi_locus *__rest
                           L.pk_w, L.pk_cnt, L.hap, L.imp, L.mean, s_hap);
 }
 
+// a / b, correctly rounded, for a = 0 or 2^-500 <= a <= 2^500 and
+// 2^-60 <= b <= 2^60, from a reciprocal y = refine(rcp(b)) computed ahead.
+// In that range v_div_scale_f64 leaves both operands unscaled (the exponent
+// difference stays below 768, the numerator's exponent far above 53, no
+// denormal reciprocal or quotient), v_div_fmas_f64 is a plain fma and
+// v_div_fixup_f64 returns its input -- so these are the very operations the
+// compiler's IEEE division issues, and the result is the same bits.  Outside
+// the range: the ordinary division.
+__device__ __forceinline__ double recip_refined(double b) {
+  double y = __builtin_amdgcn_rcp(b);
+  double e = fma(-b, y, 1.0);
+  y = fma(y, e, y);
+  e = fma(-b, y, 1.0);
+  return fma(y, e, y);
+}
+__device__ __forceinline__ double div_with_recip(double a, double b, double y) {
+  const double q = a * y;
+  const double r = fma(-b, q, a);
+  return fma(r, y, q);
+}
+
+// k_phase4: the split-lane level schedule (one haplotype per lane, pairs meet
+// by DPP) with the per-chunk serial path cut down (round 6):
+//   * 256 lanes (one wave per SIMD), 128 schedule entries per chunk: the
+//     widest config-2 level is 144 entries and most are 75-118, so no SIMD
+//     runs a second wave's instruction stream;
+//   * two named register sets alternate (loop unrolled by two), so the
+//     prefetched lists are not copied;
+//   * the chunk table (bounds + the chunk's longest list in 4-wide segments,
+//     computed once, a wave per chunk) is read a chunk ahead;
+//   * irr[i] is gathered with the neighbour values, the unit-weight
+//     denominator s_unit[k] is read before the add chain, and the first
+//     division's reciprocal is refined while the chain runs.
+// Operation order and every rounding are those of ph2_run (bit-exact).
+// PROBE (tools build, GRID_PHASE_PROBE 4-7, wrong results, timing only):
+// 4 = no barriers, 5 = no neighbour gathers / arithmetic / writes,
+// 6 = no list prefetch, 7 = barriers only (no prefetch, no work)
+template <bool UNITW, int CAPT, int PROBE = 0>
+__global__ __launch_bounds__(256) void k_phase4(int64_t n, const double *__restrict__ irr,
+                                               const int64_t *__restrict__ off, const int32_t *__restrict__ nbr,
+                                               const double *__restrict__ w, int64_t min_nbr, int64_t iters,
+                                               const int32_t *__restrict__ order, const int32_t *__restrict__ loff,
+                                               int nlev, const int32_t *__restrict__ pk_nbr,
+                                               const double *__restrict__ pk_w, const int32_t *__restrict__ pk_cnt,
+                                               double *hap_g, double *__restrict__ imp,
+                                               double *__restrict__ mean_out) {
+  constexpr int NT = 256, CHK = NT / 2;
+  extern __shared__ __attribute__((aligned(16))) double s_hap[];
+  __shared__ double s_mean;
+  __shared__ double2 s_unit[CAPT + 1];      // {1e-9 + 1 + ... + 1 (k terms), its refined reciprocal}
+  __shared__ int s_nch;
+  double *hap = s_hap;
+  // LDS: hap[2n] | irr[n] | level offsets[nlev+1] | phased flags[n] | chunk table (int4, 16-B aligned)
+  double *irs = s_hap + 2 * n;
+  int32_t *lof = reinterpret_cast<int32_t *>(s_hap + 3 * n);
+  uint8_t *okf = reinterpret_cast<uint8_t *>(lof + nlev + 1);
+  const size_t chk_at = ((size_t)3 * n * 8 + (size_t)(nlev + 1) * 4 + (size_t)n + 15) & ~(size_t)15;
+  int4 *chk = reinterpret_cast<int4 *>(reinterpret_cast<uint8_t *>(s_hap) + chk_at);
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    double u = 1e-9;
+    for (int k = 0; k <= CAPT; k++) {
+      s_unit[k] = make_double2(u, recip_refined(u));
+      u = u + 1.0;
+    }
+  }
+  for (int64_t i = tid; i < n; i += NT) irs[i] = irr[i];
+  for (int l = tid; l <= nlev; l += NT) lof[l] = loff[l];
+  const double qnan = __builtin_nan("");
+  for (int64_t i = tid; i < n; i += NT) {
+    const bool ok = (off[2 * i + 1] - off[2 * i] >= min_nbr) && (off[2 * i + 2] - off[2 * i + 1] >= min_nbr);
+    const double v = ok ? irr[i] / 2 : qnan;
+    hap[2 * i] = v;
+    hap[2 * i + 1] = v;
+    okf[i] = ok;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    // mean_IRRs: sequential sum in sample order (hi_inference.py:189-201)
+    double m = 0.0;
+    int64_t c = 0;
+    for (int64_t i = 0; i < n; i++) {
+      if (okf[i]) { m = m + hap[2 * i] * 2.0; c++; }
+    }
+    if (c > 0) m = m / (double)c;
+    s_mean = m;
+    int nc = 0;
+    for (int l = 0; l < nlev; l++)
+      for (int b = lof[l]; b < lof[l + 1]; b += CHK) chk[nc++] = make_int4(b, min(b + CHK, lof[l + 1]), 0, 0);
+    s_nch = nc;
+  }
+  __syncthreads();
+  const int nch = s_nch;
+  {
+    // each chunk's longest list, in 4-wide gather segments (a wave per chunk);
+    // lists longer than CAPT take the CSR loop and need no gathers
+    const int wid = tid >> 6, lane = tid & 63;
+    for (int c = wid; c < nch; c += NT / 64) {
+      const int e0 = chk[c].x, e1 = chk[c].y;
+      int mx = 0;
+      for (int j = 2 * e0 + lane; j < 2 * e1; j += 64) {
+        const int cc = pk_cnt[j];
+        mx = max(mx, (cc < 0 || cc > CAPT) ? 0 : cc);
+      }
+#pragma unroll
+      for (int o = 32; o; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
+      if (lane == 0) chk[c].z = (mx + 3) / 4;
+    }
+  }
+  __syncthreads();
+  if (iters > 0 && nch > 0) {
+    const int h = tid & 1, eo = tid >> 1;
+    auto pin = [&](PhReg1<UNITW, CAPT> &it) {
+#pragma unroll
+      for (int t = 0; t < CAPT; t++) asm volatile("" : "+v"(it.nb[t]));
+      if (!UNITW) {
+#pragma unroll
+        for (int t = 0; t < CAPT; t++) asm volatile("" : "+v"(it.wt[UNITW ? 0 : t]));
+      }
+      asm volatile("" : "+v"(it.i), "+v"(it.c), "+v"(it.ok));
+      it.i = it.ok ? it.i : -1;
+      it.c = (it.c < 0 || it.c > CAPT) ? CAPT + 1 : it.c;
+    };
+    auto fetch = [&](const int4 cb, PhReg1<UNITW, CAPT> &it) {
+      ph3_fetch<UNITW, CAPT>(cb.x + eo, cb.y, h, order, pk_nbr, pk_w, pk_cnt, it);
+    };
+    auto work = [&](PhReg1<UNITW, CAPT> &cur, const int nseg_v) {
+      if (PROBE == 5 || PROBE == 7) {
+        wg_barrier<true>();
+        wg_barrier<true>();
+        return;
+      }
+      const int nseg = __builtin_amdgcn_readfirstlane(nseg_v);
+      const int me = cur.i >= 0 ? cur.i : 0;
+      const double hv = hap[2 * me];
+      const double ir = irs[me];
+      double x[CAPT];
+#pragma unroll
+      for (int sg = 0; sg < CAPT / 4; sg++)
+        if (sg < nseg) {
+#pragma unroll
+          for (int j = 0; j < 4; j++) x[4 * sg + j] = hap[cur.nb[4 * sg + j]];
+        }
+#pragma unroll
+      for (int t = 0; t < CAPT; t++) asm volatile("" : "+v"(x[t]));
+      const bool act = cur.i >= 0 && hv == hv;     // the same for both lanes of a pair
+      const bool lng = cur.c > CAPT;
+      double m = 0.0;
+      if (act) {
+        double ws, wv;
+        if (lng) {
+          nbr_mean_h(cur.i, h, hap, off, nbr, w, ws, wv);
+          m = wv / ws;
+        } else {
+          bool tk[CAPT];
+          int k = 0;
+#pragma unroll
+          for (int sg = 0; sg < CAPT / 4; sg++)
+            if (sg < nseg) {
+#pragma unroll
+              for (int j = 0; j < 4; j++) {
+                const int t = 4 * sg + j;
+                tk[t] = t < cur.c && x[t] == x[t];
+                k += tk[t];
+              }
+            }
+          double sw = 1e-9, sv = 0.0;
+          double2 uy = make_double2(0.0, 0.0);
+          if (UNITW) uy = s_unit[k];                 // read before the chain (independent of it)
+#pragma unroll
+          for (int sg = 0; sg < CAPT / 4; sg++)
+            if (sg < nseg) {
+#pragma unroll
+              for (int j = 0; j < 4; j++) {
+                const int t = 4 * sg + j;
+                if (UNITW) {
+                  sv = sv + (tk[t] ? x[t] : 0.0);
+                } else {
+                  const double wt = cur.wt[UNITW ? 0 : t];
+                  const double p = wt * x[t];
+                  sw = sw + (tk[t] ? wt : 0.0);
+                  sv = sv + (tk[t] ? p : 0.0);
+                }
+              }
+            }
+          if (UNITW) sw = uy.x;
+          if (UNITW && (sv == 0.0 || (sv >= 0x1p-500 && sv <= 0x1p500))) {
+            m = div_with_recip(sv, sw, uy.y);        // every s_unit value lies in [2^-60, 2^60]
+          } else {
+            m = sv / sw;
+          }
+        }
+      }
+      // all lanes are active here, so the partner's value is always readable
+      const uint64_t mb = (uint64_t)__double_as_longlong(m);
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)mb, 0xB1, 0xF, 0xF, false);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(mb >> 32), 0xB1, 0xF, 0xF, false);
+      const double mo = __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+      bool upd = false;
+      double nv = 0.0;
+      if (act) {
+        const double den = h ? mo + m : m + mo;   // m0 + m1
+        if (den > 0.0) {
+          nv = ir * m / den;
+          upd = true;
+        }
+      }
+      if (PROBE != 4) wg_barrier<true>();
+      if (upd) hap[2 * cur.i + h] = nv;
+      if (PROBE != 4) wg_barrier<true>();
+    };
+    auto next = [&](int c) { return c + 1 == nch ? 0 : c + 1; };
+    const int64_t total = iters * (int64_t)nch;
+    PhReg1<UNITW, CAPT> ra, rb;
+    int c = 0;
+    int4 cba = chk[0];                      // bounds of the chunk in ra
+    fetch(cba, ra);
+    pin(ra);
+    if (PROBE == 6 || PROBE == 7) rb = ra;  // probes without prefetch: valid (stale) lists
+    int4 cbb = chk[next(c)];                // bounds of the chunk after it
+    for (int64_t g = 0; g < total; g += 2) {
+      const int c1 = next(c), c2 = next(c1);
+      if (g + 1 < total && PROBE != 6 && PROBE != 7) fetch(cbb, rb);
+      asm volatile("" ::: "memory");
+      const int4 cbn = chk[c2];
+      work(ra, cba.z);
+      if (g + 1 >= total) break;
+      pin(rb);
+      if (g + 2 < total && PROBE != 6 && PROBE != 7) fetch(cbn, ra);
+      asm volatile("" ::: "memory");
+      const int4 cbn2 = chk[next(c2)];
+      work(rb, cbb.z);
+      pin(ra);
+      c = c2;
+      cba = cbn;
+      cbb = cbn2;
+    }
+  }
+  const double mean = s_mean;
+  for (int64_t i = tid; i < n; i += NT) {
+    double ws[2], wv[2];
+    nbr_means(i, hap, off, nbr, w, ws, wv);
+    double i0 = wv[0] / ws[0];
+    double i1 = wv[1] / ws[1];
+    if (ws[0] <= 1e-9) i0 = mean / 2;
+    if (ws[1] <= 1e-9) i1 = mean / 2;
+    imp[2 * i] = i0;
+    imp[2 * i + 1] = i1;
+  }
+  __syncthreads();
+  for (int64_t e = tid; e < 2 * n; e += NT) hap_g[e] = hap[e];
+  if (tid == 0) *mean_out = mean;
+}
+
 }  // namespace
 
 extern "C" {
@@ -844,7 +1098,29 @@ int grid_hi_phase(grid_ctx *ctx, int64_t n, const double *d_irr, const int64_t *
   const size_t lds2 = lds + 32 + (size_t)(nlevels + n / PT + 2) * 8;
   const size_t lds_g = 32 + (size_t)(nlevels + n / PT + 2) * 8;   // hap in global memory
   const bool unitw = flags & GRID_HI_UNIT_WEIGHTS;
-  if (lds2 <= 120 * 1024 && !(flags & GRID_HI_LEGACY)) {
+  // k_phase4's LDS: hap, irr, level offsets, flags, then a 16-B aligned int4 chunk table
+  const size_t lds4 = ((lds + 15) & ~(size_t)15) + (size_t)(nlevels + n / 128 + 2) * 16;
+  if (lds4 <= 120 * 1024 && !(flags & (GRID_HI_LEGACY | GRID_HI_PAIRED | GRID_HI_PH2))) {
+    auto kern = unitw ? (max_list <= 8 ? k_phase4<true, 8> : k_phase4<true, 16>)
+                      : (max_list <= 8 ? k_phase4<false, 8> : k_phase4<false, 16>);
+    int slot = (unitw ? 2 : 0) + (max_list <= 8 ? 0 : 1);
+#ifdef GRID_PROBES
+    const char *pe4 = getenv("GRID_PHASE_PROBE");
+    const int probe4 = pe4 ? atoi(pe4) : 0;
+    if (probe4 == 4) kern = k_phase4<true, 16, 4>;
+    if (probe4 == 5) kern = k_phase4<true, 16, 5>;
+    if (probe4 == 6) kern = k_phase4<true, 16, 6>;
+    if (probe4 == 7) kern = k_phase4<true, 16, 7>;
+    if (probe4 >= 4 && probe4 <= 7) slot = probe4;
+#endif
+    static bool attr4[8] = {};
+    if (!attr4[slot]) {
+      HIPCHK(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024));
+      attr4[slot] = true;
+    }
+    hipLaunchKernelGGL(kern, dim3(1), dim3(256), lds4, ctx->stream, n, d_irr, d_off, d_nbr, d_w, min_nbr, n_iters,
+                       d_order, d_loff, nlevels, d_pk_nbr, d_pk_w, d_pk_cnt, d_hap, d_imp, d_mean);
+  } else if (lds2 <= 120 * 1024 && !(flags & GRID_HI_LEGACY)) {
     // register-pipelined kernel; CAPT covers the longest list when it can
     // default: 512 lanes, one haplotype per lane (256 entries per chunk);
     // GRID_HI_PAIRED: 256 lanes, both haplotypes per lane

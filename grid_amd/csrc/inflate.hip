@@ -66,6 +66,7 @@ constexpr uint32_t K_LIT = 1, K_LEN = 2, K_EOB = 4, K_LIT2 = 8, K_DIST = 1;
 // occupancy they force are slower (60.8 / 50.5 GB/s) -- so off
 #define GRID_INFLATE_PAIRS 0
 #endif
+
 constexpr int F_LEN = 1 << icore::LFAST, F_DIST = 1 << icore::DFAST;
 
 __device__ __forceinline__ uint32_t fast_entry(int ft, uint32_t sym, uint32_t l) {
@@ -302,9 +303,6 @@ struct DevP {
     uint64_t vb;                        // the bit buffer, in VGPRs
     asm volatile("v_mov_b64 %0, %1" : "=v"(vb) : "s"(inf.bb));
     int bc = inf.bc, ret = 0, flush_at = flushed + FLUSH;
-    auto low = [&](int sh) -> uint32_t {   // bits [sh, sh + 32) of the buffer (sh < 32)
-      return __builtin_amdgcn_alignbit((uint32_t)(vb >> 32), (uint32_t)vb, (uint32_t)sh);
-    };
     auto slow = [&](int co, int so) -> int {   // puff's canonical walk (-1: no such code)
       int code = 0, first = 0, index = 0;
 #pragma unroll 1
@@ -370,10 +368,15 @@ struct DevP {
         bc |= 56;
       }
       // the entry stays in a VGPR (its fields are cut on the vector unit);
-      // a scalar copy steers
+      // a scalar copy steers.  Every kind has its own bit: one scalar bit
+      // test per kind, in order of frequency (round 6: masked compares of the
+      // kind field cost ~10 scalar instructions before a literal was stored;
+      // 64.4 -> 82.0 GB/s of text, profiles/r06i_*).  Each path keeps its own
+      // tail: one shared tail (the symbol's bits consumed once, one limit
+      // test) compiled to flag-steered branches, 74.5 GB/s (r06j); literal
+      // runs in an inner loop with one exit, 75.4 vs 81.5 GB/s (r06k)
       const uint32_t ev = ftab[(uint32_t)vb & (uint32_t)(F_LEN - 1)];
       const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane((int)ev);
-      const uint32_t kind = e & 0xf0u;
       uint32_t len;
       if (__builtin_expect((e & (K_LEN << 4)) != 0, 1)) {
         const uint32_t lv = ev & 15u, xv = (ev >> 8) & 7u, lxv = lv + xv;
@@ -382,7 +385,16 @@ struct DevP {
         len = (uint32_t)__builtin_amdgcn_readfirstlane((int)((ev >> 16) + xb));
         vb >>= lxv;
         bc -= __builtin_amdgcn_readfirstlane((int)lxv);
-      } else if (kind == (K_LIT2 << 4)) {
+      } else if (__builtin_expect((e & (K_LIT << 4)) != 0, 1)) {
+        const uint32_t lv = ev & 15u;
+        vb >>= lv;
+        bc -= __builtin_amdgcn_readfirstlane((int)lv);
+        ring[pos & RMASK] = (uint8_t)(ev >> 16);
+        __builtin_amdgcn_wave_barrier();
+        pos++;
+        if (pos >= lim && !limit()) break;
+        continue;
+      } else if (GRID_INFLATE_PAIRS && (e & (K_LIT2 << 4)) != 0) {
         const uint32_t lv = ev & 15u;
         vb >>= lv;
         bc -= __builtin_amdgcn_readfirstlane((int)lv);
@@ -392,16 +404,7 @@ struct DevP {
         pos += 2;
         if (pos >= lim && !limit()) break;
         continue;
-      } else if (kind == (K_LIT << 4)) {
-        const uint32_t lv = ev & 15u;
-        vb >>= lv;
-        bc -= __builtin_amdgcn_readfirstlane((int)lv);
-        ring[pos & RMASK] = (uint8_t)(ev >> 16);
-        __builtin_amdgcn_wave_barrier();
-        pos++;
-        if (pos >= lim && !limit()) break;
-        continue;
-      } else if (kind == (K_EOB << 4)) {
+      } else if ((e & (K_EOB << 4)) != 0) {
         const int l = e & 15;
         vb >>= l;
         bc -= l;

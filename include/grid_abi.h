@@ -428,8 +428,9 @@ int grid_dipcn(grid_ctx *ctx, int64_t n, const double *d_reads, const uint8_t *d
  * sequential order.  Outputs hap[2n] (NaN = unphased), imp[2n], *h_mean.
  * grid_hi_phase flags: GRID_HI_UNIT_WEIGHTS when every weight is 1.0;
  * max_list = longest list (selects the register capacity of the kernel).
- * Default kernel: one workgroup of 512 lanes, one haplotype per lane, with hap
- * in LDS while 3n doubles fit (about 4,800 samples) and in d_hap otherwise.
+ * Default kernel: one workgroup, one haplotype per lane, with hap in LDS while
+ * 3n doubles fit (about 4,700 samples; 256 lanes, k_phase4) and in d_hap
+ * otherwise (512 lanes).
  * Every flag selects a kernel with the same results. */
 int grid_hi_levels(int64_t n, const int64_t *h_off, const int32_t *h_nbr, int32_t *h_order,
                    int32_t *h_level_off, int32_t *h_nlevels);
@@ -448,6 +449,7 @@ int grid_hi_phase(grid_ctx *ctx, int64_t n, const double *d_irr, const int64_t *
 #define GRID_HI_UNIT_WEIGHTS 1   /* every weight is 1.0 (IBS lists): weights are not read */
 #define GRID_HI_LEGACY 2         /* A/B: the previous (per-neighbour LDS round trip) kernel */
 #define GRID_HI_PAIRED 4         /* A/B: register-pipelined kernel with both haplotypes per lane */
+#define GRID_HI_PH2 8            /* A/B: round 5's split-lane kernel (512 lanes) instead of k_phase4 */
 
 /* Haplotype-neighbour files -> CSR (host C++; Python text semantics for ASCII
  * input).  ids_nl: the dipCN file's sample IDs joined by '\n' (index = line

@@ -89,6 +89,11 @@ def cases():
     yield "top_end", v[:1001], 0.999
     yield "one", np.array([3.25]), 0.0
     yield "inf", np.concatenate([v[:100], [np.inf, -np.inf]]), 0.2
+    # many compaction blocks (4096 values each) and many equal leading digits
+    big = rng.gamma(2.0, 3.0, 200_003)
+    big[rng.random(big.size) < 0.05] = np.nan
+    big[::7] = 4.0
+    yield "large", big, 0.1
 
 
 @pytest.mark.parametrize("name,vals,top_frac", list(cases()), ids=[c[0] for c in cases()])
