@@ -342,113 +342,123 @@ struct DevP {
     // per refill: r > rmax means the window must move, or the input is
     // within 16 bytes of its end (the core finishes the block)
     int r = ip - fbase, rmax = min(244, nin - 16 - fbase);
+    // the decode loop's only exits are breaks to one place: a limit (the next
+    // flush or the end of the output room) ends the inner loop, the outer one
+    // flushes and re-enters -- the flush code is not inlined at every symbol's
+    // limit test (round 6: 82.2 vs 81.9 GB/s, r06m)
+    int why = 0;                        // 1: the inner loop stopped at the limit
     for (;;) {
-      if (bc < 48) {                    // 8 more bytes, of which 7 - bc / 8 are kept (libdeflate's refill)
-        if (r > rmax || r < 0) {
-          ip = fbase + r;
-          if (ip + 16 > nin) break;
-          fbase = ip & ~3;
-          fcur = load_word(fbase);
-          r = ip - fbase;
-          rmax = min(244, nin - 16 - fbase);
+      for (;;) {
+        if (bc < 48) {                    // 8 more bytes, of which 7 - bc / 8 are kept (libdeflate's refill)
+          if (r > rmax || r < 0) {
+            ip = fbase + r;
+            if (ip + 16 > nin) break;
+            fbase = ip & ~3;
+            fcur = load_word(fbase);
+            r = ip - fbase;
+            rmax = min(244, nin - 16 - fbase);
+          }
+          // words i..i+2 of the window broadcast by the LDS crossbar, the 8
+          // bytes from byte r & 3 of word i funnelled out: vector work
+          uint32_t rv;
+          asm volatile("v_mov_b32 %0, %1" : "=v"(rv) : "s"(r));
+          const int a = (int)(rv & ~3u);
+          const uint32_t w0 = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)fcur);
+          const uint32_t w1 = (uint32_t)__builtin_amdgcn_ds_bpermute(a + 4, (int)fcur);
+          const uint32_t w2 = (uint32_t)__builtin_amdgcn_ds_bpermute(a + 8, (int)fcur);
+          const uint32_t shv = (rv & 3u) * 8u;
+          const uint32_t vlo = __builtin_amdgcn_alignbit(w1, w0, shv);
+          const uint32_t vhi = __builtin_amdgcn_alignbit(w2, w1, shv);
+          vb |= (((uint64_t)vhi << 32) | vlo) << bc;
+          r += 7 - (bc >> 3);
+          bc |= 56;
         }
-        // words i..i+2 of the window broadcast by the LDS crossbar, the 8
-        // bytes from byte r & 3 of word i funnelled out: vector work
-        uint32_t rv;
-        asm volatile("v_mov_b32 %0, %1" : "=v"(rv) : "s"(r));
-        const int a = (int)(rv & ~3u);
-        const uint32_t w0 = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)fcur);
-        const uint32_t w1 = (uint32_t)__builtin_amdgcn_ds_bpermute(a + 4, (int)fcur);
-        const uint32_t w2 = (uint32_t)__builtin_amdgcn_ds_bpermute(a + 8, (int)fcur);
-        const uint32_t shv = (rv & 3u) * 8u;
-        const uint32_t vlo = __builtin_amdgcn_alignbit(w1, w0, shv);
-        const uint32_t vhi = __builtin_amdgcn_alignbit(w2, w1, shv);
-        vb |= (((uint64_t)vhi << 32) | vlo) << bc;
-        r += 7 - (bc >> 3);
-        bc |= 56;
-      }
-      // the entry stays in a VGPR (its fields are cut on the vector unit);
-      // a scalar copy steers.  Every kind has its own bit: one scalar bit
-      // test per kind, in order of frequency (round 6: masked compares of the
-      // kind field cost ~10 scalar instructions before a literal was stored;
-      // 64.4 -> 82.0 GB/s of text, profiles/r06i_*).  Each path keeps its own
-      // tail: one shared tail (the symbol's bits consumed once, one limit
-      // test) compiled to flag-steered branches, 74.5 GB/s (r06j); literal
-      // runs in an inner loop with one exit, 75.4 vs 81.5 GB/s (r06k)
-      const uint32_t ev = ftab[(uint32_t)vb & (uint32_t)(F_LEN - 1)];
-      const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane((int)ev);
-      uint32_t len;
-      if (__builtin_expect((e & (K_LEN << 4)) != 0, 1)) {
-        const uint32_t lv = ev & 15u, xv = (ev >> 8) & 7u, lxv = lv + xv;
-        const uint32_t xb = __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit((uint32_t)(vb >> 32), (uint32_t)vb, lv),
-                                                  0u, xv);
-        len = (uint32_t)__builtin_amdgcn_readfirstlane((int)((ev >> 16) + xb));
-        vb >>= lxv;
-        bc -= __builtin_amdgcn_readfirstlane((int)lxv);
-      } else if (__builtin_expect((e & (K_LIT << 4)) != 0, 1)) {
-        const uint32_t lv = ev & 15u;
-        vb >>= lv;
-        bc -= __builtin_amdgcn_readfirstlane((int)lv);
-        ring[pos & RMASK] = (uint8_t)(ev >> 16);
-        __builtin_amdgcn_wave_barrier();
-        pos++;
-        if (pos >= lim && !limit()) break;
-        continue;
-      } else if (GRID_INFLATE_PAIRS && (e & (K_LIT2 << 4)) != 0) {
-        const uint32_t lv = ev & 15u;
-        vb >>= lv;
-        bc -= __builtin_amdgcn_readfirstlane((int)lv);
-        ring[pos & RMASK] = (uint8_t)(ev >> 16);
-        ring[(pos + 1) & RMASK] = (uint8_t)(ev >> 24);
-        __builtin_amdgcn_wave_barrier();
-        pos += 2;
-        if (pos >= lim && !limit()) break;
-        continue;
-      } else if ((e & (K_EOB << 4)) != 0) {
-        const int l = e & 15;
-        vb >>= l;
-        bc -= l;
-        ret = 1;
-        break;
-      } else {                          // a code longer than LFAST bits, or 286/287
-        const int sym = slow(icore::T_LCNT, icore::T_LSYM);
-        if (sym < 0 || sym > 285) { inf.err = icore::E_DATA; ret = -1; break; }
-        if (sym == 256) { ret = 1; break; }
-        if (sym < 256) {
-          ring[pos & RMASK] = (uint8_t)sym;
+        // the entry stays in a VGPR (its fields are cut on the vector unit);
+        // a scalar copy steers.  Every kind has its own bit: one scalar bit
+        // test per kind, in order of frequency (round 6: masked compares of the
+        // kind field cost ~10 scalar instructions before a literal was stored;
+        // 64.4 -> 82.0 GB/s of text, profiles/r06i_*).  Each path keeps its own
+        // tail: one shared tail (the symbol's bits consumed once, one limit
+        // test) compiled to flag-steered branches, 74.5 GB/s (r06j); literal
+        // runs in an inner loop with one exit, 75.4 vs 81.5 GB/s (r06k)
+        const uint32_t ev = ftab[(uint32_t)vb & (uint32_t)(F_LEN - 1)];
+        const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane((int)ev);
+        uint32_t len;
+        if (__builtin_expect((e & (K_LEN << 4)) != 0, 1)) {
+          const uint32_t lv = ev & 15u, xv = (ev >> 8) & 7u, lxv = lv + xv;
+          const uint32_t xb = __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit((uint32_t)(vb >> 32), (uint32_t)vb, lv),
+                                                    0u, xv);
+          len = (uint32_t)__builtin_amdgcn_readfirstlane((int)((ev >> 16) + xb));
+          vb >>= lxv;
+          bc -= __builtin_amdgcn_readfirstlane((int)lxv);
+        } else if (__builtin_expect((e & (K_LIT << 4)) != 0, 1)) {
+          const uint32_t lv = ev & 15u;
+          vb >>= lv;
+          bc -= __builtin_amdgcn_readfirstlane((int)lv);
+          ring[pos & RMASK] = (uint8_t)(ev >> 16);
           __builtin_amdgcn_wave_barrier();
           pos++;
-          if (pos >= lim && !limit()) break;
+          if (pos >= lim) { why = 1; break; }
           continue;
+        } else if (GRID_INFLATE_PAIRS && (e & (K_LIT2 << 4)) != 0) {
+          const uint32_t lv = ev & 15u;
+          vb >>= lv;
+          bc -= __builtin_amdgcn_readfirstlane((int)lv);
+          ring[pos & RMASK] = (uint8_t)(ev >> 16);
+          ring[(pos + 1) & RMASK] = (uint8_t)(ev >> 24);
+          __builtin_amdgcn_wave_barrier();
+          pos += 2;
+          if (pos >= lim) { why = 1; break; }
+          continue;
+        } else if ((e & (K_EOB << 4)) != 0) {
+          const int l = e & 15;
+          vb >>= l;
+          bc -= l;
+          ret = 1;
+          break;
+        } else {                          // a code longer than LFAST bits, or 286/287
+          const int sym = slow(icore::T_LCNT, icore::T_LSYM);
+          if (sym < 0 || sym > 285) { inf.err = icore::E_DATA; ret = -1; break; }
+          if (sym == 256) { ret = 1; break; }
+          if (sym < 256) {
+            ring[pos & RMASK] = (uint8_t)sym;
+            __builtin_amdgcn_wave_barrier();
+            pos++;
+            if (pos >= lim) { why = 1; break; }
+            continue;
+          }
+          const int x = icore::kLenExtra[sym - 257];
+          len = icore::kLenBase[sym - 257] + (uint32_t)__builtin_amdgcn_readfirstlane((int)extra(x));
         }
-        const int x = icore::kLenExtra[sym - 257];
-        len = icore::kLenBase[sym - 257] + (uint32_t)__builtin_amdgcn_readfirstlane((int)extra(x));
+        const uint32_t dv = ftab[F_LEN + ((uint32_t)vb & (uint32_t)(F_DIST - 1))];
+        const uint32_t d = (uint32_t)__builtin_amdgcn_readfirstlane((int)dv);
+        uint32_t dist, distv;
+        if (__builtin_expect((d & (K_DIST << 4)) != 0, 1)) {
+          const uint32_t lv = dv & 15u, xv = (dv >> 8) & 15u, lxv = lv + xv;
+          const uint32_t xb = __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit((uint32_t)(vb >> 32), (uint32_t)vb, lv),
+                                                    0u, xv);
+          distv = (dv >> 17) + xb;
+          dist = (uint32_t)__builtin_amdgcn_readfirstlane((int)distv);
+          vb >>= lxv;
+          bc -= __builtin_amdgcn_readfirstlane((int)lxv);
+        } else {
+          const int ds = slow(icore::T_DCNT, icore::T_DSYM);
+          if (ds < 0 || ds >= 30) { inf.err = icore::E_DATA; ret = -1; break; }
+          const int x = icore::kDistExtra[ds];
+          dist = icore::kDistBase[ds] + (uint32_t)__builtin_amdgcn_readfirstlane((int)extra(x));
+          distv = dist;
+        }
+        if (dist > (uint32_t)NEAR) {      // a far copy reads HBM: test it here
+          if (dist > (uint32_t)(pos - mstart)) { inf.err = icore::E_DATA; ret = -1; break; }
+        } else {
+          verr |= distv > (uint32_t)(pos - mstart) ? 1u : 0u;
+        }
+        copy_bytes(dist, len);
+        if (pos >= lim) { why = 1; break; }
       }
-      const uint32_t dv = ftab[F_LEN + ((uint32_t)vb & (uint32_t)(F_DIST - 1))];
-      const uint32_t d = (uint32_t)__builtin_amdgcn_readfirstlane((int)dv);
-      uint32_t dist, distv;
-      if (__builtin_expect((d & (K_DIST << 4)) != 0, 1)) {
-        const uint32_t lv = dv & 15u, xv = (dv >> 8) & 15u, lxv = lv + xv;
-        const uint32_t xb = __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit((uint32_t)(vb >> 32), (uint32_t)vb, lv),
-                                                  0u, xv);
-        distv = (dv >> 17) + xb;
-        dist = (uint32_t)__builtin_amdgcn_readfirstlane((int)distv);
-        vb >>= lxv;
-        bc -= __builtin_amdgcn_readfirstlane((int)lxv);
-      } else {
-        const int ds = slow(icore::T_DCNT, icore::T_DSYM);
-        if (ds < 0 || ds >= 30) { inf.err = icore::E_DATA; ret = -1; break; }
-        const int x = icore::kDistExtra[ds];
-        dist = icore::kDistBase[ds] + (uint32_t)__builtin_amdgcn_readfirstlane((int)extra(x));
-        distv = dist;
-      }
-      if (dist > (uint32_t)NEAR) {      // a far copy reads HBM: test it here
-        if (dist > (uint32_t)(pos - mstart)) { inf.err = icore::E_DATA; ret = -1; break; }
-      } else {
-        verr |= distv > (uint32_t)(pos - mstart) ? 1u : 0u;
-      }
-      copy_bytes(dist, len);
-      if (pos >= lim && !limit()) break;
+      if (why != 1) break;
+      why = 0;
+      if (!limit()) break;
     }
     if (ret >= 0 && __builtin_amdgcn_readfirstlane((int)verr)) { inf.err = icore::E_DATA; ret = -1; }
     ip = fbase + r;
