@@ -120,15 +120,32 @@ __global__ __launch_bounds__(256) void k_md_count(const uint8_t *__restrict__ te
   }
 }
 
-// per file: newlines before each chunk (exclusive prefix over its chunks)
-__global__ void k_md_scan(const int32_t *__restrict__ cfirst, const int32_t *__restrict__ cnl,
-                          int64_t *__restrict__ cline0, int nfiles) {
-  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+// per file: newlines before each chunk (exclusive prefix over its chunks).
+// A workgroup per file, 256 chunks per round: a file of a config-2 batch has
+// ~6,000 chunks, which one thread walked serially (3 ms per batch, r06l)
+__global__ __launch_bounds__(256) void k_md_scan(const int32_t *__restrict__ cfirst, const int32_t *__restrict__ cnl,
+                                                 int64_t *__restrict__ cline0, int nfiles) {
+  __shared__ int64_t s_w[4];
+  const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (f >= nfiles) return;
-  int64_t s = 0;
-  for (int c = cfirst[f]; c < cfirst[f + 1]; c++) {
-    cline0[c] = s;
-    s += cnl[c];
+  const int c0 = cfirst[f], c1 = cfirst[f + 1];
+  int64_t base = 0;
+  for (int r = c0; r < c1; r += 256) {
+    const int c = r + tid;
+    const int64_t v = c < c1 ? cnl[c] : 0;
+    int64_t incl = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int64_t y = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += y;
+    }
+    if (lane == 63) s_w[wv] = incl;
+    __syncthreads();
+    int64_t before = base;
+    for (int w = 0; w < wv; w++) before += s_w[w];
+    if (c < c1) cline0[c] = before + incl - v;
+    base += s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    __syncthreads();
   }
 }
 
@@ -213,8 +230,17 @@ struct PadText {
 // thread owns a 256-byte segment and parses the lines that START in it, found
 // from the newline bit masks of its 16 words; line numbers come from a block
 // scan of the per-segment newline counts.
+// waves per SIMD the parse is held to, and 16-B loads in flight per thread
+// while the chunk fills LDS: 8 / 3 fit 62 VGPRs without spills and 8
+// workgroups per CU (134 KiB of LDS); 5 / 6 was round 5's (96 VGPRs)
+#ifndef GRID_MDPARSE_WPE
+#define GRID_MDPARSE_WPE 8
+#endif
+#ifndef GRID_MDPARSE_G
+#define GRID_MDPARSE_G 3
+#endif
 template <int MODE>
-__global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(5))) void k_md_parse(const uint8_t *__restrict__ text, const int64_t *__restrict__ toff,
+__global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(GRID_MDPARSE_WPE))) void k_md_parse(const uint8_t *__restrict__ text, const int64_t *__restrict__ toff,
                                                   const int64_t *__restrict__ tlen,
                                                   const int32_t *__restrict__ cfile,
                                                   const int64_t *__restrict__ cstart,
@@ -243,7 +269,7 @@ __global__ __launch_bounds__(PTH) __attribute__((amdgpu_waves_per_eu(5))) void k
   // file's last partial word byte by byte, zeros past the file end
   {
     const int64_t lo = a - HALO, hi = min(L, b + MAXLINE);
-    constexpr int NW = SPAN / 16, G = 6;            // words; loads in flight per thread
+    constexpr int NW = SPAN / 16, G = GRID_MDPARSE_G;   // words; loads in flight per thread
     for (int k0 = 0; k0 * PTH < NW; k0 += G) {
       uint4 v[G];
 #pragma unroll
@@ -580,7 +606,7 @@ int grid_md_count(grid_ctx *ctx, const uint8_t *d_text, const int64_t *d_toff, c
   hipLaunchKernelGGL(k_md_count, dim3((unsigned)nchunks), dim3(256), 0, ctx->stream, d_text, d_toff, d_tlen, d_cfile,
                      d_cstart, d_cnl, d_flags, d_fstatus);
   LAUNCHCHK();
-  hipLaunchKernelGGL(k_md_scan, dim3((unsigned)((nfiles + 63) / 64)), dim3(64), 0, ctx->stream, d_cfirst, d_cnl,
+  hipLaunchKernelGGL(k_md_scan, dim3((unsigned)nfiles), dim3(256), 0, ctx->stream, d_cfirst, d_cnl,
                      d_cline0, (int)nfiles);
   LAUNCHCHK();
   return GRID_OK;
