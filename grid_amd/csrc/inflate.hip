@@ -617,13 +617,11 @@ __global__ __launch_bounds__(CT) void k_gz_crc(const uint8_t *__restrict__ out, 
   if (tid == 0 && s_bad) status[f] = GRID_GZ_ECRC;
 }
 
-// BGZF units (one member each, mcap == 1): one WAVE per member.  The text is
-// read in 1 KiB rows, lane l taking the 16 bytes [16 l, 16 l + 16) of every
-// row -- each wave load is 1 KiB contiguous -- and keeping the raw register
-// (from state 0) of its column of blocks: acc_l = M^1024 acc_l ^ crc0(block).
-// A 6-level tree of M^(16 2^k) (c_crc_pow[4 + k]) joins the columns (lane l's
-// last block is followed by 63 - l blocks of its row), lane 0 adds the tail
-// row byte by byte and the initial register.  Same raw-register convention as
+// BGZF units (one member each, mcap == 1): one WAVE per member.  Lane l
+// computes the raw register (from state 0) of the 1 KiB chunks l, l + 64, ...
+// with the slicing tables, joins them with M^65536, shifts the result to its
+// place (the chunks after its last) and the lanes XOR; lane 0 adds the tail
+// (< 1 KiB) byte by byte and the initial register.  Same raw-register convention as
 // k_gz_crc; a member whose CRC differs gets GRID_GZ_ECRC.
 __global__ __launch_bounds__(256) void k_member_check(const uint8_t *__restrict__ out,
                                                       const int64_t *__restrict__ out_off,
@@ -654,27 +652,42 @@ __global__ __launch_bounds__(256) void k_member_check(const uint8_t *__restrict_
     c ^= w;
     return t4[3][c & 255] ^ t4[2][(c >> 8) & 255] ^ t4[1][(c >> 16) & 255] ^ t4[0][c >> 24];
   };
+  // round 6: lane l takes the contiguous 1 KiB chunks l, l + 64, ... (a
+  // BGZF member has at most 64: one per lane), so a lane shifts its register
+  // once per KiB of its own instead of once per 16 B (the M^1024 product was
+  // most of the kernel's work); the lanes' registers then meet with one shift
+  // each to their chunk's place and an XOR
   uint32_t acc = 0;
   const bool al = ((uintptr_t)base & 15) == 0;
-  for (int64_t k = 0; k < R; k++) {
-    const uint8_t *p = base + (k << 10) + 16 * lane;
-    uint32_t w0, w1, w2, w3;
-    if (al) {
-      const uint4 v = *reinterpret_cast<const uint4 *>(p);
-      w0 = v.x; w1 = v.y; w2 = v.z; w3 = v.w;
-    } else {                                            // a member's text at any byte offset
-      uint32_t b[4] = {0, 0, 0, 0};
-      for (int e = 0; e < 16; e++) b[e >> 2] |= (uint32_t)p[e] << (8 * (e & 3));
-      w0 = b[0]; w1 = b[1]; w2 = b[2]; w3 = b[3];
+  int64_t nl = 0;                                       // chunks of this lane
+  for (int64_t k = lane; k < R; k += 64, nl++) {
+    const uint8_t *p = base + (k << 10);
+    uint32_t c = 0;
+    for (int q = 0; q < 64; q += 4) {
+      uint32_t w[16];
+      if (al) {
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          const uint4 v = *reinterpret_cast<const uint4 *>(p + 16 * (q + e));
+          w[4 * e] = v.x; w[4 * e + 1] = v.y; w[4 * e + 2] = v.z; w[4 * e + 3] = v.w;
+        }
+      } else {                                          // a member's text at any byte offset
+#pragma unroll
+        for (int e = 0; e < 16; e++) w[e] = 0;
+        for (int e = 0; e < 64; e++) w[e >> 2] |= (uint32_t)p[16 * q + e] << (8 * (e & 3));
+      }
+#pragma unroll
+      for (int e = 0; e < 16; e++) c = step4(c, w[e]);
     }
-    const uint32_t c = step4(step4(step4(step4(0u, w0), w1), w2), w3);
-    acc = gf2_apply(c_crc_pow[10], acc) ^ c;
+    acc = (nl ? gf2_apply(c_crc_pow[16], acc) : 0u) ^ c;     // M^65536: 64 chunks later
+  }
+  if (nl) {
+    // this lane's last chunk is chunk lane + 64 (nl - 1); R - 1 - that chunks follow it
+    const int64_t after = R - 1 - (lane + 64 * (nl - 1));
+    acc = crc_shift(acc, (uint64_t)after << 10);
   }
 #pragma unroll
-  for (int k = 0; k < 6; k++) {
-    const uint32_t o = __shfl_down(acc, 1 << k, 64);
-    if ((lane & ((2 << k) - 1)) == 0) acc = gf2_apply(c_crc_pow[4 + k], acc) ^ o;
-  }
+  for (int k = 32; k > 0; k >>= 1) acc ^= __shfl_xor(acc, k, 64);
   if (lane == 0) {
     uint32_t c = acc;                                   // raw CRC of the R full rows, from state 0
     for (int64_t e = R << 10; e < L; e++) c = t4[0][(c ^ base[e]) & 255] ^ (c >> 8);

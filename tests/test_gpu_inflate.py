@@ -146,6 +146,10 @@ def test_streams_at_any_offset(dev, mcap):
             streams.append(bg[s_:s_ + l_])
             refs.append(zlib.decompress(bg[s_:s_ + l_], 31))
             assert len(refs[-1]) == i_
+    # one member far past 64 KiB (several 1 KiB chunks per lane in the check),
+    # first, so the corrupt copies below stay within the 64 KiB cap
+    streams.insert(0, gzip.compress(texts[2], 6))
+    refs.insert(0, texts[2])
     streams.append(gzip.compress(texts[1], 1)[:-9])        # truncated
     refs.append(None)
     for k in (1, len(streams) // 2, len(streams) - 2):    # a wrong trailer CRC: every byte decodes
