@@ -85,6 +85,18 @@ def test_random_cohorts(dev, tmp_path, split):
     _dev_vs_host(dev, d, sorted(files), chrom="1", start=500_000, end=2_000_000, excluded={"chr1": {7, 8, 900}})
 
 
+def test_files_of_many_parse_chunks(dev, tmp_path):
+    """Files of ~4.5 MB of text: ~275 16 KiB parse chunks each, so the
+    per-file newline scan (k_md_scan, a workgroup per file, 256 chunks a
+    round) carries its running base across rounds; the device matrix must equal
+    the host parser's."""
+    rng = np.random.default_rng(5)
+    files = {f"L{i}": _rand_lines(rng, 200_000 - 7919 * i) for i in range(3)}
+    d = _cohort(tmp_path, files, members=1)
+    a = _dev_vs_host(dev, d, sorted(files))
+    assert len(a[0]) == 3
+
+
 def test_golden_cohorts(dev, tmp_path):
     """g1b / g1c on the device path; g1's chr10 decoy lines repeat chr1's
     (start, end) keys (reference quirk Q1, last line wins) -- outside the
