@@ -210,6 +210,13 @@ def load():
     # the file list the library hashed (its build info), so the two sides
     # cannot drift apart when a source is added to the Makefile
     files = info.get("src_files")
+    if files and (_CSRC / "Makefile").exists():          # a source tree, not an installed copy
+        # a source added to the Makefile after the library was built: the
+        # library's own list no longer names every hashed file
+        named = sorted(n for n in files.split() if not n.startswith(".."))
+        if named != _HASHED:
+            raise GridNativeError(f"{LIB_PATH} hashed other source files ({' '.join(named)}) than this tree "
+                                  f"lists: rebuild with `make -C grid_amd/csrc`")
     want = source_sha256(files.split() if files else None)
     if want is not None and info.get("src_sha256") != want:
         raise GridNativeError(f"{LIB_PATH} was built from other sources (library {info.get('src_sha256')}, "

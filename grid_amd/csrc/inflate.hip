@@ -40,6 +40,10 @@ namespace {
 // 4 KiB ring: 15 waves, r03r.)
 constexpr int RING = 2048, RMASK = RING - 1, FLUSH = 1024, NEAR = RING - 258;
 static_assert(NEAR > FLUSH + 266 + 257, "far copies must read flushed bytes only");
+// the unmasked 64-lane copy (copy_bytes) writes slots pos + len .. pos + 63:
+// they must hold flushed bytes only, and no near copy may read them
+static_assert(FLUSH + 266 + 64 <= RING, "the unmasked copy writes flushed slots only");
+static_assert(NEAR < RING - 63, "near copies never read the unmasked copy's spare slots");
 
 __constant__ uint32_t c_crc_pow[48][32];   // columns of M^(2^k), M = one zero byte
 
@@ -513,7 +517,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GRID_INFLATE
   p.n_in = in_len[f] + skew;
   p.tab = s_tab;
   p.ftab = s_ftab;
-  p.fbase = -(1 << 30);                         // no window yet
+  // no window yet: r = ip - fbase < 0 forces the first load; fbase + 256
+  // bytes of input stay below 2^31 (fits), so neither r nor rmax overflows
+  p.fbase = 0x7fffff00;
   p.ring = s_ring;
   p.out = out + out_off[f];
   // 32-bit positions (DevP): a stream or an output of 2^31 bytes or more is

@@ -130,6 +130,12 @@ def test_library_provenance_matches_the_tree(monkeypatch):
     assert sorted(n for n in names if not n.startswith("..")) == _abi._HASHED
     assert info["arch"] == "gfx950" and info["built_utc"]
     monkeypatch.setattr(_abi, "_lib", None)
+    # a source the tree hashes that the library did not: refused
+    monkeypatch.setattr(_abi, "_HASHED", sorted(_abi._HASHED + ["added_later.hip"]))
+    with pytest.raises(_abi.GridNativeError, match="other source files"):
+        _abi.load()
+    monkeypatch.undo()
+    monkeypatch.setattr(_abi, "_lib", None)
     monkeypatch.setattr(_abi, "source_sha256", lambda names=None: "0" * 64)
     with pytest.raises(_abi.GridNativeError, match="other sources"):
         _abi.load()
