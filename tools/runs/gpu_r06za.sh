@@ -1,6 +1,7 @@
 #!/bin/bash
 # round 6: ingest batch ramp (1 GB, 2 GB, then 4 GB batches) -- GPU ingest tests, then
 # from-files K = 2 alternating ramp / no ramp on one cohort, per-batch trace
+# (the GRID_INGEST_RAMP knob this script sets was dropped with the ramp: profiles/r06za_ingest_ramp_ab.json)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r06za
