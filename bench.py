@@ -307,6 +307,85 @@ def files_prepare(args, rank, local, world, note):
     return {"skipped": "timed out waiting for rank 0's cohort"}
 
 
+def inflate_roofline(data, dev, note, max_bytes=4 << 30, reps=3):
+    """The from-files headline's dominant kernel against HBM: k_inflate is
+    ~2/3 of that step's GPU time (profiles/r06zp_bench_files_headline_kernel_stats.csv,
+    the ingest ~70 % of its wall).  One pipelined ingest batch's worth of the
+    cohort's BGZF files (<= 4 GB compressed, what a batch holds) is inflated
+    in HBM by the ingest's own launch, grid_gunzip_batch (k_inflate, one wave
+    per member, + k_member_check, each member's CRC and ISIZE; k_inflate ~96 %
+    of it), timed with HIP events on the context's stream.  Algorithmic HBM
+    bytes per launch = compressed bytes read + text written + text re-read by
+    the check.  The kernel is issue-bound (one serial Huffman stream per wave,
+    DESIGN round-6 item 5), so the HBM fraction is small by construction."""
+    import glob
+    import numpy as np
+    from grid_amd import _abi
+    names = sorted(glob.glob(os.path.join(data, "mosdepth", "*.regions.bed.gz")))
+    blobs, tot = [], 0
+    for f in names:
+        sz = os.path.getsize(f)
+        if blobs and tot + sz > max_bytes:
+            break
+        with open(f, "rb") as fh:
+            blobs.append(fh.read())
+        tot += sz
+    io, il, oo, oc = [], [], [], []
+    pos = opos = 0
+    for b in blobs:
+        ms, ml, mi = _abi.gz_members(b)
+        cum = np.zeros(len(mi), np.int64)
+        np.cumsum(mi[:-1], out=cum[1:])
+        io.append(pos + ms)
+        il.append(ml)
+        oo.append(opos + cum)
+        oc.append(mi.astype(np.int64))
+        pos += -(-len(b) // 256) * 256
+        opos += -(-int(mi.sum()) // 256) * 256
+    io, il, oo, oc = (np.concatenate(x).astype(np.int64) for x in (io, il, oo, oc))
+    src = np.zeros(pos + 256, np.uint8)
+    p = 0
+    for b in blobs:
+        src[p:p + len(b)] = np.frombuffer(b, np.uint8)
+        p += -(-len(b) // 256) * 256
+    del blobs
+    d_src = dev.upload(src)
+    del src
+    d = [dev.upload(x) for x in (io, il, oo, oc)]
+    nu = len(io)
+    out = dev.alloc(opos + 256, np.uint8)
+    mem = dev.alloc(nu * _abi.GZ_MEMBER_BYTES, np.uint8)
+    st_d, ln_d, nm_d = dev.alloc(nu, np.int32), dev.alloc(nu, np.int64), dev.alloc(nu, np.int32)
+    ms_l = []
+    for rep in range(reps + 1):                   # the first launch untimed
+        dev.record(0)
+        _abi.call("grid_gunzip_batch", dev.ctx, d_src.ptr, d[0].ptr, d[1].ptr, nu, out.ptr, d[2].ptr, d[3].ptr,
+                  mem.ptr, 1, st_d.ptr, ln_d.ptr, nm_d.ptr)
+        dev.record(1)
+        t = dev.elapsed_ms(0, 1)
+        if rep:
+            ms_l.append(t)
+    ust, uln = st_d.numpy(), ln_d.numpy()
+    if not (ust == 0).all():
+        raise RuntimeError(f"inflate leg: member statuses {np.unique(ust, return_counts=True)}")
+    text = int(uln.sum())
+    if text != int(oc.sum()):
+        raise RuntimeError("inflate leg: text length differs from the members' ISIZEs")
+    comp = int(il.sum())
+    ms = float(np.mean(ms_l))
+    alg = comp + 2 * text
+    peak = 8000.0
+    ach = alg / (ms * 1e-3) / 1e9
+    note(f"inflate leg: {len(io)} members, {comp / 1e9:.2f} GB -> {text / 1e9:.2f} GB text in {ms:.1f} ms")
+    return {"kernel": "grid_gunzip_batch (k_inflate + k_member_check, the ingest's launch)", "bound": "hbm",
+            "achieved": ach, "peak": peak, "unit": "GB/s", "frac": ach / peak, "traffic": None,
+            "algorithmic_bytes_per_launch": alg, "bytes_def": "compressed read + text written + text re-read (CRC)",
+            "compressed_bytes": comp, "text_bytes": text, "members": int(nu), "launch_ms": ms,
+            "launch_ms_each": ms_l, "text_gbs": text / (ms * 1e-3) / 1e9,
+            "note": "issue-bound (one serial Huffman stream per wave, 8 waves per SIMD): the HBM fraction is small "
+                    "by construction; the line's `roofline` is the device chain's Gram"}
+
+
 def files_leg(args, prep, steps, warmup, world, rank, dist, note):
     """The headline: ``steps`` timed runs of run_wgs_pipeline (the drop-in
     `grid wgs`, steps 4-7 from the mosdepth files to every output file) after
@@ -840,6 +919,12 @@ def main():
         c3["gram_frac_2N2R"] = o3["roofline"]["frac"]
         c3["executed_frac"] = o3["roofline"]["executed_frac"]
         out["config3_1gpu"] = c3
+    if rank == 0 and world == 1 and headline == "files" and files is not None and "value" in files:
+        try:
+            out["ingest_roofline"] = inflate_roofline(files_paths(args)[0], dev, note)
+        except Exception as e:                     # the line still prints; the reason is on it
+            out["ingest_roofline"] = {"error": repr(e)[:300]}
+        torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         c0 = 0
         ns, ms = min(args.cpu_samples, n), min(args.cpu_bins, m)
